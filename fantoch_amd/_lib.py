@@ -1,0 +1,106 @@
+"""ctypes binding of libfantoch_hip.so (the C ABI in include/fantoch_hip.h).
+
+The product path is the HIP library: there is no CPU fallback.  If the shared
+library is missing or fails to load this module raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfantoch_hip.so")
+
+FH_OK, FH_EINVAL, FH_EHIP, FH_EOOM, FH_EINVARIANT, FH_ECAP, FH_ENOTIMPL = range(7)
+STATUS_NAMES = ["FH_OK", "FH_EINVAL", "FH_EHIP", "FH_EOOM", "FH_EINVARIANT", "FH_ECAP",
+                "FH_ENOTIMPL"]
+
+
+class FhError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        name = STATUS_NAMES[status] if 0 <= status < len(STATUS_NAMES) else str(status)
+        super().__init__(f"{name}: {msg}")
+        self.status = status
+
+
+class fh_config(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("f", C.c_uint32), ("shard_count", C.c_uint32),
+                ("device", C.c_int32), ("key_space", C.c_uint64)]
+
+
+class fh_stream_desc(C.Structure):
+    _fields_ = [("n", C.c_size_t), ("keys_per_cmd", C.c_uint32), ("views", C.c_uint32),
+                ("nproc", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class fh_workload(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n", C.c_uint32), ("keys_per_cmd", C.c_uint32),
+                ("kind", C.c_uint32), ("conflict_rate", C.c_uint32), ("pool_size", C.c_uint32),
+                ("clients", C.c_uint32), ("zipf_s", C.c_double), ("key_count", C.c_uint64),
+                ("views", C.c_uint32), ("window", C.c_uint32)]
+
+
+V, S, P = C.c_void_p, C.c_size_t, C.POINTER
+
+# name -> (restype, argtypes); every symbol declared in include/fantoch_hip.h
+SIGNATURES = {
+    "fh_version": (C.c_char_p, []),
+    "fh_last_error": (C.c_char_p, []),
+    "fh_device_count": (C.c_int, [P(C.c_int)]),
+    "fh_keydeps_create": (C.c_int, [C.c_uint64, P(fh_config), P(V)]),
+    "fh_keydeps_destroy": (C.c_int, [V]),
+    "fh_keydeps_add_batch": (C.c_int, [V, S, V, V, V, V, V, V, V, V, S, P(S)]),
+    "fh_keydeps_cmd_deps": (C.c_int, [V, S, V, V, S, P(S)]),
+    "fh_keydeps_noop_deps": (C.c_int, [V, V, S, P(S)]),
+    "fh_graph_create": (C.c_int, [C.c_uint32, C.c_uint64, P(fh_config), P(V)]),
+    "fh_graph_destroy": (C.c_int, [V]),
+    "fh_graph_add_batch": (C.c_int, [V, S, V, V, V, V, V]),
+    "fh_graph_drain": (C.c_int, [V, V, V, S, P(S)]),
+    "fh_graph_mark_executed": (C.c_int, [V, S, V]),
+    "fh_graph_set_executed_frontier": (C.c_int, [V, C.c_uint32, C.c_uint64]),
+    "fh_graph_pending": (C.c_int, [V, P(S)]),
+    "fh_graph_missing": (C.c_int, [V, V, S, P(S)]),
+    "fh_engine_create": (C.c_int, [P(fh_config), P(V)]),
+    "fh_engine_destroy": (C.c_int, [V]),
+    "fh_engine_reset": (C.c_int, [V]),
+    "fh_engine_stage": (C.c_int, [V, P(fh_stream_desc), V, V, V, V]),
+    "fh_engine_run": (C.c_int, [V, P(C.c_float)]),
+    "fh_engine_results": (C.c_int, [V, V, V, S, P(S), V, V, V, V]),
+    "fh_engine_kernel_times": (C.c_int, [V, P(C.c_char_p), P(C.c_float), S, P(S)]),
+    "fh_engine_set_profiling": (C.c_int, [V, C.c_int]),
+    "fh_workload_key_space": (C.c_uint64, [P(fh_workload)]),
+    "fh_workload_generate": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V, V, V]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the HIP library (raises if it is missing: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build it with `python -m fantoch_amd.build` "
+            "(the HIP engine has no CPU fallback)")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int) -> None:
+    if status != FH_OK:
+        msg = load().fh_last_error()
+        raise FhError(status, msg.decode() if msg else "")
+
+
+def ptr(a):
+    """numpy array -> void* (None for empty/None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(V)

@@ -1,0 +1,109 @@
+// fh_common.h -- shared host/device helpers for the fantoch_hip engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+
+#include "../../include/fantoch_hip.h"
+
+namespace fh {
+
+// --- dots (fantoch/src/id.rs:21-27) -------------------------
+__host__ __device__ inline uint64_t make_dot(uint32_t src, uint64_t seq) {
+  return (uint64_t(src) << 56) | seq;
+}
+__host__ __device__ inline uint32_t dot_src(uint64_t d) { return uint32_t(d >> 56); }
+__host__ __device__ inline uint64_t dot_seq(uint64_t d) { return d & 0x00FFFFFFFFFFFFFFull; }
+
+// --- errors -----------------------------------------------------------------
+struct Error : std::runtime_error {
+  fh_status code;
+  Error(fh_status c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define FH_HIP(expr)                                                          \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess)                                                     \
+      throw ::fh::Error(_e == hipErrorOutOfMemory ? FH_EOOM : FH_EHIP,        \
+                        std::string(#expr) + ": " + hipGetErrorString(_e) +   \
+                            " (" __FILE__ ":" + std::to_string(__LINE__) +    \
+                            ")");                                             \
+  } while (0)
+
+#define FH_CHECK(cond, code, msg)                                             \
+  do {                                                                        \
+    if (!(cond)) throw ::fh::Error((code), (msg));                            \
+  } while (0)
+
+// --- device buffer ----------------------------------------------------------
+template <class T>
+struct DBuf {
+  T *p = nullptr;
+  size_t cap = 0;
+  DBuf() = default;
+  DBuf(const DBuf &) = delete;
+  DBuf &operator=(const DBuf &) = delete;
+  ~DBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  // Ensure capacity for n elements (contents not preserved).
+  T *ensure(size_t n) {
+    if (n <= cap && p) return p;
+    release();
+    size_t c = n < 16 ? 16 : n;
+    FH_HIP(hipMalloc(reinterpret_cast<void **>(&p), c * sizeof(T)));
+    cap = c;
+    return p;
+  }
+  T *get() const { return p; }
+};
+
+inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 8192) {
+  size_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return unsigned(g);
+}
+
+// Number of significant bits of (x - 1), at least 1: bits needed for ids < x.
+inline int bits_for(uint64_t x) {
+  int b = 1;
+  while (b < 64 && (uint64_t(1) << b) < x) b++;
+  return b;
+}
+
+// Device selection per SURVEY §8b (shard -> device, or env override).
+int pick_device(const fh_config *cfg, uint64_t shard_id);
+
+// Thread-local last error.
+void set_last_error(const std::string &m);
+
+}  // namespace fh
+
+// C-ABI wrappers: map exceptions to fh_status + thread-local message.
+#define FH_API_BEGIN try {
+#define FH_API_END                                                                \
+  return FH_OK;                                                                   \
+  }                                                                               \
+  catch (const fh::Error &e) {                                                    \
+    fh::set_last_error(e.what());                                                 \
+    return e.code;                                                                \
+  }                                                                               \
+  catch (const std::bad_alloc &) {                                                \
+    fh::set_last_error("host allocation failed");                                 \
+    return FH_EOOM;                                                               \
+  }                                                                               \
+  catch (const std::exception &e) {                                               \
+    fh::set_last_error(e.what());                                                 \
+    return FH_EINVARIANT;                                                         \
+  }
+

@@ -1,0 +1,163 @@
+"""HipKeyDeps -- the KeyDeps trait backed by the HIP engine.
+
+Mirrors fantoch_ps/src/protocol/common/graph/deps/keys/mod.rs:37-63:
+
+    KeyDeps::new(shard_id)                     -> HipKeyDeps(shard_id, ...)
+    add_cmd(dot, &cmd, past) -> HashSet<Dep>   -> add_cmd(dot, cmd, past)
+    add_noop(dot) -> HashSet<Dep>              -> add_noop(dot)
+    cmd_deps(&cmd) / noop_deps() (test-only)   -> cmd_deps(cmd) / noop_deps()
+    parallel() -> bool                         -> parallel()  (False, like SequentialKeyDeps)
+
+plus the batched form the engine is built for, add_batch(), which computes a
+whole arrival-ordered batch of add_cmd/add_noop calls in one device pass.
+
+Results are sets of packed dots.  `Dependency.shards` (keys/mod.rs:18-35) is a
+function of the dependency's dot (the shard set of that command), so dot-set
+equality is the parity contract; `dependencies()` rebuilds
+full Dependency values from the shard sets the instance has seen.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import FrozenSet, Iterable, Optional
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass(frozen=True)
+class Dependency:
+    """Dependency{dot, shards} (deps/keys/mod.rs:18-35); shards None = noop."""
+    dot: int
+    shards: Optional[FrozenSet[int]]
+
+
+class KeyInterner:
+    """Key = String (fantoch/src/kvs.rs:6) -> dense id < key_space (no hashing,
+    no collisions)."""
+
+    def __init__(self, key_space: int):
+        self.key_space = key_space
+        self.ids = {}
+
+    def __call__(self, key) -> int:
+        i = self.ids.get(key)
+        if i is None:
+            i = len(self.ids)
+            if i >= self.key_space:
+                raise L.FhError(L.FH_EINVAL, f"more than key_space={self.key_space} keys")
+            self.ids[key] = i
+        return i
+
+    def many(self, keys: Iterable) -> list:
+        return [self(k) for k in keys]
+
+
+def make_config(n=1, f=0, shard_count=1, device=-1, key_space=1 << 20) -> L.fh_config:
+    return L.fh_config(n=n, f=f, shard_count=shard_count, device=device, key_space=key_space)
+
+
+class HipKeyDeps:
+    """KeyDeps implementation over fh_keydeps_* (include/fantoch_hip.h)."""
+
+    def __init__(self, shard_id: int = 0, key_space: int = 1 << 20, device: int = -1,
+                 intern: bool = True):
+        self._lib = L.load()
+        self.shard_id = shard_id
+        self.cfg = make_config(device=device, key_space=key_space)
+        h = C.c_void_p()
+        L.check(self._lib.fh_keydeps_create(shard_id, C.byref(self.cfg), C.byref(h)))
+        self._h = h
+        self.keys = KeyInterner(key_space) if intern else None
+        self._shards = {}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.fh_keydeps_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @staticmethod
+    def parallel() -> bool:
+        return False  # SequentialKeyDeps::parallel (sequential.rs:60-62)
+
+    # -- helpers ---------------------------------------------------------
+    def _key_ids(self, cmd):
+        keys = cmd.keys(self.shard_id) if hasattr(cmd, "keys") else cmd
+        return self.keys.many(keys) if self.keys is not None else [int(k) for k in keys]
+
+    def _note_shards(self, dot, cmd):
+        if hasattr(cmd, "shards"):
+            self._shards[dot] = frozenset(cmd.shards())
+
+    def dependencies(self, dots) -> set:
+        return {Dependency(d, self._shards.get(d)) for d in dots}
+
+    # -- KeyDeps ---------------------------------------------------------
+    def add_cmd(self, dot: int, cmd, past: Optional[Iterable[int]] = None) -> set:
+        self._note_shards(dot, cmd)
+        past_l = None if past is None else [p.dot if isinstance(p, Dependency) else int(p)
+                                            for p in past]
+        off, deps = self.add_batch([dot], [self._key_ids(cmd)], None,
+                                   None if past_l is None else [past_l])
+        return set(int(x) for x in deps[off[0]:off[1]])
+
+    def add_noop(self, dot: int) -> set:
+        off, deps = self.add_batch([dot], [[]], [True], None)
+        return set(int(x) for x in deps[off[0]:off[1]])
+
+    def cmd_deps(self, cmd) -> set:
+        k = np.asarray(self._key_ids(cmd), dtype=np.uint64)
+        cap = len(k) + 1
+        out = np.zeros(cap, dtype=np.uint64)
+        n = C.c_size_t(0)
+        L.check(self._lib.fh_keydeps_cmd_deps(self._h, len(k), L.ptr(k), L.ptr(out), cap,
+                                              C.byref(n)))
+        return set(int(x) for x in out[:n.value])
+
+    def noop_deps(self) -> set:
+        n = C.c_size_t(0)
+        L.check(self._lib.fh_keydeps_noop_deps(self._h, None, 0, C.byref(n)))
+        out = np.zeros(max(1, n.value), dtype=np.uint64)
+        L.check(self._lib.fh_keydeps_noop_deps(self._h, L.ptr(out), len(out), C.byref(n)))
+        return set(int(x) for x in out[:n.value])
+
+    # -- batched form ------------------------------------------------------
+    def add_batch(self, dots, keys, is_noop=None, past=None):
+        """dots: sequence of packed dots; keys: per-command key-id lists (or a
+        (key_off, key_ids) pair of arrays); is_noop: optional bools; past:
+        optional per-command dot lists (None = no past for every command).
+        Returns (dep_off[n+1], dep_dots) as numpy arrays."""
+        n = len(dots)
+        dot_a = np.ascontiguousarray(dots, dtype=np.uint64)
+        if isinstance(keys, tuple):
+            key_off = np.ascontiguousarray(keys[0], dtype=np.uint32)
+            key_ids = np.ascontiguousarray(keys[1], dtype=np.uint64)
+        else:
+            key_off = np.zeros(n + 1, dtype=np.uint32)
+            key_off[1:] = np.cumsum([len(k) for k in keys]) if n else []
+            key_ids = np.asarray([k for ks in keys for k in ks], dtype=np.uint64)
+        noop = None if is_noop is None else np.ascontiguousarray(is_noop, dtype=np.uint8)
+        past_off = past_dot = None
+        if past is not None:
+            past_off = np.zeros(n + 1, dtype=np.uint32)
+            past_off[1:] = np.cumsum([len(p) for p in past]) if n else []
+            past_dot = np.asarray([x for p in past for x in p], dtype=np.uint64)
+        out_off = np.zeros(n + 1, dtype=np.uint32)
+        cap = int(len(key_ids) + n + (0 if past_dot is None else len(past_dot)) + 1)
+        while True:
+            out = np.zeros(cap, dtype=np.uint64)
+            ln = C.c_size_t(0)
+            st = self._lib.fh_keydeps_add_batch(
+                self._h, n, L.ptr(dot_a), L.ptr(key_off), L.ptr(key_ids) if len(key_ids) else None,
+                L.ptr(noop), L.ptr(past_off),
+                L.ptr(past_dot) if past_dot is not None and len(past_dot) else None,
+                L.ptr(out_off), L.ptr(out), cap, C.byref(ln))
+            if st == L.FH_ECAP:
+                cap = int(ln.value)
+                continue
+            L.check(st)
+            return out_off, out[:ln.value]

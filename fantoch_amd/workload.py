@@ -1,0 +1,86 @@
+"""Seeded synthetic command streams (fh_workload_*, see csrc/workload.cpp).
+
+Mirrors the knobs of fantoch's client Workload + KeyGen
+(fantoch/src/client/workload.rs:11-61, key_gen.rs:10-19) for the BASELINE.json
+configurations.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+ZIPF, CONFLICT_RATE, CONFLICT_POOL = 0, 1, 2
+
+
+@dataclass
+class Stream:
+    dots: np.ndarray          # u64[n]
+    keys: np.ndarray          # u64[n, k]
+    fq_proc: np.ndarray       # u8[n, views] or None
+    fq_time: np.ndarray       # u64[n, views] or None
+    key_space: int
+
+    @property
+    def n(self):
+        return len(self.dots)
+
+    @property
+    def k(self):
+        return self.keys.shape[1]
+
+    def key_off(self):
+        return (np.arange(self.n + 1, dtype=np.uint64) * self.k).astype(np.uint32)
+
+
+@dataclass
+class Workload:
+    seed: int = 0xFA170C4000000000
+    n: int = 5                  # processes (dot sources 1..n)
+    keys_per_cmd: int = 1
+    kind: int = ZIPF
+    conflict_rate: int = 0
+    pool_size: int = 0
+    clients: int = 1024
+    zipf_s: float = 0.7
+    key_count: int = 1 << 20
+    views: int = 0              # fast quorum size (0 = single view)
+    window: int = 64            # reorder window W
+
+    @classmethod
+    def zipf(cls, s, key_count, k=1, **kw):
+        return cls(kind=ZIPF, zipf_s=s, key_count=key_count, keys_per_cmd=k, **kw)
+
+    @classmethod
+    def conflict_rate_(cls, rate, k=1, **kw):
+        return cls(kind=CONFLICT_RATE, conflict_rate=rate, keys_per_cmd=k, **kw)
+
+    @classmethod
+    def conflict_pool(cls, rate, pool, k=2, **kw):
+        return cls(kind=CONFLICT_POOL, conflict_rate=rate, pool_size=pool, keys_per_cmd=k, **kw)
+
+    def _c(self) -> L.fh_workload:
+        return L.fh_workload(seed=self.seed, n=self.n, keys_per_cmd=self.keys_per_cmd,
+                             kind=self.kind, conflict_rate=self.conflict_rate,
+                             pool_size=self.pool_size, clients=self.clients, zipf_s=self.zipf_s,
+                             key_count=self.key_count, views=self.views, window=self.window)
+
+    def key_space(self) -> int:
+        w = self._c()
+        return int(L.load().fh_workload_key_space(C.byref(w)))
+
+    def generate(self, count: int, first: int = 0) -> Stream:
+        lib = L.load()
+        w = self._c()
+        dots = np.zeros(count, dtype=np.uint64)
+        keys = np.zeros((count, self.keys_per_cmd), dtype=np.uint64)
+        fq_proc = fq_time = None
+        if self.views:
+            fq_proc = np.zeros((count, self.views), dtype=np.uint8)
+            fq_time = np.zeros((count, self.views), dtype=np.uint64)
+        L.check(lib.fh_workload_generate(C.byref(w), first, count, L.ptr(dots), L.ptr(keys),
+                                         L.ptr(fq_proc), L.ptr(fq_time)))
+        return Stream(dots, keys, fq_proc, fq_time, self.key_space())

@@ -1,0 +1,236 @@
+/*
+ * fantoch_hip.h -- C ABI of the MI355X batched dependency engine.
+ *
+ * This is the drop-in boundary for fantoch's dependency hot path: every entry
+ * point below replaces one reference interface (cited file:line, paths
+ * relative to the reference repository root).  The reference-side binding a
+ * maintainer would add (a `fantoch_hip` Rust crate: extern "C" decls,
+ * `impl KeyDeps for HipKeyDeps`, `impl Executor for HipGraphExecutor`) is
+ * given in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Dots are packed u64: ProcessId (u8) in bits 56..63, sequence in bits
+ *    0..55.  The packed order equals the derived Ord of fantoch's
+ *    Id{source, sequence} (fantoch/src/id.rs:21-27).  A dot is never 0.
+ *  - Keys are dense interned ids `< fh_config.key_space` (fantoch keys are
+ *    Strings, fantoch/src/kvs.rs:6; the shim interns them, no hashing, so
+ *    there are no collisions).
+ *  - All pointers passed in are HOST pointers owned by the caller unless the
+ *    name says `_device`; no pointer is retained after a call returns.  The
+ *    library owns device state behind opaque handles.
+ *  - Every function returns an fh_status.  On error fh_last_error() gives a
+ *    thread-local message.  The reference panics on every invariant
+ *    violation on this path; the shim turns non-OK into panic!.
+ *  - A handle is single-threaded (external synchronisation) and owns one HIP
+ *    stream on one device.
+ */
+#ifndef FANTOCH_HIP_H
+#define FANTOCH_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FH_ABI_VERSION 1
+
+typedef enum fh_status {
+  FH_OK = 0,
+  FH_EINVAL = 1,      /* bad argument (null pointer, key id >= key_space, ...) */
+  FH_EHIP = 2,        /* HIP runtime error (no device, launch failure, ...)    */
+  FH_EOOM = 3,        /* device allocation failed                              */
+  FH_EINVARIANT = 4,  /* internal invariant violated (reference: panic!)       */
+  FH_ECAP = 5,        /* output buffer too small; *len receives the size needed,
+                         no state was changed                                  */
+  FH_ENOTIMPL = 6     /* configuration not supported by this build             */
+} fh_status;
+
+/* Mirrors the parts of fantoch::config::Config the hot path reads
+ * (fantoch/src/config.rs:7-43) plus device placement. */
+typedef struct fh_config {
+  uint32_t n;           /* processes per shard            Config::n           */
+  uint32_t f;           /* tolerated faults               Config::f           */
+  uint32_t shard_count; /* shards                         Config::shard_count */
+  int32_t device;       /* HIP device ordinal; -1 = env FANTOCH_HIP_DEVICE,
+                           else shard_id % device count          */
+  uint64_t key_space;   /* interned key ids are < key_space (<= 2^31)         */
+} fh_config;
+
+const char *fh_version(void);
+/* Thread-local message for the last non-OK status returned on this thread. */
+const char *fh_last_error(void);
+fh_status fh_device_count(int *out);
+
+/* ======================================================================
+ * KeyDeps -- conflict detection.
+ * Replaces SequentialKeyDeps
+ * (fantoch_ps/src/protocol/common/graph/deps/keys/sequential.rs:7-144)
+ * behind the KeyDeps trait (fantoch_ps/src/protocol/common/graph/deps/keys/
+ * mod.rs:37-63).
+ * ==================================================================== */
+typedef struct fh_keydeps fh_keydeps;
+
+/* KeyDeps::new(shard_id)  keys/mod.rs:39 */
+fh_status fh_keydeps_create(uint64_t shard_id, const fh_config *cfg,
+                            fh_keydeps **out);
+fh_status fh_keydeps_destroy(fh_keydeps *h);
+
+/* A batch of KeyDeps::add_cmd / add_noop calls in arrival order
+ * (keys/mod.rs:44-52; sequential.rs:24-42, do_add_cmd :72-104,
+ * do_add_noop :106-123).  Result i equals what the i-th sequential call
+ * would have returned.
+ *   dot[n]                 command dots
+ *   key_off[n+1], key_id[] the command's keys on this shard (Command::keys,
+ *                          fantoch/src/command.rs:95-100); ignored for noops
+ *   is_noop[n]             NULL = no noops
+ *   past_off[n+1], past_dot[]  the `past: Option<HashSet<Dependency>>`
+ *                          argument (NULL = None for every command)
+ *   out_dep_off[n+1], out_dep_dot[out_cap]  dependency dots per command,
+ *                          ascending, no duplicates (a HashSet<Dependency>;
+ *                          `shards` is a function of the dot)
+ * Upper bound needed for out_cap: sum_i(keys_i + past_i + 1) for commands
+ * plus (distinct keys seen + 1) per noop; if out_cap is smaller, FH_ECAP is
+ * returned with *out_len = that bound and no state changes. */
+fh_status fh_keydeps_add_batch(fh_keydeps *h, size_t n, const uint64_t *dot,
+                               const uint32_t *key_off, const uint64_t *key_id,
+                               const uint8_t *is_noop, const uint32_t *past_off,
+                               const uint64_t *past_dot, uint32_t *out_dep_off,
+                               uint64_t *out_dep_dot, size_t out_cap,
+                               size_t *out_len);
+
+/* KeyDeps::cmd_deps (test-only query, keys/mod.rs:54-56;
+ * sequential.rs:44-50): latest noop + latest dot of each key, no update. */
+fh_status fh_keydeps_cmd_deps(fh_keydeps *h, size_t nkeys,
+                              const uint64_t *key_id, uint64_t *out,
+                              size_t cap, size_t *out_len);
+/* KeyDeps::noop_deps (keys/mod.rs:58-60; sequential.rs:52-58). */
+fh_status fh_keydeps_noop_deps(fh_keydeps *h, uint64_t *out, size_t cap,
+                               size_t *out_len);
+
+/* ======================================================================
+ * Graph executor -- SCC + execution order.
+ * Replaces GraphExecutor / DependencyGraph / TarjanSCCFinder
+ * (fantoch_ps/src/executor/graph/executor.rs:19-197, mod.rs:45-679,
+ * tarjan.rs:25-359, index.rs:18-211) behind the Executor trait
+ * (fantoch/src/executor/mod.rs:27-88).
+ * ==================================================================== */
+typedef struct fh_graph fh_graph;
+
+/* Executor::new(process_id, shard_id, config)  executor/mod.rs:39;
+ * DependencyGraph::new  graph/mod.rs:83-125 */
+fh_status fh_graph_create(uint32_t process_id, uint64_t shard_id,
+                          const fh_config *cfg, fh_graph **out);
+fh_status fh_graph_destroy(fh_graph *h);
+
+/* A batch of GraphExecutionInfo::Add{dot, cmd, deps} in arrival order
+ * (executor.rs:78-86 -> DependencyGraph::handle_add, graph/mod.rs:215-277).
+ * Vertices whose dependencies are all executed or present are ordered and
+ * become drainable; the rest stay pending (carried to later batches) exactly
+ * like the reference's PendingIndex (graph/index.rs:145-211). */
+fh_status fh_graph_add_batch(fh_graph *h, size_t n, const uint64_t *dot,
+                             const uint32_t *key_off, const uint64_t *key_id,
+                             const uint32_t *dep_off, const uint64_t *dep_dot);
+
+/* Drain commands ready to execute, in execution order
+ * (DependencyGraph::command_to_execute, graph/mod.rs:133-135): SCCs in
+ * topological order of the condensation, members of an SCC in dot order
+ * (tarjan.rs:14-15, mod.rs:497-524).  scc_label (may be NULL) receives the
+ * minimum dot of the command's SCC. */
+fh_status fh_graph_drain(fh_graph *h, uint64_t *exec_dot, uint64_t *scc_label,
+                         size_t cap, size_t *len);
+
+/* Executed-clock updates (AEClock::add; graph/mod.rs:199-212, 397-405). */
+fh_status fh_graph_mark_executed(fh_graph *h, size_t n, const uint64_t *dot);
+fh_status fh_graph_set_executed_frontier(fh_graph *h, uint32_t source,
+                                         uint64_t seq);
+/* Number of pending vertices (VertexIndex size, graph/index.rs:18-51). */
+fh_status fh_graph_pending(fh_graph *h, size_t *count);
+/* Missing dependencies of pending vertices (deps neither executed nor
+ * indexed; the dots PendingIndex waits on, index.rs:171-205). */
+fh_status fh_graph_missing(fh_graph *h, uint64_t *dots, size_t cap,
+                           size_t *len);
+
+/* ======================================================================
+ * Fused engine -- a committed command stream, device resident end to end:
+ * KeyDeps (one replica, or the fast-quorum views of Atlas/EPaxos with the
+ * QuorumDeps union, quorum.rs:28-98) -> dependency graph -> SCC ->
+ * execution order -> per-key execution sequence (ExecutionOrderMonitor,
+ * fantoch/src/executor/monitor.rs:20-28).  This is the batched entry the
+ * throughput metric is measured on.
+ * ==================================================================== */
+typedef struct fh_engine fh_engine;
+
+typedef struct fh_stream_desc {
+  size_t n;               /* commands in the batch                         */
+  uint32_t keys_per_cmd;  /* k: fixed keys per command (<= 8)              */
+  uint32_t views;         /* 0 = single replica view (stream order);
+                             >0 = fast-quorum size fq (replica views)      */
+  uint32_t nproc;         /* processes (replica ids 1..nproc) when views>0 */
+  uint32_t pad;
+} fh_stream_desc;
+
+fh_status fh_engine_create(const fh_config *cfg, fh_engine **out);
+fh_status fh_engine_destroy(fh_engine *h);
+/* Reset all persistent state (latest tables, executed clock). */
+fh_status fh_engine_reset(fh_engine *h);
+/* Stage a batch into device memory (host -> HBM, not part of the timed
+ * path).  key_id[n*k]; for views>0, fq_proc[n*fq] (replica of each member,
+ * member 0 = coordinator) and fq_time[n*fq] (arrival time of the command at
+ * that member; members process commands in (time, index) order). */
+fh_status fh_engine_stage(fh_engine *h, const fh_stream_desc *desc,
+                          const uint64_t *dot, const uint64_t *key_id,
+                          const uint8_t *fq_proc, const uint64_t *fq_time);
+/* Run the staged batch on the device (inputs already resident).  If
+ * device_ms is non-NULL the stream is synchronised and the device time of
+ * the run (HIP events on the engine's stream) is returned. */
+fh_status fh_engine_run(fh_engine *h, float *device_ms);
+/* Copy results back (each pointer may be NULL):
+ *   dep_off[n+1], dep_dot[cap]   committed deps per command (ascending)
+ *   scc_label[n]                 min dot of each command's SCC
+ *   exec_rank[n]                 position of each command in exec order
+ *   key_off[key_space+1], key_seq[n*k]  per-key execution sequence (dots) */
+fh_status fh_engine_results(fh_engine *h, uint32_t *dep_off, uint64_t *dep_dot,
+                            size_t dep_cap, size_t *dep_len,
+                            uint64_t *scc_label, uint32_t *exec_rank,
+                            uint32_t *key_off, uint64_t *key_seq);
+/* Per-kernel device times of the last run (ms), for the roofline report.
+ * names/ms arrays of length cap; *len = number of recorded kernels. */
+fh_status fh_engine_kernel_times(fh_engine *h, const char **names, float *ms,
+                                 size_t cap, size_t *len);
+/* Enable/disable per-kernel event timing (adds events between kernels). */
+fh_status fh_engine_set_profiling(fh_engine *h, int on);
+
+/* ======================================================================
+ * Synthetic workload (fantoch/src/client/{workload,key_gen}.rs semantics,
+ * seeded and counter-based so every consumer sees the same stream).
+ * ==================================================================== */
+typedef struct fh_workload {
+  uint64_t seed;
+  uint32_t n;             /* processes per shard (dot sources 1..n)        */
+  uint32_t keys_per_cmd;  /* k                                             */
+  uint32_t kind;          /* 0 = Zipf{s, key_count}; 1 = ConflictRate{r};
+                             2 = ConflictPool{r, pool} (key0 = shared key
+                             with prob r%, key1.. from a pool)             */
+  uint32_t conflict_rate; /* percent, kinds 1/2                            */
+  uint32_t pool_size;     /* kind 2                                        */
+  uint32_t clients;       /* clients (round-robin submission), kinds 1/2   */
+  double zipf_s;          /* kind 0                                        */
+  uint64_t key_count;     /* kind 0: keys ranked 1..key_count -> ids 0..   */
+  uint32_t views;         /* fast quorum size (0 = single view)            */
+  uint32_t window;        /* reorder window W for replica views            */
+} fh_workload;
+
+/* Key space the workload's ids live in. */
+uint64_t fh_workload_key_space(const fh_workload *w);
+/* Generate commands [first, first+count): dot[count], key_id[count*k] and,
+ * if views>0, fq_proc[count*views], fq_time[count*views]. */
+fh_status fh_workload_generate(const fh_workload *w, uint64_t first,
+                               size_t count, uint64_t *dot, uint64_t *key_id,
+                               uint8_t *fq_proc, uint64_t *fq_time);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FANTOCH_HIP_H */
