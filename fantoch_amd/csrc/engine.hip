@@ -1,0 +1,584 @@
+// engine.hip -- fused, device-resident dependency engine (fh_engine_*).
+//
+// One batch of committed commands goes through, without leaving HBM:
+//   KeyDeps    per replica view: stable radix sort of (replica, key, arrival)
+//              elements, previous element of each (replica, key) segment is the
+//              dependency (SequentialKeyDeps::do_add_cmd,
+//              fantoch_ps/src/protocol/common/graph/deps/keys/sequential.rs:72-104);
+//              the persistent latest table answers segment heads
+//   union      the committed deps of a command are the union of its fast-quorum
+//              members' reports (QuorumDeps, deps/quorum.rs:28-98, called at
+//              atlas.rs:356-366 / epaxos.rs:333-342); each member's report is
+//              the coordinator's deps plus its own (atlas.rs:303-309)
+//   graph      SCC + execution order + per-key sequence (graph_core.hip)
+//   clock      the executed clock advances (AEClock::add, tarjan.rs:296)
+// With a single view every dependency points to an earlier arrival, so the
+// arrival order is already topological and the per-key order is the key-sorted
+// element order: the graph stage certifies that and reuses it.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "graph_core.h"
+
+namespace fh {
+namespace {
+
+constexpr unsigned B = 256;
+#define GRID_STRIDE(i, n) \
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
+
+// composite sort key for replica views: ((replica * K + key) << tb) | time
+__global__ void k_view_keys(uint32_t M, uint32_t k, uint32_t fq, uint64_t K,
+                            const uint32_t *__restrict__ key32, const uint8_t *__restrict__ fq_proc,
+                            const uint64_t *__restrict__ fq_time, uint64_t tmin, int tb,
+                            uint64_t *__restrict__ out) {
+  GRID_STRIDE(e, M) {
+    const uint32_t s = e % k;
+    const uint32_t ij = e / k;  // i * fq + j
+    const uint32_t i = ij / fq;
+    const uint64_t seg = uint64_t(fq_proc[ij]) * K + key32[i * k + s];
+    out[e] = (seg << tb) | (fq_time[ij] - tmin);
+  }
+}
+
+// Element dependency = previous element of its segment (in-batch vid) or the
+// persistent latest entry of the segment (external dot) at the head.
+template <class KT>
+__global__ void k_prev_engine(uint32_t M, const KT *__restrict__ ks, const uint32_t *__restrict__ vs,
+                              int tb, uint32_t per_cmd, const uint64_t *__restrict__ latest,
+                              uint32_t *__restrict__ dep_vid,
+                              uint64_t *__restrict__ dep_ext, uint8_t *__restrict__ tail,
+                              uint32_t *__restrict__ sorted_vid) {
+  GRID_STRIDE(j, M) {
+    const uint32_t e = vs[j];
+    const KT seg = ks[j] >> tb;
+    const bool head = j == 0 || (ks[j - 1] >> tb) != seg;
+    const bool is_tail = j + 1 == M || (ks[j + 1] >> tb) != seg;
+    if (head) {
+      // the segment id is the latest-table slot: key, or replica * K + key
+      dep_vid[e] = ~0u;
+      dep_ext[e] = latest[uint64_t(seg)];
+    } else {
+      dep_vid[e] = vs[j - 1] / per_cmd;
+      dep_ext[e] = 0;
+    }
+    tail[e] = is_tail;
+    if (sorted_vid) sorted_vid[j] = e / per_cmd;
+  }
+}
+
+__device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
+  for (uint32_t i = 1; i < n; i++) {
+    const uint64_t x = a[i];
+    uint32_t j = i;
+    while (j > 0 && a[j - 1] > x) {
+      a[j] = a[j - 1];
+      j--;
+    }
+    a[j] = x;
+  }
+  uint32_t w = n ? 1 : 0;
+  for (uint32_t i = 1; i < n; i++)
+    if (a[i] != a[w - 1]) a[w++] = a[i];
+  return w;
+}
+
+// Per command: union of its fast-quorum members' element deps (vids and
+// external dots), committed dep dots (sorted, fixed stride S), graph edges
+// (vids, padded with the vertex itself), latest-table update at tails and the
+// missing-dependency flag for external deps that are not executed.
+__global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
+                             const uint32_t *__restrict__ key32, const uint8_t *__restrict__ fq_proc,
+                             const uint64_t *__restrict__ dot, const uint32_t *__restrict__ dep_vid,
+                             const uint64_t *__restrict__ dep_ext, const uint8_t *__restrict__ tail,
+                             uint64_t *__restrict__ latest, const uint64_t *__restrict__ frontier,
+                             uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ dep_cnt,
+                             uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
+                             uint32_t *nblocked) {
+  const uint32_t S = fq * k;
+  GRID_STRIDE(i, n) {
+    uint64_t *dd = dep_dot + size_t(i) * S;
+    uint32_t *ds = dst + size_t(i) * S;
+    uint32_t nv = 0, nd = 0;
+    bool missing = false;
+    const uint64_t self = dot[i];
+    for (uint32_t t = 0; t < S; t++) {
+      const uint32_t e = i * S + t;
+      const uint32_t v = dep_vid[e];
+      if (v != ~0u) {
+        bool dup = false;
+        for (uint32_t q = 0; q < nv; q++) dup |= ds[q] == v;
+        if (!dup) ds[nv++] = v;
+        dd[nd++] = dot[v];
+      } else {
+        const uint64_t x = dep_ext[e];
+        if (x) {
+          dd[nd++] = x;
+          // executed? (AEClock frontier; exceptions are not carried by the
+          // fused engine: every earlier batch executed completely)
+          if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
+        }
+      }
+      if (tail[e]) {
+        const uint32_t j = t / k, s = t % k;
+        const uint64_t slot = fq_proc ? uint64_t(fq_proc[i * fq + j]) * K + key32[i * k + s]
+                                      : uint64_t(key32[i * k + s]);
+        latest[slot] = self;
+      }
+    }
+    for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
+    const uint32_t m = S == 1 ? nd : sort_unique_u64(dd, nd);
+    for (uint32_t q = m; q < S; q++) dd[q] = 0;
+    dep_cnt[i] = m;
+    if (blocked0) blocked0[i] = missing;
+    if (missing) atomicAdd(nblocked, 1u);
+  }
+}
+
+__global__ void k_seq_dots(uint32_t m, const uint32_t *__restrict__ pk_vid,
+                           const uint64_t *__restrict__ dot, uint64_t *__restrict__ seq) {
+  GRID_STRIDE(j, m) seq[j] = dot[pk_vid[j]];
+}
+
+// executed-clock frontier advance for a fully executed batch: per-source
+// min / max / count of the batch's sequences, reduced in LDS first
+__global__ void __launch_bounds__(256)
+    k_src_stats(uint32_t n, const uint64_t *__restrict__ dot, unsigned long long *__restrict__ mn,
+                unsigned long long *__restrict__ mx, unsigned int *__restrict__ cnt) {
+  __shared__ unsigned long long s_mn[256], s_mx[256];
+  __shared__ unsigned int s_cnt[256];
+  s_mn[threadIdx.x] = ~0ull;
+  s_mx[threadIdx.x] = 0;
+  s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  GRID_STRIDE(i, n) {
+    const uint64_t d = dot[i];
+    const uint32_t s = uint32_t(d >> 56);
+    const unsigned long long q = d & 0x00FFFFFFFFFFFFFFull;
+    atomicMin(&s_mn[s], q);
+    atomicMax(&s_mx[s], q);
+    atomicAdd(&s_cnt[s], 1u);
+  }
+  __syncthreads();
+  const uint32_t s = threadIdx.x;
+  if (s_cnt[s]) {
+    atomicMin(&mn[s], s_mn[s]);
+    atomicMax(&mx[s], s_mx[s]);
+    atomicAdd(&cnt[s], s_cnt[s]);
+  }
+}
+
+__global__ void k_frontier_update(const unsigned long long *__restrict__ mn,
+                                  const unsigned long long *__restrict__ mx,
+                                  const unsigned int *__restrict__ cnt, uint64_t *frontier,
+                                  uint32_t *err) {
+  const uint32_t s = threadIdx.x;
+  if (s >= 256 || cnt[s] == 0) return;
+  if (mn[s] == frontier[s] + 1 && mx[s] - mn[s] + 1 == cnt[s])
+    frontier[s] = mx[s];
+  else
+    atomicOr(err, 1u);  // non-contiguous executed set: needs exceptions
+}
+
+__global__ void k_bcast_u32(uint32_t n, uint32_t *p, uint32_t v) { GRID_STRIDE(i, n) p[i] = v; }
+
+__global__ void k_identity_labels(uint32_t n, const uint64_t *__restrict__ dot,
+                                  uint64_t *__restrict__ lab, uint32_t *__restrict__ rank) {
+  GRID_STRIDE(i, n) {
+    lab[i] = dot[i];
+    rank[i] = i;
+  }
+}
+
+__global__ void k_key_hist(uint32_t m, const uint32_t *__restrict__ keys, uint32_t *__restrict__ h) {
+  GRID_STRIDE(j, m) atomicAdd(&h[keys[j]], 1u);
+}
+
+__global__ void k_compact_deps(uint32_t n, uint32_t S, const uint64_t *__restrict__ dd,
+                               const uint32_t *__restrict__ off, uint64_t *__restrict__ out) {
+  GRID_STRIDE(i, n) {
+    const uint32_t c = off[i + 1] - off[i];
+    for (uint32_t q = 0; q < c; q++) out[off[i] + q] = dd[size_t(i) * S + q];
+  }
+}
+
+}  // namespace
+
+struct EngineDevice {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t key_space = 0;
+  int key_bits = 1;
+  uint32_t n_config = 0;
+  // persistent state
+  DBuf<uint64_t> latest;     // [(nproc+1) * K]
+  DBuf<uint64_t> frontier;   // [256] executed-clock frontier per source
+  uint32_t latest_slots = 1; // replica slots allocated in `latest`
+  DBuf<uint32_t> err;
+  // staged batch
+  fh_stream_desc desc{};
+  bool staged = false;
+  uint64_t tmin = 0;
+  int tbits = 0;
+  DBuf<uint64_t> dot, fq_time;
+  DBuf<uint32_t> key32;
+  DBuf<uint8_t> fq_proc;
+  // scratch / outputs
+  DBuf<uint64_t> vkeys, sk64a, sk64b, dep_ext, dep_dot, seq_dot, lab;
+  DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_vid, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
+  DBuf<uint8_t> tail, blocked0;
+  DBuf<uint32_t> scal;
+  DBuf<unsigned long long> srcstats;
+  SortWorkspace sort_ws;
+  ScanWorkspace scan_ws;
+  GraphCore graph;
+  GraphOutput gout;
+  // timing
+  bool profile = false;
+  std::vector<std::pair<const char *, hipEvent_t>> marks;
+  std::vector<std::pair<std::string, float>> last_times;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+  explicit EngineDevice(const fh_config &cfg) {
+    FH_CHECK(cfg.key_space >= 1 && cfg.key_space <= (uint64_t(1) << 31), FH_EINVAL,
+             "key_space must be in [1, 2^31]");
+    key_space = cfg.key_space;
+    key_bits = bits_for(key_space);
+    n_config = cfg.n;
+    device = pick_device(&cfg, 0);
+    FH_HIP(hipSetDevice(device));
+    FH_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    FH_HIP(hipEventCreate(&ev0));
+    FH_HIP(hipEventCreate(&ev1));
+    graph.stream = stream;
+    graph.marks = &marks;
+    err.ensure(4);
+    scal.ensure(16);
+    frontier.ensure(256);
+    reset();
+  }
+  ~EngineDevice() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    clear_marks();
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  void clear_marks() {
+    for (auto &m : marks) (void)hipEventDestroy(m.second);
+    marks.clear();
+  }
+  void mark(const char *name) {
+    if (!profile) return;
+    hipEvent_t e;
+    FH_HIP(hipEventCreate(&e));
+    FH_HIP(hipEventRecord(e, stream));
+    marks.push_back({name, e});
+  }
+
+  void ensure_latest(uint32_t slots) {
+    if (latest.get() && slots <= latest_slots) return;
+    latest_slots = std::max<uint32_t>(slots, 1);
+    latest.ensure(size_t(latest_slots) * key_space);
+    FH_HIP(hipMemsetAsync(latest.get(), 0, size_t(latest_slots) * key_space * sizeof(uint64_t),
+                          stream));
+  }
+
+  void reset() {
+    FH_HIP(hipSetDevice(device));
+    ensure_latest(latest_slots);
+    FH_HIP(hipMemsetAsync(latest.get(), 0, size_t(latest_slots) * key_space * sizeof(uint64_t),
+                          stream));
+    FH_HIP(hipMemsetAsync(frontier.get(), 0, 256 * sizeof(uint64_t), stream));
+    FH_HIP(hipMemsetAsync(err.get(), 0, 4 * sizeof(uint32_t), stream));
+    FH_HIP(hipStreamSynchronize(stream));
+  }
+
+  void stage(const fh_stream_desc &d, const uint64_t *h_dot, const uint64_t *h_key,
+             const uint8_t *h_proc, const uint64_t *h_time) {
+    FH_CHECK(h_dot && h_key, FH_EINVAL, "null argument");
+    FH_CHECK(d.keys_per_cmd >= 1 && d.keys_per_cmd <= 8, FH_EINVAL, "keys_per_cmd in [1, 8]");
+    const uint32_t fq = d.views ? d.views : 1;
+    FH_CHECK(fq <= 16, FH_EINVAL, "views <= 16");
+    FH_CHECK(size_t(d.n) * fq * d.keys_per_cmd < (size_t(1) << 30), FH_EINVAL,
+             "batch too large (elements >= 2^30)");
+    FH_CHECK(!d.views || (h_proc && h_time && d.nproc >= 1 && d.nproc <= 255), FH_EINVAL,
+             "replica views need fq_proc, fq_time and nproc");
+    FH_HIP(hipSetDevice(device));
+    const size_t n = d.n, nk = n * d.keys_per_cmd;
+    std::vector<uint32_t> k32(nk);
+    for (size_t e = 0; e < nk; e++) {
+      FH_CHECK(h_key[e] < key_space, FH_EINVAL, "stage: key id >= key_space");
+      k32[e] = uint32_t(h_key[e]);
+    }
+    FH_HIP(hipMemcpyAsync(dot.ensure(n + 1), h_dot, n * sizeof(uint64_t), hipMemcpyHostToDevice,
+                          stream));
+    FH_HIP(hipMemcpyAsync(key32.ensure(nk + 1), k32.data(), nk * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, stream));
+    if (d.views) {
+      const size_t nv = n * fq;
+      uint64_t lo = ~0ull, hi = 0;
+      for (size_t i = 0; i < nv; i++) {
+        FH_CHECK(h_proc[i] >= 1 && h_proc[i] <= d.nproc, FH_EINVAL, "fq_proc out of range");
+        lo = std::min(lo, h_time[i]);
+        hi = std::max(hi, h_time[i]);
+      }
+      tmin = n ? lo : 0;
+      tbits = bits_for(n ? hi - lo + 1 : 1);
+      FH_CHECK(bits_for(uint64_t(d.nproc + 1) * key_space) + tbits <= 64, FH_ENOTIMPL,
+               "replica-view sort key wider than 64 bits");
+      FH_HIP(hipMemcpyAsync(fq_proc.ensure(nv + 1), h_proc, nv, hipMemcpyHostToDevice, stream));
+      FH_HIP(hipMemcpyAsync(fq_time.ensure(nv + 1), h_time, nv * sizeof(uint64_t),
+                            hipMemcpyHostToDevice, stream));
+      ensure_latest(d.nproc + 1);
+    }
+    FH_HIP(hipStreamSynchronize(stream));
+    desc = d;
+    staged = true;
+  }
+
+  // The device run of one batch: everything below is the timed hot path.
+  void run(float *ms) {
+    FH_CHECK(staged, FH_EINVAL, "no batch staged");
+    FH_HIP(hipSetDevice(device));
+    clear_marks();
+    graph.profile = profile;
+    const uint32_t n = uint32_t(desc.n), k = desc.keys_per_cmd;
+    const uint32_t fq = desc.views ? desc.views : 1;
+    const uint32_t S = fq * k;
+    const uint32_t M = n * S;
+    const bool views = desc.views != 0;
+    FH_HIP(hipEventRecord(ev0, stream));
+    mark("start");
+    uint32_t *vs = nullptr;
+    uint32_t *dvid = dep_vid.ensure(M + 1);
+    uint64_t *dext = dep_ext.ensure(M + 1);
+    uint8_t *tl = tail.ensure(M + 1);
+    uint32_t *svid = sorted_vid.ensure(M + 1);
+    const uint32_t *sorted_keys32 = nullptr;
+    if (!views) {
+      uint32_t *ks = nullptr;
+      sort_pairs<uint32_t>(key32.get(), nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
+                           sk32b.ensure(M + 1), svb.ensure(M + 1), M, key_bits, sort_ws, stream,
+                           &ks, &vs);
+      mark("keydeps_sort");
+      k_prev_engine<uint32_t><<<grid_for(M, B), B, 0, stream>>>(
+          M, ks, vs, 0, S, latest.get(), dvid, dext, tl, k == 1 ? nullptr : svid);
+      sorted_keys32 = ks;
+      if (k == 1) svid = vs;  // element id == vid
+    } else {
+      uint64_t *vk = vkeys.ensure(M + 1);
+      k_view_keys<<<grid_for(M, B), B, 0, stream>>>(M, k, fq, key_space, key32.get(),
+                                                     fq_proc.get(), fq_time.get(), tmin, tbits,
+                                                     vk);
+      uint64_t *ks = nullptr;
+      const int bits = bits_for(uint64_t(desc.nproc + 1) * key_space) + tbits;
+      sort_pairs<uint64_t>(vk, nullptr, sk64a.ensure(M + 1), sva.ensure(M + 1),
+                           sk64b.ensure(M + 1), svb.ensure(M + 1), M, bits, sort_ws, stream, &ks,
+                           &vs);
+      mark("keydeps_sort");
+      k_prev_engine<uint64_t><<<grid_for(M, B), B, 0, stream>>>(
+          M, ks, vs, tbits, S, latest.get(), dvid, dext, tl, nullptr);
+    }
+    mark("keydeps_prev");
+    uint64_t *ddot = dep_dot.ensure(M + 1);
+    uint32_t *dcnt = dep_cnt.ensure(n + 1);
+    uint32_t *dd = dst.ensure(M + 1);
+    FH_HIP(hipMemsetAsync(scal.get(), 0, sizeof(uint32_t), stream));
+    k_cmd_engine<<<grid_for(n, B), B, 0, stream>>>(
+        n, k, fq, key_space, key32.get(), views ? fq_proc.get() : nullptr, dot.get(), dvid, dext,
+        tl, latest.get(), frontier.get(), ddot, dcnt, dd, nullptr, scal.get());
+    mark("keydeps_union");
+    // graph stage
+    GraphInput gin;
+    gin.V = n;
+    gin.off = nullptr;
+    gin.stride = S;
+    gin.dst = dd;
+    gin.blocked0 = nullptr;  // see k_cmd_engine: no pending carried by the fused engine
+    gin.dot = dot.get();
+    gin.k = k;
+    gin.key32 = key32.get();
+    gin.key_bits = key_bits;
+    if (!views) {
+      gin.no_forward_hint = true;  // single view: deps always point backwards
+      gin.sorted_keys = sorted_keys32;
+      gin.sorted_vid = svid;
+    }
+    graph.run(gin, gout);
+    FH_CHECK(gout.npending == 0, FH_EINVARIANT, "fused engine batch left pending vertices");
+    // per-key sequence of dots (ExecutionOrderMonitor::add order)
+    uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
+    k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, dot.get(), sq);
+    mark("per_key_dots");
+    // executed clock: the whole batch executed
+    unsigned long long *st = srcstats.ensure(3 * 256);
+    FH_HIP(hipMemsetAsync(st, 0xFF, 256 * sizeof(unsigned long long), stream));
+    FH_HIP(hipMemsetAsync(st + 256, 0, 512 * sizeof(unsigned long long), stream));
+    k_src_stats<<<grid_for(n, B, 512), B, 0, stream>>>(n, dot.get(), st, st + 256,
+                                                   reinterpret_cast<unsigned int *>(st + 512));
+    k_frontier_update<<<1, 256, 0, stream>>>(st, st + 256,
+                                             reinterpret_cast<unsigned int *>(st + 512),
+                                             frontier.get(), err.get());
+    mark("executed_clock");
+    FH_HIP(hipEventRecord(ev1, stream));
+    if (ms) {
+      FH_HIP(hipEventSynchronize(ev1));
+      FH_HIP(hipEventElapsedTime(ms, ev0, ev1));
+    }
+    if (profile) collect_times();
+  }
+
+  void collect_times() {
+    FH_HIP(hipStreamSynchronize(stream));
+    last_times.clear();
+    for (size_t i = 1; i < marks.size(); i++) {
+      float t = 0;
+      FH_HIP(hipEventElapsedTime(&t, marks[i - 1].second, marks[i].second));
+      last_times.push_back({marks[i].first, t});
+    }
+  }
+
+  void check_err() {
+    uint32_t e = 0;
+    FH_HIP(hipMemcpyAsync(&e, err.get(), sizeof(e), hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    FH_CHECK(e == 0, FH_ENOTIMPL,
+             "executed clock: non-contiguous executed dots per process (exceptions not supported "
+             "by the fused engine)");
+  }
+
+  void results(uint32_t *dep_off, uint64_t *dep_out, size_t dep_cap, size_t *dep_len,
+               uint64_t *scc_label, uint32_t *exec_rank, uint32_t *key_off, uint64_t *key_seq) {
+    FH_HIP(hipSetDevice(device));
+    FH_HIP(hipStreamSynchronize(stream));
+    check_err();
+    const uint32_t n = uint32_t(desc.n), k = desc.keys_per_cmd;
+    const uint32_t S = (desc.views ? desc.views : 1) * k;
+    if (dep_off || dep_out || dep_len) {
+      uint32_t *off = u32tmp.ensure(n + 1);
+      exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
+      uint32_t total = 0;
+      FH_HIP(hipMemcpyAsync(&total, off + n, sizeof(total), hipMemcpyDeviceToHost, stream));
+      FH_HIP(hipStreamSynchronize(stream));
+      if (dep_len) *dep_len = total;
+      if (dep_off)
+        FH_HIP(hipMemcpyAsync(dep_off, off, (n + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              stream));
+      if (dep_out) {
+        FH_CHECK(dep_cap >= total, FH_ECAP, "dep output capacity too small");
+        uint64_t *c = sk64a.ensure(total + 1);
+        k_compact_deps<<<grid_for(n, B), B, 0, stream>>>(n, S, dep_dot.get(), off, c);
+        FH_HIP(hipMemcpyAsync(dep_out, c, size_t(total) * sizeof(uint64_t),
+                              hipMemcpyDeviceToHost, stream));
+      }
+    }
+    if (scc_label || exec_rank) {
+      uint64_t *lb = gout.scc_label;
+      uint32_t *rk = gout.exec_rank;
+      if (gout.trivial) {
+        lb = lab.ensure(n + 1);
+        rk = rank_tmp.ensure(n + 1);
+        k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, dot.get(), lb, rk);
+      }
+      if (scc_label)
+        FH_HIP(hipMemcpyAsync(scc_label, lb, size_t(n) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              stream));
+      if (exec_rank)
+        FH_HIP(hipMemcpyAsync(exec_rank, rk, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              stream));
+    }
+    if (key_off) {
+      uint32_t *h = u32tmp.ensure(key_space + 1);
+      uint32_t *o = rank_tmp.ensure(key_space + 2);
+      FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
+      k_key_hist<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_key, h);
+      exclusive_scan_u32(h, o, key_space, scan_ws, stream);
+      FH_HIP(hipMemcpyAsync(key_off, o, (key_space + 1) * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost, stream));
+    }
+    if (key_seq)
+      FH_HIP(hipMemcpyAsync(key_seq, seq_dot.get(), size_t(gout.nelem) * sizeof(uint64_t),
+                            hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+  }
+};
+
+}  // namespace fh
+
+struct fh_engine {
+  fh::EngineDevice dev;
+  explicit fh_engine(const fh_config &c) : dev(c) {}
+};
+
+extern "C" {
+
+fh_status fh_engine_create(const fh_config *cfg, fh_engine **out) {
+  FH_API_BEGIN
+  FH_CHECK(cfg && out, FH_EINVAL, "null argument");
+  *out = new fh_engine(*cfg);
+  FH_API_END
+}
+
+fh_status fh_engine_destroy(fh_engine *h) {
+  FH_API_BEGIN
+  delete h;
+  FH_API_END
+}
+
+fh_status fh_engine_reset(fh_engine *h) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.reset();
+  FH_API_END
+}
+
+fh_status fh_engine_stage(fh_engine *h, const fh_stream_desc *desc, const uint64_t *dot,
+                          const uint64_t *key_id, const uint8_t *fq_proc, const uint64_t *fq_time) {
+  FH_API_BEGIN
+  FH_CHECK(h && desc, FH_EINVAL, "null argument");
+  h->dev.stage(*desc, dot, key_id, fq_proc, fq_time);
+  FH_API_END
+}
+
+fh_status fh_engine_run(fh_engine *h, float *device_ms) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.run(device_ms);
+  FH_API_END
+}
+
+fh_status fh_engine_results(fh_engine *h, uint32_t *dep_off, uint64_t *dep_dot, size_t dep_cap,
+                            size_t *dep_len, uint64_t *scc_label, uint32_t *exec_rank,
+                            uint32_t *key_off, uint64_t *key_seq) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.results(dep_off, dep_dot, dep_cap, dep_len, scc_label, exec_rank, key_off, key_seq);
+  FH_API_END
+}
+
+fh_status fh_engine_kernel_times(fh_engine *h, const char **names, float *ms, size_t cap,
+                                 size_t *len) {
+  FH_API_BEGIN
+  FH_CHECK(h && len, FH_EINVAL, "null argument");
+  const auto &t = h->dev.last_times;
+  *len = t.size();
+  for (size_t i = 0; i < t.size() && i < cap; i++) {
+    if (names) names[i] = t[i].first.c_str();
+    if (ms) ms[i] = t[i].second;
+  }
+  FH_API_END
+}
+
+fh_status fh_engine_set_profiling(fh_engine *h, int on) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.profile = on != 0;
+  FH_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// graph_core.h -- batch SCC + execution order on the device.
+//
+// Input: V vertices in arrival order (vid = arrival position), dependency
+// edges as vids (CSR), an optional "blocked" flag per vertex (it has a
+// dependency that is neither executed nor in the batch), the vertex dots and
+// keys.  Output: the SCC partition, the execution order and the per-key
+// execution sequence the reference's incremental DependencyGraph
+// (fantoch_ps/src/executor/graph/mod.rs:215-644) + TarjanSCCFinder
+// (tarjan.rs:98-319) produce for the same arrival order, and the set of
+// vertices that stay pending (PendingIndex, index.rs:145-211).
+//
+// Batch equivalence: a vertex executes iff nothing it
+// reaches is missing; the SCCs found are the SCCs of the final graph; the
+// reference executes SCC S at arrival time H(S) = max arrival position
+// reachable from S ("ready time"), deps first.  The device computes
+//   kappa(S) = max(kappa0(S), max_{S->S'} kappa(S') + 1),
+//   kappa0(S) = (maxpos(S), 0)  packed as (H << 32 | depth)
+// whose fixpoint is a strict topological order of the condensation that
+// orders SCCs by ready time; members of an SCC run in dot order
+// (tarjan.rs:14-15).
+//
+// SCC discovery: every cycle contains a forward edge (dep arrived later).
+// Windows of 128 arrival positions (stride 64) compute their local transitive
+// closure with a bit-matrix Warshall held in one wave's registers; mutually
+// reachable vertices are united with a lock-free union-find.  Overlapping
+// local SCCs chain into large ones (e.g. one stream-wide SCC under 100%
+// conflict).  Convergence of kappa certifies the partition (a missed cycle
+// would make kappa grow forever); if it does not converge within a bound the
+// exact coloring fallback (Orzan-style, over the condensation) completes it.
+#pragma once
+
+#include <utility>
+#include <vector>
+
+#include "fh_common.h"
+#include "scan.h"
+#include "sort.h"
+
+namespace fh {
+
+struct GraphInput {
+  uint32_t V = 0;
+  const uint32_t *off = nullptr;     // [V+1]; null = fixed stride
+  uint32_t stride = 0;               // edges of v at dst[v*stride ..) when off == null
+  const uint32_t *dst = nullptr;     // [E] dependency vids (v itself = padding)
+  const uint8_t *blocked0 = nullptr; // [V] or null: has a missing dependency
+  const uint64_t *dot = nullptr;     // [V]
+  // keys: fixed k per vertex (key_off == null) or CSR
+  uint32_t k = 0;
+  const uint32_t *key_off = nullptr; // [V+1] or null
+  const uint32_t *key32 = nullptr;   // [elements]
+  int key_bits = 1;
+  // fast path hint: elements already sorted by (key, arrival) -- reused as
+  // the per-key order when the graph turns out to be trivially ordered
+  const uint32_t *sorted_keys = nullptr;  // [M]
+  const uint32_t *sorted_vid = nullptr;   // [M] vid of each sorted element
+  bool no_forward_hint = false;           // edges all point backwards
+};
+
+struct GraphOutput {
+  // device pointers owned by GraphCore, valid until the next run
+  uint32_t nexec = 0;          // executed vertices
+  uint32_t npending = 0;
+  bool trivial = false;        // no forward edges, no pending: arrival order
+  bool fallback_used = false;
+  uint32_t kappa_iters = 0;
+  uint32_t *rep = nullptr;        // [V] representative (min vid) of the SCC
+  uint64_t *scc_label = nullptr;  // [V] min dot of the SCC
+  uint8_t *blocked = nullptr;     // [V] pending
+  uint32_t *exec_order = nullptr; // [nexec] vids in execution order (null if trivial)
+  uint32_t *exec_rank = nullptr;  // [V] position in exec order, ~0u if pending
+  uint32_t nelem = 0;             // per-key sequence length
+  uint32_t *pk_key = nullptr;     // [nelem] keys, ascending
+  uint32_t *pk_vid = nullptr;     // [nelem] vids in per-key execution order
+};
+
+struct GraphCore {
+  hipStream_t stream = nullptr;
+  SortWorkspace sort_ws;
+  ScanWorkspace scan_ws;
+  DBuf<uint32_t> rep, cnt, pos, order, rank, tmp32a, tmp32b, tmp32c, tmp32d, flags;
+  DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c;
+  DBuf<uint8_t> blocked;
+  DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)
+  bool profile = false;
+  // per-kernel timing (engine profiling)
+  std::vector<std::pair<const char *, hipEvent_t>> *marks = nullptr;
+
+  void run(const GraphInput &in, GraphOutput &out);
+
+ private:
+  void mark(const char *name);
+  uint32_t read_scalar(int i);
+  void pending_closure(const GraphInput &in, GraphOutput &out);
+  uint64_t count_forward(const GraphInput &in);
+  void find_sccs(const GraphInput &in);
+  bool order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters);
+  void coloring_fallback(const GraphInput &in);
+  void build_orders(const GraphInput &in, GraphOutput &out);
+};
+
+}  // namespace fh

@@ -1,0 +1,611 @@
+// graph_core.hip -- batch SCC + execution order (see graph_core.h).
+#include <vector>
+
+#include "graph_core.h"
+
+namespace fh {
+namespace {
+
+constexpr unsigned B = 256;
+
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_u64(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+#define EB(v) (off ? off[v] : (v) * stride)
+#define EE(v) (off ? off[(v) + 1] : ((v) + 1) * stride)
+#define GRID_STRIDE(i, n) \
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------- pending
+__global__ void k_blocked_init(uint32_t V, const uint8_t *__restrict__ b0,
+                               uint8_t *__restrict__ blocked) {
+  GRID_STRIDE(v, V) blocked[v] = b0 ? b0[v] : 0;
+}
+
+// A vertex that reaches a missing dependency stays pending
+// (TarjanSCCFinder gives up on the first missing dep, tarjan.rs:150-170,
+// and check_pending retries it later, mod.rs:558-644).
+__global__ void k_blocked_iter(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+                               const uint32_t *__restrict__ dst, uint8_t *blocked,
+                               uint32_t *changed) {
+  GRID_STRIDE(v, V) {
+    if (blocked[v]) continue;
+    for (uint32_t e = EB(v); e < EE(v); e++) {
+      if (__hip_atomic_load(&blocked[dst[e]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        blocked[v] = 1;
+        *changed = 1;
+        break;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- forward edges
+__global__ void k_count_forward(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+                                const uint32_t *__restrict__ dst,
+                                const uint8_t *__restrict__ blocked,
+                                unsigned long long *count) {
+  unsigned long long c = 0;
+  GRID_STRIDE(v, V) {
+    if (blocked[v]) continue;
+    for (uint32_t e = EB(v); e < EE(v); e++) c += dst[e] > v;
+  }
+  // wave reduce then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+}
+
+// ---------------------------------------------------------------- union-find
+__device__ uint32_t uf_find(uint32_t *parent, uint32_t x) {
+  for (;;) {
+    const uint32_t p = ld_u32(&parent[x]);
+    if (p == x) return x;
+    const uint32_t gp = ld_u32(&parent[p]);
+    if (gp != p) atomicCAS(&parent[x], p, gp);  // path halving
+    x = gp;
+  }
+}
+
+// Link the larger root under the smaller: the final root is the component's
+// minimum vid (= earliest arrival).
+__device__ void uf_union(uint32_t *parent, uint32_t a, uint32_t b) {
+  for (;;) {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    if (a == b) return;
+    if (a < b) {
+      const uint32_t t = a;
+      a = b;
+      b = t;
+    }
+    if (atomicCAS(&parent[a], a, b) == a) return;
+  }
+}
+
+__global__ void k_iota(uint32_t V, uint32_t *__restrict__ p) { GRID_STRIDE(v, V) p[v] = v; }
+
+__global__ void k_uf_compress(uint32_t V, uint32_t *parent) {
+  GRID_STRIDE(v, V) parent[v] = uf_find(parent, v);
+}
+
+__device__ __forceinline__ uint64_t rl64(uint64_t x, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(x), lane);
+  const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(x >> 32), lane);
+  return (uint64_t(hi) << 32) | lo;
+}
+
+// One wave per window [64w, 64w+128): lane l owns rows l and 64+l of the
+// window's reachability bit-matrix (two u64 words per row).  Warshall over
+// the 128 pivots, broadcast by readlane; then each vertex unites with the
+// smallest vertex it mutually reaches.
+__global__ void __launch_bounds__(256)
+    k_windows(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride, const uint32_t *__restrict__ dst,
+              const uint8_t *__restrict__ blocked, uint32_t *parent, uint32_t nwin) {
+  __shared__ uint64_t s_rows[4][128][2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t win = blockIdx.x * 4 + wv;
+  if (win >= nwin) return;
+  const uint32_t base = win * 64;
+  uint64_t r[2][2] = {{0, 0}, {0, 0}};
+  bool fwd = false;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t v = base + h * 64 + lane;
+    if (v < V && !blocked[v]) {
+      for (uint32_t e = EB(v); e < EE(v); e++) {
+        const uint32_t u = dst[e];
+        if (u >= base && u < base + 128 && u != v && !blocked[u]) {
+          const uint32_t bit = u - base;
+          r[h][bit >> 6] |= uint64_t(1) << (bit & 63);
+          fwd |= u > v;
+        }
+      }
+    }
+  }
+  if (!__any(fwd)) return;  // no forward edge inside: no local cycle
+  // pivots 0..63 live in rows r[0][*] of lane k, pivots 64..127 in r[1][*];
+  // the two halves are separate loops so every register index is static
+#define FH_WARSHALL_HALF(H)                                  \
+  for (int k = 0; k < 64; k++) {                             \
+    const uint64_t k0 = rl64(r[H][0], k);                    \
+    const uint64_t k1 = rl64(r[H][1], k);                    \
+    const uint64_t m = uint64_t(1) << k;                     \
+    if (r[0][H] & m) {                                       \
+      r[0][0] |= k0;                                         \
+      r[0][1] |= k1;                                         \
+    }                                                        \
+    if (r[1][H] & m) {                                       \
+      r[1][0] |= k0;                                         \
+      r[1][1] |= k1;                                         \
+    }                                                        \
+  }
+  FH_WARSHALL_HALF(0)
+  FH_WARSHALL_HALF(1)
+#undef FH_WARSHALL_HALF
+  s_rows[wv][lane][0] = r[0][0];
+  s_rows[wv][lane][1] = r[0][1];
+  s_rows[wv][64 + lane][0] = r[1][0];
+  s_rows[wv][64 + lane][1] = r[1][1];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t x = h * 64 + lane;
+    if (base + x >= V) continue;
+    // smallest u < x with x ->+ u and u ->+ x
+    for (int wd = 0; wd <= h; wd++) {
+      uint64_t cand = r[h][wd];
+      if (wd == h) cand &= (uint64_t(1) << (x & 63)) - 1;
+      bool found = false;
+      while (cand) {
+        const int b = __builtin_ctzll(cand);
+        cand &= cand - 1;
+        const uint32_t u = wd * 64 + b;
+        if ((s_rows[wv][u][x >> 6] >> (x & 63)) & 1) {
+          uf_union(parent, base + x, base + u);
+          found = true;
+          break;
+        }
+      }
+      if (found) break;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- kappa
+__global__ void k_kap_init(uint32_t V, const uint8_t *__restrict__ blocked,
+                           const uint32_t *__restrict__ rep, uint64_t *kap) {
+  GRID_STRIDE(v, V) {
+    if (!blocked[v]) atomicMax((unsigned long long *)&kap[rep[v]], (unsigned long long)v << 32);
+  }
+}
+
+__global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+                            const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
+                            const uint32_t *__restrict__ rep, uint64_t *kap, uint32_t *changed) {
+  GRID_STRIDE(v, V) {
+    if (blocked[v]) continue;
+    const uint32_t r = rep[v];
+    uint64_t best = 0;
+    for (uint32_t e = EB(v); e < EE(v); e++) {
+      const uint32_t ru = rep[dst[e]];
+      if (ru != r) {
+        const uint64_t c = ld_u64(&kap[ru]) + 1;
+        best = c > best ? c : best;
+      }
+    }
+    if (best > ld_u64(&kap[r])) {
+      const uint64_t old = atomicMax((unsigned long long *)&kap[r], (unsigned long long)best);
+      if (old < best) *changed = 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- exact fallback
+// Orzan-style coloring over the condensation of the current partition:
+// H[S] = max arrival position reachable from S (among active SCCs); each
+// class {S : H[S] = t} is reached from its root rep(t), and the members the
+// root reaches form one SCC with it.
+__global__ void k_fb_init(uint32_t V, const uint8_t *__restrict__ blocked,
+                          const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
+                          uint32_t *H, uint8_t *reached) {
+  GRID_STRIDE(v, V) {
+    if (rep[v] == v) reached[v] = 0;
+    if (!blocked[v] && !done[v]) atomicMax(&H[rep[v]], v);
+  }
+}
+
+__global__ void k_fb_hprop(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+                           const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
+                           const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
+                           uint32_t *H, uint32_t *changed) {
+  GRID_STRIDE(v, V) {
+    if (blocked[v] || done[v]) continue;
+    const uint32_t r = rep[v];
+    uint32_t best = 0;
+    for (uint32_t e = EB(v); e < EE(v); e++) {
+      const uint32_t u = dst[e];
+      const uint32_t ru = rep[u];
+      if (ru != r && !done[u]) {
+        const uint32_t h = ld_u32(&H[ru]);
+        best = h > best ? h : best;
+      }
+    }
+    if (best > ld_u32(&H[r])) {
+      if (atomicMax(&H[r], best) < best) *changed = 1;
+    }
+  }
+}
+
+__global__ void k_fb_roots(uint32_t V, const uint8_t *__restrict__ blocked,
+                           const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
+                           const uint32_t *__restrict__ H, uint8_t *reached) {
+  GRID_STRIDE(v, V) {
+    if (blocked[v] || done[v]) continue;
+    if (H[rep[v]] == v) reached[rep[v]] = 1;  // v is the class maximum: its SCC is the root
+  }
+}
+
+__global__ void k_fb_reach(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+                           const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
+                           const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
+                           const uint32_t *__restrict__ H, uint8_t *reached, uint32_t *changed) {
+  GRID_STRIDE(v, V) {
+    if (blocked[v] || done[v]) continue;
+    const uint32_t r = rep[v];
+    if (!__hip_atomic_load(&reached[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
+    const uint32_t hr = H[r];
+    for (uint32_t e = EB(v); e < EE(v); e++) {
+      const uint32_t u = dst[e];
+      const uint32_t ru = rep[u];
+      if (ru != r && !done[u] && H[ru] == hr &&
+          !__hip_atomic_load(&reached[ru], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(&reached[ru], uint8_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *changed = 1;
+      }
+    }
+  }
+}
+
+__global__ void k_fb_merge(uint32_t V, const uint8_t *__restrict__ blocked, uint8_t *done,
+                           const uint32_t *__restrict__ rep, const uint32_t *__restrict__ H,
+                           const uint8_t *__restrict__ reached, uint32_t *parent,
+                           uint32_t *remaining) {
+  GRID_STRIDE(v, V) {
+    if (blocked[v] || done[v]) continue;
+    const uint32_t r = rep[v];
+    if (reached[r]) {
+      done[v] = 1;
+      if (r == v) uf_union(parent, v, rep[H[r]]);
+    } else {
+      *remaining = 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- orders
+__global__ void k_label_init(uint32_t V, uint64_t *label) { GRID_STRIDE(v, V) label[v] = ~0ull; }
+
+__global__ void k_label_min(uint32_t V, const uint32_t *__restrict__ rep,
+                            const uint64_t *__restrict__ dot, uint64_t *label) {
+  GRID_STRIDE(v, V) atomicMin((unsigned long long *)&label[rep[v]], (unsigned long long)dot[v]);
+}
+
+__global__ void k_label_bcast(uint32_t V, const uint32_t *__restrict__ rep,
+                              const uint64_t *__restrict__ lab_rep, uint64_t *__restrict__ out) {
+  GRID_STRIDE(v, V) out[v] = lab_rep[rep[v]];
+}
+
+__global__ void k_rank_from_sorted(uint32_t n, const uint32_t *__restrict__ vals,
+                                   uint32_t *__restrict__ rank) {
+  GRID_STRIDE(j, n) rank[vals[j]] = j;
+}
+
+__global__ void k_rep_flags(uint32_t V, const uint8_t *__restrict__ blocked,
+                            const uint32_t *__restrict__ rep, uint32_t *__restrict__ flags) {
+  GRID_STRIDE(v, V) flags[v] = (!blocked[v] && rep[v] == v) ? 1u : 0u;
+}
+
+__global__ void k_exec_flags(uint32_t V, const uint8_t *__restrict__ blocked,
+                             uint32_t *__restrict__ flags) {
+  GRID_STRIDE(v, V) flags[v] = blocked[v] ? 0u : 1u;
+}
+
+// SCC sort key: (ready time H, depth d) from kappa, both < 2^bits.
+__global__ void k_rep_keys(uint32_t V, const uint32_t *__restrict__ flags,
+                           const uint32_t *__restrict__ pos, const uint64_t *__restrict__ kap,
+                           int bits, uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  GRID_STRIDE(v, V) {
+    if (!flags[v]) continue;
+    const uint64_t k = kap[v];
+    const uint64_t h = k >> 32, d = k & 0xFFFFFFFFull;
+    keys[pos[v]] = (h << bits) | d;
+    vals[pos[v]] = v;
+  }
+}
+
+__global__ void k_vertex_keys(uint32_t V, const uint32_t *__restrict__ flags,
+                              const uint32_t *__restrict__ pos, const uint32_t *__restrict__ rep,
+                              const uint32_t *__restrict__ scc_rank,
+                              const uint32_t *__restrict__ dot_rank, int bits,
+                              uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  GRID_STRIDE(v, V) {
+    if (!flags[v]) continue;
+    keys[pos[v]] = (uint64_t(scc_rank[rep[v]]) << bits) | dot_rank[v];
+    vals[pos[v]] = v;
+  }
+}
+
+__global__ void k_exec_rank(uint32_t V, uint32_t *__restrict__ rank) {
+  GRID_STRIDE(v, V) rank[v] = ~0u;
+}
+
+__global__ void k_elem_counts(uint32_t n, const uint32_t *__restrict__ order, uint32_t k,
+                              const uint32_t *__restrict__ key_off, uint32_t *__restrict__ cnt) {
+  GRID_STRIDE(j, n) {
+    const uint32_t v = order[j];
+    cnt[j] = key_off ? key_off[v + 1] - key_off[v] : k;
+  }
+}
+
+__global__ void k_elem_fill(uint32_t n, const uint32_t *__restrict__ order, uint32_t k,
+                            const uint32_t *__restrict__ key_off,
+                            const uint32_t *__restrict__ key32, const uint32_t *__restrict__ pos,
+                            uint32_t *__restrict__ ek, uint32_t *__restrict__ ev) {
+  GRID_STRIDE(j, n) {
+    const uint32_t v = order[j];
+    const uint32_t a = key_off ? key_off[v] : v * k;
+    const uint32_t c = key_off ? key_off[v + 1] - a : k;
+    for (uint32_t s = 0; s < c; s++) {
+      ek[pos[j] + s] = key32[a + s];
+      ev[pos[j] + s] = v;
+    }
+  }
+}
+
+__global__ void k_copy_dot(uint32_t V, const uint64_t *__restrict__ dot, uint64_t *__restrict__ out) {
+  GRID_STRIDE(v, V) out[v] = dot[v];
+}
+
+}  // namespace
+
+void GraphCore::mark(const char *name) {
+  if (!profile || !marks) return;
+  hipEvent_t e;
+  FH_HIP(hipEventCreate(&e));
+  FH_HIP(hipEventRecord(e, stream));
+  marks->push_back({name, e});
+}
+
+uint32_t GraphCore::read_scalar(int i) {
+  uint32_t v = 0;
+  FH_HIP(hipMemcpyAsync(&v, scalars.get() + i, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  FH_HIP(hipStreamSynchronize(stream));
+  return v;
+}
+
+void GraphCore::pending_closure(const GraphInput &in, GraphOutput &out) {
+  const uint32_t V = in.V;
+  k_blocked_init<<<grid_for(V, B), B, 0, stream>>>(V, in.blocked0, blocked.get());
+  if (!in.blocked0) return;
+  for (int it = 0;; it++) {
+    FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
+    k_blocked_iter<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(),
+                                                      scalars.get());
+    if (!read_scalar(0)) break;
+  }
+  mark("pending_closure");
+}
+
+uint64_t GraphCore::count_forward(const GraphInput &in) {
+  unsigned long long *c = reinterpret_cast<unsigned long long *>(scalars.get() + 8);
+  FH_HIP(hipMemsetAsync(c, 0, sizeof(unsigned long long), stream));
+  k_count_forward<<<grid_for(in.V, B, 2048), B, 0, stream>>>(in.V, in.off, in.stride, in.dst, blocked.get(),
+                                                              c);
+  unsigned long long h = 0;
+  FH_HIP(hipMemcpyAsync(&h, c, sizeof(h), hipMemcpyDeviceToHost, stream));
+  FH_HIP(hipStreamSynchronize(stream));
+  mark("count_forward");
+  return h;
+}
+
+void GraphCore::find_sccs(const GraphInput &in) {
+  const uint32_t V = in.V;
+  k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
+  const uint32_t nwin = (V + 63) / 64;
+  k_windows<<<(nwin + 3) / 4, 256, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), rep.get(), nwin);
+  mark("scc_windows");
+  k_uf_compress<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
+  mark("scc_compress");
+}
+
+bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters) {
+  const uint32_t V = in.V;
+  FH_HIP(hipMemsetAsync(kap.get(), 0, size_t(V) * sizeof(uint64_t), stream));
+  k_kap_init<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get());
+  for (uint32_t it = 0; it < max_iters; it++) {
+    FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
+    k_kap_relax<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), rep.get(),
+                                                   kap.get(), scalars.get());
+    iters = it + 1;
+    if (!read_scalar(0)) {
+      mark("kappa");
+      return true;
+    }
+  }
+  mark("kappa");
+  return false;
+}
+
+void GraphCore::coloring_fallback(const GraphInput &in) {
+  const uint32_t V = in.V;
+  uint8_t *done = reinterpret_cast<uint8_t *>(tmp32d.ensure((V + 3) / 4 + 1));
+  uint8_t *reached = reinterpret_cast<uint8_t *>(flags.ensure((V + 3) / 4 + 1));
+  uint32_t *H = tmp32c.ensure(V);
+  FH_HIP(hipMemsetAsync(done, 0, V, stream));
+  for (;;) {
+    FH_HIP(hipMemsetAsync(H, 0, size_t(V) * sizeof(uint32_t), stream));
+    k_fb_init<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), done, rep.get(), H, reached);
+    do {
+      FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
+      k_fb_hprop<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), done,
+                                                    rep.get(), H, scalars.get());
+    } while (read_scalar(0));
+    k_fb_roots<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), done, rep.get(), H, reached);
+    do {
+      FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
+      k_fb_reach<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), done,
+                                                    rep.get(), H, reached, scalars.get());
+    } while (read_scalar(0));
+    FH_HIP(hipMemsetAsync(scalars.get() + 1, 0, sizeof(uint32_t), stream));
+    // unions go to a separate parent array so rep[] stays stable while read
+    uint32_t *parent = tmp32a.ensure(V);
+    FH_HIP(hipMemcpyAsync(parent, rep.get(), size_t(V) * sizeof(uint32_t),
+                          hipMemcpyDeviceToDevice, stream));
+    k_fb_merge<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), done, rep.get(), H, reached,
+                                                  parent, scalars.get() + 1);
+    k_uf_compress<<<grid_for(V, B), B, 0, stream>>>(V, parent);
+    FH_HIP(hipMemcpyAsync(rep.get(), parent, size_t(V) * sizeof(uint32_t),
+                          hipMemcpyDeviceToDevice, stream));
+    if (!read_scalar(1)) break;
+  }
+  mark("scc_fallback");
+}
+
+void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
+  const uint32_t V = in.V;
+  const int bv = bits_for(uint64_t(V) + 1);
+  // SCC labels: min dot of each SCC
+  uint64_t *lab = label.ensure(V);
+  uint64_t *lab_out = tmp64c.ensure(V);
+  k_label_init<<<grid_for(V, B), B, 0, stream>>>(V, lab);
+  k_label_min<<<grid_for(V, B), B, 0, stream>>>(V, rep.get(), in.dot, lab);
+  k_label_bcast<<<grid_for(V, B), B, 0, stream>>>(V, rep.get(), lab, lab_out);
+  out.scc_label = lab_out;
+  mark("scc_label");
+  // dot rank (intra-SCC order is dot order)
+  uint64_t *ka = tmp64a.ensure(V), *kb = tmp64b.ensure(V);
+  uint32_t *va = tmp32a.ensure(V), *vb = tmp32b.ensure(V);
+  uint64_t *ks = nullptr;
+  uint32_t *vs = nullptr;
+  uint32_t *dot_rank = rank.ensure(V);
+  sort_pairs<uint64_t>(in.dot, nullptr, ka, va, kb, vb, V, 64, sort_ws, stream, &ks, &vs);
+  k_rank_from_sorted<<<grid_for(V, B), B, 0, stream>>>(V, vs, dot_rank);
+  mark("dot_rank");
+  // SCC order by kappa
+  uint32_t *fl = cnt.ensure(V);
+  uint32_t *ps = pos.ensure(V + 1);
+  k_rep_flags<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), fl);
+  exclusive_scan_u32(fl, ps, V, scan_ws, stream);
+  uint32_t nrep = 0;
+  FH_HIP(hipMemcpyAsync(&nrep, ps + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  k_rep_keys<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, kap.get(), bv, ka, va);
+  FH_HIP(hipStreamSynchronize(stream));
+  uint32_t *scc_rank = tmp32c.ensure(V);
+  sort_pairs<uint64_t>(ka, va, ka, va, kb, vb, nrep, 2 * bv, sort_ws, stream, &ks, &vs);
+  k_rank_from_sorted<<<grid_for(nrep, B), B, 0, stream>>>(nrep, vs, scc_rank);
+  mark("scc_order");
+  // vertex order: (scc rank, dot rank)
+  k_exec_flags<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), fl);
+  exclusive_scan_u32(fl, ps, V, scan_ws, stream);
+  uint32_t nexec = 0;
+  FH_HIP(hipMemcpyAsync(&nexec, ps + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  k_vertex_keys<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, rep.get(), scc_rank, dot_rank, bv,
+                                                   ka, va);
+  FH_HIP(hipStreamSynchronize(stream));
+  sort_pairs<uint64_t>(ka, va, ka, va, kb, vb, nexec, 2 * bv, sort_ws, stream, &ks, &vs);
+  uint32_t *ord = order.ensure(nexec + 1);
+  FH_HIP(hipMemcpyAsync(ord, vs, size_t(nexec) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                        stream));
+  uint32_t *er = tmp32d.ensure(V);
+  k_exec_rank<<<grid_for(V, B), B, 0, stream>>>(V, er);
+  k_rank_from_sorted<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, er);
+  out.exec_order = ord;
+  out.exec_rank = er;
+  out.nexec = nexec;
+  out.npending = V - nexec;
+  mark("exec_order");
+  // per-key sequence: elements in exec order, stable-sorted by key
+  uint32_t *ec = cnt.ensure(nexec + 1);
+  uint32_t *ep = pos.ensure(nexec + 1);
+  k_elem_counts<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, in.k, in.key_off, ec);
+  exclusive_scan_u32(ec, ep, nexec, scan_ws, stream);
+  uint32_t nelem = 0;
+  FH_HIP(hipMemcpyAsync(&nelem, ep + nexec, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  FH_HIP(hipStreamSynchronize(stream));
+  uint32_t *ek = tmp32a.ensure(nelem + 1), *ev = tmp32b.ensure(nelem + 1);
+  k_elem_fill<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, in.k, in.key_off, in.key32, ep,
+                                                     ek, ev);
+  uint32_t *k2 = flags.ensure(nelem + 1), *v2 = rank.ensure(nelem + 1);
+  uint32_t *ko = nullptr, *vo = nullptr;
+  // ek/ev are sorted into (k2, v2) or back into (ek, ev)
+  sort_pairs<uint32_t>(ek, ev, k2, v2, ek, ev, nelem, in.key_bits, sort_ws, stream, &ko, &vo);
+  out.pk_key = ko;
+  out.pk_vid = vo;
+  out.nelem = nelem;
+  mark("per_key_order");
+}
+
+void GraphCore::run(const GraphInput &in, GraphOutput &out) {
+  const uint32_t V = in.V;
+  out = GraphOutput();
+  scalars.ensure(32);
+  blocked.ensure(V + 1);
+  rep.ensure(V + 1);
+  kap.ensure(V + 1);
+  out.blocked = blocked.get();
+  out.rep = rep.get();
+  if (V == 0) {
+    out.trivial = true;
+    return;
+  }
+  pending_closure(in, out);
+  // trivial: nothing pending and every edge points to an earlier arrival ->
+  // every SCC is a singleton and arrival order is a topological order
+  bool any_blocked = false;
+  if (in.blocked0) {
+    uint32_t *fl = cnt.ensure(V);
+    uint32_t *ps = pos.ensure(V + 1);
+    k_exec_flags<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), fl);
+    exclusive_scan_u32(fl, ps, V, scan_ws, stream);
+    uint32_t ne = 0;
+    FH_HIP(hipMemcpyAsync(&ne, ps + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    any_blocked = ne != V;
+  }
+  const uint64_t nfwd = in.no_forward_hint ? 0 : count_forward(in);
+  if (nfwd == 0 && !any_blocked && in.sorted_keys && in.sorted_vid) {
+    // every SCC is a singleton and the execution order is the arrival order:
+    // nothing to materialise (rep[v] = v, label = own dot, rank = v)
+    out.trivial = true;
+    out.rep = nullptr;
+    out.scc_label = nullptr;
+    out.nexec = V;
+    out.npending = 0;
+    out.pk_key = const_cast<uint32_t *>(in.sorted_keys);
+    out.pk_vid = const_cast<uint32_t *>(in.sorted_vid);
+    out.nelem = in.key_off ? 0 : V * in.k;
+    mark("trivial_order");
+    return;
+  }
+  if (nfwd) {
+    find_sccs(in);
+  } else {
+    k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
+  }
+  uint32_t iters = 0;
+  bool ok = order_kappa(in, nfwd ? 64 : 4, iters);
+  if (!ok) {
+    coloring_fallback(in);
+    out.fallback_used = true;
+    ok = order_kappa(in, 1u << 30, iters);
+  }
+  out.kappa_iters = iters;
+  build_orders(in, out);
+}
+
+}  // namespace fh

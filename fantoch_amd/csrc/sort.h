@@ -25,7 +25,7 @@ struct SortWorkspace {
 // Sorts n pairs stably by the low `key_bits` bits of the key.  vals_in ==
 // nullptr means values are the input positions 0..n-1.  Data ping-pongs
 // between (ka, va) and (kb, vb); *kout / *vout point at the sorted result
-// (one of the two).  keys_in may alias ka.  n must be < 2^30.
+// (one of the two).  keys_in/vals_in may alias either pair.  n < 2^30.
 template <class K>
 void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va,
                 K *kb, uint32_t *vb, size_t n, int key_bits, SortWorkspace &ws,

@@ -201,8 +201,11 @@ void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va, 
   k_hist<K><<<grid_for(n, 256, 1024), 256, 0, s>>>(keys_in, uint32_t(n), passes, ghist);
   const K *ki = keys_in;
   const uint32_t *vi = vals_in;
-  K *ko = ka;
-  uint32_t *vo = va;
+  // never write pass 0 over its own input
+  const bool alias_a = (const void *)keys_in == (const void *)ka ||
+                       (vals_in && (const void *)vals_in == (const void *)va);
+  K *ko = alias_a ? kb : ka;
+  uint32_t *vo = alias_a ? vb : va;
   for (int p = 0; p < passes; p++) {
     uint32_t *st = status + size_t(p) * tiles * 256;
     // each pass gets its own ticket counter ctr[p] ... use ctr[p] via offset

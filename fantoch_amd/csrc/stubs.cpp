@@ -14,14 +14,4 @@ STUB(fh_status fh_graph_mark_executed(fh_graph *, size_t, const uint64_t *))
 STUB(fh_status fh_graph_set_executed_frontier(fh_graph *, uint32_t, uint64_t))
 STUB(fh_status fh_graph_pending(fh_graph *, size_t *))
 STUB(fh_status fh_graph_missing(fh_graph *, uint64_t *, size_t, size_t *))
-STUB(fh_status fh_engine_create(const fh_config *, fh_engine **))
-STUB(fh_status fh_engine_destroy(fh_engine *))
-STUB(fh_status fh_engine_reset(fh_engine *))
-STUB(fh_status fh_engine_stage(fh_engine *, const fh_stream_desc *, const uint64_t *,
-                               const uint64_t *, const uint8_t *, const uint64_t *))
-STUB(fh_status fh_engine_run(fh_engine *, float *))
-STUB(fh_status fh_engine_results(fh_engine *, uint32_t *, uint64_t *, size_t, size_t *,
-                                 uint64_t *, uint32_t *, uint32_t *, uint64_t *))
-STUB(fh_status fh_engine_kernel_times(fh_engine *, const char **, float *, size_t, size_t *))
-STUB(fh_status fh_engine_set_profiling(fh_engine *, int))
 }

@@ -1,0 +1,83 @@
+"""Engine -- the fused device-resident dependency engine (fh_engine_*).
+
+deps (KeyDeps per replica view + QuorumDeps union) -> SCC -> execution order
+-> per-key execution sequence, for one batch of commands staged in HBM.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .keydeps import make_config
+
+
+class Engine:
+    def __init__(self, key_space: int, n: int = 5, f: int = 1, device: int = -1):
+        self._lib = L.load()
+        self.key_space = key_space
+        self.cfg = make_config(n=n, f=f, device=device, key_space=key_space)
+        h = C.c_void_p()
+        L.check(self._lib.fh_engine_create(C.byref(self.cfg), C.byref(h)))
+        self._h = h
+        self.n = 0
+        self.k = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.fh_engine_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def reset(self):
+        L.check(self._lib.fh_engine_reset(self._h))
+
+    def set_profiling(self, on: bool):
+        L.check(self._lib.fh_engine_set_profiling(self._h, 1 if on else 0))
+
+    def stage(self, stream, nproc: int = 5):
+        """stream: fantoch_amd.workload.Stream (views taken from it)."""
+        views = 0 if stream.fq_proc is None else stream.fq_proc.shape[1]
+        d = L.fh_stream_desc(n=stream.n, keys_per_cmd=stream.k, views=views,
+                             nproc=nproc if views else 0, pad=0)
+        dots = np.ascontiguousarray(stream.dots, dtype=np.uint64)
+        keys = np.ascontiguousarray(stream.keys, dtype=np.uint64)
+        proc = None if not views else np.ascontiguousarray(stream.fq_proc, dtype=np.uint8)
+        tim = None if not views else np.ascontiguousarray(stream.fq_time, dtype=np.uint64)
+        L.check(self._lib.fh_engine_stage(self._h, C.byref(d), L.ptr(dots), L.ptr(keys),
+                                          L.ptr(proc), L.ptr(tim)))
+        self.n, self.k = stream.n, stream.k
+
+    def run(self, sync: bool = True) -> float:
+        ms = C.c_float(0)
+        L.check(self._lib.fh_engine_run(self._h, C.byref(ms) if sync else None))
+        return float(ms.value)
+
+    def kernel_times(self):
+        n = C.c_size_t(0)
+        L.check(self._lib.fh_engine_kernel_times(self._h, None, None, 0, C.byref(n)))
+        names = (C.c_char_p * max(1, n.value))()
+        ms = (C.c_float * max(1, n.value))()
+        L.check(self._lib.fh_engine_kernel_times(self._h, names, ms, n.value, C.byref(n)))
+        return [(names[i].decode(), float(ms[i])) for i in range(n.value)]
+
+    def results(self):
+        n = self.n
+        dep_off = np.zeros(n + 1, dtype=np.uint32)
+        ln = C.c_size_t(0)
+        L.check(self._lib.fh_engine_results(self._h, L.ptr(dep_off), None, 0, C.byref(ln), None,
+                                            None, None, None))
+        deps = np.zeros(max(1, ln.value), dtype=np.uint64)
+        label = np.zeros(n, dtype=np.uint64)
+        rank = np.zeros(n, dtype=np.uint32)
+        key_off = np.zeros(self.key_space + 1, dtype=np.uint32)
+        L.check(self._lib.fh_engine_results(self._h, None, None, 0, None, None, None,
+                                            L.ptr(key_off), None))
+        key_seq = np.zeros(max(1, int(key_off[-1])), dtype=np.uint64)
+        L.check(self._lib.fh_engine_results(self._h, L.ptr(dep_off), L.ptr(deps), len(deps),
+                                            C.byref(ln), L.ptr(label), L.ptr(rank), None,
+                                            L.ptr(key_seq)))
+        return {"dep_off": dep_off, "deps": deps[:ln.value], "scc_label": label,
+                "exec_rank": rank, "key_off": key_off, "key_seq": key_seq[:int(key_off[-1])]}

@@ -1,0 +1,122 @@
+"""The fused engine (fh_engine_*) against the oracle: bit-exact committed
+deps, SCC partition (min-dot labels) and per-key execution sequences."""
+import numpy as np
+import pytest
+
+from fantoch_amd.engine import Engine
+from fantoch_amd.workload import Workload
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_pipeline(s, nproc=5):
+    """Reference CPU path on the same stream: SequentialKeyDeps (one view) or
+    per-replica KeyDeps + QuorumDeps union (views), then GraphExecutor in
+    arrival (= stream) order with the per-key monitor."""
+    key_off = s.key_off()
+    keys = s.keys.reshape(-1)
+    if s.fq_proc is None:
+        dep_off, deps = O.keydeps_run(s.dots, key_off, keys)
+    else:
+        dep_off, deps = O.views_run(0, nproc, s.dots, key_off, keys, s.fq_proc, s.fq_time)
+    ex, lab, kso, ks = O.graph_run(s.dots, key_off, keys, dep_off, deps, s.key_space)
+    return dep_off, deps, ex, lab, kso, ks
+
+
+def check_engine(s, nproc=5, batches=1):
+    eng = Engine(s.key_space, n=nproc)
+    dep_off, deps, ex, lab, kso, ks = oracle_pipeline(s, nproc)
+    assert len(ex) == s.n, "oracle must execute every command"
+    if batches == 1:
+        eng.stage(s, nproc)
+        eng.run()
+        r = eng.results()
+        assert np.array_equal(r["dep_off"], dep_off)
+        assert np.array_equal(r["deps"], deps)
+        # SCC partition: label = min dot of the command's SCC
+        want_label = dict(zip(ex.tolist(), lab.tolist()))
+        got_label = dict(zip(s.dots.tolist(), r["scc_label"].tolist()))
+        assert got_label == want_label
+        # per-key execution sequence
+        assert np.array_equal(r["key_off"], kso)
+        assert np.array_equal(r["key_seq"], ks)
+        # execution order respects every dependency edge
+        rank = dict(zip(s.dots.tolist(), r["exec_rank"].tolist()))
+        lab_of = got_label
+        for i in range(min(s.n, 20000)):
+            for d in deps[dep_off[i]:dep_off[i + 1]]:
+                d = int(d)
+                if lab_of[d] != lab_of[int(s.dots[i])]:
+                    assert rank[d] < rank[int(s.dots[i])]
+        return r
+    # streaming batches: deps and per-key sequences concatenate
+    bounds = np.linspace(0, s.n, batches + 1).astype(int)
+    got_deps, got_seq = [], {}
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        sub = type(s)(s.dots[a:b], s.keys[a:b], None, None, s.key_space)
+        eng.stage(sub, nproc)
+        eng.run()
+        r = eng.results()
+        for i in range(b - a):
+            got_deps.append(r["deps"][r["dep_off"][i]:r["dep_off"][i + 1]])
+        ko = r["key_off"]
+        for key in np.nonzero(np.diff(ko))[0]:
+            got_seq.setdefault(int(key), []).extend(r["key_seq"][ko[key]:ko[key + 1]].tolist())
+    for i in range(s.n):
+        assert np.array_equal(got_deps[i], deps[dep_off[i]:dep_off[i + 1]])
+    for key in np.nonzero(np.diff(kso))[0]:
+        assert got_seq[int(key)] == ks[kso[key]:kso[key + 1]].tolist()
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_single_view_zipf(k):
+    s = Workload.zipf(0.99, 2000, k=k, seed=3 + k).generate(30_000)
+    check_engine(s)
+
+
+def test_single_view_streaming_batches():
+    s = Workload.zipf(0.7, 5000, k=1, seed=21).generate(40_000)
+    check_engine(s, batches=4)
+
+
+def test_c1_atlas_n5_conflict10_views():
+    """C1: Atlas n=5 f=1, ConflictRate 10%, 1 key, 10k cmds, replica views."""
+    s = Workload.conflict_rate_(10, k=1, views=3, window=64, seed=1).generate(10_000)
+    check_engine(s)
+
+
+@pytest.mark.parametrize("w", [8, 64])
+def test_c3_like_conflict_pool_views_large_sccs(w):
+    """C3-like: 100% conflict on key 0 plus a pool key, EPaxos fq=3 views."""
+    s = Workload.conflict_pool(100, 16, k=2, views=3, window=w, seed=5).generate(6_000)
+    r = check_engine(s)
+    # there are large SCCs
+    _, counts = np.unique(r["scc_label"], return_counts=True)
+    assert counts.max() > 50
+
+
+def test_c4_like_zipf099_views():
+    s = Workload.zipf(0.99, 1 << 14, k=1, views=3, window=64, seed=7).generate(40_000)
+    r = check_engine(s)
+    _, counts = np.unique(r["scc_label"], return_counts=True)
+    assert counts.max() > 1  # non-trivial SCCs exist
+
+
+def test_c5_like_multikey_views():
+    s = Workload.zipf(0.99, 4096, k=4, views=3, window=64, seed=9).generate(8_000)
+    check_engine(s)
+
+
+def test_c2_full_size():
+    """C2 at full size: 1M cmds, Zipf 0.7 over 1M keys, 1 key/cmd."""
+    s = Workload.zipf(0.7, 1 << 20, k=1).generate(1_000_000)
+    eng = Engine(s.key_space)
+    eng.stage(s)
+    eng.run()
+    r = eng.results()
+    dep_off, deps, ex, lab, kso, ks = oracle_pipeline(s)
+    assert np.array_equal(r["dep_off"], dep_off)
+    assert np.array_equal(r["deps"], deps)
+    assert np.array_equal(r["key_off"], kso)
+    assert np.array_equal(r["key_seq"], ks)
