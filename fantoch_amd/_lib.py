@@ -64,10 +64,13 @@ SIGNATURES = {
     "fh_engine_destroy": (C.c_int, [V]),
     "fh_engine_reset": (C.c_int, [V]),
     "fh_engine_stage": (C.c_int, [V, P(fh_stream_desc), V, V, V, V]),
+    "fh_engine_stage_many": (C.c_int, [V, P(fh_stream_desc), S, V, V, V, V]),
     "fh_engine_run": (C.c_int, [V, P(C.c_float)]),
     "fh_engine_results": (C.c_int, [V, V, V, S, P(S), V, V, V, V]),
     "fh_engine_kernel_times": (C.c_int, [V, P(C.c_char_p), P(C.c_float), S, P(S)]),
     "fh_engine_set_profiling": (C.c_int, [V, C.c_int]),
+    "fh_engine_set_probe": (C.c_int, [V, C.c_char_p]),
+    "fh_engine_probe_stats": (C.c_int, [V, P(C.c_float), P(S), P(C.c_double)]),
     "fh_workload_key_space": (C.c_uint64, [P(fh_workload)]),
     "fh_workload_generate": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V, V, V]),
 }

@@ -12,6 +12,8 @@ thread_local std::string g_last_error;
 
 void set_last_error(const std::string &m) { g_last_error = m; }
 
+thread_local Probe *t_probe = nullptr;
+
 int pick_device(const fh_config *cfg, uint64_t shard_id) {
   int count = 0;
   FH_HIP(hipGetDeviceCount(&count));

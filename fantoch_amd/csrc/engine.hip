@@ -137,6 +137,128 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
   }
 }
 
+// ---- single view, one key per command: two fused passes over the sorted
+// (key, vid) elements.  Deps and the per-key sequence in one pass; the
+// latest-table update (segment tails) and the executed-clock advance in the
+// next, so no head reads a latest entry a tail of the same batch rewrote.
+// dep encoding in the single-view path: 0 = none, (vid + 1) for an in-batch
+// dependency (the top byte of a dot is its ProcessId, never 0), otherwise the
+// external dot from the latest table
+__device__ __forceinline__ uint64_t enc_vid(uint32_t v) { return uint64_t(v) + 1; }
+
+__global__ void __launch_bounds__(256)
+    k_sv_deps(uint32_t M, const uint32_t *__restrict__ ks, const uint32_t *__restrict__ vs,
+              const uint64_t *__restrict__ latest, uint64_t *__restrict__ dep_sorted) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool ok = j < M;
+  const uint32_t key = ok ? ks[j] : 0u;
+  const uint32_t vid = ok ? vs[j] : 0u;
+  uint32_t pkey = __shfl_up(key, 1, 64);
+  uint32_t pvid = __shfl_up(vid, 1, 64);
+  if (lane == 0 && ok && j > 0) {
+    pkey = ks[j - 1];
+    pvid = vs[j - 1];
+  }
+  if (!ok) return;
+  const bool head = j == 0 || pkey != key;
+  // sequential.rs:83-96: the previous command on the key, or the latest
+  // command on it from an earlier batch
+  dep_sorted[j] = head ? latest[key] : enc_vid(pvid);
+}
+
+// Per-source {min, max, count} of a wave's dots: the lanes holding one source
+// are grouped by ballot (a batch has few sources), reduced with shuffles, and
+// the group leader folds the result into LDS.
+__device__ __forceinline__ void src_stats_wave(bool ok, uint64_t d, unsigned long long *s_mn,
+                                               unsigned long long *s_mx, unsigned int *s_cnt) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t src = uint32_t(d >> 56);
+  const unsigned long long q = d & 0x00FFFFFFFFFFFFFFull;
+  uint64_t rem = __ballot(ok);
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const uint32_t s0 = __shfl(src, leader, 64);
+    const bool mine = ok && src == s0;
+    const uint64_t m = __ballot(mine);
+    unsigned long long vmn = mine ? q : ~0ull, vmx = mine ? q : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long a = __shfl_xor(vmn, o, 64), b = __shfl_xor(vmx, o, 64);
+      vmn = a < vmn ? a : vmn;
+      vmx = b > vmx ? b : vmx;
+    }
+    if (lane == leader) {
+      atomicMin(&s_mn[s0], vmn);
+      atomicMax(&s_mx[s0], vmx);
+      atomicAdd(&s_cnt[s0], unsigned(__popcll(m)));
+    }
+    rem &= ~m;
+  }
+}
+
+// Segment tails update the latest table; every batch dot is executed, which
+// advances the executed clock: per source the frontier becomes the max
+// sequence and the executed count grows by the batch's count (the executed
+// set is contiguous from 1 iff count == frontier, checked when results are
+// read).  4096 elements per workgroup (16 per thread, loads issued up front),
+// per-source partials in LDS, one global atomic per source per workgroup.
+constexpr int kTailItems = 16;
+constexpr int kTailTile = 256 * kTailItems;
+
+__global__ void __launch_bounds__(256)
+    k_sv_tails(uint32_t M, const uint32_t *__restrict__ ks, const uint32_t *__restrict__ vs,
+               const uint64_t *__restrict__ dot, uint64_t *__restrict__ latest,
+               unsigned long long *__restrict__ frontier, unsigned long long *__restrict__ excount) {
+  __shared__ unsigned long long s_mx[256];
+  __shared__ unsigned int s_cnt[256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  s_mx[tid] = 0;
+  s_cnt[tid] = 0;
+  const uint32_t base = blockIdx.x * kTailTile + uint32_t(w) * 64 * kTailItems;
+  uint32_t key[kTailItems + 1];
+  uint64_t d[kTailItems];
+#pragma unroll
+  for (int i = 0; i < kTailItems; i++) {
+    const uint32_t j = base + i * 64 + lane;
+    key[i] = j < M ? ks[j] : ~0u;
+    d[i] = j < M ? dot[j] : 0ull;  // batch dots in arrival order
+  }
+  {
+    const uint32_t j = base + kTailItems * 64;  // first element after this wave's run
+    key[kTailItems] = j < M ? ks[j] : ~0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kTailItems; i++) {
+    const uint32_t j = base + i * 64 + lane;
+    uint32_t nk = __shfl_down(key[i], 1, 64);
+    const uint32_t nxt = __shfl(key[i + 1], 0, 64);
+    if (lane == 63) nk = nxt;
+    if (j < M) {
+      if (j + 1 == M || nk != key[i]) latest[key[i]] = dot[vs[j]];  // sequential.rs:88-95
+      const uint32_t src = uint32_t(d[i] >> 56);
+      atomicMax(&s_mx[src], d[i] & 0x00FFFFFFFFFFFFFFull);
+      atomicAdd(&s_cnt[src], 1u);
+    }
+  }
+  __syncthreads();
+  if (s_cnt[tid]) {
+    atomicMax(&frontier[tid], s_mx[tid]);
+    atomicAdd(&excount[tid], (unsigned long long)s_cnt[tid]);
+  }
+}
+
+// results: single-view sorted deps -> per-command dep dots
+__global__ void k_sv_unpermute(uint32_t M, const uint32_t *__restrict__ vs,
+                               const uint64_t *__restrict__ dep_sorted,
+                               const uint64_t *__restrict__ dot, uint64_t *__restrict__ dep_dot) {
+  GRID_STRIDE(j, M) {
+    const uint64_t x = dep_sorted[j];
+    dep_dot[vs[j]] = (x != 0 && (x >> 56) == 0) ? dot[x - 1] : x;
+  }
+}
+
 __global__ void k_seq_dots(uint32_t m, const uint32_t *__restrict__ pk_vid,
                            const uint64_t *__restrict__ dot, uint64_t *__restrict__ seq) {
   GRID_STRIDE(j, m) seq[j] = dot[pk_vid[j]];
@@ -173,13 +295,19 @@ __global__ void __launch_bounds__(256)
 __global__ void k_frontier_update(const unsigned long long *__restrict__ mn,
                                   const unsigned long long *__restrict__ mx,
                                   const unsigned int *__restrict__ cnt, uint64_t *frontier,
-                                  uint32_t *err) {
+                                  unsigned long long *excount, uint32_t *err) {
   const uint32_t s = threadIdx.x;
   if (s >= 256 || cnt[s] == 0) return;
-  if (mn[s] == frontier[s] + 1 && mx[s] - mn[s] + 1 == cnt[s])
+  if (mn[s] == frontier[s] + 1 && mx[s] - mn[s] + 1 == cnt[s]) {
     frontier[s] = mx[s];
-  else
+    excount[s] += cnt[s];
+  } else {
     atomicOr(err, 1u);  // non-contiguous executed set: needs exceptions
+  }
+}
+
+__global__ void k_cnt_nonzero(uint32_t n, const uint64_t *__restrict__ d, uint32_t *__restrict__ c) {
+  GRID_STRIDE(i, n) c[i] = d[i] != 0;
 }
 
 __global__ void k_bcast_u32(uint32_t n, uint32_t *p, uint32_t v) { GRID_STRIDE(i, n) p[i] = v; }
@@ -217,9 +345,11 @@ struct EngineDevice {
   DBuf<uint64_t> frontier;   // [256] executed-clock frontier per source
   uint32_t latest_slots = 1; // replica slots allocated in `latest`
   DBuf<uint32_t> err;
-  // staged batch
+  // staged batches
   fh_stream_desc desc{};
   bool staged = false;
+  size_t nbatches = 0, cursor = 0, last = 0;
+  std::vector<uint64_t> tmins;
   uint64_t tmin = 0;
   int tbits = 0;
   DBuf<uint64_t> dot, fq_time;
@@ -235,6 +365,18 @@ struct EngineDevice {
   ScanWorkspace scan_ws;
   GraphCore graph;
   GraphOutput gout;
+  Probe probe;
+  bool sv_fused = false;
+  const uint32_t *sorted_keys32 = nullptr;  // single-view: keys in sorted order
+  const uint32_t *sv_vs = nullptr;          // single-view: vids in sorted order
+  DBuf<unsigned long long> excount;  // executed dots per source (single-view clock)
+  unsigned long long *excount_ptr() {
+    if (!excount.get()) {
+      excount.ensure(256);
+      FH_HIP(hipMemsetAsync(excount.get(), 0, 256 * sizeof(unsigned long long), stream));
+    }
+    return excount.get();
+  }
   // timing
   bool profile = false;
   std::vector<std::pair<const char *, hipEvent_t>> marks;
@@ -294,13 +436,14 @@ struct EngineDevice {
     FH_HIP(hipMemsetAsync(latest.get(), 0, size_t(latest_slots) * key_space * sizeof(uint64_t),
                           stream));
     FH_HIP(hipMemsetAsync(frontier.get(), 0, 256 * sizeof(uint64_t), stream));
+    FH_HIP(hipMemsetAsync(excount_ptr(), 0, 256 * sizeof(unsigned long long), stream));
     FH_HIP(hipMemsetAsync(err.get(), 0, 4 * sizeof(uint32_t), stream));
     FH_HIP(hipStreamSynchronize(stream));
   }
 
-  void stage(const fh_stream_desc &d, const uint64_t *h_dot, const uint64_t *h_key,
+  void stage(const fh_stream_desc &d, size_t nb, const uint64_t *h_dot, const uint64_t *h_key,
              const uint8_t *h_proc, const uint64_t *h_time) {
-    FH_CHECK(h_dot && h_key, FH_EINVAL, "null argument");
+    FH_CHECK(h_dot && h_key && nb >= 1, FH_EINVAL, "null argument");
     FH_CHECK(d.keys_per_cmd >= 1 && d.keys_per_cmd <= 8, FH_EINVAL, "keys_per_cmd in [1, 8]");
     const uint32_t fq = d.views ? d.views : 1;
     FH_CHECK(fq <= 16, FH_EINVAL, "views <= 16");
@@ -310,40 +453,47 @@ struct EngineDevice {
              "replica views need fq_proc, fq_time and nproc");
     FH_HIP(hipSetDevice(device));
     const size_t n = d.n, nk = n * d.keys_per_cmd;
-    std::vector<uint32_t> k32(nk);
-    for (size_t e = 0; e < nk; e++) {
+    std::vector<uint32_t> k32(nk * nb);
+    for (size_t e = 0; e < nk * nb; e++) {
       FH_CHECK(h_key[e] < key_space, FH_EINVAL, "stage: key id >= key_space");
       k32[e] = uint32_t(h_key[e]);
     }
-    FH_HIP(hipMemcpyAsync(dot.ensure(n + 1), h_dot, n * sizeof(uint64_t), hipMemcpyHostToDevice,
-                          stream));
-    FH_HIP(hipMemcpyAsync(key32.ensure(nk + 1), k32.data(), nk * sizeof(uint32_t),
+    FH_HIP(hipMemcpyAsync(dot.ensure(n * nb + 1), h_dot, n * nb * sizeof(uint64_t),
                           hipMemcpyHostToDevice, stream));
+    FH_HIP(hipMemcpyAsync(key32.ensure(nk * nb + 1), k32.data(), nk * nb * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, stream));
+    tmins.assign(nb, 0);
+    tbits = 0;
     if (d.views) {
       const size_t nv = n * fq;
-      uint64_t lo = ~0ull, hi = 0;
-      for (size_t i = 0; i < nv; i++) {
-        FH_CHECK(h_proc[i] >= 1 && h_proc[i] <= d.nproc, FH_EINVAL, "fq_proc out of range");
-        lo = std::min(lo, h_time[i]);
-        hi = std::max(hi, h_time[i]);
+      for (size_t b = 0; b < nb; b++) {
+        uint64_t lo = ~0ull, hi = 0;
+        for (size_t i = b * nv; i < (b + 1) * nv; i++) {
+          FH_CHECK(h_proc[i] >= 1 && h_proc[i] <= d.nproc, FH_EINVAL, "fq_proc out of range");
+          lo = std::min(lo, h_time[i]);
+          hi = std::max(hi, h_time[i]);
+        }
+        tmins[b] = n ? lo : 0;
+        tbits = std::max(tbits, bits_for(n ? hi - lo + 1 : 1));
       }
-      tmin = n ? lo : 0;
-      tbits = bits_for(n ? hi - lo + 1 : 1);
       FH_CHECK(bits_for(uint64_t(d.nproc + 1) * key_space) + tbits <= 64, FH_ENOTIMPL,
                "replica-view sort key wider than 64 bits");
-      FH_HIP(hipMemcpyAsync(fq_proc.ensure(nv + 1), h_proc, nv, hipMemcpyHostToDevice, stream));
-      FH_HIP(hipMemcpyAsync(fq_time.ensure(nv + 1), h_time, nv * sizeof(uint64_t),
+      FH_HIP(hipMemcpyAsync(fq_proc.ensure(nv * nb + 1), h_proc, nv * nb, hipMemcpyHostToDevice,
+                            stream));
+      FH_HIP(hipMemcpyAsync(fq_time.ensure(nv * nb + 1), h_time, nv * nb * sizeof(uint64_t),
                             hipMemcpyHostToDevice, stream));
       ensure_latest(d.nproc + 1);
     }
     FH_HIP(hipStreamSynchronize(stream));
     desc = d;
+    nbatches = nb;
+    cursor = 0;
     staged = true;
   }
 
   // The device run of one batch: everything below is the timed hot path.
   void run(float *ms) {
-    FH_CHECK(staged, FH_EINVAL, "no batch staged");
+    FH_CHECK(staged && cursor < nbatches, FH_EINVAL, "no staged batch left to run");
     FH_HIP(hipSetDevice(device));
     clear_marks();
     graph.profile = profile;
@@ -352,29 +502,75 @@ struct EngineDevice {
     const uint32_t S = fq * k;
     const uint32_t M = n * S;
     const bool views = desc.views != 0;
+    const size_t b = cursor++;
+    last = b;
+    const uint64_t *bdot = dot.get() + b * n;
+    const uint32_t *bkey = key32.get() + b * size_t(n) * k;
+    const uint8_t *bproc = views ? fq_proc.get() + b * size_t(n) * fq : nullptr;
+    const uint64_t *btime = views ? fq_time.get() + b * size_t(n) * fq : nullptr;
+    tmin = tmins[b];
     FH_HIP(hipEventRecord(ev0, stream));
     mark("start");
+    struct ProbeGuard {
+      ProbeGuard(Probe *p) { t_probe = p; }
+      ~ProbeGuard() { t_probe = nullptr; }
+    } probe_guard(probe.target.empty() ? nullptr : &probe);
     uint32_t *vs = nullptr;
     uint32_t *dvid = dep_vid.ensure(M + 1);
     uint64_t *dext = dep_ext.ensure(M + 1);
     uint8_t *tl = tail.ensure(M + 1);
     uint32_t *svid = sorted_vid.ensure(M + 1);
-    const uint32_t *sorted_keys32 = nullptr;
-    if (!views) {
+    sorted_keys32 = nullptr;
+    if (!views && k == 1) {
       uint32_t *ks = nullptr;
-      sort_pairs<uint32_t>(key32.get(), nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
+      sort_pairs<uint32_t>(bkey, nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
+                           sk32b.ensure(M + 1), svb.ensure(M + 1), M, key_bits, sort_ws, stream,
+                           &ks, &vs);
+      mark("keydeps_sort");
+      uint64_t *dsorted = dep_ext.ensure(M + 1);
+      const unsigned g = unsigned((M + 255) / 256);
+      {
+        // read key + vid (8), write the dependency (8)
+        ProbeScope probe("sv_deps", stream, double(M) * 16.0);
+        k_sv_deps<<<g, 256, 0, stream>>>(M, ks, vs, latest.get(), dsorted);
+      }
+      mark("deps");
+      {
+        // read key (4) and the batch dot (8)
+        ProbeScope probe("sv_tails", stream, double(M) * 12.0);
+        const unsigned gt = unsigned((M + kTailTile - 1) / kTailTile);
+        k_sv_tails<<<gt, 256, 0, stream>>>(
+            M, ks, vs, bdot, latest.get(), reinterpret_cast<unsigned long long *>(frontier.get()),
+            excount_ptr());
+      }
+      mark("tails_and_clock");
+      sv_vs = vs;
+      // dependency graph: every dep is an earlier arrival (previous element of
+      // a key segment sorted by arrival, or a latest entry from an executed
+      // earlier batch), so SCCs are singletons and arrival order is a
+      // topological order; the per-key sequence is the sorted element order.
+      gout = GraphOutput();
+      gout.trivial = true;
+      gout.nexec = n;
+      gout.nelem = M;
+      gout.pk_key = ks;
+      gout.pk_vid = vs;
+      sv_fused = true;
+    } else if (!views) {
+      sv_fused = false;
+      uint32_t *ks = nullptr;
+      sort_pairs<uint32_t>(bkey, nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
                            sk32b.ensure(M + 1), svb.ensure(M + 1), M, key_bits, sort_ws, stream,
                            &ks, &vs);
       mark("keydeps_sort");
       k_prev_engine<uint32_t><<<grid_for(M, B), B, 0, stream>>>(
           M, ks, vs, 0, S, latest.get(), dvid, dext, tl, k == 1 ? nullptr : svid);
       sorted_keys32 = ks;
-      if (k == 1) svid = vs;  // element id == vid
     } else {
+      sv_fused = false;
       uint64_t *vk = vkeys.ensure(M + 1);
-      k_view_keys<<<grid_for(M, B), B, 0, stream>>>(M, k, fq, key_space, key32.get(),
-                                                     fq_proc.get(), fq_time.get(), tmin, tbits,
-                                                     vk);
+      k_view_keys<<<grid_for(M, B), B, 0, stream>>>(M, k, fq, key_space, bkey, bproc, btime, tmin,
+                                                     tbits, vk);
       uint64_t *ks = nullptr;
       const int bits = bits_for(uint64_t(desc.nproc + 1) * key_space) + tbits;
       sort_pairs<uint64_t>(vk, nullptr, sk64a.ensure(M + 1), sva.ensure(M + 1),
@@ -384,13 +580,28 @@ struct EngineDevice {
       k_prev_engine<uint64_t><<<grid_for(M, B), B, 0, stream>>>(
           M, ks, vs, tbits, S, latest.get(), dvid, dext, tl, nullptr);
     }
+    if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bproc, bdot);
+    FH_HIP(hipEventRecord(ev1, stream));
+    if (ms) {
+      FH_HIP(hipEventSynchronize(ev1));
+      FH_HIP(hipEventElapsedTime(ms, ev0, ev1));
+    }
+    if (profile) collect_times();
+  }
+
+  void run_general(uint32_t n, uint32_t k, uint32_t fq, uint32_t S, uint32_t M, bool views,
+                   const uint32_t *bkey, const uint8_t *bproc, const uint64_t *bdot) {
+    uint32_t *dvid = dep_vid.get();
+    uint64_t *dext = dep_ext.get();
+    uint8_t *tl = tail.get();
+    uint32_t *svid = sorted_vid.get();
     mark("keydeps_prev");
     uint64_t *ddot = dep_dot.ensure(M + 1);
     uint32_t *dcnt = dep_cnt.ensure(n + 1);
     uint32_t *dd = dst.ensure(M + 1);
     FH_HIP(hipMemsetAsync(scal.get(), 0, sizeof(uint32_t), stream));
     k_cmd_engine<<<grid_for(n, B), B, 0, stream>>>(
-        n, k, fq, key_space, key32.get(), views ? fq_proc.get() : nullptr, dot.get(), dvid, dext,
+        n, k, fq, key_space, bkey, bproc, bdot, dvid, dext,
         tl, latest.get(), frontier.get(), ddot, dcnt, dd, nullptr, scal.get());
     mark("keydeps_union");
     // graph stage
@@ -400,9 +611,9 @@ struct EngineDevice {
     gin.stride = S;
     gin.dst = dd;
     gin.blocked0 = nullptr;  // see k_cmd_engine: no pending carried by the fused engine
-    gin.dot = dot.get();
+    gin.dot = bdot;
     gin.k = k;
-    gin.key32 = key32.get();
+    gin.key32 = bkey;
     gin.key_bits = key_bits;
     if (!views) {
       gin.no_forward_hint = true;  // single view: deps always point backwards
@@ -413,24 +624,18 @@ struct EngineDevice {
     FH_CHECK(gout.npending == 0, FH_EINVARIANT, "fused engine batch left pending vertices");
     // per-key sequence of dots (ExecutionOrderMonitor::add order)
     uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
-    k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, dot.get(), sq);
+    k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, bdot, sq);
     mark("per_key_dots");
     // executed clock: the whole batch executed
-    unsigned long long *st = srcstats.ensure(3 * 256);
+    unsigned long long *st = srcstats.ensure(4 * 256);
     FH_HIP(hipMemsetAsync(st, 0xFF, 256 * sizeof(unsigned long long), stream));
     FH_HIP(hipMemsetAsync(st + 256, 0, 512 * sizeof(unsigned long long), stream));
-    k_src_stats<<<grid_for(n, B, 512), B, 0, stream>>>(n, dot.get(), st, st + 256,
+    k_src_stats<<<grid_for(n, B, 512), B, 0, stream>>>(n, bdot, st, st + 256,
                                                    reinterpret_cast<unsigned int *>(st + 512));
     k_frontier_update<<<1, 256, 0, stream>>>(st, st + 256,
                                              reinterpret_cast<unsigned int *>(st + 512),
-                                             frontier.get(), err.get());
+                                             frontier.get(), excount_ptr(), err.get());
     mark("executed_clock");
-    FH_HIP(hipEventRecord(ev1, stream));
-    if (ms) {
-      FH_HIP(hipEventSynchronize(ev1));
-      FH_HIP(hipEventElapsedTime(ms, ev0, ev1));
-    }
-    if (profile) collect_times();
   }
 
   void collect_times() {
@@ -446,6 +651,14 @@ struct EngineDevice {
   void check_err() {
     uint32_t e = 0;
     FH_HIP(hipMemcpyAsync(&e, err.get(), sizeof(e), hipMemcpyDeviceToHost, stream));
+    if (excount.get()) {
+      uint64_t f[256], c[256];
+      FH_HIP(hipMemcpyAsync(f, frontier.get(), sizeof(f), hipMemcpyDeviceToHost, stream));
+      FH_HIP(hipMemcpyAsync(c, excount.get(), sizeof(c), hipMemcpyDeviceToHost, stream));
+      FH_HIP(hipStreamSynchronize(stream));
+      for (int s = 0; s < 256; s++)
+        if (c[s] != f[s]) e = 1;  // executed set not contiguous from 1
+    }
     FH_HIP(hipStreamSynchronize(stream));
     FH_CHECK(e == 0, FH_ENOTIMPL,
              "executed clock: non-contiguous executed dots per process (exceptions not supported "
@@ -461,6 +674,12 @@ struct EngineDevice {
     const uint32_t S = (desc.views ? desc.views : 1) * k;
     if (dep_off || dep_out || dep_len) {
       uint32_t *off = u32tmp.ensure(n + 1);
+      if (sv_fused) {  // one dependency slot per command: decode, count = slot used
+        k_sv_unpermute<<<grid_for(n, B), B, 0, stream>>>(n, sv_vs, dep_ext.get(),
+                                                          dot.get() + last * n,
+                                                          dep_dot.ensure(n + 1));
+        k_cnt_nonzero<<<grid_for(n, B), B, 0, stream>>>(n, dep_dot.get(), dep_cnt.ensure(n + 1));
+      }
       exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
       uint32_t total = 0;
       FH_HIP(hipMemcpyAsync(&total, off + n, sizeof(total), hipMemcpyDeviceToHost, stream));
@@ -483,7 +702,7 @@ struct EngineDevice {
       if (gout.trivial) {
         lb = lab.ensure(n + 1);
         rk = rank_tmp.ensure(n + 1);
-        k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, dot.get(), lb, rk);
+        k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, dot.get() + last * n, lb, rk);
       }
       if (scc_label)
         FH_HIP(hipMemcpyAsync(scc_label, lb, size_t(n) * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -501,9 +720,14 @@ struct EngineDevice {
       FH_HIP(hipMemcpyAsync(key_off, o, (key_space + 1) * sizeof(uint32_t),
                             hipMemcpyDeviceToHost, stream));
     }
-    if (key_seq)
+    if (key_seq) {
+      if (sv_fused)  // per-key sequence is (sorted keys, sorted vids): gather the dots
+        k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid,
+                                                               dot.get() + last * n,
+                                                               seq_dot.ensure(gout.nelem + 1));
       FH_HIP(hipMemcpyAsync(key_seq, seq_dot.get(), size_t(gout.nelem) * sizeof(uint64_t),
                             hipMemcpyDeviceToHost, stream));
+    }
     FH_HIP(hipStreamSynchronize(stream));
   }
 };
@@ -541,7 +765,16 @@ fh_status fh_engine_stage(fh_engine *h, const fh_stream_desc *desc, const uint64
                           const uint64_t *key_id, const uint8_t *fq_proc, const uint64_t *fq_time) {
   FH_API_BEGIN
   FH_CHECK(h && desc, FH_EINVAL, "null argument");
-  h->dev.stage(*desc, dot, key_id, fq_proc, fq_time);
+  h->dev.stage(*desc, 1, dot, key_id, fq_proc, fq_time);
+  FH_API_END
+}
+
+fh_status fh_engine_stage_many(fh_engine *h, const fh_stream_desc *desc, size_t nbatches,
+                               const uint64_t *dot, const uint64_t *key_id,
+                               const uint8_t *fq_proc, const uint64_t *fq_time) {
+  FH_API_BEGIN
+  FH_CHECK(h && desc, FH_EINVAL, "null argument");
+  h->dev.stage(*desc, nbatches, dot, key_id, fq_proc, fq_time);
   FH_API_END
 }
 
@@ -571,6 +804,34 @@ fh_status fh_engine_kernel_times(fh_engine *h, const char **names, float *ms, si
     if (names) names[i] = t[i].first.c_str();
     if (ms) ms[i] = t[i].second;
   }
+  FH_API_END
+}
+
+fh_status fh_engine_set_probe(fh_engine *h, const char *kernel) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_HIP(hipStreamSynchronize(h->dev.stream));
+  h->dev.probe.target = kernel ? kernel : "";
+  h->dev.probe.reset();
+  FH_API_END
+}
+
+fh_status fh_engine_probe_stats(fh_engine *h, float *avg_ms, size_t *launches,
+                                double *bytes_per_launch) {
+  FH_API_BEGIN
+  FH_CHECK(h && avg_ms && launches && bytes_per_launch, FH_EINVAL, "null argument");
+  FH_HIP(hipStreamSynchronize(h->dev.stream));
+  auto &p = h->dev.probe;
+  const size_t n = p.next / 2;
+  double tot = 0;
+  for (size_t i = 0; i < n; i++) {
+    float ms = 0;
+    FH_HIP(hipEventElapsedTime(&ms, p.ev[2 * i], p.ev[2 * i + 1]));
+    tot += ms;
+  }
+  *launches = n;
+  *avg_ms = n ? float(tot / double(n)) : 0.f;
+  *bytes_per_launch = n ? p.bytes / double(n) : 0.0;
   FH_API_END
 }
 

@@ -8,6 +8,7 @@
 #include <stdexcept>
 #include <string>
 #include <utility>
+#include <vector>
 
 #include "../../include/fantoch_hip.h"
 
@@ -80,6 +81,47 @@ inline int bits_for(uint64_t x) {
   while (b < 64 && (uint64_t(1) << b) < x) b++;
   return b;
 }
+
+// Roofline probe: HIP events around every launch of one named kernel on the
+// stream it runs on, plus the algorithmic bytes each launch moves.
+struct Probe {
+  std::string target;
+  std::vector<hipEvent_t> ev;
+  size_t next = 0;
+  double bytes = 0;
+  bool on(const char *name) const { return !target.empty() && target == name; }
+  void rec(hipStream_t s) {
+    if (next >= ev.size()) {
+      hipEvent_t e;
+      FH_HIP(hipEventCreate(&e));
+      ev.push_back(e);
+    }
+    FH_HIP(hipEventRecord(ev[next++], s));
+  }
+  void reset() {
+    next = 0;
+    bytes = 0;
+  }
+  ~Probe() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+  }
+};
+extern thread_local Probe *t_probe;
+
+struct ProbeScope {
+  bool active;
+  hipStream_t s;
+  ProbeScope(const char *name, hipStream_t st, double bytes) : active(false), s(st) {
+    if (t_probe && t_probe->on(name)) {
+      active = true;
+      t_probe->bytes += bytes;
+      t_probe->rec(s);
+    }
+  }
+  ~ProbeScope() {
+    if (active) t_probe->rec(s);
+  }
+};
 
 // Device selection per SURVEY §8b (shard -> device, or env override).
 int pick_device(const fh_config *cfg, uint64_t shard_id);

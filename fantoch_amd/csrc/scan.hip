@@ -1,4 +1,7 @@
-// scan.hip -- single-pass exclusive scan for gfx950 (see scan.h).
+// scan.hip -- exclusive prefix sum for gfx950, reduce-then-scan (see scan.h).
+// Three launches, no inter-workgroup hand-off inside a launch (cross-XCD
+// hand-offs cost microseconds each on MI355X; a chained scan serialises on
+// them).
 #include "scan.h"
 
 namespace fh {
@@ -7,85 +10,72 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
-constexpr uint32_t kAgg = 1u << 30;
-constexpr uint32_t kInc = 2u << 30;
-constexpr uint32_t kCnt = (1u << 30) - 1;
 
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(uint32_t *p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ void __launch_bounds__(kThreads)
-    k_scan(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint32_t n,
-           uint32_t *status) {
-  __shared__ uint32_t s_wave[kThreads / 64];
-  __shared__ uint32_t s_tile, s_prefix;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(&status[0], 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
-  // blocked arrangement: thread t owns items [base + t*kItems, +kItems)
-  const uint32_t base = tile * kTile + uint32_t(tid) * kItems;
-  uint32_t v[kItems];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = base + i;
-    v[i] = idx < n ? in[idx] : 0u;
-    sum += v[i];
-  }
-  // block exclusive scan of per-thread sums
-  uint32_t x = sum;
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_tmp,
+                                                    uint32_t *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t t = __shfl_up(x, o, 64);
     if (lane >= o) x += t;
   }
-  if (lane == 63) s_wave[w] = x;
+  if (lane == 63) s_tmp[w] = x;
   __syncthreads();
-  uint32_t wpre = 0, total = 0;
+  uint32_t pre = 0, tot = 0;
 #pragma unroll
   for (int i = 0; i < kThreads / 64; i++) {
-    if (i < w) wpre += s_wave[i];
-    total += s_wave[i];
-  }
-  uint32_t texcl = wpre + x - sum;
-  if (tid == 0) {
-    uint32_t *my = status + 2 + tile;
-    uint32_t excl = 0;
-    if (tile == 0) {
-      st_agent(my, kInc | total);
-    } else {
-      st_agent(my, kAgg | total);
-      int t = int(tile) - 1;
-      uint32_t spins = 0;
-      while (t >= 0) {
-        const uint32_t sv = ld_agent(status + 2 + t);
-        const uint32_t flag = sv & ~kCnt;
-        if (flag == kInc) {
-          excl += sv & kCnt;
-          break;
-        }
-        if (flag == kAgg) {
-          excl += sv & kCnt;
-          t--;
-          continue;
-        }
-        if (++spins > (1u << 24)) {
-          atomicOr(&status[1], 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      st_agent(my, kInc | (excl + total));
-    }
-    s_prefix = excl;
+    if (i < w) pre += s_tmp[i];
+    tot += s_tmp[i];
   }
   __syncthreads();
-  uint32_t run = s_prefix + texcl;
+  if (total) *total = tot;
+  return pre + x - v;
+}
+
+__global__ void __launch_bounds__(kThreads)
+    k_scan_reduce(const uint32_t *__restrict__ in, uint32_t n, uint32_t *__restrict__ bsum) {
+  __shared__ uint32_t s_tmp[kThreads / 64];
+  const uint32_t base = blockIdx.x * kTile;
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kItems; i++) {
+    const uint32_t idx = base + i * kThreads + threadIdx.x;
+    s += idx < n ? in[idx] : 0u;
+  }
+  uint32_t tot = 0;
+  block_excl_scan(s, s_tmp, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kThreads) k_scan_top(uint32_t *__restrict__ bsum, uint32_t nb) {
+  __shared__ uint32_t s_tmp[kThreads / 64];
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += kThreads) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint32_t v = b < nb ? bsum[b] : 0u;
+    uint32_t tot = 0;
+    const uint32_t ex = block_excl_scan(v, s_tmp, &tot);
+    if (b < nb) bsum[b] = carry + ex;
+    carry += tot;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+    k_scan_down(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint32_t n,
+                const uint32_t *__restrict__ bsum) {
+  __shared__ uint32_t s_tmp[kThreads / 64];
+  // blocked: thread t owns kItems consecutive elements
+  const uint32_t base = blockIdx.x * kTile + threadIdx.x * kItems;
+  uint32_t v[kItems];
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kItems; i++) {
+    const uint32_t idx = base + i;
+    v[i] = idx < n ? in[idx] : 0u;
+    s += v[i];
+  }
+  uint32_t run = bsum[blockIdx.x] + block_excl_scan(s, s_tmp, nullptr);
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + i;
@@ -99,15 +89,16 @@ __global__ void __launch_bounds__(kThreads)
 
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
                         hipStream_t s) {
-  FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "scan: too many elements");
+  FH_CHECK(n < (size_t(1) << 31), FH_EINVAL, "scan: too many elements");
   if (n == 0) {
     FH_HIP(hipMemsetAsync(out, 0, sizeof(uint32_t), s));
     return;
   }
-  const size_t tiles = (n + kTile - 1) / kTile;
-  uint32_t *st = ws.status.ensure(tiles + 2);
-  FH_HIP(hipMemsetAsync(st, 0, (tiles + 2) * sizeof(uint32_t), s));
-  k_scan<<<unsigned(tiles), kThreads, 0, s>>>(in, out, uint32_t(n), st);
+  const uint32_t nb = uint32_t((n + kTile - 1) / kTile);
+  uint32_t *bsum = ws.status.ensure(nb + 1);
+  k_scan_reduce<<<nb, kThreads, 0, s>>>(in, uint32_t(n), bsum);
+  k_scan_top<<<1, kThreads, 0, s>>>(bsum, nb);
+  k_scan_down<<<nb, kThreads, 0, s>>>(in, out, uint32_t(n), bsum);
 }
 
 }  // namespace fh

@@ -1,12 +1,8 @@
-// sort.h -- stable LSD radix sort of (key, u32 value) pairs, onesweep style.
+// sort.h -- stable LSD radix sort of (key, u32 value) pairs, reduce-then-scan.
 //
-// One histogram launch computes every 8-bit digit histogram; then one launch
-// per digit: each 256-thread workgroup takes a 4096-item tile (tile id from an
-// atomic ticket, so a tile only waits on tiles already running), ranks its
-// items stably with wave64 ballot matching, publishes per-digit counts and
-// resolves its global offsets by decoupled look-back over 32-bit
-// {flag, count} granules (single sc1 stores/loads, MI355X_MICROARCH.md
-// "Valid forms", R2), and writes its items coalesced from LDS.
+// 8-bit digits, per pass: tile digit counts, a two-level scan of the counts
+// (no inter-workgroup hand-off inside any launch), and a stable LDS-staged
+// scatter whose tile ranks come from wave64 ballot matching.
 #pragma once
 
 #include "fh_common.h"
@@ -18,8 +14,9 @@ constexpr int kSortItems = 16;
 constexpr int kSortTile = kSortThreads * kSortItems;  // 4096
 
 struct SortWorkspace {
-  DBuf<uint32_t> meta;  // [hist: 8*256][ctr: 16][status: passes*tiles*256]
+  DBuf<uint32_t> meta;  // [tile digit counts: tiles*256][group sums: groups*256]
   size_t meta_words(size_t n, int passes) const;
+  void prepare(size_t tiles, int passes, hipStream_t s);
 };
 
 // Sorts n pairs stably by the low `key_bits` bits of the key.  vals_in ==
@@ -31,8 +28,5 @@ void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va,
                 K *kb, uint32_t *vb, size_t n, int key_bits, SortWorkspace &ws,
                 hipStream_t s, K **kout, uint32_t **vout);
 
-// Device error word of the last sort (look-back spin timeout); 0 = ok.
-// Lives at meta[8*256 + 8].
-constexpr int kSortErrWord = 8 * 256 + 8;
 
 }  // namespace fh

@@ -50,10 +50,35 @@ class Engine:
                                           L.ptr(proc), L.ptr(tim)))
         self.n, self.k = stream.n, stream.k
 
+    def stage_many(self, batches, nproc: int = 5):
+        """Stage a list of equally sized Streams; each run() processes the next."""
+        first = batches[0]
+        views = 0 if first.fq_proc is None else first.fq_proc.shape[1]
+        d = L.fh_stream_desc(n=first.n, keys_per_cmd=first.k, views=views,
+                             nproc=nproc if views else 0, pad=0)
+        assert all(b.n == first.n and b.k == first.k for b in batches)
+        dots = np.ascontiguousarray(np.concatenate([b.dots for b in batches]), dtype=np.uint64)
+        keys = np.ascontiguousarray(np.concatenate([b.keys for b in batches]), dtype=np.uint64)
+        proc = tim = None
+        if views:
+            proc = np.ascontiguousarray(np.concatenate([b.fq_proc for b in batches]), np.uint8)
+            tim = np.ascontiguousarray(np.concatenate([b.fq_time for b in batches]), np.uint64)
+        L.check(self._lib.fh_engine_stage_many(self._h, C.byref(d), len(batches), L.ptr(dots),
+                                               L.ptr(keys), L.ptr(proc), L.ptr(tim)))
+        self.n, self.k = first.n, first.k
+
     def run(self, sync: bool = True) -> float:
         ms = C.c_float(0)
         L.check(self._lib.fh_engine_run(self._h, C.byref(ms) if sync else None))
         return float(ms.value)
+
+    def set_probe(self, kernel):
+        L.check(self._lib.fh_engine_set_probe(self._h, kernel.encode() if kernel else None))
+
+    def probe_stats(self):
+        ms, n, b = C.c_float(0), C.c_size_t(0), C.c_double(0)
+        L.check(self._lib.fh_engine_probe_stats(self._h, C.byref(ms), C.byref(n), C.byref(b)))
+        return float(ms.value), int(n.value), float(b.value)
 
     def kernel_times(self):
         n = C.c_size_t(0)

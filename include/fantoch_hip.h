@@ -182,7 +182,15 @@ fh_status fh_engine_reset(fh_engine *h);
 fh_status fh_engine_stage(fh_engine *h, const fh_stream_desc *desc,
                           const uint64_t *dot, const uint64_t *key_id,
                           const uint8_t *fq_proc, const uint64_t *fq_time);
-/* Run the staged batch on the device (inputs already resident).  If
+/* Stage `nbatches` consecutive batches of desc->n commands each (arrays hold
+ * nbatches * n commands, batch-major).  Each fh_engine_run processes the next
+ * staged batch, carrying KeyDeps and executed-clock state from the previous
+ * one (a committed stream fed batch by batch). */
+fh_status fh_engine_stage_many(fh_engine *h, const fh_stream_desc *desc,
+                               size_t nbatches, const uint64_t *dot,
+                               const uint64_t *key_id, const uint8_t *fq_proc,
+                               const uint64_t *fq_time);
+/* Run the next staged batch on the device (inputs already resident).  If
  * device_ms is non-NULL the stream is synchronised and the device time of
  * the run (HIP events on the engine's stream) is returned. */
 fh_status fh_engine_run(fh_engine *h, float *device_ms);
@@ -199,6 +207,13 @@ fh_status fh_engine_results(fh_engine *h, uint32_t *dep_off, uint64_t *dep_dot,
  * names/ms arrays of length cap; *len = number of recorded kernels. */
 fh_status fh_engine_kernel_times(fh_engine *h, const char **names, float *ms,
                                  size_t cap, size_t *len);
+/* Roofline probe: record HIP events (on the engine's stream) around every
+ * launch of one kernel during subsequent runs ("onesweep" = the key+value
+ * radix passes, "sv_deps", "sv_tails"; NULL = off), then report its average
+ * device duration and the algorithmic bytes one launch moves. */
+fh_status fh_engine_set_probe(fh_engine *h, const char *kernel);
+fh_status fh_engine_probe_stats(fh_engine *h, float *avg_ms, size_t *launches,
+                                double *bytes_per_launch);
 /* Enable/disable per-kernel event timing (adds events between kernels). */
 fh_status fh_engine_set_profiling(fh_engine *h, int on);
 

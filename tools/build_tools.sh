@@ -1,0 +1,7 @@
+#!/bin/bash
+# Builds the standalone tool binaries against the in-tree library.
+set -e
+cd "$(dirname "$0")/.."
+python -m fantoch_amd.build
+/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ifantoch_amd/csrc \
+  tools/sortbench.hip -o tools/sortbench -Lfantoch_amd -lfantoch_hip -Wl,-rpath,'$ORIGIN/../fantoch_amd'
