@@ -56,33 +56,11 @@ def parse():
 
 
 def shard_batches(args, rank, world, nbatches):
-    """The rank's key shard of the global stream, re-sequenced per shard."""
-    from fantoch_amd.workload import Workload, Stream
+    """The rank's key shard of the global C2 stream (fantoch_amd/shard.py)."""
+    from fantoch_amd.shard import shard_batches as sb
+    from fantoch_amd.workload import Workload
     w = Workload.zipf(args.zipf, args.keys, k=1, seed=args.seed, n=5)
-    per = args.batch
-    out = []
-    first = 0
-    carry_k = []
-    local_count = 0
-    while len(out) < nbatches:
-        s = w.generate(per * world, first=first)
-        first += per * world
-        keys = s.keys[:, 0]
-        mine = keys % np.uint64(world) == np.uint64(rank)
-        carry_k.append((keys[mine] // np.uint64(world)).astype(np.uint64))
-        allk = np.concatenate(carry_k)
-        while len(allk) >= per and len(out) < nbatches:
-            kk = allk[:per]
-            allk = allk[per:]
-            idx = np.arange(local_count, local_count + per, dtype=np.uint64)
-            local_count += per
-            src = np.uint64(rank * 5 + 1) + idx % np.uint64(5)   # shard processes
-            seq = idx // np.uint64(5) + np.uint64(1)
-            dots = (src << np.uint64(56)) | seq
-            out.append(Stream(dots, kk.reshape(-1, 1).copy(), None, None,
-                              (args.keys + world - 1) // world))
-        carry_k = [allk]
-    return out
+    return sb(w, rank, world, args.batch, nbatches)
 
 
 def pmc_traffic(kernel):

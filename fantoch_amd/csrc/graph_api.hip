@@ -1,0 +1,382 @@
+// graph_api.hip -- the GraphExecutor drop-in (fh_graph_*).
+//
+// DependencyGraph semantics (fantoch_ps/src/executor/graph/mod.rs:45-679) for
+// batches of GraphExecutionInfo::Add: vertices = carried pending vertices
+// (earlier arrivals) + the batch; dependency dots resolve to vertex ids by a
+// device sort of the vertex dots and binary search; a dependency that is
+// neither a vertex nor executed is missing (the vertex stays pending, exactly
+// like TarjanSCCFinder's MissingDependencies, tarjan.rs:150-170, and the
+// PendingIndex retry, mod.rs:558-644); SCCs, execution order and per-key
+// order come from GraphCore on the device.  The executed clock is an
+// AEClock<ProcessId> (frontier + exceptions, threshold crate) kept on the
+// host and mirrored to the device per batch.
+#include <algorithm>
+#include <deque>
+#include <unordered_set>
+#include <vector>
+
+#include "graph_core.h"
+
+namespace fh {
+namespace {
+
+constexpr unsigned B = 256;
+#define GRID_STRIDE(i, n) \
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
+
+__device__ __forceinline__ bool executed_dev(uint64_t d, const uint64_t *__restrict__ frontier,
+                                             const uint64_t *__restrict__ exc, uint32_t nexc) {
+  if ((d & 0x00FFFFFFFFFFFFFFull) <= frontier[d >> 56]) return true;
+  uint32_t lo = 0, hi = nexc;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (exc[mid] < d)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < nexc && exc[lo] == d;
+}
+
+__device__ __forceinline__ int64_t find_vid(uint64_t d, const uint64_t *__restrict__ sd,
+                                            const uint32_t *__restrict__ sv, uint32_t V) {
+  uint32_t lo = 0, hi = V;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sd[mid] < d)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return (lo < V && sd[lo] == d) ? int64_t(sv[lo]) : -1;
+}
+
+__global__ void k_dup_check(uint32_t V, const uint64_t *__restrict__ sd, uint32_t *err) {
+  GRID_STRIDE(j, V) {
+    if (j > 0 && sd[j] == sd[j - 1]) atomicOr(err, 1u);
+  }
+}
+
+// per vertex: count resolved edges, flag missing dependencies
+// (tarjan.rs:131-170: self and executed deps are ignored)
+__global__ void k_resolve_count(uint32_t V, const uint64_t *__restrict__ dot,
+                                const uint32_t *__restrict__ doff, const uint64_t *__restrict__ ddot,
+                                const uint64_t *__restrict__ sd, const uint32_t *__restrict__ sv,
+                                const uint64_t *__restrict__ frontier,
+                                const uint64_t *__restrict__ exc, uint32_t nexc,
+                                uint32_t *__restrict__ cnt, uint8_t *__restrict__ blocked0) {
+  GRID_STRIDE(v, V) {
+    uint32_t c = 0;
+    bool missing = false;
+    const uint64_t self = dot[v];
+    for (uint32_t e = doff[v]; e < doff[v + 1]; e++) {
+      const uint64_t d = ddot[e];
+      if (d == self || executed_dev(d, frontier, exc, nexc)) continue;
+      if (find_vid(d, sd, sv, V) >= 0)
+        c++;
+      else
+        missing = true;
+    }
+    cnt[v] = c;
+    blocked0[v] = missing;
+  }
+}
+
+__global__ void k_resolve_fill(uint32_t V, const uint64_t *__restrict__ dot,
+                               const uint32_t *__restrict__ doff, const uint64_t *__restrict__ ddot,
+                               const uint64_t *__restrict__ sd, const uint32_t *__restrict__ sv,
+                               const uint64_t *__restrict__ frontier,
+                               const uint64_t *__restrict__ exc, uint32_t nexc,
+                               const uint32_t *__restrict__ off, uint32_t *__restrict__ dst) {
+  GRID_STRIDE(v, V) {
+    uint32_t o = off[v];
+    const uint64_t self = dot[v];
+    for (uint32_t e = doff[v]; e < doff[v + 1]; e++) {
+      const uint64_t d = ddot[e];
+      if (d == self || executed_dev(d, frontier, exc, nexc)) continue;
+      const int64_t u = find_vid(d, sd, sv, V);
+      if (u >= 0) dst[o++] = uint32_t(u);
+    }
+  }
+}
+
+}  // namespace
+
+// AEClock<ProcessId>: per-process contiguous frontier + exception set.
+struct AEClock {
+  uint64_t frontier[256] = {0};
+  std::unordered_set<uint64_t> exc;
+  bool contains(uint64_t d) const {
+    return (d & 0x00FFFFFFFFFFFFFFull) <= frontier[d >> 56] || exc.count(d);
+  }
+  void add(uint64_t d) {
+    const uint32_t s = uint32_t(d >> 56);
+    const uint64_t q = d & 0x00FFFFFFFFFFFFFFull;
+    if (q <= frontier[s]) return;
+    if (q == frontier[s] + 1) {
+      frontier[s] = q;
+      while (!exc.empty()) {
+        auto it = exc.find(make_dot(s, frontier[s] + 1));
+        if (it == exc.end()) break;
+        exc.erase(it);
+        frontier[s]++;
+      }
+    } else {
+      exc.insert(d);
+    }
+  }
+};
+
+struct GraphDevice {
+  uint32_t process_id;
+  uint64_t shard_id;
+  fh_config cfg;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int key_bits = 1;
+  AEClock clock;
+  // carried pending vertices (arrival order)
+  std::vector<uint64_t> p_dot, p_keys, p_deps;
+  std::vector<uint32_t> p_koff{0}, p_doff{0};
+  // drain queue
+  std::deque<std::pair<uint64_t, uint64_t>> ready;
+  std::vector<uint64_t> missing_now;
+  // device buffers
+  DBuf<uint64_t> d_dot, d_ddot, d_sd, d_sd2, d_frontier, d_exc;
+  DBuf<uint32_t> d_koff, d_key32, d_doff, d_cnt, d_off, d_dst, d_sv, d_sv2, d_err;
+  DBuf<uint8_t> d_blocked0;
+  SortWorkspace sort_ws;
+  ScanWorkspace scan_ws;
+  GraphCore core;
+
+  GraphDevice(uint32_t pid, uint64_t sid, const fh_config &c) : process_id(pid), shard_id(sid), cfg(c) {
+    FH_CHECK(c.key_space >= 1 && c.key_space <= (uint64_t(1) << 31), FH_EINVAL,
+             "key_space must be in [1, 2^31]");
+    key_bits = bits_for(c.key_space);
+    device = pick_device(&c, sid);
+    FH_HIP(hipSetDevice(device));
+    FH_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    core.stream = stream;
+    d_err.ensure(4);
+    d_frontier.ensure(256);
+  }
+  ~GraphDevice() {
+    (void)hipSetDevice(device);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+
+  void add_batch(size_t n, const uint64_t *dot, const uint32_t *key_off, const uint64_t *key_id,
+                 const uint32_t *dep_off, const uint64_t *dep_dot) {
+    FH_CHECK(n == 0 || (dot && key_off && dep_off), FH_EINVAL, "null argument");
+    FH_HIP(hipSetDevice(device));
+    // vertices: carried pending (earlier arrivals) then the batch
+    const size_t P = p_dot.size();
+    const size_t V = P + n;
+    FH_CHECK(V < (size_t(1) << 30), FH_EINVAL, "too many vertices");
+    std::vector<uint64_t> vdot(p_dot);
+    vdot.insert(vdot.end(), dot, dot + n);
+    std::vector<uint32_t> koff(p_koff), doff(p_doff);
+    std::vector<uint64_t> keys(p_keys), deps(p_deps);
+    for (size_t i = 0; i < n; i++) {
+      for (uint32_t e = key_off[i]; e < key_off[i + 1]; e++) {
+        FH_CHECK(key_id[e] < cfg.key_space, FH_EINVAL, "key id >= key_space");
+        keys.push_back(key_id[e]);
+      }
+      koff.push_back(uint32_t(keys.size()));
+      deps.insert(deps.end(), dep_dot + dep_off[i], dep_dot + dep_off[i + 1]);
+      doff.push_back(uint32_t(deps.size()));
+    }
+    if (V == 0) return;
+    std::vector<uint32_t> k32(keys.begin(), keys.end());
+    // executed clock mirror
+    std::vector<uint64_t> exc(clock.exc.begin(), clock.exc.end());
+    std::sort(exc.begin(), exc.end());
+    FH_HIP(hipMemcpyAsync(d_frontier.get(), clock.frontier, sizeof(clock.frontier),
+                          hipMemcpyHostToDevice, stream));
+    uint64_t *dexc = d_exc.ensure(exc.size() + 1);
+    if (!exc.empty())
+      FH_HIP(hipMemcpyAsync(dexc, exc.data(), exc.size() * sizeof(uint64_t),
+                            hipMemcpyHostToDevice, stream));
+    uint64_t *ddot_v = d_dot.ensure(V);
+    FH_HIP(hipMemcpyAsync(ddot_v, vdot.data(), V * sizeof(uint64_t), hipMemcpyHostToDevice,
+                          stream));
+    uint32_t *dko = d_koff.ensure(V + 1);
+    FH_HIP(hipMemcpyAsync(dko, koff.data(), (V + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          stream));
+    uint32_t *dk = d_key32.ensure(k32.size() + 1);
+    if (!k32.empty())
+      FH_HIP(hipMemcpyAsync(dk, k32.data(), k32.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                            stream));
+    uint32_t *ddo = d_doff.ensure(V + 1);
+    FH_HIP(hipMemcpyAsync(ddo, doff.data(), (V + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          stream));
+    uint64_t *dd = d_ddot.ensure(deps.size() + 1);
+    if (!deps.empty())
+      FH_HIP(hipMemcpyAsync(dd, deps.data(), deps.size() * sizeof(uint64_t),
+                            hipMemcpyHostToDevice, stream));
+    // dot -> vid index
+    uint64_t *sd = nullptr;
+    uint32_t *sv = nullptr;
+    sort_pairs<uint64_t>(ddot_v, nullptr, d_sd.ensure(V), d_sv.ensure(V), d_sd2.ensure(V),
+                         d_sv2.ensure(V), V, 64, sort_ws, stream, &sd, &sv);
+    FH_HIP(hipMemsetAsync(d_err.get(), 0, sizeof(uint32_t), stream));
+    k_dup_check<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), sd, d_err.get());
+    uint32_t *cnt = d_cnt.ensure(V + 1);
+    uint8_t *b0 = d_blocked0.ensure(V + 1);
+    k_resolve_count<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), ddot_v, ddo, dd, sd, sv,
+                                                       d_frontier.get(), dexc,
+                                                       uint32_t(exc.size()), cnt, b0);
+    uint32_t *off = d_off.ensure(V + 1);
+    exclusive_scan_u32(cnt, off, V, scan_ws, stream);
+    uint32_t E = 0, dup = 0;
+    FH_HIP(hipMemcpyAsync(&E, off + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipMemcpyAsync(&dup, d_err.get(), sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    // mod.rs:235-240: indexing an already indexed dot panics
+    FH_CHECK(dup == 0, FH_EINVARIANT, "Graph::handle_add tried to index already indexed dot");
+    uint32_t *dst = d_dst.ensure(E + 1);
+    k_resolve_fill<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), ddot_v, ddo, dd, sd, sv,
+                                                      d_frontier.get(), dexc,
+                                                      uint32_t(exc.size()), off, dst);
+    GraphInput gin;
+    gin.V = uint32_t(V);
+    gin.off = off;
+    gin.dst = dst;
+    gin.blocked0 = b0;
+    gin.dot = ddot_v;
+    gin.k = 0;
+    gin.key_off = dko;
+    gin.key32 = dk;
+    gin.key_bits = key_bits;
+    gin.want_per_key = false;  // the executor's monitor is fed from the drain order
+    GraphOutput out;
+    core.run(gin, out);
+    // results to host
+    std::vector<uint32_t> order(out.nexec);
+    std::vector<uint64_t> label(V);
+    std::vector<uint8_t> blocked(V);
+    if (out.nexec)
+      FH_HIP(hipMemcpyAsync(order.data(), out.exec_order, out.nexec * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipMemcpyAsync(label.data(), out.scc_label, V * sizeof(uint64_t),
+                          hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipMemcpyAsync(blocked.data(), out.blocked, V, hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    for (uint32_t j = 0; j < out.nexec; j++) {
+      const uint32_t v = order[j];
+      ready.emplace_back(vdot[v], label[v]);
+      clock.add(vdot[v]);  // executed clock update (tarjan.rs:296)
+    }
+    // carry pending vertices; record their missing dependencies
+    p_dot.clear();
+    p_keys.clear();
+    p_deps.clear();
+    p_koff.assign(1, 0);
+    p_doff.assign(1, 0);
+    std::unordered_set<uint64_t> present;
+    for (size_t v = 0; v < V; v++)
+      if (blocked[v]) present.insert(vdot[v]);
+    missing_now.clear();
+    std::unordered_set<uint64_t> seen;
+    for (size_t v = 0; v < V; v++) {
+      if (!blocked[v]) continue;
+      p_dot.push_back(vdot[v]);
+      p_keys.insert(p_keys.end(), keys.begin() + koff[v], keys.begin() + koff[v + 1]);
+      p_koff.push_back(uint32_t(p_keys.size()));
+      p_deps.insert(p_deps.end(), deps.begin() + doff[v], deps.begin() + doff[v + 1]);
+      p_doff.push_back(uint32_t(p_deps.size()));
+      for (uint32_t e = doff[v]; e < doff[v + 1]; e++) {
+        const uint64_t d = deps[e];
+        if (d != vdot[v] && !clock.contains(d) && !present.count(d) && seen.insert(d).second)
+          missing_now.push_back(d);
+      }
+    }
+    std::sort(missing_now.begin(), missing_now.end());
+  }
+
+  size_t drain(uint64_t *dots, uint64_t *labels, size_t cap) {
+    size_t c = 0;
+    while (!ready.empty() && c < cap) {
+      if (dots) dots[c] = ready.front().first;
+      if (labels) labels[c] = ready.front().second;
+      ready.pop_front();
+      c++;
+    }
+    return c;
+  }
+};
+
+}  // namespace fh
+
+struct fh_graph {
+  fh::GraphDevice dev;
+  fh_graph(uint32_t p, uint64_t s, const fh_config &c) : dev(p, s, c) {}
+};
+
+extern "C" {
+
+fh_status fh_graph_create(uint32_t process_id, uint64_t shard_id, const fh_config *cfg,
+                          fh_graph **out) {
+  FH_API_BEGIN
+  FH_CHECK(cfg && out, FH_EINVAL, "null argument");
+  *out = new fh_graph(process_id, shard_id, *cfg);
+  FH_API_END
+}
+
+fh_status fh_graph_destroy(fh_graph *h) {
+  FH_API_BEGIN
+  delete h;
+  FH_API_END
+}
+
+fh_status fh_graph_add_batch(fh_graph *h, size_t n, const uint64_t *dot, const uint32_t *key_off,
+                             const uint64_t *key_id, const uint32_t *dep_off,
+                             const uint64_t *dep_dot) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.add_batch(n, dot, key_off, key_id, dep_off, dep_dot);
+  FH_API_END
+}
+
+fh_status fh_graph_drain(fh_graph *h, uint64_t *exec_dot, uint64_t *scc_label, size_t cap,
+                         size_t *len) {
+  FH_API_BEGIN
+  FH_CHECK(h && len, FH_EINVAL, "null argument");
+  *len = h->dev.drain(exec_dot, scc_label, exec_dot || scc_label ? cap : 0);
+  FH_API_END
+}
+
+fh_status fh_graph_mark_executed(fh_graph *h, size_t n, const uint64_t *dot) {
+  FH_API_BEGIN
+  FH_CHECK(h && (n == 0 || dot), FH_EINVAL, "null argument");
+  for (size_t i = 0; i < n; i++) h->dev.clock.add(dot[i]);
+  FH_API_END
+}
+
+fh_status fh_graph_set_executed_frontier(fh_graph *h, uint32_t source, uint64_t seq) {
+  FH_API_BEGIN
+  FH_CHECK(h && source < 256, FH_EINVAL, "bad argument");
+  h->dev.clock.frontier[source] = seq;
+  FH_API_END
+}
+
+fh_status fh_graph_pending(fh_graph *h, size_t *count) {
+  FH_API_BEGIN
+  FH_CHECK(h && count, FH_EINVAL, "null argument");
+  *count = h->dev.p_dot.size();
+  FH_API_END
+}
+
+fh_status fh_graph_missing(fh_graph *h, uint64_t *dots, size_t cap, size_t *len) {
+  FH_API_BEGIN
+  FH_CHECK(h && len, FH_EINVAL, "null argument");
+  const auto &m = h->dev.missing_now;
+  *len = m.size();
+  for (size_t i = 0; i < m.size() && i < cap && dots; i++) dots[i] = m[i];
+  FH_API_END
+}
+
+}  // extern "C"

@@ -55,6 +55,7 @@ struct GraphInput {
   const uint32_t *sorted_keys = nullptr;  // [M]
   const uint32_t *sorted_vid = nullptr;   // [M] vid of each sorted element
   bool no_forward_hint = false;           // edges all point backwards
+  bool want_per_key = true;               // build the per-key sequence
 };
 
 struct GraphOutput {

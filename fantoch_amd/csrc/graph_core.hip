@@ -529,6 +529,7 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   out.nexec = nexec;
   out.npending = V - nexec;
   mark("exec_order");
+  if (!in.want_per_key) return;
   // per-key sequence: elements in exec order, stable-sorted by key
   uint32_t *ec = cnt.ensure(nexec + 1);
   uint32_t *ep = pos.ensure(nexec + 1);

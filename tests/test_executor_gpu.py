@@ -1,0 +1,138 @@
+"""HipGraphExecutor (fh_graph_*) -- the GraphExecutor drop-in -- against the
+reference's known-answer tests (executor/graph/mod.rs:716-1350) and against
+the oracle's incremental DependencyGraph on shuffled arrival orders."""
+import itertools
+import random
+
+import numpy as np
+import pytest
+
+from conftest import D, load_golden
+from fantoch_amd.command import Command
+from fantoch_amd.executor import GraphExecutionInfo, HipGraphExecutor
+from fantoch_amd.workload import Workload
+from oracle import oracle as O
+from test_oracle_golden import random_adds
+
+pytestmark = pytest.mark.gpu
+
+
+def check_termination(n, args, batch=1):
+    """graph/mod.rs:1047-1115 through the HIP executor (per-call handle when
+    batch == 1, handle_batch otherwise)."""
+    ex = HipGraphExecutor(process_id=1, shard_id=0, n=n, f=1, key_space=64)
+    infos = []
+    for a in args:
+        dot = D(a["dot"])
+        keys = a["keys"] if a["keys"] is not None else ["CONF"]
+        infos.append(GraphExecutionInfo.add(dot, Command(dot, keys), [D(x) for x in a["deps"]]))
+    for i in range(0, len(infos), batch):
+        if batch == 1:
+            ex.handle(infos[i])
+        else:
+            ex.handle_batch(infos[i:i + batch])
+    assert ex.pending() == 0, "every command executes exactly once"
+    out = ex.monitor()
+    assert sum(len(v) for v in out.values()) == sum(len(a["keys"] or ["CONF"]) for a in args)
+    return out
+
+
+def test_simple():
+    g = load_golden("graph_simple.json")
+    ex = HipGraphExecutor(g["process_id"], g["shard_id"], g["n"], g["f"], key_space=8)
+    order = []
+    for a in g["adds"]:
+        dot = D(a["dot"])
+        ex.handle(GraphExecutionInfo.add(dot, Command(dot, a["keys"]), [D(x) for x in a["deps"]]))
+        got = []
+        while (r := ex.to_clients()) is not None:
+            got.append(r[0])
+        assert got == [D(x) for x in a["expect_executed"]]
+
+
+@pytest.mark.parametrize("batch", [1, 3])
+def test_cycle_all_permutations(batch):
+    g = load_golden("graph_cycle.json")
+    want = {k: [D(x) for x in v] for k, v in g["expect_order"].items()}
+    for perm in itertools.permutations(g["args"]):
+        assert check_termination(g["n"], list(perm), batch) == want
+
+
+@pytest.mark.parametrize("name", ["regression_1.json", "regression_2.json"])
+def test_transitive_conflicts_regressions(name):
+    g = load_golden(name)
+    a = check_termination(g["n"], g["order_a"])
+    b = check_termination(g["n"], g["order_b"])
+    assert a != b
+    assert a == {k: [D(x) for x in v] for k, v in g["derived_order_a"].items()}
+    assert b == {k: [D(x) for x in v] for k, v in g["derived_order_b"].items()}
+
+
+def test_sccs_found_and_missing_dep():
+    g = load_golden("sccs_found_and_missing_dep.json")
+    ex = HipGraphExecutor(g["process_id"], g["shard_id"], g["n"], g["f"], key_space=8)
+    for i, seq in enumerate(g["executed_clock"]):
+        ex.set_executed_frontier(i + 1, seq)
+    infos = [GraphExecutionInfo.add(D(v["dot"]), Command(D(v["dot"]), g["keys"]),
+                                    [D(x) for x in v["deps"]]) for v in g["vertices"]]
+    ex.handle_batch(infos)
+    got = []
+    while (r := ex.to_clients()) is not None:
+        got.append(r[0])
+    assert got == [D([4, s]) for s in range(31, 41)]  # the SCCs found are executed
+    assert ex.pending() == 1                           # the root stays pending
+    assert ex.missing() == [D(x) for x in g["expect"]["missing"]]
+    # RequestReply::Executed for the missing dependency (mod.rs:397-405) marks
+    # it executed; the next batch retries the pending vertex, which executes
+    ex.mark_executed([D([5, 61])])
+    ex.handle_batch([])
+    assert ex.pending() == 0
+    assert ex.to_clients()[0] == D([5, 70])
+
+
+@pytest.mark.parametrize("it", range(10))
+@pytest.mark.parametrize("batch", [1, 2, 6])
+def test_add_random_all_permutations(it, batch):
+    rng = random.Random(0xFA17 + it)
+    args = random_adds(rng, 2, 3)
+    total = check_termination(2, args, batch)
+    perms = list(itertools.permutations(args))
+    for perm in (perms if batch == 1 else perms[::37]):
+        assert check_termination(2, list(perm), batch) == total
+
+
+@pytest.mark.parametrize("batch", [1, 7, 500, 4000])
+def test_views_stream_shuffled_arrivals_match_oracle(batch):
+    """Committed deps from replica views, delivered to the executor in a
+    shuffled commit order and in batches: per-key order equals the oracle's
+    incremental executor on the same arrival order."""
+    s = Workload.zipf(0.99, 512, k=2, views=3, window=64, seed=17).generate(4000)
+    key_off = s.key_off()
+    keys = s.keys.reshape(-1)
+    dep_off, deps = O.views_run(0, 5, s.dots, key_off, keys, s.fq_proc, s.fq_time)
+    # commit arrival: stream order perturbed within a window
+    rng = np.random.default_rng(3)
+    arrival = np.argsort(np.arange(s.n) + rng.integers(0, 200, size=s.n), kind="stable")
+    a_dots = s.dots[arrival]
+    a_keys = s.keys[arrival]
+    a_key_off = (np.arange(s.n + 1) * s.k).astype(np.uint32)
+    a_dep_off = np.zeros(s.n + 1, dtype=np.uint32)
+    a_deps = []
+    for j, i in enumerate(arrival):
+        a_deps.extend(deps[dep_off[i]:dep_off[i + 1]])
+        a_dep_off[j + 1] = len(a_deps)
+    a_deps = np.asarray(a_deps, dtype=np.uint64)
+    ex_o, lab_o, kso, ks = O.graph_run(a_dots, a_key_off, a_keys.reshape(-1), a_dep_off, a_deps,
+                                       s.key_space)
+    want = {int(k): ks[kso[k]:kso[k + 1]].tolist() for k in np.nonzero(np.diff(kso))[0]}
+    ex = HipGraphExecutor(1, 0, 5, 1, key_space=s.key_space)
+    for b0 in range(0, s.n, batch):
+        infos = [GraphExecutionInfo.add(int(a_dots[j]), [int(x) for x in a_keys[j]],
+                                        a_deps[a_dep_off[j]:a_dep_off[j + 1]].tolist())
+                 for j in range(b0, min(s.n, b0 + batch))]
+        ex.handle_batch(infos)
+    assert ex.pending() == 0
+    got = {k: v for k, v in ex.monitor().items()}
+    assert got == want
+    # SCC partition equals the oracle's
+    assert ex.last_labels == dict(zip(ex_o.tolist(), lab_o.tolist()))
