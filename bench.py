@@ -65,7 +65,7 @@ def shard_batches(args, rank, world, nbatches):
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, written by profiles/collect_pmc.py from
+    (profiles/pmc_traffic.json, written by tools/collect_pmc.py from
     separate FETCH_SIZE / WRITE_SIZE passes of this same command), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:

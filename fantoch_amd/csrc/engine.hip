@@ -531,17 +531,18 @@ struct EngineDevice {
       const unsigned g = unsigned((M + 255) / 256);
       {
         // read key + vid (8), write the dependency (8)
-        ProbeScope probe("sv_deps", stream, double(M) * 16.0);
-        k_sv_deps<<<g, 256, 0, stream>>>(M, ks, vs, latest.get(), dsorted);
+        probed_launch("sv_deps", double(M) * 16.0, k_sv_deps, dim3(g), dim3(256), stream, M,
+                      (const uint32_t *)ks, (const uint32_t *)vs, (const uint64_t *)latest.get(),
+                      dsorted);
       }
       mark("deps");
       {
         // read key (4) and the batch dot (8)
-        ProbeScope probe("sv_tails", stream, double(M) * 12.0);
         const unsigned gt = unsigned((M + kTailTile - 1) / kTailTile);
-        k_sv_tails<<<gt, 256, 0, stream>>>(
-            M, ks, vs, bdot, latest.get(), reinterpret_cast<unsigned long long *>(frontier.get()),
-            excount_ptr());
+        probed_launch("sv_tails", double(M) * 12.0, k_sv_tails, dim3(gt), dim3(256), stream, M,
+                      (const uint32_t *)ks, (const uint32_t *)vs, (const uint64_t *)bdot,
+                      latest.get(), reinterpret_cast<unsigned long long *>(frontier.get()),
+                      excount_ptr());
       }
       mark("tails_and_clock");
       sv_vs = vs;

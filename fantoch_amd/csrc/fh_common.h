@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstddef>
 #include <cstdint>
@@ -90,13 +91,13 @@ struct Probe {
   size_t next = 0;
   double bytes = 0;
   bool on(const char *name) const { return !target.empty() && target == name; }
-  void rec(hipStream_t s) {
+  hipEvent_t take() {
     if (next >= ev.size()) {
       hipEvent_t e;
       FH_HIP(hipEventCreate(&e));
       ev.push_back(e);
     }
-    FH_HIP(hipEventRecord(ev[next++], s));
+    return ev[next++];
   }
   void reset() {
     next = 0;
@@ -108,20 +109,22 @@ struct Probe {
 };
 extern thread_local Probe *t_probe;
 
-struct ProbeScope {
-  bool active;
-  hipStream_t s;
-  ProbeScope(const char *name, hipStream_t st, double bytes) : active(false), s(st) {
-    if (t_probe && t_probe->on(name)) {
-      active = true;
-      t_probe->bytes += bytes;
-      t_probe->rec(s);
-    }
+// Launch `k` on stream `s`; when the thread's probe targets `name`, the launch
+// carries a start/stop event pair via hipExtLaunchKernel, so the recorded
+// interval is the kernel's own dispatch begin/end (the interval rocprofv3's
+// kernel trace reports), not an event-marker bracket around it.
+template <class F, class... Args>
+inline void probed_launch(const char *name, double bytes, F k, dim3 grid, dim3 block,
+                          hipStream_t s, Args... args) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (t_probe && t_probe->on(name)) {
+    t_probe->bytes += bytes;
+    e0 = t_probe->take();
+    e1 = t_probe->take();
   }
-  ~ProbeScope() {
-    if (active) t_probe->rec(s);
-  }
-};
+  hipExtLaunchKernelGGL(k, grid, block, 0, s, e0, e1, 0, args...);
+  FH_HIP(hipGetLastError());
+}
 
 // Device selection per SURVEY §8b (shard -> device, or env override).
 int pick_device(const fh_config *cfg, uint64_t shard_id);

@@ -311,9 +311,10 @@ void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va, 
     } else {
       // algorithmic traffic of a key+value scatter pass: read and write every
       // pair once
-      ProbeScope probe("sort_scatter", s, double(n) * 2.0 * (sizeof(K) + sizeof(uint32_t)));
-      k_down<K, false><<<tiles, kThreads, 0, s>>>(ki, vi, ko, vo, uint32_t(n), shift, counts,
-                                                   gsum, gsize, dbase);
+      probed_launch("sort_scatter", double(n) * 2.0 * (sizeof(K) + sizeof(uint32_t)),
+                    k_down<K, false>, dim3(tiles), dim3(kThreads), s, ki, vi, ko, vo,
+                    uint32_t(n), shift, (const uint32_t *)counts, (const uint32_t *)gsum, gsize,
+                    (const uint32_t *)dbase);
     }
     ki = ko;
     vi = vo;

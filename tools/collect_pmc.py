@@ -1,0 +1,111 @@
+#!/usr/bin/env python
+"""collect_pmc.py -- HBM traffic per launch from rocprofv3 PMC passes.
+
+Reads the counter CSVs of four separate `rocprofv3 --pmc` runs (FETCH_SIZE and
+WRITE_SIZE cannot share a pass on gfx950, MI355X_MICROARCH.md §rocprofv3 PMC
+slots):
+
+  <root>/fetch        rocprofv3 --pmc FETCH_SIZE  -- python3 bench.py ...
+  <root>/write        rocprofv3 --pmc WRITE_SIZE  -- python3 bench.py ...
+  <root>/calib_fetch  rocprofv3 --pmc FETCH_SIZE  -- tools/pmc_calib
+  <root>/calib_write  rocprofv3 --pmc WRITE_SIZE  -- tools/pmc_calib
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  FETCH_SIZE under-reports reads on gfx950
+(½ for 16-B/lane streams; other widths uncalibrated, §HBM), so the
+calibration kernels stream exactly 1 GiB at 4/8/16 B per lane and the
+per-width factor counter/true is measured on the same box.  The engine's
+kernels read and write 4-B-per-lane streams, so their raw bytes are divided
+by the 4-B factors.
+
+Writes profiles/pmc_traffic.json: {probe: {"hbm_bytes_per_launch": ...}, ...},
+which bench.py reports as roofline.traffic.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+from collections import defaultdict
+
+# probe name (fh_engine_set_probe) -> kernel-name pattern
+PROBES = {
+    "sort_scatter": r"k_down<unsigned int, false>",
+    "sort_scatter_iota": r"k_down<unsigned int, true>",
+    "sort_up": r"k_up<unsigned int>",
+    "sort_scan": r"k_scan_fused",
+    "sv_deps": r"k_sv_deps",
+    "sv_tails": r"k_sv_tails",
+}
+CALIB_BYTES = 1 << 30
+
+
+def read_counters(d, counter):
+    """-> {kernel name: [per-dispatch value]} for `counter` under dir `d`."""
+    per = defaultdict(lambda: defaultdict(float))
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    for f in files:
+        with open(f, newline="") as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                key = (f, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                per[row["Kernel_Name"]][key] += float(row["Counter_Value"])
+    return {k: list(v.values()) for k, v in per.items()}
+
+
+def calib(root):
+    out = {}
+    for kind, sub, counter in (("read", "calib_fetch", "FETCH_SIZE"),
+                               ("write", "calib_write", "WRITE_SIZE")):
+        rows = read_counters(os.path.join(root, sub), counter)
+        for name, vals in rows.items():
+            m = re.search(r"calib_(read|write)<(.*)>\s*\(", name)
+            if not m or m.group(1) != kind:
+                continue
+            t = m.group(2)
+            w = 16 if "4u" in t else 8 if "2u" in t else 4
+            vals = sorted(vals)
+            med = vals[len(vals) // 2] * 1024.0
+            out[f"{kind}{w}"] = med / CALIB_BYTES
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
+                                                  "pmc_traffic.json"))
+    ap.add_argument("--command", default="")
+    a = ap.parse_args()
+    cal = calib(a.root)
+    fetch = read_counters(os.path.join(a.root, "fetch"), "FETCH_SIZE")
+    write = read_counters(os.path.join(a.root, "write"), "WRITE_SIZE")
+    rf, wf = cal.get("read4", 1.0), cal.get("write4", 1.0)
+    res = {"_calibration": {"counter_bytes_over_true_bytes": cal,
+                            "note": "1 GiB streams per access width; raw engine counters are "
+                                    "divided by read4 / write4"},
+           "_command": a.command}
+    for probe, pat in PROBES.items():
+        fv = [v for k, vs in fetch.items() if pat in k for v in vs]
+        wv = [v for k, vs in write.items() if pat in k for v in vs]
+        if not fv or not wv:
+            continue
+        fr = sum(fv) / len(fv) * 1024.0
+        wr = sum(wv) / len(wv) * 1024.0
+        res[probe] = {"hbm_bytes_per_launch": fr / rf + wr / wf,
+                      "fetch_bytes_raw": fr, "write_bytes_raw": wr,
+                      "read_bytes_corrected": fr / rf, "write_bytes_corrected": wr / wf,
+                      "launches": [len(fv), len(wv)]}
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    with open(a.out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
