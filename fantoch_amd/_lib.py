@@ -71,6 +71,7 @@ SIGNATURES = {
     "fh_engine_set_profiling": (C.c_int, [V, C.c_int]),
     "fh_engine_set_probe": (C.c_int, [V, C.c_char_p]),
     "fh_engine_probe_stats": (C.c_int, [V, P(C.c_float), P(S), P(C.c_double)]),
+    "fh_engine_probe_stats_for": (C.c_int, [V, C.c_char_p, P(C.c_float), P(S), P(C.c_double)]),
     "fh_workload_key_space": (C.c_uint64, [P(fh_workload)]),
     "fh_workload_generate": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V, V, V]),
 }

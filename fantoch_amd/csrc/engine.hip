@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "graph_core.h"
+#include "keybucket.h"
 
 namespace fh {
 namespace {
@@ -48,7 +49,7 @@ __global__ void k_view_keys(uint32_t M, uint32_t k, uint32_t fq, uint64_t K,
 template <class KT>
 __global__ void k_prev_engine(uint32_t M, const KT *__restrict__ ks, const uint32_t *__restrict__ vs,
                               int tb, uint32_t per_cmd, const uint64_t *__restrict__ latest,
-                              uint32_t *__restrict__ dep_vid,
+                              uint64_t lmul, uint64_t lmask, uint32_t *__restrict__ dep_vid,
                               uint64_t *__restrict__ dep_ext, uint8_t *__restrict__ tail,
                               uint32_t *__restrict__ sorted_vid) {
   GRID_STRIDE(j, M) {
@@ -59,7 +60,7 @@ __global__ void k_prev_engine(uint32_t M, const KT *__restrict__ ks, const uint3
     if (head) {
       // the segment id is the latest-table slot: key, or replica * K + key
       dep_vid[e] = ~0u;
-      dep_ext[e] = latest[uint64_t(seg)];
+      dep_ext[e] = latest[(uint64_t(seg) * lmul) & lmask];
     } else {
       dep_vid[e] = vs[j - 1] / per_cmd;
       dep_ext[e] = 0;
@@ -93,7 +94,8 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
                              const uint32_t *__restrict__ key32, const uint8_t *__restrict__ fq_proc,
                              const uint64_t *__restrict__ dot, const uint32_t *__restrict__ dep_vid,
                              const uint64_t *__restrict__ dep_ext, const uint8_t *__restrict__ tail,
-                             uint64_t *__restrict__ latest, const uint64_t *__restrict__ frontier,
+                             uint64_t *__restrict__ latest, uint64_t lmul, uint64_t lmask,
+                             const uint64_t *__restrict__ frontier,
                              uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ dep_cnt,
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked) {
@@ -124,7 +126,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
       if (tail[e]) {
         const uint32_t j = t / k, s = t % k;
         const uint64_t slot = fq_proc ? uint64_t(fq_proc[i * fq + j]) * K + key32[i * k + s]
-                                      : uint64_t(key32[i * k + s]);
+                                      : (uint64_t(key32[i * k + s]) * lmul) & lmask;
         latest[slot] = self;
       }
     }
@@ -148,7 +150,8 @@ __device__ __forceinline__ uint64_t enc_vid(uint32_t v) { return uint64_t(v) + 1
 
 __global__ void __launch_bounds__(256)
     k_sv_deps(uint32_t M, const uint32_t *__restrict__ ks, const uint32_t *__restrict__ vs,
-              const uint64_t *__restrict__ latest, uint64_t *__restrict__ dep_sorted) {
+              const uint64_t *__restrict__ latest, uint32_t lmul, uint32_t lmask,
+              uint64_t *__restrict__ dep_sorted) {
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const bool ok = j < M;
@@ -164,7 +167,7 @@ __global__ void __launch_bounds__(256)
   const bool head = j == 0 || pkey != key;
   // sequential.rs:83-96: the previous command on the key, or the latest
   // command on it from an earlier batch
-  dep_sorted[j] = head ? latest[key] : enc_vid(pvid);
+  dep_sorted[j] = head ? latest[(key * lmul) & lmask] : enc_vid(pvid);
 }
 
 // Per-source {min, max, count} of a wave's dots: the lanes holding one source
@@ -208,8 +211,9 @@ constexpr int kTailTile = 256 * kTailItems;
 
 __global__ void __launch_bounds__(256)
     k_sv_tails(uint32_t M, const uint32_t *__restrict__ ks, const uint32_t *__restrict__ vs,
-               const uint64_t *__restrict__ dot, uint64_t *__restrict__ latest,
-               unsigned long long *__restrict__ frontier, unsigned long long *__restrict__ excount) {
+               const uint64_t *__restrict__ dot, uint64_t *__restrict__ latest, uint32_t lmul,
+               uint32_t lmask, unsigned long long *__restrict__ frontier,
+               unsigned long long *__restrict__ excount) {
   __shared__ unsigned long long s_mx[256];
   __shared__ unsigned int s_cnt[256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -236,7 +240,7 @@ __global__ void __launch_bounds__(256)
     const uint32_t nxt = __shfl(key[i + 1], 0, 64);
     if (lane == 63) nk = nxt;
     if (j < M) {
-      if (j + 1 == M || nk != key[i]) latest[key[i]] = dot[vs[j]];  // sequential.rs:88-95
+      if (j + 1 == M || nk != key[i]) latest[(key[i] * lmul) & lmask] = dot[vs[j]];  // :88-95
       const uint32_t src = uint32_t(d[i] >> 56);
       atomicMax(&s_mx[src], d[i] & 0x00FFFFFFFFFFFFFFull);
       atomicAdd(&s_cnt[src], 1u);
@@ -306,6 +310,23 @@ __global__ void k_frontier_update(const unsigned long long *__restrict__ mn,
   }
 }
 
+// per-key sequence in key-grouped (not key-ascending) order -> ascending
+// layout: the first position of each key's run, then every element moves to
+// off[key] + (its position - the run's first position)
+__global__ void k_run_heads(uint32_t m, const uint32_t *__restrict__ keys, uint32_t *__restrict__ hp) {
+  GRID_STRIDE(j, m) if (j == 0 || keys[j - 1] != keys[j]) hp[keys[j]] = j;
+}
+
+__global__ void k_run_scatter(uint32_t m, const uint32_t *__restrict__ keys,
+                              const uint32_t *__restrict__ vids, const uint32_t *__restrict__ hp,
+                              const uint32_t *__restrict__ off, const uint64_t *__restrict__ dot,
+                              uint64_t *__restrict__ out) {
+  GRID_STRIDE(j, m) {
+    const uint32_t k = keys[j];
+    out[off[k] + (j - hp[k])] = dot[vids[j]];
+  }
+}
+
 __global__ void k_cnt_nonzero(uint32_t n, const uint64_t *__restrict__ d, uint32_t *__restrict__ c) {
   GRID_STRIDE(i, n) c[i] = d[i] != 0;
 }
@@ -340,6 +361,14 @@ struct EngineDevice {
   uint64_t key_space = 0;
   int key_bits = 1;
   uint32_t n_config = 0;
+  // single-view latest table: indexed by the mapped key (keybucket.h) over a
+  // region of kp = 2^key_bits entries; replica slots follow it
+  bool lat_mapped = false;
+  uint64_t kp = 0;
+  uint32_t lmul = 1, lmask = 0xFFFFFFFFu;
+  KeyBucketWorkspace kb_ws;
+  bool bucket_order = false;  // single-view per-key runs are key-grouped, not ascending
+  DBuf<uint32_t> key_hist, key_offs, headpos;
   // persistent state
   DBuf<uint64_t> latest;     // [(nproc+1) * K]
   DBuf<uint64_t> frontier;   // [256] executed-clock frontier per source
@@ -389,6 +418,13 @@ struct EngineDevice {
     key_space = cfg.key_space;
     key_bits = bits_for(key_space);
     n_config = cfg.n;
+    lat_mapped = key_bits <= 22;
+    kp = key_space;
+    if (lat_mapped) {
+      uint32_t kinv = 0;
+      keybucket_map(key_bits, &lmul, &kinv, &lmask);
+      kp = uint64_t(1) << key_bits;
+    }
     device = pick_device(&cfg, 0);
     FH_HIP(hipSetDevice(device));
     FH_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -422,19 +458,22 @@ struct EngineDevice {
     marks.push_back({name, e});
   }
 
+  // [single view: kp][replica 1: K][replica 2: K]...
+  size_t latest_words(uint32_t slots) const { return size_t(kp) + size_t(slots - 1) * key_space; }
+  // replica r's entry for key is views_latest()[r * K + key] (r >= 1)
+  uint64_t *views_latest() { return latest.get() + (kp - key_space); }
+
   void ensure_latest(uint32_t slots) {
     if (latest.get() && slots <= latest_slots) return;
     latest_slots = std::max<uint32_t>(slots, 1);
-    latest.ensure(size_t(latest_slots) * key_space);
-    FH_HIP(hipMemsetAsync(latest.get(), 0, size_t(latest_slots) * key_space * sizeof(uint64_t),
-                          stream));
+    latest.ensure(latest_words(latest_slots));
+    FH_HIP(hipMemsetAsync(latest.get(), 0, latest_words(latest_slots) * sizeof(uint64_t), stream));
   }
 
   void reset() {
     FH_HIP(hipSetDevice(device));
     ensure_latest(latest_slots);
-    FH_HIP(hipMemsetAsync(latest.get(), 0, size_t(latest_slots) * key_space * sizeof(uint64_t),
-                          stream));
+    FH_HIP(hipMemsetAsync(latest.get(), 0, latest_words(latest_slots) * sizeof(uint64_t), stream));
     FH_HIP(hipMemsetAsync(frontier.get(), 0, 256 * sizeof(uint64_t), stream));
     FH_HIP(hipMemsetAsync(excount_ptr(), 0, 256 * sizeof(unsigned long long), stream));
     FH_HIP(hipMemsetAsync(err.get(), 0, 4 * sizeof(uint32_t), stream));
@@ -514,7 +553,7 @@ struct EngineDevice {
     struct ProbeGuard {
       ProbeGuard(Probe *p) { t_probe = p; }
       ~ProbeGuard() { t_probe = nullptr; }
-    } probe_guard(probe.target.empty() ? nullptr : &probe);
+    } probe_guard(probe.slots.empty() ? nullptr : &probe);
     uint32_t *vs = nullptr;
     uint32_t *dvid = dep_vid.ensure(M + 1);
     uint64_t *dext = dep_ext.ensure(M + 1);
@@ -523,33 +562,46 @@ struct EngineDevice {
     sorted_keys32 = nullptr;
     if (!views && k == 1) {
       uint32_t *ks = nullptr;
-      sort_pairs<uint32_t>(bkey, nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
-                           sk32b.ensure(M + 1), svb.ensure(M + 1), M, key_bits, sort_ws, stream,
-                           &ks, &vs);
-      mark("keydeps_sort");
       uint64_t *dsorted = dep_ext.ensure(M + 1);
-      const unsigned g = unsigned((M + 255) / 256);
-      {
-        // read key + vid (8), write the dependency (8)
-        probed_launch("sv_deps", double(M) * 16.0, k_sv_deps, dim3(g), dim3(256), stream, M,
-                      (const uint32_t *)ks, (const uint32_t *)vs, (const uint64_t *)latest.get(),
-                      dsorted);
+      const KeyBucketPlan plan = lat_mapped ? keybucket_plan(M, key_bits) : KeyBucketPlan();
+      if (plan.ok) {
+        // two launches: tile partition by key bucket, per-bucket order + deps
+        ks = sk32a.ensure(M + 1);
+        vs = sva.ensure(M + 1);
+        keybucket_run(plan, M, bkey, bdot, latest.get(),
+                      reinterpret_cast<unsigned long long *>(frontier.get()), excount_ptr(),
+                      kb_ws, ks, vs, dsorted, stream);
+        mark("keydeps_bucket");
+        bucket_order = true;
+      } else {
+        sort_pairs<uint32_t>(bkey, nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
+                             sk32b.ensure(M + 1), svb.ensure(M + 1), M, key_bits, sort_ws, stream,
+                             &ks, &vs);
+        mark("keydeps_sort");
+        const unsigned g = unsigned((M + 255) / 256);
+        {
+          // read key + vid (8), write the dependency (8)
+          probed_launch("sv_deps", double(M) * 16.0, k_sv_deps, dim3(g), dim3(256), stream, M,
+                        (const uint32_t *)ks, (const uint32_t *)vs,
+                        (const uint64_t *)latest.get(), lmul, lmask, dsorted);
+        }
+        mark("deps");
+        {
+          // read key (4) and the batch dot (8)
+          const unsigned gt = unsigned((M + kTailTile - 1) / kTailTile);
+          probed_launch("sv_tails", double(M) * 12.0, k_sv_tails, dim3(gt), dim3(256), stream, M,
+                        (const uint32_t *)ks, (const uint32_t *)vs, (const uint64_t *)bdot,
+                        latest.get(), lmul, lmask,
+                        reinterpret_cast<unsigned long long *>(frontier.get()), excount_ptr());
+        }
+        mark("tails_and_clock");
+        bucket_order = false;
       }
-      mark("deps");
-      {
-        // read key (4) and the batch dot (8)
-        const unsigned gt = unsigned((M + kTailTile - 1) / kTailTile);
-        probed_launch("sv_tails", double(M) * 12.0, k_sv_tails, dim3(gt), dim3(256), stream, M,
-                      (const uint32_t *)ks, (const uint32_t *)vs, (const uint64_t *)bdot,
-                      latest.get(), reinterpret_cast<unsigned long long *>(frontier.get()),
-                      excount_ptr());
-      }
-      mark("tails_and_clock");
       sv_vs = vs;
-      // dependency graph: every dep is an earlier arrival (previous element of
-      // a key segment sorted by arrival, or a latest entry from an executed
+      // dependency graph: every dep is an earlier arrival (previous command
+      // on the key in arrival order, or a latest entry from an executed
       // earlier batch), so SCCs are singletons and arrival order is a
-      // topological order; the per-key sequence is the sorted element order.
+      // topological order; the per-key sequence is the key-grouped order.
       gout = GraphOutput();
       gout.trivial = true;
       gout.nexec = n;
@@ -565,7 +617,8 @@ struct EngineDevice {
                            &ks, &vs);
       mark("keydeps_sort");
       k_prev_engine<uint32_t><<<grid_for(M, B), B, 0, stream>>>(
-          M, ks, vs, 0, S, latest.get(), dvid, dext, tl, k == 1 ? nullptr : svid);
+          M, ks, vs, 0, S, latest.get(), uint64_t(lmul), uint64_t(lmask), dvid, dext, tl,
+          k == 1 ? nullptr : svid);
       sorted_keys32 = ks;
     } else {
       sv_fused = false;
@@ -579,7 +632,7 @@ struct EngineDevice {
                            &vs);
       mark("keydeps_sort");
       k_prev_engine<uint64_t><<<grid_for(M, B), B, 0, stream>>>(
-          M, ks, vs, tbits, S, latest.get(), dvid, dext, tl, nullptr);
+          M, ks, vs, tbits, S, views_latest(), 1ull, ~0ull, dvid, dext, tl, nullptr);
     }
     if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bproc, bdot);
     FH_HIP(hipEventRecord(ev1, stream));
@@ -602,8 +655,9 @@ struct EngineDevice {
     uint32_t *dd = dst.ensure(M + 1);
     FH_HIP(hipMemsetAsync(scal.get(), 0, sizeof(uint32_t), stream));
     k_cmd_engine<<<grid_for(n, B), B, 0, stream>>>(
-        n, k, fq, key_space, bkey, bproc, bdot, dvid, dext,
-        tl, latest.get(), frontier.get(), ddot, dcnt, dd, nullptr, scal.get());
+        n, k, fq, key_space, bkey, bproc, bdot, dvid, dext, tl,
+        views ? views_latest() : latest.get(), views ? 1ull : uint64_t(lmul),
+        views ? ~0ull : uint64_t(lmask), frontier.get(), ddot, dcnt, dd, nullptr, scal.get());
     mark("keydeps_union");
     // graph stage
     GraphInput gin;
@@ -712,22 +766,31 @@ struct EngineDevice {
         FH_HIP(hipMemcpyAsync(exec_rank, rk, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               stream));
     }
-    if (key_off) {
-      uint32_t *h = u32tmp.ensure(key_space + 1);
-      uint32_t *o = rank_tmp.ensure(key_space + 2);
+    if (key_off || key_seq) {
+      // per-key offsets over the ascending key space (histogram + scan)
+      uint32_t *h = key_hist.ensure(key_space + 1);
+      uint32_t *o = key_offs.ensure(key_space + 2);
       FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
       k_key_hist<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_key, h);
       exclusive_scan_u32(h, o, key_space, scan_ws, stream);
-      FH_HIP(hipMemcpyAsync(key_off, o, (key_space + 1) * sizeof(uint32_t),
-                            hipMemcpyDeviceToHost, stream));
-    }
-    if (key_seq) {
-      if (sv_fused)  // per-key sequence is (sorted keys, sorted vids): gather the dots
-        k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid,
-                                                               dot.get() + last * n,
-                                                               seq_dot.ensure(gout.nelem + 1));
-      FH_HIP(hipMemcpyAsync(key_seq, seq_dot.get(), size_t(gout.nelem) * sizeof(uint64_t),
-                            hipMemcpyDeviceToHost, stream));
+      if (key_off)
+        FH_HIP(hipMemcpyAsync(key_off, o, (key_space + 1) * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, stream));
+      if (key_seq) {
+        uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
+        const uint64_t *bd = dot.get() + last * n;
+        if (sv_fused && bucket_order) {
+          // key-grouped runs -> ascending keys
+          uint32_t *hp = headpos.ensure(key_space + 1);
+          k_run_heads<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_key, hp);
+          k_run_scatter<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_key,
+                                                                    gout.pk_vid, hp, o, bd, sq);
+        } else if (sv_fused) {  // (sorted keys, sorted vids): gather the dots
+          k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, bd, sq);
+        }
+        FH_HIP(hipMemcpyAsync(key_seq, sq, size_t(gout.nelem) * sizeof(uint64_t),
+                              hipMemcpyDeviceToHost, stream));
+      }
     }
     FH_HIP(hipStreamSynchronize(stream));
   }
@@ -812,28 +875,34 @@ fh_status fh_engine_set_probe(fh_engine *h, const char *kernel) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
   FH_HIP(hipStreamSynchronize(h->dev.stream));
-  h->dev.probe.target = kernel ? kernel : "";
-  h->dev.probe.reset();
+  h->dev.probe.set(kernel ? kernel : "");
+  FH_API_END
+}
+
+fh_status fh_engine_probe_stats_for(fh_engine *h, const char *kernel, float *avg_ms,
+                                    size_t *launches, double *bytes_per_launch) {
+  FH_API_BEGIN
+  FH_CHECK(h && avg_ms && launches && bytes_per_launch, FH_EINVAL, "null argument");
+  FH_HIP(hipStreamSynchronize(h->dev.stream));
+  auto &pr = h->dev.probe;
+  fh::ProbeSlot *p = kernel ? pr.find(kernel) : (pr.slots.empty() ? nullptr : &pr.slots[0]);
+  FH_CHECK(p, FH_EINVAL, "kernel is not probed");
+  const size_t n = p->next / 2;
+  double tot = 0;
+  for (size_t i = 0; i < n; i++) {
+    float ms = 0;
+    FH_HIP(hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]));
+    tot += ms;
+  }
+  *launches = n;
+  *avg_ms = n ? float(tot / double(n)) : 0.f;
+  *bytes_per_launch = n ? p->bytes / double(n) : 0.0;
   FH_API_END
 }
 
 fh_status fh_engine_probe_stats(fh_engine *h, float *avg_ms, size_t *launches,
                                 double *bytes_per_launch) {
-  FH_API_BEGIN
-  FH_CHECK(h && avg_ms && launches && bytes_per_launch, FH_EINVAL, "null argument");
-  FH_HIP(hipStreamSynchronize(h->dev.stream));
-  auto &p = h->dev.probe;
-  const size_t n = p.next / 2;
-  double tot = 0;
-  for (size_t i = 0; i < n; i++) {
-    float ms = 0;
-    FH_HIP(hipEventElapsedTime(&ms, p.ev[2 * i], p.ev[2 * i + 1]));
-    tot += ms;
-  }
-  *launches = n;
-  *avg_ms = n ? float(tot / double(n)) : 0.f;
-  *bytes_per_launch = n ? p.bytes / double(n) : 0.0;
-  FH_API_END
+  return fh_engine_probe_stats_for(h, nullptr, avg_ms, launches, bytes_per_launch);
 }
 
 fh_status fh_engine_set_profiling(fh_engine *h, int on) {

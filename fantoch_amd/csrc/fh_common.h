@@ -83,29 +83,49 @@ inline int bits_for(uint64_t x) {
   return b;
 }
 
-// Roofline probe: HIP events around every launch of one named kernel on the
-// stream it runs on, plus the algorithmic bytes each launch moves.
-struct Probe {
-  std::string target;
+// Roofline probe: HIP events around every launch of the named kernels on the
+// stream they run on, plus the algorithmic bytes each launch moves.
+struct ProbeSlot {
+  std::string name;
   std::vector<hipEvent_t> ev;
   size_t next = 0;
   double bytes = 0;
-  bool on(const char *name) const { return !target.empty() && target == name; }
-  hipEvent_t take() {
-    if (next >= ev.size()) {
+};
+struct Probe {
+  std::vector<ProbeSlot> slots;
+  // comma-separated kernel names ("" = off)
+  void set(const std::string &csv) {
+    for (auto &sl : slots)
+      for (auto e : sl.ev) (void)hipEventDestroy(e);
+    slots.clear();
+    size_t a = 0;
+    while (a < csv.size()) {
+      size_t b = csv.find(',', a);
+      if (b == std::string::npos) b = csv.size();
+      if (b > a) slots.push_back(ProbeSlot{csv.substr(a, b - a)});
+      a = b + 1;
+    }
+  }
+  ProbeSlot *find(const char *name) {
+    for (auto &sl : slots)
+      if (sl.name == name) return &sl;
+    return nullptr;
+  }
+  hipEvent_t take(ProbeSlot &sl) {
+    if (sl.next >= sl.ev.size()) {
       hipEvent_t e;
       FH_HIP(hipEventCreate(&e));
-      ev.push_back(e);
+      sl.ev.push_back(e);
     }
-    return ev[next++];
+    return sl.ev[sl.next++];
   }
   void reset() {
-    next = 0;
-    bytes = 0;
+    for (auto &sl : slots) {
+      sl.next = 0;
+      sl.bytes = 0;
+    }
   }
-  ~Probe() {
-    for (auto e : ev) (void)hipEventDestroy(e);
-  }
+  ~Probe() { set(""); }
 };
 extern thread_local Probe *t_probe;
 
@@ -117,10 +137,12 @@ template <class F, class... Args>
 inline void probed_launch(const char *name, double bytes, F k, dim3 grid, dim3 block,
                           hipStream_t s, Args... args) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (t_probe && t_probe->on(name)) {
-    t_probe->bytes += bytes;
-    e0 = t_probe->take();
-    e1 = t_probe->take();
+  if (t_probe) {
+    if (ProbeSlot *sl = t_probe->find(name)) {
+      sl->bytes += bytes;
+      e0 = t_probe->take(*sl);
+      e1 = t_probe->take(*sl);
+    }
   }
   hipExtLaunchKernelGGL(k, grid, block, 0, s, e0, e1, 0, args...);
   FH_HIP(hipGetLastError());

@@ -73,11 +73,16 @@ class Engine:
         return float(ms.value)
 
     def set_probe(self, kernel):
+        """kernel: a name, a comma-separated list of names, or None (off)."""
+        if isinstance(kernel, (list, tuple)):
+            kernel = ",".join(kernel)
         L.check(self._lib.fh_engine_set_probe(self._h, kernel.encode() if kernel else None))
 
-    def probe_stats(self):
+    def probe_stats(self, kernel=None):
+        """(average device ms per launch, launches, algorithmic bytes per launch)."""
         ms, n, b = C.c_float(0), C.c_size_t(0), C.c_double(0)
-        L.check(self._lib.fh_engine_probe_stats(self._h, C.byref(ms), C.byref(n), C.byref(b)))
+        L.check(self._lib.fh_engine_probe_stats_for(self._h, kernel.encode() if kernel else None,
+                                                    C.byref(ms), C.byref(n), C.byref(b)))
         return float(ms.value), int(n.value), float(b.value)
 
     def kernel_times(self):

@@ -208,12 +208,16 @@ fh_status fh_engine_results(fh_engine *h, uint32_t *dep_off, uint64_t *dep_dot,
 fh_status fh_engine_kernel_times(fh_engine *h, const char **names, float *ms,
                                  size_t cap, size_t *len);
 /* Roofline probe: record HIP events (on the engine's stream) around every
- * launch of one kernel during subsequent runs ("onesweep" = the key+value
- * radix passes, "sv_deps", "sv_tails"; NULL = off), then report its average
- * device duration and the algorithmic bytes one launch moves. */
+ * launch of the named kernels during subsequent runs (comma-separated:
+ * "kb_partition", "kb_order" = the two single-view launches, "sort_scatter"
+ * = the key+value radix passes, "sv_deps", "sv_tails"; NULL = off), then
+ * report a kernel's average device duration and the algorithmic bytes one
+ * launch moves (probe_stats: the first named kernel). */
 fh_status fh_engine_set_probe(fh_engine *h, const char *kernel);
 fh_status fh_engine_probe_stats(fh_engine *h, float *avg_ms, size_t *launches,
                                 double *bytes_per_launch);
+fh_status fh_engine_probe_stats_for(fh_engine *h, const char *kernel, float *avg_ms,
+                                    size_t *launches, double *bytes_per_launch);
 /* Enable/disable per-kernel event timing (adds events between kernels). */
 fh_status fh_engine_set_profiling(fh_engine *h, int on);
 

@@ -24,11 +24,11 @@ def oracle_pipeline(s, nproc=5):
     return dep_off, deps, ex, lab, kso, ks
 
 
-def check_engine(s, nproc=5, batches=1):
+def check_engine(s, nproc=5, batches=1, bounds=None):
     eng = Engine(s.key_space, n=nproc)
     dep_off, deps, ex, lab, kso, ks = oracle_pipeline(s, nproc)
     assert len(ex) == s.n, "oracle must execute every command"
-    if batches == 1:
+    if batches == 1 and bounds is None:
         eng.stage(s, nproc)
         eng.run()
         r = eng.results()
@@ -51,22 +51,27 @@ def check_engine(s, nproc=5, batches=1):
                     assert rank[d] < rank[int(s.dots[i])]
         return r
     # streaming batches: deps and per-key sequences concatenate
-    bounds = np.linspace(0, s.n, batches + 1).astype(int)
-    got_deps, got_seq = [], {}
+    if bounds is None:
+        bounds = np.linspace(0, s.n, batches + 1).astype(int)
+    got_off, got_deps, got_seq = [np.zeros(1, dtype=np.int64)], [], {}
+    base = 0
     for a, b in zip(bounds[:-1], bounds[1:]):
         sub = type(s)(s.dots[a:b], s.keys[a:b], None, None, s.key_space)
         eng.stage(sub, nproc)
         eng.run()
         r = eng.results()
-        for i in range(b - a):
-            got_deps.append(r["deps"][r["dep_off"][i]:r["dep_off"][i + 1]])
+        got_off.append(r["dep_off"][1:].astype(np.int64) + base)
+        got_deps.append(r["deps"])
+        base += len(r["deps"])
         ko = r["key_off"]
         for key in np.nonzero(np.diff(ko))[0]:
-            got_seq.setdefault(int(key), []).extend(r["key_seq"][ko[key]:ko[key + 1]].tolist())
-    for i in range(s.n):
-        assert np.array_equal(got_deps[i], deps[dep_off[i]:dep_off[i + 1]])
-    for key in np.nonzero(np.diff(kso))[0]:
-        assert got_seq[int(key)] == ks[kso[key]:kso[key + 1]].tolist()
+            got_seq.setdefault(int(key), []).append(r["key_seq"][ko[key]:ko[key + 1]])
+    assert np.array_equal(np.concatenate(got_off), dep_off.astype(np.int64))
+    assert np.array_equal(np.concatenate(got_deps), deps)
+    keys_with = np.nonzero(np.diff(kso))[0]
+    assert sorted(got_seq) == keys_with.tolist()
+    for key in keys_with:
+        assert np.array_equal(np.concatenate(got_seq[int(key)]), ks[kso[key]:kso[key + 1]])
 
 
 @pytest.mark.parametrize("k", [1, 2])
@@ -78,6 +83,20 @@ def test_single_view_zipf(k):
 def test_single_view_streaming_batches():
     s = Workload.zipf(0.7, 5000, k=1, seed=21).generate(40_000)
     check_engine(s, batches=4)
+
+
+def test_single_view_hot_buckets_multichunk():
+    """Buckets far larger than the bucket kernel's LDS chunk: 16 keys (one key
+    per bucket) under Zipf 0.99, and a ConflictRate hot key (50%)."""
+    check_engine(Workload.zipf(0.99, 16, k=1, seed=11).generate(60_000))
+    check_engine(Workload.conflict_rate_(50, k=1, clients=64, seed=12).generate(50_000), batches=3)
+
+
+def test_single_view_bucket_then_sort_path():
+    """A batch above the bucket plan's size limit (> 1024 tiles) between two
+    bucket-path batches: both paths share the mapped latest table."""
+    s = Workload.zipf(0.9, 1 << 12, k=1, seed=13).generate(4_250_000)
+    check_engine(s, bounds=[0, 20_000, 4_230_000, 4_250_000])
 
 
 def test_c1_atlas_n5_conflict10_views():

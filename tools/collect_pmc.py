@@ -38,6 +38,8 @@ PROBES = {
     "sort_scan": r"k_scan_fused",
     "sv_deps": r"k_sv_deps",
     "sv_tails": r"k_sv_tails",
+    "kb_partition": r"k_kb_partition",
+    "kb_order": r"k_kb_order",
 }
 CALIB_BYTES = 1 << 30
 
