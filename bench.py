@@ -49,9 +49,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=4_000_000,
                     help="commands in the CPU-baseline sample")
-    ap.add_argument("--probe", default="kb_partition,kb_order",
+    ap.add_argument("--probe", default="kb_step,kb_partition,kb_order",
                     help="kernels whose launches are timed (comma-separated); the roofline "
-                         "entry reports the one with the longest average launch")
+                         "entry reports the one with the most device time")
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase profile pass")
     return ap.parse_args()
 
@@ -108,7 +108,10 @@ def main():
 
     from fantoch_amd.engine import Engine
 
-    nb = args.warmup + args.steps
+    # warmup + the timed steps + a probe pass of the same length (per-launch
+    # HIP events cost ~3 us of stream time each, so they stay out of the
+    # timed region)
+    nb = args.warmup + 2 * args.steps
     batches = shard_batches(args, rank, world, nb)
     key_space = batches[0].key_space
     eng = Engine(key_space, n=5, device=local)
@@ -122,9 +125,7 @@ def main():
         eng.run(sync=False)
     torch.cuda.synchronize()
 
-    # timed region: exactly `steps` batches; HIP events bracket every launch of
-    # the probed kernel on the engine's stream (roofline entry)
-    eng.set_probe(args.probe)
+    # timed region: exactly `steps` batches, no instrumentation
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -133,6 +134,12 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
+    # probe pass: the next `steps` batches with HIP events on the stream of
+    # every launch of the probed kernels (their own dispatch begin/end)
+    eng.set_probe(args.probe)
+    for _ in range(args.steps):
+        eng.run(sync=False)
+    torch.cuda.synchronize()
     probes = {}
     for name in [x for x in args.probe.split(",") if x]:
         ms_, nl_, by_ = eng.probe_stats(name)
@@ -141,7 +148,9 @@ def main():
                             "algorithmic_bytes_per_launch": by_,
                             "achieved_GBs": by_ / (ms_ * 1e-3) / 1e9 if ms_ > 0 else 0.0}
     eng.set_probe(None)
-    dominant = max(probes, key=lambda k: probes[k]["avg_launch_us"]) if probes else args.probe
+    # dominant kernel: most device time over the pass (average x launches)
+    dominant = (max(probes, key=lambda k: probes[k]["avg_launch_us"] * probes[k]["launches"])
+                if probes else args.probe)
     pd = probes.get(dominant, {"avg_launch_us": 0.0, "launches": 0,
                                "algorithmic_bytes_per_launch": 0.0})
     probe_ms, probe_launches = pd["avg_launch_us"] * 1e-3, pd["launches"]

@@ -95,6 +95,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
                              const uint64_t *__restrict__ dot, const uint32_t *__restrict__ dep_vid,
                              const uint64_t *__restrict__ dep_ext, const uint8_t *__restrict__ tail,
                              uint64_t *__restrict__ latest, uint64_t lmul, uint64_t lmask,
+                             const uint64_t *__restrict__ dlog, uint64_t log_base,
                              const uint64_t *__restrict__ frontier,
                              uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ dep_cnt,
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
@@ -115,7 +116,8 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
         if (!dup) ds[nv++] = v;
         dd[nd++] = dot[v];
       } else {
-        const uint64_t x = dep_ext[e];
+        uint64_t x = dep_ext[e];
+        if (is_log_ref(x)) x = dlog[x - kLogFlag];  // single view: command-log reference
         if (x) {
           dd[nd++] = x;
           // executed? (AEClock frontier; exceptions are not carried by the
@@ -127,7 +129,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
         const uint32_t j = t / k, s = t % k;
         const uint64_t slot = fq_proc ? uint64_t(fq_proc[i * fq + j]) * K + key32[i * k + s]
                                       : (uint64_t(key32[i * k + s]) * lmul) & lmask;
-        latest[slot] = self;
+        latest[slot] = fq_proc ? self : (kLogFlag | (log_base + i));
       }
     }
     for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
@@ -211,8 +213,8 @@ constexpr int kTailTile = 256 * kTailItems;
 
 __global__ void __launch_bounds__(256)
     k_sv_tails(uint32_t M, const uint32_t *__restrict__ ks, const uint32_t *__restrict__ vs,
-               const uint64_t *__restrict__ dot, uint64_t *__restrict__ latest, uint32_t lmul,
-               uint32_t lmask, unsigned long long *__restrict__ frontier,
+               const uint64_t *__restrict__ dot, uint64_t log_base, uint64_t *__restrict__ latest,
+               uint32_t lmul, uint32_t lmask, unsigned long long *__restrict__ frontier,
                unsigned long long *__restrict__ excount) {
   __shared__ unsigned long long s_mx[256];
   __shared__ unsigned int s_cnt[256];
@@ -240,7 +242,8 @@ __global__ void __launch_bounds__(256)
     const uint32_t nxt = __shfl(key[i + 1], 0, 64);
     if (lane == 63) nk = nxt;
     if (j < M) {
-      if (j + 1 == M || nk != key[i]) latest[(key[i] * lmul) & lmask] = dot[vs[j]];  // :88-95
+      if (j + 1 == M || nk != key[i])  // sequential.rs:88-95
+        latest[(key[i] * lmul) & lmask] = kLogFlag | (log_base + vs[j]);
       const uint32_t src = uint32_t(d[i] >> 56);
       atomicMax(&s_mx[src], d[i] & 0x00FFFFFFFFFFFFFFull);
       atomicAdd(&s_cnt[src], 1u);
@@ -256,10 +259,13 @@ __global__ void __launch_bounds__(256)
 // results: single-view sorted deps -> per-command dep dots
 __global__ void k_sv_unpermute(uint32_t M, const uint32_t *__restrict__ vs,
                                const uint64_t *__restrict__ dep_sorted,
-                               const uint64_t *__restrict__ dot, uint64_t *__restrict__ dep_dot) {
+                               const uint64_t *__restrict__ dot, const uint64_t *__restrict__ dlog,
+                               uint64_t *__restrict__ dep_dot) {
   GRID_STRIDE(j, M) {
     const uint64_t x = dep_sorted[j];
-    dep_dot[vs[j]] = (x != 0 && (x >> 56) == 0) ? dot[x - 1] : x;
+    dep_dot[vs[j]] = is_log_ref(x) ? dlog[x - kLogFlag]  // an earlier batch
+                     : (x != 0 && (x >> 56) == 0) ? dot[x - 1]  // in-batch index + 1
+                     : x;
   }
 }
 
@@ -366,7 +372,9 @@ struct EngineDevice {
   bool lat_mapped = false;
   uint64_t kp = 0;
   uint32_t lmul = 1, lmask = 0xFFFFFFFFu;
-  KeyBucketWorkspace kb_ws;
+  KeyBucketWorkspace kb_ws[2];      // double-buffered by batch parity
+  size_t kb_next_part = ~size_t(0); // staged batch already partitioned by the last step
+  DBuf<unsigned long long> kb_clk;  // executed-clock shard sets (2) of the bucket path
   bool bucket_order = false;  // single-view per-key runs are key-grouped, not ascending
   DBuf<uint32_t> key_hist, key_offs, headpos;
   // persistent state
@@ -381,7 +389,9 @@ struct EngineDevice {
   std::vector<uint64_t> tmins;
   uint64_t tmin = 0;
   int tbits = 0;
-  DBuf<uint64_t> dot, fq_time;
+  DBuf<uint64_t> dot, fq_time;  // dot: the command log (every staged batch, appended)
+  size_t log_len = 0;            // dots in the log
+  size_t stage_base = 0;         // log position of the first staged batch
   DBuf<uint32_t> key32;
   DBuf<uint8_t> fq_proc;
   // scratch / outputs
@@ -430,6 +440,7 @@ struct EngineDevice {
     FH_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     FH_HIP(hipEventCreate(&ev0));
     FH_HIP(hipEventCreate(&ev1));
+
     graph.stream = stream;
     graph.marks = &marks;
     err.ensure(4);
@@ -470,14 +481,38 @@ struct EngineDevice {
     FH_HIP(hipMemsetAsync(latest.get(), 0, latest_words(latest_slots) * sizeof(uint64_t), stream));
   }
 
+  // stream idle (staged data, the command log and the clock shards may be
+  // rewritten afterwards); forgets a partition done ahead
+  void sync_all() {
+    if (kb_next_part != ~size_t(0) && kb_clk.get()) {
+      // a batch partitioned ahead will not be ordered: drop its clock shards
+      FH_HIP(hipMemsetAsync(kb_clk.get() + (kb_next_part & 1) * kKeyBucketClockWords, 0,
+                            kKeyBucketClockWords * sizeof(unsigned long long), stream));
+    }
+    FH_HIP(hipStreamSynchronize(stream));
+    kb_next_part = ~size_t(0);
+  }
+  KeyBucketClock kb_clock(size_t batch) {
+    KeyBucketClock c;
+    c.fold = kb_clk.get() + (batch & 1) * kKeyBucketClockWords;
+    c.frontier = reinterpret_cast<unsigned long long *>(frontier.get());
+    c.excount = excount_ptr();
+    return c;
+  }
+
   void reset() {
     FH_HIP(hipSetDevice(device));
+    sync_all();
     ensure_latest(latest_slots);
     FH_HIP(hipMemsetAsync(latest.get(), 0, latest_words(latest_slots) * sizeof(uint64_t), stream));
     FH_HIP(hipMemsetAsync(frontier.get(), 0, 256 * sizeof(uint64_t), stream));
     FH_HIP(hipMemsetAsync(excount_ptr(), 0, 256 * sizeof(unsigned long long), stream));
+    FH_HIP(hipMemsetAsync(kb_clk.ensure(2 * kKeyBucketClockWords), 0,
+                          2 * kKeyBucketClockWords * sizeof(unsigned long long), stream));
     FH_HIP(hipMemsetAsync(err.get(), 0, 4 * sizeof(uint32_t), stream));
     FH_HIP(hipStreamSynchronize(stream));
+    log_len = 0;
+    staged = false;
   }
 
   void stage(const fh_stream_desc &d, size_t nb, const uint64_t *h_dot, const uint64_t *h_key,
@@ -491,14 +526,30 @@ struct EngineDevice {
     FH_CHECK(!d.views || (h_proc && h_time && d.nproc >= 1 && d.nproc <= 255), FH_EINVAL,
              "replica views need fq_proc, fq_time and nproc");
     FH_HIP(hipSetDevice(device));
+    sync_all();
     const size_t n = d.n, nk = n * d.keys_per_cmd;
     std::vector<uint32_t> k32(nk * nb);
     for (size_t e = 0; e < nk * nb; e++) {
       FH_CHECK(h_key[e] < key_space, FH_EINVAL, "stage: key id >= key_space");
       k32[e] = uint32_t(h_key[e]);
     }
-    FH_HIP(hipMemcpyAsync(dot.ensure(n * nb + 1), h_dot, n * nb * sizeof(uint64_t),
+    // append the batches' dots to the command log (grown by doubling, old
+    // entries kept: earlier batches stay referenced by the latest table)
+    const size_t need = log_len + n * nb + 1;
+    if (need > dot.cap || !dot.get()) {
+      DBuf<uint64_t> grown;
+      grown.ensure(std::max(need, 2 * dot.cap));
+      if (log_len)
+        FH_HIP(hipMemcpyAsync(grown.get(), dot.get(), log_len * sizeof(uint64_t),
+                              hipMemcpyDeviceToDevice, stream));
+      FH_HIP(hipStreamSynchronize(stream));
+      dot.swap(grown);
+    }
+    FH_CHECK(log_len + n * nb < kLogFlag, FH_ENOTIMPL, "command log exceeds 2^48 commands");
+    FH_HIP(hipMemcpyAsync(dot.get() + log_len, h_dot, n * nb * sizeof(uint64_t),
                           hipMemcpyHostToDevice, stream));
+    stage_base = log_len;
+    log_len += n * nb;
     FH_HIP(hipMemcpyAsync(key32.ensure(nk * nb + 1), k32.data(), nk * nb * sizeof(uint32_t),
                           hipMemcpyHostToDevice, stream));
     tmins.assign(nb, 0);
@@ -543,12 +594,13 @@ struct EngineDevice {
     const bool views = desc.views != 0;
     const size_t b = cursor++;
     last = b;
-    const uint64_t *bdot = dot.get() + b * n;
+    const uint64_t bbase = stage_base + b * n;  // log position of this batch
+    const uint64_t *bdot = dot.get() + bbase;
     const uint32_t *bkey = key32.get() + b * size_t(n) * k;
     const uint8_t *bproc = views ? fq_proc.get() + b * size_t(n) * fq : nullptr;
     const uint64_t *btime = views ? fq_time.get() + b * size_t(n) * fq : nullptr;
     tmin = tmins[b];
-    FH_HIP(hipEventRecord(ev0, stream));
+    if (ms || profile) FH_HIP(hipEventRecord(ev0, stream));
     mark("start");
     struct ProbeGuard {
       ProbeGuard(Probe *p) { t_probe = p; }
@@ -568,9 +620,20 @@ struct EngineDevice {
         // two launches: tile partition by key bucket, per-bucket order + deps
         ks = sk32a.ensure(M + 1);
         vs = sva.ensure(M + 1);
-        keybucket_run(plan, M, bkey, bdot, latest.get(),
-                      reinterpret_cast<unsigned long long *>(frontier.get()), excount_ptr(),
-                      kb_ws, ks, vs, dsorted, stream);
+        // one launch per step: order this batch (partitioned by the previous
+        // step, or now) and partition the next staged batch in the same grid
+        const size_t q = b & 1;
+        const KeyBucketClock clock = kb_clock(b);
+        if (kb_next_part != b)
+          keybucket_partition(plan, M, bkey, bdot, clock.fold, kb_ws[q], stream);
+        kb_next_part = ~size_t(0);
+        if (b + 1 < nbatches) {
+          keybucket_step(plan, M, bbase, latest.get(), kb_ws[q], ks, vs, dsorted, clock, plan, M,
+                         bkey + M, bdot + M, kb_clock(b + 1).fold, kb_ws[q ^ 1], stream);
+          kb_next_part = b + 1;
+        } else {
+          keybucket_order(plan, M, bbase, latest.get(), kb_ws[q], ks, vs, dsorted, clock, stream);
+        }
         mark("keydeps_bucket");
         bucket_order = true;
       } else {
@@ -591,7 +654,7 @@ struct EngineDevice {
           const unsigned gt = unsigned((M + kTailTile - 1) / kTailTile);
           probed_launch("sv_tails", double(M) * 12.0, k_sv_tails, dim3(gt), dim3(256), stream, M,
                         (const uint32_t *)ks, (const uint32_t *)vs, (const uint64_t *)bdot,
-                        latest.get(), lmul, lmask,
+                        bbase, latest.get(), lmul, lmask,
                         reinterpret_cast<unsigned long long *>(frontier.get()), excount_ptr());
         }
         mark("tails_and_clock");
@@ -634,8 +697,8 @@ struct EngineDevice {
       k_prev_engine<uint64_t><<<grid_for(M, B), B, 0, stream>>>(
           M, ks, vs, tbits, S, views_latest(), 1ull, ~0ull, dvid, dext, tl, nullptr);
     }
-    if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bproc, bdot);
-    FH_HIP(hipEventRecord(ev1, stream));
+    if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bproc, bdot, bbase);
+    if (ms || profile) FH_HIP(hipEventRecord(ev1, stream));
     if (ms) {
       FH_HIP(hipEventSynchronize(ev1));
       FH_HIP(hipEventElapsedTime(ms, ev0, ev1));
@@ -644,7 +707,8 @@ struct EngineDevice {
   }
 
   void run_general(uint32_t n, uint32_t k, uint32_t fq, uint32_t S, uint32_t M, bool views,
-                   const uint32_t *bkey, const uint8_t *bproc, const uint64_t *bdot) {
+                   const uint32_t *bkey, const uint8_t *bproc, const uint64_t *bdot,
+                   uint64_t bbase) {
     uint32_t *dvid = dep_vid.get();
     uint64_t *dext = dep_ext.get();
     uint8_t *tl = tail.get();
@@ -657,7 +721,8 @@ struct EngineDevice {
     k_cmd_engine<<<grid_for(n, B), B, 0, stream>>>(
         n, k, fq, key_space, bkey, bproc, bdot, dvid, dext, tl,
         views ? views_latest() : latest.get(), views ? 1ull : uint64_t(lmul),
-        views ? ~0ull : uint64_t(lmask), frontier.get(), ddot, dcnt, dd, nullptr, scal.get());
+        views ? ~0ull : uint64_t(lmask), (const uint64_t *)dot.get(), bbase, frontier.get(), ddot,
+        dcnt, dd, nullptr, scal.get());
     mark("keydeps_union");
     // graph stage
     GraphInput gin;
@@ -731,8 +796,8 @@ struct EngineDevice {
       uint32_t *off = u32tmp.ensure(n + 1);
       if (sv_fused) {  // one dependency slot per command: decode, count = slot used
         k_sv_unpermute<<<grid_for(n, B), B, 0, stream>>>(n, sv_vs, dep_ext.get(),
-                                                          dot.get() + last * n,
-                                                          dep_dot.ensure(n + 1));
+                                                          dot.get() + stage_base + last * n,
+                                                          dot.get(), dep_dot.ensure(n + 1));
         k_cnt_nonzero<<<grid_for(n, B), B, 0, stream>>>(n, dep_dot.get(), dep_cnt.ensure(n + 1));
       }
       exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
@@ -757,7 +822,7 @@ struct EngineDevice {
       if (gout.trivial) {
         lb = lab.ensure(n + 1);
         rk = rank_tmp.ensure(n + 1);
-        k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, dot.get() + last * n, lb, rk);
+        k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, dot.get() + stage_base + last * n, lb, rk);
       }
       if (scc_label)
         FH_HIP(hipMemcpyAsync(scc_label, lb, size_t(n) * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -778,7 +843,7 @@ struct EngineDevice {
                               hipMemcpyDeviceToHost, stream));
       if (key_seq) {
         uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
-        const uint64_t *bd = dot.get() + last * n;
+        const uint64_t *bd = dot.get() + stage_base + last * n;
         if (sv_fused && bucket_order) {
           // key-grouped runs -> ascending keys
           uint32_t *hp = headpos.ensure(key_space + 1);

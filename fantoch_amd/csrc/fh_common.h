@@ -67,7 +67,18 @@ struct DBuf {
     return p;
   }
   T *get() const { return p; }
+  void swap(DBuf &o) {
+    std::swap(p, o.p);
+    std::swap(cap, o.cap);
+  }
 };
+
+// The fused engine keeps every staged command's dot in a device-resident
+// command log; the single-view latest table stores log positions tagged with
+// kLogFlag (top byte 0, so never a dot; >= 2^48, so never an in-batch
+// "index + 1" dependency).  Dots are read from the log when results are read.
+constexpr uint64_t kLogFlag = uint64_t(1) << 48;
+__host__ __device__ inline bool is_log_ref(uint64_t x) { return (x >> 56) == 0 && x >= kLogFlag; }
 
 inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 8192) {
   size_t g = (n + block - 1) / block;

@@ -17,9 +17,9 @@
 //                   bucket (high bits of the mapped key), tile-local bucket
 //                   offsets (u16), executed-clock partials
 //   k_kb_order      per bucket: gather its runs from every tile in tile
-//                   (= arrival) order, per-slot rank and predecessor with
-//                   wave64 ballot matching, write the key-grouped sequence and
-//                   each command's dependency; tails update latest
+//                   (= arrival) order, stable LDS sort by slot (wave64 ballot
+//                   ranks), write the key-grouped sequence and each command's
+//                   dependency; tails update latest
 #pragma once
 
 #include "fh_common.h"
@@ -37,7 +37,7 @@ struct KeyBucketPlan {
 };
 
 // Plan for n commands over ids < 2^kb; ok == false if the batch does not fit
-// the two-launch path (kb > 22, more than 1024 tiles, or packed width > 32).
+// the two-launch path (kb > 22, more than 4M commands, or packed width > 32).
 KeyBucketPlan keybucket_plan(size_t n, int kb);
 
 // The key bijection alone (same multiplier as the plan), for paths that share
@@ -47,17 +47,48 @@ void keybucket_map(int kb, uint32_t *kmul, uint32_t *kinv, uint32_t *kmask);
 struct KeyBucketWorkspace {
   DBuf<uint32_t> part;  // [n] tile-partitioned (slot << vb | command index)
   DBuf<uint16_t> toff;  // [tiles][B + 1] tile-local bucket offsets
+  DBuf<uint32_t> mc;    // [B][4][4096] slot tables of multi-chunk buckets
 };
 
-// Runs both launches on stream s.  Outputs, in key-grouped order (buckets
+// The executed clock the path maintains (AEClock::add for every executed
+// dot, tarjan.rs:296): a partition launch adds its batch's per-source max
+// sequence / count to 8 shards of [max[256], count[256]] (u64) in `fold`;
+// the launch that orders the batch folds them into frontier (max) and
+// excount (sum) and clears them.  Batch parity selects one of two shard sets.
+struct KeyBucketClock {
+  unsigned long long *fold = nullptr;
+  unsigned long long *frontier = nullptr;
+  unsigned long long *excount = nullptr;
+};
+constexpr size_t kKeyBucketClockWords = 8 * 512;
+
+// Both launches on stream s.  Outputs, in key-grouped order (buckets
 // ascending, slots ascending, arrival order inside a key): sk = key ids,
 // sv = command indices, dep_sorted = dependency of that command (0 none,
-// index + 1 in-batch, otherwise the dot from latest).  latest is indexed by
-// the mapped key; frontier / excount receive the per-source executed-clock
-// max / count of the batch.
+// index + 1 in-batch, otherwise the latest entry: a command-log reference,
+// kLogFlag | position).  latest is indexed by the mapped key; the batch's
+// commands sit at log positions log_base + index.
 void keybucket_run(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32, const uint64_t *dot,
-                   uint64_t *latest, unsigned long long *frontier, unsigned long long *excount,
+                   uint64_t log_base, uint64_t *latest, const KeyBucketClock &clock,
                    KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
                    hipStream_t s);
+
+// The two launches separately: keybucket_order reads the workspace
+// keybucket_partition filled; clk = the shard set of that batch.
+void keybucket_partition(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32,
+                         const uint64_t *dot, unsigned long long *clk, KeyBucketWorkspace &ws,
+                         hipStream_t s);
+void keybucket_order(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
+                     KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
+                     const KeyBucketClock &clock, hipStream_t s);
+
+// One launch that orders batch b (partitioned earlier into ws, clock shards
+// clock.fold) and partitions batch b+1 (p2 / n2 / key32_2 / dot_2) into ws2
+// with its clock shards in clk.
+void keybucket_step(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
+                    KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
+                    const KeyBucketClock &clock, const KeyBucketPlan &p2, uint32_t n2,
+                    const uint32_t *key32_2, const uint64_t *dot_2, unsigned long long *clk,
+                    KeyBucketWorkspace &ws2, hipStream_t s);
 
 }  // namespace fh
