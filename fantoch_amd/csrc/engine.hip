@@ -375,6 +375,8 @@ struct EngineDevice {
   KeyBucketWorkspace kb_ws[2];      // double-buffered by batch parity
   size_t kb_next_part = ~size_t(0); // staged batch already partitioned by the last step
   DBuf<unsigned long long> kb_clk;  // executed-clock shard sets (2) of the bucket path
+  KeyBucketSched kb_sched;          // largest-first order-workgroup schedule
+  uint64_t kb_launches = 0;         // order launches (schedule refresh cadence)
   bool bucket_order = false;  // single-view per-key runs are key-grouped, not ascending
   DBuf<uint32_t> key_hist, key_offs, headpos;
   // persistent state
@@ -625,15 +627,20 @@ struct EngineDevice {
         const size_t q = b & 1;
         const KeyBucketClock clock = kb_clock(b);
         if (kb_next_part != b)
-          keybucket_partition(plan, M, bkey, bdot, clock.fold, kb_ws[q], stream);
+          keybucket_partition(plan, M, bkey, bdot, clock.fold, kb_ws[q], stream, &kb_sched);
         kb_next_part = ~size_t(0);
         if (b + 1 < nbatches) {
           keybucket_step(plan, M, bbase, latest.get(), kb_ws[q], ks, vs, dsorted, clock, plan, M,
-                         bkey + M, bdot + M, kb_clock(b + 1).fold, kb_ws[q ^ 1], stream);
+                         bkey + M, bdot + M, kb_clock(b + 1).fold, kb_ws[q ^ 1], stream,
+                         &kb_sched);
           kb_next_part = b + 1;
         } else {
-          keybucket_order(plan, M, bbase, latest.get(), kb_ws[q], ks, vs, dsorted, clock, stream);
+          keybucket_order(plan, M, bbase, latest.get(), kb_ws[q], ks, vs, dsorted, clock, stream,
+                          &kb_sched);
         }
+        // refresh the schedule from the sizes just recorded: after the first
+        // launch, then every 32 (the key distribution drifts slowly)
+        if ((kb_launches++ & 31) == 0) keybucket_sched(kb_sched, stream);
         mark("keydeps_bucket");
         bucket_order = true;
       } else {

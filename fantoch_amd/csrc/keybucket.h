@@ -46,7 +46,8 @@ void keybucket_map(int kb, uint32_t *kmul, uint32_t *kinv, uint32_t *kmask);
 
 struct KeyBucketWorkspace {
   DBuf<uint32_t> part;  // [n] tile-partitioned (slot << vb | command index)
-  DBuf<uint16_t> toff;  // [tiles][B + 1] tile-local bucket offsets
+  DBuf<uint32_t> hot;   // [16] hot mapped keys the batch was partitioned with
+  DBuf<uint32_t> toff;  // [BT][tiles] tile-local bucket offset | count << 16
   DBuf<uint32_t> mc;    // [B][4][4096] slot tables of multi-chunk buckets
 };
 
@@ -62,6 +63,28 @@ struct KeyBucketClock {
 };
 constexpr size_t kKeyBucketClockWords = 8 * 512;
 
+// Workgroup schedule of the order role (a performance hint; any permutation
+// orders correctly): order launches record each bucket's size, and
+// keybucket_sched turns the last recorded sizes into a largest-first
+// permutation used by the following launches, so the few Zipf-hot buckets
+// start in the first round of workgroups instead of finishing last.
+//
+// Hot keys: a key with at least hot_min commands in one batch (a Zipf head)
+// is routed by the partition to one of 16 hot-key buckets after the B
+// regular ones; such a bucket holds one key, so it needs no sort, and the
+// regular buckets stay near n / B.  Order launches offer candidates (key
+// runs >= hot_min); keybucket_sched rebuilds the table.
+struct KeyBucketSched {
+  DBuf<uint32_t> sizes;  // [BT] commands per bucket (B regular + 16 hot), last order launch
+  DBuf<uint32_t> perm;   // [BT] workgroup -> bucket
+  DBuf<uint32_t> hot;    // [16] hot mapped keys (~0 empty), [1] candidates, [64][2] (count, key)
+  uint32_t B = 0;        // BT of the plan the buffers were prepared for
+  int bb = -1;
+  uint32_t hot_min = 0;
+  bool valid = false;    // perm computed for this width
+};
+void keybucket_sched(KeyBucketSched &sc, hipStream_t s);
+
 // Both launches on stream s.  Outputs, in key-grouped order (buckets
 // ascending, slots ascending, arrival order inside a key): sk = key ids,
 // sv = command indices, dep_sorted = dependency of that command (0 none,
@@ -71,16 +94,16 @@ constexpr size_t kKeyBucketClockWords = 8 * 512;
 void keybucket_run(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32, const uint64_t *dot,
                    uint64_t log_base, uint64_t *latest, const KeyBucketClock &clock,
                    KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                   hipStream_t s);
+                   hipStream_t s, KeyBucketSched *sc = nullptr);
 
 // The two launches separately: keybucket_order reads the workspace
 // keybucket_partition filled; clk = the shard set of that batch.
 void keybucket_partition(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32,
                          const uint64_t *dot, unsigned long long *clk, KeyBucketWorkspace &ws,
-                         hipStream_t s);
+                         hipStream_t s, KeyBucketSched *sc = nullptr);
 void keybucket_order(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
                      KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                     const KeyBucketClock &clock, hipStream_t s);
+                     const KeyBucketClock &clock, hipStream_t s, KeyBucketSched *sc = nullptr);
 
 // One launch that orders batch b (partitioned earlier into ws, clock shards
 // clock.fold) and partitions batch b+1 (p2 / n2 / key32_2 / dot_2) into ws2
@@ -89,6 +112,6 @@ void keybucket_step(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint6
                     KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
                     const KeyBucketClock &clock, const KeyBucketPlan &p2, uint32_t n2,
                     const uint32_t *key32_2, const uint64_t *dot_2, unsigned long long *clk,
-                    KeyBucketWorkspace &ws2, hipStream_t s);
+                    KeyBucketWorkspace &ws2, hipStream_t s, KeyBucketSched *sc = nullptr);
 
 }  // namespace fh

@@ -53,9 +53,17 @@ constexpr int kMaxTiles = 1024;           // batches up to 4M commands
 // order
 constexpr int kOThreads = 1024;
 constexpr int kOWaves = kOThreads / 64;
-constexpr int kChunk = kOThreads * 16;    // bucket commands staged in LDS at once
+constexpr int kChunk = kOThreads * 8;     // bucket commands staged in LDS at once
+                                          // (2 order workgroups fit one CU)
 constexpr int kSlotBits = 12;             // at most 4096 keys per bucket
 constexpr int kDigit = 6;                 // LDS sort digit bits
+constexpr int kHot = 16;                  // hot-key buckets (after the B regular ones)
+constexpr int kCand = 64;                 // hot-key candidates per schedule refresh
+// hot table words: [kHot] mapped keys, [1] candidate count, [kCand][2] (count, key)
+constexpr int kHotWords = kHot + 1 + 2 * kCand;
+#ifndef FH_MATCH_BLOCK
+#define FH_MATCH_BLOCK 4                  // items whose ballot matches are interleaved
+#endif
 
 // Peer masks of N independent items at once: peers[i] = lanes whose BITS-bit
 // value d[i] equals this lane's (valid lanes only).  The bits loop is
@@ -70,10 +78,12 @@ __device__ __forceinline__ void match_many(const uint32_t (&d)[N], const bool (&
   for (int b = 0; b < BITS; b++) {
 #pragma unroll
     for (int i = 0; i < N; i++) {
-      const uint32_t bit = (d[i] >> b) & 1u;
-      const uint64_t m = __ballot(bit);
-      const uint32_t nm = bit - 1u;  // 0 if bit, else all ones
-      peers[i] &= m ^ ((uint64_t(nm) << 32) | nm);
+      // m = lanes with bit b set; mk = all ones where this lane's bit is set;
+      // keep the lanes whose bit equals ours: ~(m ^ mk) on both halves
+      const uint64_t m = __builtin_amdgcn_ballot_w64(__builtin_amdgcn_ubfe(d[i], b, 1) != 0u);
+      const uint32_t mk = uint32_t(__builtin_amdgcn_sbfe(int(d[i]), b, 1));
+      const uint32_t lo = ~(uint32_t(m) ^ mk), hi = ~(uint32_t(m >> 32) ^ mk);
+      peers[i] &= (uint64_t(hi) << 32) | lo;
     }
   }
 }
@@ -160,14 +170,38 @@ struct PartSmem {
   static constexpr size_t bytes = tmp + 2 * kWaves * 4;
 };
 
+// A tile's inputs, loaded into registers (item i of lane l in wave w is
+// command base + w 64 kItems + i 64 + l).  The fused step issues these loads
+// before ordering a bucket, so they land while the bucket is sorted.
+struct TileLoad {
+  uint32_t key[kItems];
+  uint64_t dot[kItems];
+};
+
+__device__ __forceinline__ void tile_load(uint32_t bid, uint32_t n,
+                                          const uint32_t *__restrict__ key32,
+                                          const uint64_t *__restrict__ dot, TileLoad &tl) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t base = bid * kTile;
+#pragma unroll
+  for (int i = 0; i < kItems; i++) {
+    const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + lane;
+    tl.key[i] = idx < n ? key32[idx] : 0u;
+    tl.dot[i] = idx < n ? dot[idx] : 0ull;
+  }
+}
+
+// Bucket ids: 0..B-1 by the high bits of the mapped key, B + h for hot key
+// h of the hot table (its commands need no sort: one key).
 template <int BB>
 __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb, int hb, int vb,
                                                uint32_t kmul, uint32_t kmask,
-                                               const uint32_t *__restrict__ key32,
-                                               const uint64_t *__restrict__ dot,
+                                               const TileLoad &tl,
                                                uint32_t *__restrict__ part,
-                                               uint16_t *__restrict__ toff,
+                                               uint32_t *__restrict__ toff,
                                                unsigned long long *__restrict__ clk,
+                                               const uint32_t *__restrict__ hot,
+                                               uint32_t *__restrict__ hot_snap,
                                                unsigned char *smem) {
   const uint32_t fh_bid = bid;
   (void)fh_bid;
@@ -182,8 +216,13 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
   uint32_t *s_nc = reinterpret_cast<uint32_t *>(smem + L::nc);
   uint32_t *s_tmp = reinterpret_cast<uint32_t *>(smem + L::tmp);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t B = 1u << bb;
+  const uint32_t B = 1u << bb, BT = B + kHot;
+  const int mb = 32 - __builtin_clz(BT - 1);  // bucket-id bits
   for (int i = tid; i < kWaves * BMAX; i += kThreads) (&s_wh[0][0])[i] = 0;
+  uint32_t hv[kHot];  // hot mapped keys (~0: empty), wave-uniform
+#pragma unroll
+  for (int j = 0; j < kHot; j++) hv[j] = hot ? hot[j] : ~0u;
+  if (bid == 0 && tid < kHot) hot_snap[tid] = hot ? hot[tid] : ~0u;
   if (tid < 256) {
     s_mx[tid] = 0;
     s_nc[tid] = 0;
@@ -198,8 +237,8 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + lane;
     vld[i] = idx < n;
-    pk[i] = vld[i] ? key32[idx] : 0u;
-    d[i] = vld[i] ? dot[idx] : 0ull;
+    pk[i] = tl.key[i];
+    d[i] = tl.dot[i];
   }
   __syncthreads();
   FH_PHASE(0, 0);
@@ -210,10 +249,13 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + lane;
     const uint32_t p = (pk[i] * kmul) & kmask;
-    bkt[i] = p >> hb;
-    pk[i] = ((p & smask) << vb) | idx;
+    uint32_t h = ~0u;
+#pragma unroll
+    for (int j = 0; j < kHot; j++) h = hv[j] == p ? uint32_t(j) : h;
+    bkt[i] = h == ~0u ? p >> hb : B + h;
+    pk[i] = (h == ~0u ? (p & smask) << vb : 0u) | idx;
   }
-  match_n<kItems>(bb, bkt, vld, peers);
+  match_n<kItems>(mb, bkt, vld, peers);
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     if (vld[i]) {
@@ -233,7 +275,7 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
   for (int r = 0; r < RB; r++) {
     const uint32_t bk = uint32_t(tid) * RB + r;
     uint32_t c = 0;
-    if (bk < B) {
+    if (bk < BT) {
       uint32_t cw[kWaves];
 #pragma unroll
       for (int ww = 0; ww < kWaves; ww++) cw[ww] = s_wh[ww][bk];
@@ -248,17 +290,17 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
   }
   uint32_t tot;
   uint32_t pre = block_scan<kWaves>(sum, s_tmp, &tot);
-  uint16_t *row = toff + size_t(bid) * (B + 1);
+  // bucket-major: the order role reads its bucket's row of all tiles at once
+  const uint32_t tiles = (n + kTile - 1) / kTile;
 #pragma unroll
   for (int r = 0; r < RB; r++) {
     const uint32_t bk = uint32_t(tid) * RB + r;
-    if (bk < B) {
+    if (bk < BT) {
       s_dex[bk] = pre;
-      row[bk] = uint16_t(pre);
+      toff[size_t(bk) * tiles + bid] = pre | (loc[r] << 16);
     }
     pre += loc[r];
   }
-  if (tid == 0) row[B] = uint16_t(tile_n);
   __syncthreads();
   FH_PHASE(0, 2);
 #pragma unroll
@@ -285,47 +327,49 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
 // ---------------------------------------------------------------- order
 // Helpers of k_kb_order (all inlined; LDS arrays passed explicitly).
 
-// tile run holding bucket element q: s_rs[t] <= q < s_rs[t + 1]
+// tile run holding bucket element q: the last t < tiles with s_rs[t] <= q
+// (fixed-step search, so several searches interleave)
 __device__ __forceinline__ uint32_t run_of(const uint32_t *s_rs, uint32_t tiles, uint32_t q) {
-  uint32_t tl = 0, th = tiles;
-  while (th - tl > 1) {
-    const uint32_t mid = (tl + th) >> 1;
-    if (s_rs[mid] <= q) tl = mid;
-    else th = mid;
-  }
-  return tl;
+  uint32_t t = 0;
+#pragma unroll
+  for (uint32_t st = kMaxTiles / 2; st >= 1; st >>= 1)
+    if (t + st < tiles && s_rs[t + st] <= q) t += st;
+  return t;
 }
 
-// bucket elements [c0, c0 + c) -> dst[0, c): thread t copies the part of
-// tile t's run that falls in the window (tiles <= threads)
-__device__ __forceinline__ void gather_runs(const uint32_t *__restrict__ part, const uint32_t *s_rs,
-                                            const uint32_t *s_src, uint32_t tiles, uint32_t c0,
-                                            uint32_t c, uint32_t *dst) {
-  const uint32_t t = threadIdx.x;
-  if (t >= tiles) return;
-  const uint32_t r0 = s_rs[t], r1 = s_rs[t + 1];
-  const uint32_t a = max(r0, c0), e = min(r1, c0 + c);
-  if (a >= e) return;
-  const uint32_t *src = part + s_src[t] + (a - r0);
-  uint32_t *out = dst + (a - c0);
-  const uint32_t len = e - a;
-  uint32_t j = 0;
-  for (; j + 4 <= len; j += 4) {
-    const uint32_t x0 = src[j], x1 = src[j + 1], x2 = src[j + 2], x3 = src[j + 3];
-    out[j] = x0;
-    out[j + 1] = x1;
-    out[j + 2] = x2;
-    out[j + 3] = x3;
+// Bucket elements [c0, c0 + c) into registers: element c0 + q with
+// q = w 64 IT + i 64 + lane is item i of this thread (the layout of the sort
+// passes).  The IT run searches interleave and every load is in flight at once.
+template <int IT>
+__device__ __forceinline__ void gather_items(const uint32_t *__restrict__ part,
+                                             const uint32_t *s_rs, const uint32_t *s_src,
+                                             uint32_t tiles, uint32_t c0, uint32_t c,
+                                             uint32_t (&xe)[IT]) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t g[IT], t[IT];
+#pragma unroll
+  for (int i = 0; i < IT; i++) {
+    g[i] = c0 + min(w * 64 * IT + uint32_t(i) * 64 + lane, c - 1);
+    t[i] = 0;
   }
-  for (; j < len; j++) out[j] = src[j];
+#pragma unroll
+  for (uint32_t st = kMaxTiles / 2; st >= 1; st >>= 1)
+#pragma unroll
+    for (int i = 0; i < IT; i++)
+      if (t[i] + st < tiles && s_rs[t[i] + st] <= g[i]) t[i] += st;
+#pragma unroll
+  for (int i = 0; i < IT; i++) {
+    const uint32_t q = w * 64 * IT + uint32_t(i) * 64 + lane;
+    xe[i] = q < c ? part[s_src[t[i]] + (g[i] - s_rs[t[i]])] : 0u;
+  }
 }
 
 // Ranks of items [H0, H0 + HALF) of a sort pass (then the next block of
 // items): ballot matches for the block, then the ordered per-wave counts.
-template <int IT, int HALF, int H0>
-__device__ __forceinline__ void rank_items(const uint32_t *src, uint32_t c, int vb, int shift,
-                                           int nbits, uint32_t (*s_h)[1 << kDigit],
-                                           uint32_t (&rk)[IT]) {
+template <int IT, int HALF, int H0, int NBITS>
+__device__ __forceinline__ void rank_items(const uint32_t (&xe)[IT], uint32_t c, int vb, int shift,
+                                           uint32_t (*s_h)[1 << kDigit], uint32_t (&rk)[IT]) {
+  constexpr int nbits = NBITS;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (uint64_t(1) << lane) - 1;
   const uint32_t dm = (1u << nbits) - 1;
@@ -336,35 +380,40 @@ __device__ __forceinline__ void rank_items(const uint32_t *src, uint32_t c, int 
   for (int i = 0; i < HALF; i++) {
     const uint32_t q = uint32_t(w) * 64 * IT + uint32_t(H0 + i) * 64 + lane;
     vld[i] = q < c;
-    dg[i] = vld[i] ? ((src[q] >> vb) >> shift) & dm : 0u;
+    dg[i] = vld[i] ? ((xe[H0 + i] >> vb) >> shift) & dm : 0u;
   }
-  match_n<HALF>(nbits, dg, vld, peers);
+  match_many<NBITS, HALF>(dg, vld, peers);
 #pragma unroll
   for (int i = 0; i < HALF; i++) {
     const uint32_t b0 = vld[i] ? s_h[w][dg[i]] : 0u;
     if (vld[i] && (peers[i] & lt) == 0) s_h[w][dg[i]] = b0 + uint32_t(__popcll(peers[i]));
     rk[H0 + i] = b0 + uint32_t(__popcll(peers[i] & lt));
   }
-  if constexpr (H0 + HALF < IT) rank_items<IT, HALF, H0 + HALF>(src, c, vb, shift, nbits, s_h, rk);
+  if constexpr (H0 + HALF < IT)
+    rank_items<IT, HALF, H0 + HALF, NBITS>(xe, c, vb, shift, s_h, rk);
 }
 
-// One stable LDS pass over src[0, c) by slot bits [shift, shift + nbits).
+// One stable pass over the elements [0, c) held in registers (xe, layout of
+// gather_items) by slot bits [shift, shift + nbits), scattered into dst.
 // Element q is item (q / 64) % IT of lane q % 64 in wave q / (64 IT), so
 // (wave, item, lane) order is element order and ballot ranks keep it stable.
-template <int IT>
-__device__ __forceinline__ void slot_sort_pass(const uint32_t *src, uint32_t *dst, uint32_t c,
-                                               int vb, int shift, int nbits,
-                                               uint32_t (*s_h)[1 << kDigit], uint32_t *s_db,
-                                               bool stamp) {
+// s_h must be zero on entry when `zeroed`.
+template <int IT, int NBITS>
+__device__ __forceinline__ void slot_sort_pass(const uint32_t (&xe)[IT], uint32_t *dst, uint32_t c,
+                                               int vb, int shift, uint32_t (*s_h)[1 << kDigit],
+                                               uint32_t *s_db, bool zeroed, bool stamp) {
+  constexpr int nbits = NBITS;
   constexpr int ND = 1 << kDigit;
-  constexpr int HALF = IT < 4 ? IT : 4;
+  constexpr int HALF = IT < FH_MATCH_BLOCK ? IT : IT % FH_MATCH_BLOCK == 0 ? FH_MATCH_BLOCK : IT % 3 == 0 ? 3 : 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < kOWaves * ND; i += kOThreads) (&s_h[0][0])[i] = 0;
-  __syncthreads();
+  if (!zeroed) {
+    for (int i = tid; i < kOWaves * ND; i += kOThreads) (&s_h[0][0])[i] = 0;
+    __syncthreads();
+  }
   if (stamp) FH_PHASE(1, 4);
   uint32_t rk[IT];
   const uint32_t dm = (1u << nbits) - 1;
-  rank_items<IT, HALF, 0>(src, c, vb, shift, nbits, s_h, rk);
+  rank_items<IT, HALF, 0, NBITS>(xe, c, vb, shift, s_h, rk);
   __syncthreads();
   if (stamp) FH_PHASE(1, 5);
   if (w == 0) {
@@ -392,32 +441,86 @@ __device__ __forceinline__ void slot_sort_pass(const uint32_t *src, uint32_t *ds
   for (int i = 0; i < IT; i++) {
     const uint32_t q = uint32_t(w) * 64 * IT + uint32_t(i) * 64 + lane;
     if (q < c) {
-      const uint32_t e = src[q], d = ((e >> vb) >> shift) & dm;
+      const uint32_t e = xe[i], d = ((e >> vb) >> shift) & dm;
       dst[s_db[d] + s_h[w][d] + rk[i]] = e;
     }
   }
   __syncthreads();
 }
 
-// sorts a[0, c) by slot (0..2 passes); returns the buffer holding the result
+// one pass with the digit width chosen at run time (the passes themselves
+// are compiled per width, so their inner loops have no width branches)
 template <int IT>
-__device__ __forceinline__ const uint32_t *sort_chunk(uint32_t *a, uint32_t *b, uint32_t c,
-                                                      int vb, int hb,
-                                                      uint32_t (*s_h)[1 << kDigit],
-                                                      uint32_t *s_db) {
-  if (hb == 0) return a;
+__device__ __forceinline__ void slot_sort_pass_n(const uint32_t (&xe)[IT], uint32_t *dst,
+                                                 uint32_t c, int vb, int shift, int nbits,
+                                                 uint32_t (*s_h)[1 << kDigit], uint32_t *s_db,
+                                                 bool zeroed, bool stamp) {
+  switch (nbits) {
+#define FH_PASS_CASE(K) \
+  case K: slot_sort_pass<IT, K>(xe, dst, c, vb, shift, s_h, s_db, zeroed, stamp); break;
+    FH_PASS_CASE(1) FH_PASS_CASE(2) FH_PASS_CASE(3) FH_PASS_CASE(4) FH_PASS_CASE(5)
+#undef FH_PASS_CASE
+    default: slot_sort_pass<IT, 6>(xe, dst, c, vb, shift, s_h, s_db, zeroed, stamp); break;
+  }
+}
+
+// Sorts the c elements in xe (gather_items layout) by slot (0..2 passes)
+// into a or b; returns the buffer holding the result.  The passes use the
+// digit tables s_h0 / s_h1, zero on entry when `zeroed`.
+template <int IT>
+__device__ __forceinline__ const uint32_t *sort_chunk(const uint32_t (&xe)[IT], uint32_t *a,
+                                                      uint32_t *b, uint32_t c, int vb, int hb,
+                                                      uint32_t (*s_h0)[1 << kDigit],
+                                                      uint32_t (*s_h1)[1 << kDigit],
+                                                      uint32_t *s_db, bool zeroed) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (hb == 0) {
+#pragma unroll
+    for (int i = 0; i < IT; i++) {
+      const uint32_t q = w * 64 * IT + uint32_t(i) * 64 + lane;
+      if (q < c) a[q] = xe[i];
+    }
+    __syncthreads();
+    return a;
+  }
   if (hb <= kDigit) {
-    slot_sort_pass<IT>(a, b, c, vb, 0, hb, s_h, s_db, true);
+    slot_sort_pass_n<IT>(xe, b, c, vb, 0, hb, s_h0, s_db, zeroed, true);
     return b;
   }
-  slot_sort_pass<IT>(a, b, c, vb, 0, kDigit, s_h, s_db, true);
-  slot_sort_pass<IT>(b, a, c, vb, kDigit, hb - kDigit, s_h, s_db, false);
+  slot_sort_pass<IT, kDigit>(xe, b, c, vb, 0, s_h0, s_db, zeroed, true);
+  uint32_t x2[IT];
+#pragma unroll
+  for (int i = 0; i < IT; i++) {
+    const uint32_t q = w * 64 * IT + uint32_t(i) * 64 + lane;
+    x2[i] = q < c ? b[q] : 0u;
+  }
+  slot_sort_pass_n<IT>(x2, a, c, vb, kDigit, hb - kDigit, s_h1, s_db, zeroed, false);
   return a;
 }
 
-// A bucket that fits one chunk: gather, sort, write the sorted chunk as is
-// (contiguous output), heads read latest; the tails' dots are loaded in the
-// same sweep and written to latest after every head has read it.
+// A bucket that fits one chunk: gather into registers, sort, write the
+// sorted chunk as is (contiguous output).  With the bucket's latest slice
+// staged in LDS (s_lat, `staged`) heads read it there and tails write latest
+// in the same sweep; otherwise heads read latest and tails write it after a
+// barrier.
+// A key run of at least `hot_min` commands ending at sorted position j
+// (its tail) is offered as a hot-key candidate (count, mapped key).
+__device__ __forceinline__ void note_hot(const uint32_t *S, uint32_t j, uint32_t slot, int vb,
+                                         uint32_t mk, uint32_t hot_min, uint32_t *cand) {
+  if (!cand || hot_min == 0 || j + 1 < hot_min || (S[j + 1 - hot_min] >> vb) != slot) return;
+  uint32_t lo = 0, hi = j + 1 - hot_min;  // first position of the run
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((S[mid] >> vb) < slot) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint32_t i = atomicAdd(&cand[kHot], 1u);
+  if (i < uint32_t(kCand)) {
+    cand[kHot + 1 + 2 * i] = j - lo + 1;
+    cand[kHot + 2 + 2 * i] = mk;
+  }
+}
+
 template <int IT>
 __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32_t b, int hb,
                                              int vb, uint32_t kinv, uint32_t kmask,
@@ -425,16 +528,35 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
                                              uint64_t log_base, uint64_t *__restrict__ latest,
                                              uint32_t *__restrict__ sk, uint32_t *__restrict__ sv,
                                              uint64_t *__restrict__ dep_sorted, uint32_t *s_a,
-                                             uint32_t *s_b, uint32_t (*s_h)[1 << kDigit],
-                                             uint32_t *s_db, const uint32_t *s_rs,
-                                             const uint32_t *s_src) {
+                                             uint32_t *s_b, uint32_t (*s_h0)[1 << kDigit],
+                                             uint32_t (*s_h1)[1 << kDigit], uint32_t *s_db,
+                                             const uint32_t *s_rs, const uint32_t *s_src,
+                                             const uint64_t *s_lat, bool staged,
+                                             uint32_t hot_min, uint32_t *cand) {
   const uint32_t tid = threadIdx.x;
   const uint32_t vmask = (1u << vb) - 1;
-  gather_runs(part, s_rs, s_src, tiles, 0, Nb, s_a);
-  __syncthreads();
+  uint32_t xe[IT];
+  gather_items<IT>(part, s_rs, s_src, tiles, 0, Nb, xe);
   FH_PHASE(1, 1);
-  const uint32_t *S = sort_chunk<IT>(s_a, s_b, Nb, vb, hb, s_h, s_db);
+  const uint32_t *S = sort_chunk<IT>(xe, s_a, s_b, Nb, vb, hb, s_h0, s_h1, s_db, true);
   FH_PHASE(1, 2);
+  if (staged) {
+    for (uint32_t j = tid; j < Nb; j += kOThreads) {
+      const uint32_t e = S[j], slot = e >> vb, vid = e & vmask;
+      const uint32_t mk = (b << hb) | slot;  // mapped key
+      const uint32_t pos = gbase + j;
+      sk[pos] = (mk * kinv) & kmask;
+      sv[pos] = vid;
+      dep_sorted[pos] = j == 0 || (S[j - 1] >> vb) != slot ? s_lat[slot]
+                                                            : uint64_t(S[j - 1] & vmask) + 1;
+      if (j + 1 == Nb || (S[j + 1] >> vb) != slot) {
+        latest[mk] = kLogFlag | (log_base + vid);
+        note_hot(S, j, slot, vb, mk, hot_min, cand);
+      }
+    }
+    FH_PHASE(1, 3);
+    return;
+  }
   for (uint32_t j = tid; j < Nb; j += kOThreads) {
     const uint32_t e = S[j], slot = e >> vb, vid = e & vmask;
     const uint32_t mk = (b << hb) | slot;  // mapped key
@@ -448,9 +570,47 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
   FH_PHASE(1, 3);
   for (uint32_t j = tid; j < Nb; j += kOThreads) {
     const uint32_t e = S[j], slot = e >> vb;
-    if (j + 1 == Nb || (S[j + 1] >> vb) != slot)
+    if (j + 1 == Nb || (S[j + 1] >> vb) != slot) {
       latest[(b << hb) | slot] = kLogFlag | (log_base + (e & vmask));
+      note_hot(S, j, slot, vb, (b << hb) | slot, hot_min, cand);
+    }
   }
+}
+
+// A hot-key bucket: one key, so its commands in arrival order are its
+// sequence; each depends on the previous one, the first on latest[mk].
+__device__ __forceinline__ void order_hot(uint32_t Nb, uint32_t gbase, uint32_t mk, int vb,
+                                          uint32_t kinv, uint32_t kmask, uint32_t tiles,
+                                          const uint32_t *__restrict__ part, uint64_t log_base,
+                                          uint64_t *__restrict__ latest,
+                                          uint32_t *__restrict__ sk, uint32_t *__restrict__ sv,
+                                          uint64_t *__restrict__ dep_sorted, uint32_t *s_a,
+                                          const uint32_t *s_rs, const uint32_t *s_src) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t vmask = (1u << vb) - 1;
+  const uint32_t key = (mk * kinv) & kmask;
+  const uint64_t first = latest[mk];
+  uint64_t prev = first;  // dependency of the next chunk's first command
+  for (uint32_t c0 = 0; c0 < Nb; c0 += kChunk) {
+    const uint32_t c = min(Nb - c0, uint32_t(kChunk));
+    uint32_t xe[8];
+    gather_items<8>(part, s_rs, s_src, tiles, c0, c, xe);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t q = w * 64 * 8 + uint32_t(i) * 64 + lane;
+      if (q < c) s_a[q] = xe[i] & vmask;
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < c; j += kOThreads) {
+      const uint32_t pos = gbase + c0 + j;
+      sk[pos] = key;
+      sv[pos] = s_a[j];
+      dep_sorted[pos] = j ? uint64_t(s_a[j - 1]) + 1 : prev;
+    }
+    prev = uint64_t(s_a[c - 1]) + 1;
+    __syncthreads();  // s_a is rewritten by the next chunk
+  }
+  if (tid == 0) latest[mk] = kLogFlag | (log_base + (prev - 1));
 }
 
 // One bucket per 1024-thread workgroup.  The bucket's commands are the
@@ -465,20 +625,23 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
 struct OrderSmem {
   static constexpr size_t a = 0;                                      // u32 [kChunk]
   static constexpr size_t b = a + size_t(kChunk) * 4;                 // u32 [kChunk]
-  static constexpr size_t h = b + size_t(kChunk) * 4;                 // u32 [kOWaves][ND]
-  static constexpr size_t db = h + size_t(kOWaves) * (1 << kDigit) * 4;  // u32 [ND]
+  static constexpr size_t lat = b + size_t(kChunk) * 4;               // u64 [1 << kSlotBits]
+  static constexpr size_t h = lat + (size_t(1) << kSlotBits) * 8;     // u32 [2][kOWaves][ND]
+  static constexpr size_t db = h + 2 * size_t(kOWaves) * (1 << kDigit) * 4;  // u32 [ND]
   static constexpr size_t rs = db + (1 << kDigit) * 4;                // u32 [kMaxTiles + 1]
   static constexpr size_t src = rs + size_t(kMaxTiles + 1) * 4 + 12;  // u32 [kMaxTiles]
   static constexpr size_t tmp = src + size_t(kMaxTiles) * 4;          // u32 [2 kOWaves]
   static constexpr size_t bytes = tmp + 2 * kOWaves * 4;
 };
-constexpr size_t kSmemBytes = OrderSmem::bytes > PartSmem<10>::bytes ? OrderSmem::bytes
-                                                                      : PartSmem<10>::bytes;
+template <int BB>
+constexpr size_t step_smem_bytes() {
+  return OrderSmem::bytes > PartSmem<BB>::bytes ? OrderSmem::bytes : PartSmem<BB>::bytes;
+}
 
 __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb, int hb, int vb,
                                              uint32_t kinv, uint32_t kmask,
                                              const uint32_t *__restrict__ part,
-                                             const uint16_t *__restrict__ toff,
+                                             const uint32_t *__restrict__ toff,
                                              uint64_t log_base, uint64_t *__restrict__ latest,
                                              uint32_t *__restrict__ sk, uint32_t *__restrict__ sv,
                                              uint64_t *__restrict__ dep_sorted,
@@ -486,6 +649,9 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
                                              unsigned long long *__restrict__ clk_fold,
                                              unsigned long long *__restrict__ frontier,
                                              unsigned long long *__restrict__ excount,
+                                             uint32_t *__restrict__ sizes,
+                                             const uint32_t *__restrict__ hot_snap,
+                                             uint32_t hot_min, uint32_t *__restrict__ cand,
                                              unsigned char *smem) {
   const uint32_t fh_bid = b;
   (void)fh_bid;
@@ -495,13 +661,16 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
   uint32_t *s_a = reinterpret_cast<uint32_t *>(smem + OrderSmem::a);
   uint32_t *s_b = reinterpret_cast<uint32_t *>(smem + OrderSmem::b);
   uint32_t(*s_h)[ND] = reinterpret_cast<uint32_t(*)[ND]>(smem + OrderSmem::h);
+  uint32_t(*s_h1)[ND] = s_h + kOWaves;
+  uint64_t *s_lat = reinterpret_cast<uint64_t *>(smem + OrderSmem::lat);
   uint32_t *s_db = reinterpret_cast<uint32_t *>(smem + OrderSmem::db);
   uint32_t *s_rs = reinterpret_cast<uint32_t *>(smem + OrderSmem::rs);  // run start per tile
   uint32_t *s_src = reinterpret_cast<uint32_t *>(smem + OrderSmem::src);  // run start in part[]
   uint32_t *s_tmp = reinterpret_cast<uint32_t *>(smem + OrderSmem::tmp);
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t B = 1u << bb, H = 1u << hb;
-  if (clk_fold && b + 1 == B && tid < 256) {
+  const bool hot = b >= B;  // hot-key bucket B + h
+  if (clk_fold && b == 0 && tid < 256) {
     // the executed clock advances by this batch (its partition wrote the
     // shards in an earlier launch): frontier = max, excount += count
     unsigned long long mx = frontier[tid], cnt = 0;
@@ -519,15 +688,32 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
   const uint32_t vmask = (1u << vb) - 1;
   const uint64_t lt = (uint64_t(1) << lane) - 1;
 
-  // this bucket's run in every tile (tiles <= threads)
+  // this bucket's run in every tile (tiles <= threads): one row of the
+  // bucket-major table, lo | count << 16
   uint32_t lo = 0, cn = 0;
   if (uint32_t(tid) < tiles) {
-    const uint16_t *row = toff + size_t(tid) * (B + 1);
-    lo = row[b];
-    cn = uint32_t(row[b + 1]) - lo;
+    const uint32_t x = toff[size_t(b) * tiles + tid];
+    lo = x & 0xFFFFu;
+    cn = x >> 16;
   }
+  // The bucket's latest slice (H entries, contiguous under the key mapping)
+  // is loaded now and staged in LDS before the sort, when it is not much
+  // larger than an average bucket; the loads overlap the scan and gather.
+  constexpr int LR = (1 << kSlotBits) / kOThreads;
+  const bool staged = !hot && H <= 2u * ((uint32_t(tiles) * uint32_t(kTile)) >> bb);
+  uint64_t lv[LR];
+  if (staged) {
+#pragma unroll
+    for (int r = 0; r < LR; r++) {
+      const uint32_t k = uint32_t(r) * kOThreads + tid;
+      lv[r] = k < H ? latest[(size_t(b) << hb) + k] : 0ull;
+    }
+  }
+  // digit tables of both sort passes start at zero
+  for (int i = tid; i < 2 * kOWaves * ND; i += kOThreads) (&s_h[0][0])[i] = 0;
   uint32_t pre, lpre, Nb, gbase;
   block_scan2<kOWaves>(cn, lo, s_tmp, &pre, &lpre, &Nb, &gbase);  // gbase: lower buckets
+  if (sizes && tid == 0) sizes[b] = Nb;
   if (uint32_t(tid) < tiles) {
     s_rs[tid] = pre;
     s_src[tid] = uint32_t(tid) * uint32_t(kTile) + lo;
@@ -537,17 +723,30 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
     FH_STAMP_END(1, 0);
     return;
   }
+  if (staged) {
+#pragma unroll
+    for (int r = 0; r < LR; r++) {
+      const uint32_t k = uint32_t(r) * kOThreads + tid;
+      if (k < H) s_lat[k] = lv[r];
+    }
+  }
   __syncthreads();
   FH_PHASE(1, 0);
 
+  if (hot) {
+    order_hot(Nb, gbase, hot_snap[b - B], vb, kinv, kmask, tiles, part, log_base, latest, sk, sv,
+              dep_sorted, s_a, s_rs, s_src);
+    FH_STAMP_END(1, Nb);
+    return;
+  }
   if (Nb <= uint32_t(kChunk)) {
 #define FH_ORDER_SINGLE(IT)                                                                 \
   order_single<IT>(Nb, gbase, b, hb, vb, kinv, kmask, tiles, part, log_base, latest, sk, sv, \
-                   dep_sorted, s_a, s_b, s_h, s_db, s_rs, s_src)
+                   dep_sorted, s_a, s_b, s_h, s_h1, s_db, s_rs, s_src, s_lat, staged, hot_min, cand)
     if (Nb <= 2048) FH_ORDER_SINGLE(2);
     else if (Nb <= 4096) FH_ORDER_SINGLE(4);
-    else if (Nb <= 8192) FH_ORDER_SINGLE(8);
-    else FH_ORDER_SINGLE(16);
+    else if (Nb <= 6144) FH_ORDER_SINGLE(6);
+    else FH_ORDER_SINGLE(8);
 #undef FH_ORDER_SINGLE
     FH_STAMP_END(1, Nb);
     return;
@@ -598,9 +797,9 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
   __syncthreads();
   for (uint32_t c0 = 0; c0 < Nb; c0 += kChunk) {
     const uint32_t c = min(Nb - c0, uint32_t(kChunk));
-    gather_runs(part, s_rs, s_src, tiles, c0, c, s_a);
-    __syncthreads();
-    const uint32_t *S = sort_chunk<16>(s_a, s_b, c, vb, hb, s_h, s_db);
+    uint32_t xe[8];
+    gather_items<8>(part, s_rs, s_src, tiles, c0, c, xe);
+    const uint32_t *S = sort_chunk<8>(xe, s_a, s_b, c, vb, hb, s_h, s_h1, s_db, false);
     for (uint32_t j = tid; j < c; j += kOThreads) {
       const uint32_t slot = S[j] >> vb;
       if (j == 0 || (S[j - 1] >> vb) != slot) g_hpos[slot] = j;
@@ -632,56 +831,159 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
     __syncthreads();
   }
   // the key's last command becomes latest (after every head read above)
-  for (uint32_t k = tid; k < H; k += kOThreads)
-    if (g_ccnt[k]) latest[(b << hb) | k] = kLogFlag | (log_base + g_clast[k]);
+  for (uint32_t k = tid; k < H; k += kOThreads) {
+    const uint32_t cnt = g_ccnt[k];
+    if (cnt) latest[(b << hb) | k] = kLogFlag | (log_base + g_clast[k]);
+    if (cand && hot_min && cnt >= hot_min) {  // hot-key candidate (see note_hot)
+      const uint32_t i = atomicAdd(&cand[kHot], 1u);
+      if (i < uint32_t(kCand)) {
+        cand[kHot + 1 + 2 * i] = cnt;
+        cand[kHot + 2 + 2 * i] = (b << hb) | k;
+      }
+    }
+  }
   FH_STAMP_END(1, Nb);
 }
 
+// Arguments of the two roles (kernel arguments by value).
+struct OrderArgs {
+  uint32_t tiles;
+  int bb, hb, vb;
+  uint32_t kinv, kmask;
+  const uint32_t *part;
+  const uint32_t *toff;
+  uint64_t log_base;
+  uint64_t *latest;
+  uint32_t *sk, *sv;
+  uint64_t *dep_sorted;
+  uint32_t *mc;
+  unsigned long long *clk_fold, *frontier, *excount;
+  const uint32_t *perm;      // workgroup -> bucket (null: identity)
+  uint32_t *sizes;           // per-bucket sizes for the schedule (nullable)
+  const uint32_t *hot_snap;  // hot keys the batch was partitioned with
+  uint32_t hot_min;
+  uint32_t *cand;            // hot table words (candidates), nullable
+};
+struct PartArgs {
+  uint32_t n;
+  int bb, hb, vb;
+  uint32_t kmul, kmask;
+  const uint32_t *key32;
+  const uint64_t *dot;
+  uint32_t *part, *toff;
+  unsigned long long *clk;
+  const uint32_t *hot;  // hot table (nullable)
+  uint32_t *hot_snap;
+};
+
 template <int BB>
-__global__ void __launch_bounds__(kThreads)
-    k_kb_partition(uint32_t n, int bb, int hb, int vb, uint32_t kmul, uint32_t kmask,
-                   const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot,
-                   uint32_t *__restrict__ part, uint16_t *__restrict__ toff,
-                   unsigned long long *__restrict__ clk) {
+__device__ __forceinline__ void part_role(const PartArgs &a, uint32_t t, const TileLoad &tl,
+                                          unsigned char *smem) {
+  partition_tile<BB>(t, a.n, a.bb, a.hb, a.vb, a.kmul, a.kmask, tl, a.part, a.toff, a.clk, a.hot,
+                     a.hot_snap, smem);
+}
+
+__device__ __forceinline__ void order_role(const OrderArgs &a, uint32_t r, unsigned char *smem) {
+  order_bucket(a.perm ? a.perm[r] : r, a.tiles, a.bb, a.hb, a.vb, a.kinv, a.kmask, a.part, a.toff,
+               a.log_base, a.latest, a.sk, a.sv, a.dep_sorted, a.mc, a.clk_fold, a.frontier,
+               a.excount, a.sizes, a.hot_snap, a.hot_min, a.cand, smem);
+}
+
+template <int BB>
+__global__ void __launch_bounds__(kThreads) k_kb_partition(PartArgs a) {
   __shared__ __align__(16) unsigned char smem[PartSmem<BB>::bytes];
-  partition_tile<BB>(blockIdx.x, n, bb, hb, vb, kmul, kmask, key32, dot, part, toff, clk, smem);
+  TileLoad tl;
+  tile_load(blockIdx.x, a.n, a.key32, a.dot, tl);
+  part_role<BB>(a, blockIdx.x, tl, smem);
 }
 
-__global__ void __launch_bounds__(kOThreads)
-    k_kb_order(uint32_t tiles, int bb, int hb, int vb, uint32_t kinv, uint32_t kmask,
-               const uint32_t *__restrict__ part, const uint16_t *__restrict__ toff,
-               uint64_t log_base, uint64_t *__restrict__ latest, uint32_t *__restrict__ sk,
-               uint32_t *__restrict__ sv, uint64_t *__restrict__ dep_sorted,
-               uint32_t *__restrict__ mc, unsigned long long *__restrict__ clk_fold,
-               unsigned long long *__restrict__ frontier,
-               unsigned long long *__restrict__ excount) {
+__global__ void __launch_bounds__(kOThreads) k_kb_order(OrderArgs a) {
   __shared__ __align__(16) unsigned char smem[OrderSmem::bytes];
-  order_bucket(blockIdx.x, tiles, bb, hb, vb, kinv, kmask, part, toff, log_base, latest, sk, sv,
-               dep_sorted, mc, clk_fold, frontier, excount, smem);
+  order_role(a, blockIdx.x, smem);
 }
 
-// One launch per pipelined step: workgroups [0, B) order batch b (its
-// partition is in workspace wa), workgroups [B, B + tiles') partition batch
-// b+1 into the other workspace.  The two roles touch disjoint memory.
+// One launch per pipelined step: the order role over batch b (its partition
+// is in a's workspace) and the partition role over batch b+1; the roles
+// touch disjoint memory.  Workgroups [0, BT) order the buckets by schedule
+// rank (largest first), the rest partition; workgroups dispatch in index
+// order, so the partition fills the CUs the short buckets release.
+// (Measured alternatives, all slower on MI355X: partition first or
+// interleaved; order + partition in one workgroup; two workgroups per CU.)
 template <int BB>
-__global__ void __launch_bounds__(kOThreads)
-    k_kb_step(uint32_t B_order, uint32_t tiles, int bb, int hb, int vb, uint32_t kinv,
-              uint32_t kmask, const uint32_t *__restrict__ part, const uint16_t *__restrict__ toff,
-              uint64_t log_base, uint64_t *__restrict__ latest, uint32_t *__restrict__ sk,
-              uint32_t *__restrict__ sv, uint64_t *__restrict__ dep_sorted,
-              uint32_t *__restrict__ mc, unsigned long long *__restrict__ clk_fold,
-              unsigned long long *__restrict__ frontier, unsigned long long *__restrict__ excount,
-              uint32_t n2, int bb2, int hb2, int vb2, uint32_t kmul2,
-              uint32_t kmask2, const uint32_t *__restrict__ key32_2,
-              const uint64_t *__restrict__ dot_2, uint32_t *__restrict__ part2,
-              uint16_t *__restrict__ toff2, unsigned long long *__restrict__ clk) {
-  __shared__ __align__(16) unsigned char smem[kSmemBytes];
-  if (blockIdx.x < B_order)
-    order_bucket(blockIdx.x, tiles, bb, hb, vb, kinv, kmask, part, toff, log_base, latest, sk,
-                 sv, dep_sorted, mc, clk_fold, frontier, excount, smem);
-  else
-    partition_tile<BB>(blockIdx.x - B_order, n2, bb2, hb2, vb2, kmul2, kmask2, key32_2, dot_2,
-                       part2, toff2, clk, smem);
+__global__ void __launch_bounds__(kOThreads) k_kb_step(OrderArgs a, uint32_t BT, PartArgs pa) {
+  __shared__ __align__(16) unsigned char smem[step_smem_bytes<BB>()];
+  const uint32_t g = blockIdx.x;
+  if (g < BT) {
+    order_role(a, g, smem);
+    return;
+  }
+  TileLoad tl;
+  tile_load(g - BT, pa.n, pa.key32, pa.dot, tl);
+  part_role<BB>(pa, g - BT, tl, smem);
+}
+
+// Schedule refresh (one workgroup), from the last order launch:
+//  * hot table: the hot keys still above hot_min / 2 commands and the
+//    candidates offered (runs >= hot_min), deduplicated, the kHot largest;
+//  * perm: buckets by recorded size, largest first (ties by index), so the
+//    longest workgroups start in the first round.
+constexpr int kMaxBT = 512 + kHot;
+__global__ void __launch_bounds__(1024)
+    k_kb_sched(uint32_t BT, uint32_t B, uint32_t hot_min, const uint32_t *__restrict__ sizes,
+               uint32_t *__restrict__ perm, uint32_t *__restrict__ hot) {
+  constexpr int NE = kHot + kCand;
+  __shared__ uint32_t s_sz[kMaxBT];
+  __shared__ uint32_t s_cnt[NE], s_key[NE], s_new[kHot];
+  const uint32_t t = threadIdx.x;
+  if (t < BT) s_sz[t] = sizes[t];
+  if (t < uint32_t(kHot)) s_new[t] = ~0u;
+  uint32_t c = 0, k = ~0u;
+  if (t < uint32_t(kHot)) {
+    k = hot[t];
+    c = k != ~0u ? sizes[B + t] : 0u;
+    if (2 * c < hot_min) k = ~0u;
+  } else if (t < uint32_t(NE)) {
+    const uint32_t i = t - kHot;
+    if (i < min(hot[kHot], uint32_t(kCand))) {
+      c = hot[kHot + 1 + 2 * i];
+      k = hot[kHot + 2 + 2 * i];
+    }
+  }
+  if (t < uint32_t(NE)) {
+    s_key[t] = k;
+    s_cnt[t] = k == ~0u ? 0u : c;
+  }
+  __syncthreads();
+  if (t < uint32_t(NE) && k != ~0u) {
+    for (uint32_t j = 0; j < t; j++)
+      if (s_key[j] == k) k = ~0u;  // keep the first entry of a key
+  }
+  __syncthreads();
+  if (t < uint32_t(NE)) {
+    s_key[t] = k;
+    s_cnt[t] = k == ~0u ? 0u : c;
+  }
+  __syncthreads();
+  if (t < uint32_t(NE) && k != ~0u) {
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < uint32_t(NE); j++) {
+      const uint32_t o = s_cnt[j];
+      r += s_key[j] != ~0u && (o > c || (o == c && j < t));
+    }
+    if (r < uint32_t(kHot)) s_new[r] = k;
+  }
+  __syncthreads();
+  if (t < uint32_t(kHot)) hot[t] = s_new[t];
+  if (t == 0) hot[kHot] = 0;
+  if (t < BT) {
+    const uint32_t my = s_sz[t];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < BT; j++) {
+      const uint32_t o = s_sz[j];
+      r += (o > my) || (o == my && j < t);
+    }
+    perm[r] = t;
+  }
 }
 
 }  // namespace
@@ -701,7 +1003,9 @@ void keybucket_map(int kb, uint32_t *kmul, uint32_t *kinv, uint32_t *kmask) {
 KeyBucketPlan keybucket_plan(size_t n, int kb) {
   KeyBucketPlan p;
   p.kb = kb;
-  // >= 256 buckets when the key space allows, at most 4096 keys per bucket
+  // 256 buckets when the key space allows (Zipf-hot keys go to the kHot
+  // hot-key buckets, so the regular ones stay near n / 256), at most 4096
+  // keys each
   p.bb = std::min(kb, 8);
   p.hb = kb - p.bb;
   if (p.hb > kSlotBits) {
@@ -711,65 +1015,147 @@ KeyBucketPlan keybucket_plan(size_t n, int kb) {
   p.vb = bits_for(n ? n : 1);
   p.tiles = uint32_t((n + kTile - 1) / kTile);
   keybucket_map(kb, &p.kmul, &p.kinv, &p.kmask);
-  p.ok = n >= 1 && n < (size_t(1) << 30) && kb >= 1 && kb <= 22 && p.bb <= 10 &&
+  p.ok = n >= 1 && n < (size_t(1) << 30) && kb >= 1 && kb <= 21 && p.bb <= 9 &&
          p.hb + p.vb <= 32 && p.tiles <= uint32_t(kMaxTiles);
   return p;
 }
 
+static uint32_t buckets_total(const KeyBucketPlan &p) { return (1u << p.bb) + kHot; }
+
+// commands of one key in one batch that make it a hot-key candidate
+static uint32_t hot_min_for(const KeyBucketPlan &p) {
+  return std::max<uint32_t>(64, (p.tiles * uint32_t(kTile)) >> (p.bb + 3));
+}
+
+// the schedule's buffers for a plan of BT buckets (reset when BT changes:
+// no hot keys, identity order, until the next refresh)
+static void sched_prepare(KeyBucketSched *sc, const KeyBucketPlan &p, hipStream_t s) {
+  if (!sc) return;
+  const uint32_t BT = buckets_total(p);
+  if (sc->B == BT && sc->bb == p.bb) return;
+  sc->B = BT;
+  sc->bb = p.bb;
+  sc->hot_min = hot_min_for(p);
+  FH_HIP(hipMemsetAsync(sc->sizes.ensure(BT), 0, BT * sizeof(uint32_t), s));
+  sc->perm.ensure(BT);
+  uint32_t *h = sc->hot.ensure(kHotWords);
+  FH_HIP(hipMemsetAsync(h, 0xFF, kHot * sizeof(uint32_t), s));
+  FH_HIP(hipMemsetAsync(h + kHot, 0, (kHotWords - kHot) * sizeof(uint32_t), s));
+  sc->valid = false;
+}
+
+void keybucket_sched(KeyBucketSched &sc, hipStream_t s) {
+  if (sc.B == 0) return;
+  k_kb_sched<<<1, 1024, 0, s>>>(sc.B, sc.B - kHot, sc.hot_min, sc.sizes.get(), sc.perm.get(),
+                                 sc.hot.get());
+  FH_HIP(hipGetLastError());
+  sc.valid = true;
+}
+
+static PartArgs part_args(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32,
+                          const uint64_t *dot, unsigned long long *clk, KeyBucketWorkspace &ws,
+                          KeyBucketSched *sc) {
+  PartArgs a;
+  a.n = n;
+  a.bb = p.bb;
+  a.hb = p.hb;
+  a.vb = p.vb;
+  a.kmul = p.kmul;
+  a.kmask = p.kmask;
+  a.key32 = key32;
+  a.dot = dot;
+  a.part = ws.part.ensure(size_t(n) + 1);
+  a.toff = ws.toff.ensure(size_t(p.tiles) * buckets_total(p));
+  a.clk = clk;
+  a.hot = sc ? sc->hot.get() : nullptr;
+  a.hot_snap = ws.hot.ensure(kHot);
+  return a;
+}
+
+static OrderArgs order_args(const KeyBucketPlan &p, uint64_t log_base, uint64_t *latest,
+                            KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv,
+                            uint64_t *dep_sorted, const KeyBucketClock &clock,
+                            KeyBucketSched *sc) {
+  OrderArgs a;
+  a.tiles = p.tiles;
+  a.bb = p.bb;
+  a.hb = p.hb;
+  a.vb = p.vb;
+  a.kinv = p.kinv;
+  a.kmask = p.kmask;
+  a.part = ws.part.get();
+  a.toff = ws.toff.get();
+  a.log_base = log_base;
+  a.latest = latest;
+  a.sk = sk;
+  a.sv = sv;
+  a.dep_sorted = dep_sorted;
+  // slot tables of buckets larger than one LDS chunk (rare)
+  a.mc = ws.mc.ensure(size_t(1u << p.bb) * 4 * (size_t(1) << kSlotBits));
+  a.clk_fold = clock.fold;
+  a.frontier = clock.frontier;
+  a.excount = clock.excount;
+  a.perm = sc && sc->valid ? sc->perm.get() : nullptr;
+  a.sizes = sc ? sc->sizes.get() : nullptr;
+  a.hot_snap = ws.hot.get();
+  a.hot_min = sc ? sc->hot_min : 0u;
+  a.cand = sc ? sc->hot.get() : nullptr;
+  return a;
+}
+
+template <typename K>
+static K by_bits(int mbits, K k8, K k9, K k10) {
+  return mbits <= 8 ? k8 : mbits == 9 ? k9 : k10;
+}
+static int id_bits(const KeyBucketPlan &p) { return 32 - __builtin_clz(buckets_total(p) - 1); }
+
 void keybucket_partition(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32,
                          const uint64_t *dot, unsigned long long *clk, KeyBucketWorkspace &ws,
-                         hipStream_t s) {
+                         hipStream_t s, KeyBucketSched *sc) {
   FH_CHECK(p.ok, FH_EINVARIANT, "keybucket: batch does not fit the bucket plan");
   if (n == 0) return;
-  const uint32_t B = 1u << p.bb;
-  uint32_t *part = ws.part.ensure(size_t(n) + 1);
-  uint16_t *toff = ws.toff.ensure(size_t(p.tiles) * (B + 1) + 1);
-  auto k1 = p.bb <= 8 ? k_kb_partition<8> : k_kb_partition<10>;
+  sched_prepare(sc, p, s);
+  const PartArgs a = part_args(p, n, key32, dot, clk, ws, sc);
+  auto k1 = by_bits(id_bits(p), k_kb_partition<8>, k_kb_partition<9>, k_kb_partition<10>);
   // read key (4) + dot (8), write the packed element (4)
-  probed_launch("kb_partition", double(n) * 16.0, k1, dim3(p.tiles), dim3(kThreads), s, n, p.bb,
-                p.hb, p.vb, p.kmul, p.kmask, key32, dot, part, toff, clk);
+  probed_launch("kb_partition", double(n) * 16.0, k1, dim3(p.tiles), dim3(kThreads), s, a);
 }
 
 void keybucket_order(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
                      KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                     const KeyBucketClock &clock, hipStream_t s) {
+                     const KeyBucketClock &clock, hipStream_t s, KeyBucketSched *sc) {
   FH_CHECK(p.ok, FH_EINVARIANT, "keybucket: batch does not fit the bucket plan");
   if (n == 0) return;
-  const uint32_t B = 1u << p.bb;
-  // slot tables of buckets larger than one LDS chunk (rare; Zipf-hot keys)
-  uint32_t *mc = ws.mc.ensure(size_t(B) * 4 * (size_t(1) << kSlotBits));
+  sched_prepare(sc, p, s);
+  const OrderArgs a = order_args(p, log_base, latest, ws, sk, sv, dep_sorted, clock, sc);
   // read the packed element (4), write key + command index + dependency (16)
-  probed_launch("kb_order", double(n) * 20.0, k_kb_order, dim3(B), dim3(kOThreads), s, p.tiles,
-                p.bb, p.hb, p.vb, p.kinv, p.kmask, (const uint32_t *)ws.part.get(),
-                (const uint16_t *)ws.toff.get(), log_base, latest, sk, sv, dep_sorted, mc,
-                clock.fold, clock.frontier, clock.excount);
+  probed_launch("kb_order", double(n) * 20.0, k_kb_order, dim3(buckets_total(p)),
+                dim3(kOThreads), s, a);
 }
 
 void keybucket_step(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
                     KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
                     const KeyBucketClock &clock, const KeyBucketPlan &p2, uint32_t n2,
                     const uint32_t *key32_2, const uint64_t *dot_2, unsigned long long *clk,
-                    KeyBucketWorkspace &ws2, hipStream_t s) {
+                    KeyBucketWorkspace &ws2, hipStream_t s, KeyBucketSched *sc) {
   FH_CHECK(p.ok && p2.ok, FH_EINVARIANT, "keybucket: batch does not fit the bucket plan");
-  const uint32_t B = 1u << p.bb, B2 = 1u << p2.bb;
-  uint32_t *mc = ws.mc.ensure(size_t(B) * 4 * (size_t(1) << kSlotBits));
-  uint32_t *part2 = ws2.part.ensure(size_t(n2) + 1);
-  uint16_t *toff2 = ws2.toff.ensure(size_t(p2.tiles) * (B2 + 1) + 1);
-  auto k = p2.bb <= 8 ? k_kb_step<8> : k_kb_step<10>;
+  FH_CHECK(p.bb == p2.bb, FH_EINVARIANT, "keybucket: step over plans of different widths");
+  sched_prepare(sc, p, s);
+  const OrderArgs a = order_args(p, log_base, latest, ws, sk, sv, dep_sorted, clock, sc);
+  const PartArgs pa = part_args(p2, n2, key32_2, dot_2, clk, ws2, sc);
+  const uint32_t BT = buckets_total(p);
+  auto k = by_bits(id_bits(p2), k_kb_step<8>, k_kb_step<9>, k_kb_step<10>);
   // order (20 B / command of batch b) + partition (16 B / command of b+1)
-  probed_launch("kb_step", double(n) * 20.0 + double(n2) * 16.0, k, dim3(B + p2.tiles),
-                dim3(kOThreads), s, B, p.tiles, p.bb, p.hb, p.vb, p.kinv, p.kmask,
-                (const uint32_t *)ws.part.get(), (const uint16_t *)ws.toff.get(), log_base, latest,
-                sk, sv, dep_sorted, mc, clock.fold, clock.frontier, clock.excount, n2, p2.bb, p2.hb,
-                p2.vb, p2.kmul, p2.kmask, key32_2, dot_2, part2, toff2, clk);
+  probed_launch("kb_step", double(n) * 20.0 + double(n2) * 16.0, k, dim3(BT + p2.tiles),
+                dim3(kOThreads), s, a, BT, pa);
 }
 
 void keybucket_run(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32, const uint64_t *dot,
                    uint64_t log_base, uint64_t *latest, const KeyBucketClock &clock,
                    KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                   hipStream_t s) {
-  keybucket_partition(p, n, key32, dot, clock.fold, ws, s);
-  keybucket_order(p, n, log_base, latest, ws, sk, sv, dep_sorted, clock, s);
+                   hipStream_t s, KeyBucketSched *sc) {
+  keybucket_partition(p, n, key32, dot, clock.fold, ws, s, sc);
+  keybucket_order(p, n, log_base, latest, ws, sk, sv, dep_sorted, clock, s, sc);
 }
 
 }  // namespace fh

@@ -92,6 +92,36 @@ def test_single_view_hot_buckets_multichunk():
     check_engine(Workload.conflict_rate_(50, k=1, clients=64, seed=12).generate(50_000), batches=3)
 
 
+def test_single_view_pipelined_hot_keys():
+    """40 equally sized batches staged at once (each run() orders one batch and
+    partitions the next in the same launch): the hot-key table fills after
+    the first launch and is rebuilt at launch 32, between a batch's partition
+    and its ordering, so the batch must be ordered with the keys it was
+    partitioned with.  Zipf 0.9 over 2^14 keys gives dozens of keys above
+    the hot threshold per batch (table churn)."""
+    nb, m = 40, 30_000
+    s = Workload.zipf(0.9, 1 << 14, k=1, seed=17).generate(nb * m)
+    dep_off, deps, ex, lab, kso, ks = oracle_pipeline(s)
+    eng = Engine(s.key_space)
+    eng.stage_many([type(s)(s.dots[i * m:(i + 1) * m], s.keys[i * m:(i + 1) * m], None, None,
+                            s.key_space) for i in range(nb)])
+    got_off, got_deps, got_seq = [np.zeros(1, dtype=np.int64)], [], {}
+    base = 0
+    for _ in range(nb):
+        eng.run()
+        r = eng.results()
+        got_off.append(r["dep_off"][1:].astype(np.int64) + base)
+        got_deps.append(r["deps"])
+        base += len(r["deps"])
+        ko = r["key_off"]
+        for key in np.nonzero(np.diff(ko))[0]:
+            got_seq.setdefault(int(key), []).append(r["key_seq"][ko[key]:ko[key + 1]])
+    assert np.array_equal(np.concatenate(got_off), dep_off.astype(np.int64))
+    assert np.array_equal(np.concatenate(got_deps), deps)
+    for key in np.nonzero(np.diff(kso))[0]:
+        assert np.array_equal(np.concatenate(got_seq[int(key)]), ks[kso[key]:kso[key + 1]])
+
+
 def test_single_view_bucket_then_sort_path():
     """A batch above the bucket plan's size limit (> 1024 tiles) between two
     bucket-path batches: both paths share the mapped latest table."""

@@ -82,7 +82,7 @@ int main(int argc, char **argv) {
   uint32_t *key32, *sk, *sv;
   uint64_t *dot, *latest, *dep;
   unsigned long long *fr, *ex, *st0, *st1;
-  const uint32_t B = 1u << p.bb;
+  const uint32_t B = (1u << p.bb) + kHot;  // order workgroups (regular + hot-key buckets)
   (void)hipMalloc(&key32, n * 4);
   (void)hipMalloc(&dot, n * 8);
   (void)hipMalloc(&sk, n * 4);
@@ -101,10 +101,11 @@ int main(int argc, char **argv) {
   unsigned long long *hst[2] = {st0, st1};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_kb_stamps), hst, sizeof(hst));
   unsigned long long *ph0, *ph1;
-  (void)hipMalloc(&ph0, p.tiles * 8 * 8);
-  (void)hipMalloc(&ph1, B * 8 * 8);
-  (void)hipMemset(ph0, 0, p.tiles * 8 * 8);
-  (void)hipMemset(ph1, 0, B * 8 * 8);
+  // phase rows are indexed by blockIdx.x: the fused step puts tiles after B
+  (void)hipMalloc(&ph0, (p.tiles + B) * 8 * 8);
+  (void)hipMalloc(&ph1, (p.tiles + B) * 8 * 8);
+  (void)hipMemset(ph0, 0, (p.tiles + B) * 8 * 8);
+  (void)hipMemset(ph1, 0, (p.tiles + B) * 8 * 8);
   unsigned long long *hph[2] = {ph0, ph1};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_kb_phase), hph, sizeof(hph));
   KeyBucketWorkspace ws;
@@ -117,14 +118,41 @@ int main(int argc, char **argv) {
   clock.fold = fr;
   clock.frontier = frt;
   clock.excount = exc;
+  const bool step = getenv("KB_STEP") != nullptr;
+  // KB_SCHED: largest-first schedule from one untimed warm-up launch
+  KeyBucketSched sched, *sc = getenv("KB_SCHED") ? &sched : nullptr;
+  if (sc) {
+    keybucket_run(p, n, key32, dot, 0, latest, clock, ws, sk, sv, dep, s, sc);
+    keybucket_sched(sched, s);
+  }
   Probe probe;
-  probe.set("kb_partition,kb_order");
-  t_probe = &probe;
-  for (int r = 0; r < reps; r++)
-    keybucket_run(p, n, key32, dot, 0, latest, clock, ws, sk, sv, dep, s);
+  probe.set("kb_partition,kb_order,kb_step");
+  if (!step) {
+    t_probe = &probe;
+    for (int r = 0; r < reps; r++)
+      keybucket_run(p, n, key32, dot, 0, latest, clock, ws, sk, sv, dep, s, sc);
+  } else {
+    // fused steps: each launch orders the batch partitioned by the previous
+    // one and partitions the same input again into the other workspace
+    KeyBucketWorkspace ws2;
+    unsigned long long *fr2;
+    (void)hipMalloc(&fr2, 8 * 512 * 8);
+    (void)hipMemset(fr2, 0, 8 * 512 * 8);
+    KeyBucketWorkspace *w[2] = {&ws, &ws2};
+    unsigned long long *f[2] = {fr, fr2};
+    keybucket_partition(p, n, key32, dot, f[0], *w[0], s, sc);
+    t_probe = &probe;
+    for (int r = 0; r < reps; r++) {
+      KeyBucketClock c = clock;
+      c.fold = f[r & 1];
+      keybucket_step(p, n, 0, latest, *w[r & 1], sk, sv, dep, c, p, n, key32, dot, f[(r & 1) ^ 1],
+                     *w[(r & 1) ^ 1], s, sc);
+    }
+  }
   (void)hipStreamSynchronize(s);
   t_probe = nullptr;
   for (auto &sl : probe.slots) {
+    if (sl.next == 0) continue;
     double tot = 0;
     for (size_t i = 0; i + 1 < sl.next; i += 2) {
       float ms;
@@ -137,10 +165,36 @@ int main(int argc, char **argv) {
   std::vector<unsigned long long> h0(p.tiles * 3), h1(B * 3);
   (void)hipMemcpy(h0.data(), st0, h0.size() * 8, hipMemcpyDeviceToHost);
   (void)hipMemcpy(h1.data(), st1, h1.size() * 8, hipMemcpyDeviceToHost);
+  std::vector<uint32_t> wg_of(B);  // bucket -> workgroup index (phase rows)
+  for (uint32_t i = 0; i < B; i++) wg_of[i] = i;
+  if (sc && sched.valid) {
+    std::vector<uint32_t> pm(B);
+    (void)hipMemcpy(pm.data(), sched.perm.get(), B * 4, hipMemcpyDeviceToHost);
+    for (uint32_t i = 0; i < B; i++) wg_of[pm[i]] = i;
+  }
+  // fused step grid: the B order workgroups (by schedule rank), then the tiles
+  std::vector<uint32_t> prow(p.tiles);
+  for (uint32_t t = 0; t < p.tiles; t++) prow[t] = step ? t + B : t;
   report("kb_partition", h0, p.tiles);
   report("kb_order", h1, B);
+  if (step) {
+    // one timeline: start/end of both roles relative to the earliest start
+    unsigned long long t0 = ~0ull;
+    for (size_t i = 0; i < p.tiles; i++) t0 = std::min(t0, h0[3 * i]);
+    for (size_t i = 0; i < B; i++) t0 = std::min(t0, h1[3 * i]);
+    auto span = [&](const std::vector<unsigned long long> &h, size_t nwg, const char *nm) {
+      double s0 = 1e9, s1 = 0, e0 = 1e9, e1 = 0;
+      for (size_t i = 0; i < nwg; i++) {
+        const double a = double(h[3 * i] - t0) * 0.01, e = double(h[3 * i + 1] - t0) * 0.01;
+        s0 = std::min(s0, a), s1 = std::max(s1, a), e0 = std::min(e0, e), e1 = std::max(e1, e);
+      }
+      printf("  step %s: starts %.2f..%.2f ends %.2f..%.2f us\n", nm, s0, s1, e0, e1);
+    };
+    span(h0, p.tiles, "partition");
+    span(h1, B, "order");
+  }
   {
-    std::vector<unsigned long long> q0(p.tiles * 8), q1(B * 8);
+    std::vector<unsigned long long> q0((p.tiles + B) * 8), q1((p.tiles + B) * 8);
     (void)hipMemcpy(q0.data(), ph0, q0.size() * 8, hipMemcpyDeviceToHost);
     (void)hipMemcpy(q1.data(), ph1, q1.size() * 8, hipMemcpyDeviceToHost);
     // median phase durations (us): phase i ends at stamp i; phase 0 starts at WG start
@@ -153,8 +207,8 @@ int main(int argc, char **argv) {
     for (int ph = 0; ph <= 4; ph++) {
       std::vector<double> v;
       for (size_t i = 0; i < p.tiles; i++) {
-        unsigned long long a = ph == 0 ? h0[3 * i] : q0[8 * i + ph - 1];
-        unsigned long long e = ph == 4 ? h0[3 * i + 1] : q0[8 * i + ph];
+        unsigned long long a = ph == 0 ? h0[3 * i] : q0[8 * prow[i] + ph - 1];
+        unsigned long long e = ph == 4 ? h0[3 * i + 1] : q0[8 * prow[i] + ph];
         v.push_back(double(e - a) * 0.01);
       }
       printf(" %s %.2f", n0[ph], med(v));
@@ -165,9 +219,9 @@ int main(int argc, char **argv) {
     for (int ph = 0; ph <= 4; ph++) {
       std::vector<double> v;
       for (size_t i = 0; i < B; i++) {
-        if (h1[3 * i + 2] == 0 || h1[3 * i + 2] > 16384) continue;
-        unsigned long long a = ph == 0 ? h1[3 * i] : q1[8 * i + ph - 1];
-        unsigned long long e = ph == 4 ? h1[3 * i + 1] : q1[8 * i + ph];
+        if (h1[3 * i + 2] == 0 || h1[3 * i + 2] > 8192) continue;
+        unsigned long long a = ph == 0 ? h1[3 * i] : q1[8 * wg_of[i] + ph - 1];
+        unsigned long long e = ph == 4 ? h1[3 * i + 1] : q1[8 * wg_of[i] + ph];
         v.push_back(double(e - a) * 0.01);
       }
       printf(" %s %.2f", n1[ph], med(v));
@@ -178,8 +232,8 @@ int main(int argc, char **argv) {
     for (int k = 0; k < 4; k++) {
       std::vector<double> v;
       for (size_t i = 0; i < B; i++) {
-        if (h1[3 * i + 2] == 0 || h1[3 * i + 2] > 16384) continue;
-        v.push_back(double(q1[8 * i + to[k]] - q1[8 * i + from[k]]) * 0.01);
+        if (h1[3 * i + 2] == 0 || h1[3 * i + 2] > 8192) continue;
+        v.push_back(double(q1[8 * wg_of[i] + to[k]] - q1[8 * wg_of[i] + from[k]]) * 0.01);
       }
       printf(" %s %.2f", n2[k], med(v));
     }
@@ -188,8 +242,20 @@ int main(int argc, char **argv) {
   std::vector<std::pair<unsigned long long, size_t>> big;
   for (size_t i = 0; i < B; i++) big.push_back({h1[3 * i + 2], i});
   std::sort(big.rbegin(), big.rend());
-  for (int i = 0; i < 6; i++)
-    printf("  bucket %zu: %llu cmds, %.2f us\n", big[i].second, big[i].first,
-           double(h1[3 * big[i].second + 1] - h1[3 * big[i].second]) * 0.01);
+  std::vector<unsigned long long> q1((p.tiles + B) * 8);
+  (void)hipMemcpy(q1.data(), ph1, q1.size() * 8, hipMemcpyDeviceToHost);
+  for (int i = 0; i < 6; i++) {
+    const size_t bk = big[i].second;
+    printf("  bucket %zu: %llu cmds, %.2f us", bk, big[i].first,
+           double(h1[3 * bk + 1] - h1[3 * bk]) * 0.01);
+    if (big[i].first <= 8192) {
+      const unsigned long long *q = &q1[8 * wg_of[bk]];
+      printf("  [toff %.2f gather %.2f sort %.2f (ranks1 %.2f) out %.2f tails %.2f]",
+             double(q[0] - h1[3 * bk]) * 0.01, double(q[1] - q[0]) * 0.01,
+             double(q[2] - q[1]) * 0.01, double(q[5] - q[4]) * 0.01, double(q[3] - q[2]) * 0.01,
+             double(h1[3 * bk + 1] - q[3]) * 0.01);
+    }
+    printf("\n");
+  }
   return 0;
 }

@@ -9,4 +9,4 @@ s = Workload.zipf(0.7, 1 << 20, k=1).generate(1_000_000)
 s.keys[:, 0].astype(np.uint32).tofile("/tmp/kb_keys.u32")
 s.dots.astype(np.uint64).tofile("/tmp/kb_dots.u64")
 PY
-timeout -k 10 60 tools/kbbench /tmp/kb_keys.u32 /tmp/kb_dots.u64 1000000 20 20
+for b in ${KB_BINS:-tools/kbbench}; do echo "== $b"; timeout -k 10 60 $b /tmp/kb_keys.u32 /tmp/kb_dots.u64 1000000 20 20; done
