@@ -40,6 +40,7 @@ PROBES = {
     "sv_tails": r"k_sv_tails",
     "kb_partition": r"k_kb_partition",
     "kb_order": r"k_kb_order",
+    "kb_step": r"k_kb_step",
 }
 CALIB_BYTES = 1 << 30
 
