@@ -332,8 +332,10 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
 __device__ __forceinline__ uint32_t run_of(const uint32_t *s_rs, uint32_t tiles, uint32_t q) {
   uint32_t t = 0;
 #pragma unroll
-  for (uint32_t st = kMaxTiles / 2; st >= 1; st >>= 1)
-    if (t + st < tiles && s_rs[t + st] <= q) t += st;
+  for (uint32_t st = kMaxTiles / 2; st >= 1; st >>= 1) {
+    const uint32_t v = s_rs[min(t + st, tiles)];
+    t = (t + st < tiles && v <= q) ? t + st : t;
+  }
   return t;
 }
 
@@ -352,11 +354,16 @@ __device__ __forceinline__ void gather_items(const uint32_t *__restrict__ part,
     g[i] = c0 + min(w * 64 * IT + uint32_t(i) * 64 + lane, c - 1);
     t[i] = 0;
   }
+  // branch-free steps: every search reads its probe (clamped to the
+  // s_rs[tiles] sentinel) so the IT reads of a step issue back to back
 #pragma unroll
-  for (uint32_t st = kMaxTiles / 2; st >= 1; st >>= 1)
+  for (uint32_t st = kMaxTiles / 2; st >= 1; st >>= 1) {
+    uint32_t v[IT];
 #pragma unroll
-    for (int i = 0; i < IT; i++)
-      if (t[i] + st < tiles && s_rs[t[i] + st] <= g[i]) t[i] += st;
+    for (int i = 0; i < IT; i++) v[i] = s_rs[min(t[i] + st, tiles)];
+#pragma unroll
+    for (int i = 0; i < IT; i++) t[i] = (t[i] + st < tiles && v[i] <= g[i]) ? t[i] + st : t[i];
+  }
 #pragma unroll
   for (int i = 0; i < IT; i++) {
     const uint32_t q = w * 64 * IT + uint32_t(i) * 64 + lane;
@@ -536,9 +543,20 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
   const uint32_t tid = threadIdx.x;
   const uint32_t vmask = (1u << vb) - 1;
   uint32_t xe[IT];
+#ifdef FH_ABL_NOGATHER  // diagnostic builds only: contiguous loads instead
+  for (int i = 0; i < IT; i++) {
+    const uint32_t q = (threadIdx.x >> 6) * 64 * IT + uint32_t(i) * 64 + (threadIdx.x & 63);
+    xe[i] = q < Nb ? part[q] : 0u;
+  }
+#else
   gather_items<IT>(part, s_rs, s_src, tiles, 0, Nb, xe);
+#endif
   FH_PHASE(1, 1);
+#ifdef FH_ABL_NOSORT  // diagnostic builds only: timing without the sort
+  const uint32_t *S = sort_chunk<IT>(xe, s_a, s_b, Nb, vb, 0, s_h0, s_h1, s_db, true);
+#else
   const uint32_t *S = sort_chunk<IT>(xe, s_a, s_b, Nb, vb, hb, s_h0, s_h1, s_db, true);
+#endif
   FH_PHASE(1, 2);
   if (staged) {
     for (uint32_t j = tid; j < Nb; j += kOThreads) {
@@ -700,7 +718,11 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
   // is loaded now and staged in LDS before the sort, when it is not much
   // larger than an average bucket; the loads overlap the scan and gather.
   constexpr int LR = (1 << kSlotBits) / kOThreads;
+#ifdef FH_ABL_NOSTAGE  // diagnostic builds only
+  const bool staged = false;
+#else
   const bool staged = !hot && H <= 2u * ((uint32_t(tiles) * uint32_t(kTile)) >> bb);
+#endif
   uint64_t lv[LR];
   if (staged) {
 #pragma unroll

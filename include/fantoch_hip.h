@@ -109,6 +109,19 @@ fh_status fh_keydeps_cmd_deps(fh_keydeps *h, size_t nkeys,
 fh_status fh_keydeps_noop_deps(fh_keydeps *h, uint64_t *out, size_t cap,
                                size_t *out_len);
 
+/* Partial replication: the owner shard's union of every shard's dependency
+ * reports for its commands -- Atlas's MShardCommit union
+ * (fantoch_ps/src/protocol/atlas.rs:559-639, union at :580-583; each shard's
+ * KeyDeps sees Command::keys(shard), fantoch/src/command.rs:95-100).
+ * Device pointers on `stream` (a hipStream_t, NULL = null stream) of
+ * `device` (-1 = current):
+ *   cmd[nrec] (< n_cmd), dep[nrec]   records, any order, duplicates allowed
+ *   out_off[n_cmd+1], out_dep[nrec]  per-command deps, ascending, unique
+ * *out_len = number of distinct deps (the call synchronises `stream`). */
+fh_status fh_dep_union(int device, size_t n_cmd, size_t nrec, const uint32_t *cmd,
+                       const uint64_t *dep, uint32_t *out_off, uint64_t *out_dep,
+                       size_t *out_len, void *stream);
+
 /* ======================================================================
  * Graph executor -- SCC + execution order.
  * Replaces GraphExecutor / DependencyGraph / TarjanSCCFinder
