@@ -15,47 +15,23 @@
 #include <unordered_set>
 #include <vector>
 
+#include "dotindex.h"
 #include "graph_core.h"
 
 namespace fh {
-namespace {
 
-constexpr unsigned B = 256;
 #define GRID_STRIDE(i, n) \
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
-
-__device__ __forceinline__ bool executed_dev(uint64_t d, const uint64_t *__restrict__ frontier,
-                                             const uint64_t *__restrict__ exc, uint32_t nexc) {
-  if ((d & 0x00FFFFFFFFFFFFFFull) <= frontier[d >> 56]) return true;
-  uint32_t lo = 0, hi = nexc;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (exc[mid] < d)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return lo < nexc && exc[lo] == d;
-}
-
-__device__ __forceinline__ int64_t find_vid(uint64_t d, const uint64_t *__restrict__ sd,
-                                            const uint32_t *__restrict__ sv, uint32_t V) {
-  uint32_t lo = 0, hi = V;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (sd[mid] < d)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return (lo < V && sd[lo] == d) ? int64_t(sv[lo]) : -1;
-}
 
 __global__ void k_dup_check(uint32_t V, const uint64_t *__restrict__ sd, uint32_t *err) {
   GRID_STRIDE(j, V) {
     if (j > 0 && sd[j] == sd[j - 1]) atomicOr(err, 1u);
   }
 }
+
+namespace {
+
+constexpr unsigned B = 256;
 
 // per vertex: count resolved edges, flag missing dependencies
 // (tarjan.rs:131-170: self and executed deps are ignored)
@@ -101,31 +77,6 @@ __global__ void k_resolve_fill(uint32_t V, const uint64_t *__restrict__ dot,
 }
 
 }  // namespace
-
-// AEClock<ProcessId>: per-process contiguous frontier + exception set.
-struct AEClock {
-  uint64_t frontier[256] = {0};
-  std::unordered_set<uint64_t> exc;
-  bool contains(uint64_t d) const {
-    return (d & 0x00FFFFFFFFFFFFFFull) <= frontier[d >> 56] || exc.count(d);
-  }
-  void add(uint64_t d) {
-    const uint32_t s = uint32_t(d >> 56);
-    const uint64_t q = d & 0x00FFFFFFFFFFFFFFull;
-    if (q <= frontier[s]) return;
-    if (q == frontier[s] + 1) {
-      frontier[s] = q;
-      while (!exc.empty()) {
-        auto it = exc.find(make_dot(s, frontier[s] + 1));
-        if (it == exc.end()) break;
-        exc.erase(it);
-        frontier[s]++;
-      }
-    } else {
-      exc.insert(d);
-    }
-  }
-};
 
 struct GraphDevice {
   uint32_t process_id;

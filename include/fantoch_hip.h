@@ -166,6 +166,34 @@ fh_status fh_graph_missing(fh_graph *h, uint64_t *dots, size_t cap,
                            size_t *len);
 
 /* ======================================================================
+ * Caesar's predecessors executor.
+ * Replaces PredecessorsExecutor / PredecessorsGraph
+ * (fantoch_ps/src/executor/pred/executor.rs, mod.rs:26-352) behind the
+ * Executor trait (fantoch/src/executor/mod.rs:27-88); Caesar wires it as its
+ * executor (fantoch_ps/src/protocol/caesar.rs:49).
+ * ==================================================================== */
+typedef struct fh_pred fh_pred;
+
+/* PredecessorsGraph::new(process_id, config) (mod.rs:42-67). */
+fh_status fh_pred_create(uint32_t process_id, uint64_t shard_id,
+                         const fh_config *cfg, fh_pred **out);
+fh_status fh_pred_destroy(fh_pred *h);
+/* A batch of PredecessorsGraph::add(dot, cmd, clock, deps) calls in arrival
+ * order (mod.rs:89-130).  clock[i] = (Clock.seq << 8) | Clock.process_id
+ * (integer order == Clock's Ord, protocol/common/pred/clocks/mod.rs:15-30).
+ * A command runs once every dep is committed and every dep with a lower
+ * clock has run; ready commands drain in clock order.  FH_EINVARIANT (no
+ * state change) for a dot already added (mod.rs:264-273). */
+fh_status fh_pred_add_batch(fh_pred *h, size_t n, const uint64_t *dot,
+                            const uint64_t *clock, const uint32_t *dep_off,
+                            const uint64_t *dep_dot);
+/* command_to_execute (mod.rs:71-73), up to cap dots. */
+fh_status fh_pred_drain(fh_pred *h, uint64_t *exec_dot, size_t cap,
+                        size_t *len);
+/* commands still waiting (phase one or two). */
+fh_status fh_pred_pending(fh_pred *h, size_t *count);
+
+/* ======================================================================
  * Fused engine -- a committed command stream, device resident end to end:
  * KeyDeps (one replica, or the fast-quorum views of Atlas/EPaxos with the
  * QuorumDeps union, quorum.rs:28-98) -> dependency graph -> SCC ->

@@ -1031,3 +1031,204 @@ size_t fo_graph_run(uint32_t process_id, uint32_t n, uint32_t f, size_t ncmd,
   fo_graph_free(g);
   return executed;
 }
+
+/* ------------------------------------------------------------------ */
+/* PredecessorsGraph -- Caesar's executor                               */
+/* (fantoch_ps/src/executor/pred/mod.rs:26-352, index.rs)               */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  uint64_t dot, clock; /* clock packed (seq << 8) | process_id: Clock's Ord */
+  uint64_t deps_at;
+  uint32_t ndeps;
+  uint32_t missing; /* Vertex::missing_deps (index.rs) */
+} pvertex;
+
+struct fo_pred {
+  aeclock committed, executed; /* mod.rs:29-30 */
+  pvertex *v;
+  size_t nv, vcap;
+  u64map index;       /* VertexIndex: dot -> slot + 1 */
+  vec64 deps;         /* dep pool */
+  u64map p1, p2;      /* PendingIndex (phase one / two): dep -> head + 1 */
+  pend_node *pn;      /* linked lists of waiting dots */
+  size_t npn, pncap;
+  vec64 to_execute;   /* mod.rs:37 */
+  vec64 stack;        /* save_to_execute cascade (explicit stack) */
+};
+
+fo_pred *fo_pred_new(uint32_t process_id) {
+  fo_pred *p = (fo_pred *)calloc(1, sizeof(fo_pred));
+  ae_init(&p->committed);
+  ae_init(&p->executed);
+  map_init(&p->index, 1024);
+  map_init(&p->p1, 256);
+  map_init(&p->p2, 256);
+  (void)process_id;
+  return p;
+}
+
+void fo_pred_free(fo_pred *p) {
+  map_free(&p->committed.exc);
+  map_free(&p->executed.exc);
+  map_free(&p->index);
+  map_free(&p->p1);
+  map_free(&p->p2);
+  free(p->v);
+  free(p->deps.a);
+  free(p->pn);
+  free(p->to_execute.a);
+  free(p->stack.a);
+  free(p);
+}
+
+static pvertex *pred_find(fo_pred *p, uint64_t dot) {
+  uint64_t *s = map_get(&p->index, dot);
+  return s ? &p->v[*s - 1] : NULL;
+}
+
+/* PendingIndex::index(dot, dep): dot waits on dep (insertion order kept) */
+static void pend_index(fo_pred *p, u64map *m, uint64_t dot, uint64_t dep) {
+  if (p->npn == p->pncap) {
+    p->pncap = p->pncap ? p->pncap * 2 : 256;
+    p->pn = (pend_node *)xrealloc(p->pn, p->pncap * sizeof(pend_node));
+  }
+  uint64_t *h = map_get(m, dep);
+  /* append at the tail: walk (lists are short) */
+  pend_node nd = {dot, -1};
+  p->pn[p->npn] = nd;
+  if (!h) {
+    map_put(m, dep, (uint64_t)p->npn + 1);
+  } else {
+    int64_t i = (int64_t)(*h - 1);
+    while (p->pn[i].next >= 0) i = p->pn[i].next;
+    p->pn[i].next = (int64_t)p->npn;
+  }
+  p->npn++;
+}
+
+/* PendingIndex::remove(dep) -> waiting dots, into out (insertion order) */
+static void pend_remove(fo_pred *p, u64map *m, uint64_t dep, vec64 *out) {
+  uint64_t head;
+  if (!map_del(m, dep, &head)) return;
+  for (int64_t i = (int64_t)(head - 1); i >= 0; i = p->pn[i].next) vpush(out, p->pn[i].child);
+}
+
+static void pred_save_to_execute(fo_pred *p, uint64_t dot);
+
+/* move_to_phase_two (mod.rs:186-253) */
+static void pred_phase_two(fo_pred *p, uint64_t dot) {
+  pvertex *v = pred_find(p, dot);
+  uint32_t count = 0;
+  for (uint32_t e = 0; e < v->ndeps; e++) {
+    uint64_t d = p->deps.a[v->deps_at + e];
+    if (ae_contains(&p->executed, d)) continue;
+    pvertex *dv = pred_find(p, d);
+    if (!dv) {
+      fprintf(stderr, "oracle: non-executed dependency must exist\n");
+      abort();
+    }
+    if (dv->clock < v->clock) { /* only deps with a lower clock (:224) */
+      count++;
+      pend_index(p, &p->p2, dot, d);
+    }
+  }
+  if (count) v->missing = count;
+  else pred_save_to_execute(p, dot);
+}
+
+/* move_to_phase_one (mod.rs:132-182) */
+static void pred_phase_one(fo_pred *p, uint64_t dot) {
+  pvertex *v = pred_find(p, dot);
+  uint32_t count = 0;
+  for (uint32_t e = 0; e < v->ndeps; e++) {
+    uint64_t d = p->deps.a[v->deps_at + e];
+    if (!ae_contains(&p->committed, d)) {
+      count++;
+      pend_index(p, &p->p1, dot, d);
+    }
+  }
+  if (count) v->missing = count;
+  else pred_phase_two(p, dot);
+}
+
+/* save_to_execute (mod.rs:322-351) and the try_phase_two_pending cascade
+ * (:299-320), depth first like the reference's recursion, on an explicit
+ * stack */
+static void pred_save_to_execute(fo_pred *p, uint64_t dot) {
+  size_t base = p->stack.len;
+  vpush(&p->stack, dot);
+  vec64 kids = {0};
+  while (p->stack.len > base) {
+    uint64_t d = p->stack.a[--p->stack.len];
+    if (ae_contains(&p->executed, d)) {
+      fprintf(stderr, "oracle: command executed twice\n");
+      abort();
+    }
+    ae_add(&p->executed, d);
+    uint64_t slot;
+    map_del(&p->index, d, &slot);
+    vpush(&p->to_execute, d);
+    kids.len = 0;
+    pend_remove(p, &p->p2, d, &kids);
+    /* children that become ready, pushed in reverse so the first runs first */
+    size_t mark = p->stack.len;
+    for (size_t i = 0; i < kids.len; i++) {
+      pvertex *c = pred_find(p, kids.a[i]);
+      if (--c->missing == 0) vpush(&p->stack, kids.a[i]);
+    }
+    if (p->stack.len > mark + 1) {
+      for (size_t i = mark, j = p->stack.len - 1; i < j; i++, j--) {
+        uint64_t t = p->stack.a[i];
+        p->stack.a[i] = p->stack.a[j];
+        p->stack.a[j] = t;
+      }
+    }
+  }
+  free(kids.a);
+}
+
+size_t fo_pred_add(fo_pred *p, uint64_t dot, uint64_t clock, const uint64_t *deps,
+                   size_t ndeps) {
+  size_t before = p->to_execute.len;
+  /* deps.remove(&dot) (mod.rs:106-109); HashSet: no duplicates */
+  size_t at = p->deps.len;
+  for (size_t i = 0; i < ndeps; i++)
+    if (deps[i] != dot) vpush(&p->deps, deps[i]);
+  size_t nd = sort_unique(p->deps.a + at, p->deps.len - at);
+  p->deps.len = at + nd;
+  /* index_committed_command (mod.rs:255-274) */
+  if (ae_contains(&p->committed, dot)) {
+    fprintf(stderr, "oracle: dot committed twice\n");
+    abort();
+  }
+  ae_add(&p->committed, dot);
+  if (p->nv == p->vcap) {
+    p->vcap = p->vcap ? p->vcap * 2 : 1024;
+    p->v = (pvertex *)xrealloc(p->v, p->vcap * sizeof(pvertex));
+  }
+  pvertex nv = {dot, clock, at, (uint32_t)nd, 0};
+  p->v[p->nv] = nv;
+  map_put(&p->index, dot, (uint64_t)p->nv + 1);
+  p->nv++;
+  /* try_phase_one_pending (mod.rs:276-297) */
+  vec64 w = {0};
+  pend_remove(p, &p->p1, dot, &w);
+  for (size_t i = 0; i < w.len; i++) {
+    pvertex *c = pred_find(p, w.a[i]);
+    if (--c->missing == 0) pred_phase_two(p, w.a[i]);
+  }
+  free(w.a);
+  /* move_to_phase_one (mod.rs:118) */
+  pred_phase_one(p, dot);
+  return p->to_execute.len - before;
+}
+
+size_t fo_pred_drain(fo_pred *p, uint64_t *dots, size_t cap) {
+  size_t n = p->to_execute.len < cap ? p->to_execute.len : cap;
+  if (dots) memcpy(dots, p->to_execute.a, n * sizeof(uint64_t));
+  memmove(p->to_execute.a, p->to_execute.a + n, (p->to_execute.len - n) * sizeof(uint64_t));
+  p->to_execute.len -= n;
+  return n;
+}
+
+size_t fo_pred_pending_count(const fo_pred *p) { return p->index.len; }

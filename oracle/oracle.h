@@ -14,6 +14,9 @@
  *   simple / cycle / test_add_random / sccs_found_and_missing_dep /
  *   transitive_conflicts_assumption_regression_test_{1,2}
  *                       fantoch_ps/src/executor/graph/mod.rs:716-1350
+ *   simple / already_mutably_borrowed_regression_test / test_add_random
+ *   (Caesar)            fantoch_ps/src/executor/pred/mod.rs:386-687
+ *                       (tests/test_oracle_pred.py)
  *
  * Dots are packed u64: source (ProcessId, u8) in bits 56..63, sequence in
  * bits 0..55.  Packed order == the derived Ord of Id{source, sequence}
@@ -145,6 +148,23 @@ size_t fo_graph_run(uint32_t process_id, uint32_t n, uint32_t f, size_t ncmd,
                     const uint64_t *deps, uint64_t *exec_dot,
                     uint64_t *scc_label, uint64_t key_space,
                     uint32_t *key_seq_off, uint64_t *key_seq);
+
+/* ---------------------------------------------------------------------
+ * PredecessorsGraph -- Caesar's executor (executor/pred/mod.rs:26-352,
+ * index.rs).  Clocks are packed (seq << 8) | process_id, which orders like
+ * Clock's derived Ord (protocol/common/pred/clocks/mod.rs:15-30).
+ * ------------------------------------------------------------------- */
+typedef struct fo_pred fo_pred;
+
+fo_pred *fo_pred_new(uint32_t process_id);
+void fo_pred_free(fo_pred *p);
+/* add(dot, cmd, clock, deps) (mod.rs:89-130).  Returns the number of
+ * commands that became ready. */
+size_t fo_pred_add(fo_pred *p, uint64_t dot, uint64_t clock, const uint64_t *deps,
+                   size_t ndeps);
+/* command_to_execute (mod.rs:71-73), in order. */
+size_t fo_pred_drain(fo_pred *p, uint64_t *dots, size_t cap);
+size_t fo_pred_pending_count(const fo_pred *p);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,15 @@ def _load():
     lib.fo_graph_drain.argtypes = [V, V, V, S]
     lib.fo_graph_pending_count.restype = S
     lib.fo_graph_pending_count.argtypes = [V]
+    lib.fo_pred_new.restype = V
+    lib.fo_pred_new.argtypes = [C.c_uint32]
+    lib.fo_pred_free.argtypes = [V]
+    lib.fo_pred_add.restype = S
+    lib.fo_pred_add.argtypes = [V, C.c_uint64, C.c_uint64, V, S]
+    lib.fo_pred_drain.restype = S
+    lib.fo_pred_drain.argtypes = [V, V, S]
+    lib.fo_pred_pending_count.restype = S
+    lib.fo_pred_pending_count.argtypes = [V]
     lib.fo_graph_run.restype = S
     lib.fo_graph_run.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, S, u64p, u32p, u64p,
                                  u32p, u64p, u64p, u64p, C.c_uint64, u32p, u64p]
@@ -264,3 +273,49 @@ def graph_run(dots, key_off, keys, dep_off, deps, key_space, process_id=1, n=1, 
                             np.ascontiguousarray(dep_off, np.uint32), deps_a, exec_dot, scc,
                             key_space, kso, ks)
     return exec_dot[:ne], scc[:ne], kso, ks[:kso[-1]]
+
+
+def clock(seq: int, process_id: int) -> int:
+    """Clock{seq, process_id} packed so that integer order == Clock's Ord
+    (protocol/common/pred/clocks/mod.rs:15-30)."""
+    return (seq << 8) | process_id
+
+
+class Pred:
+    """PredecessorsGraph (Caesar, executor/pred/mod.rs:26-352)."""
+
+    def __init__(self, process_id=1):
+        self._h = lib().fo_pred_new(process_id)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().fo_pred_free(self._h)
+            self._h = None
+
+    def add(self, dot_, clock_, deps):
+        d = _arr(deps)
+        return lib().fo_pred_add(self._h, dot_, clock_, _ptr(d), len(d))
+
+    def drain(self):
+        out = []
+        buf = np.zeros(1024, dtype=np.uint64)
+        while True:
+            n = lib().fo_pred_drain(self._h, _ptr(buf), 1024)
+            out.extend(int(x) for x in buf[:n])
+            if n < 1024:
+                return out
+
+    def pending(self):
+        return lib().fo_pred_pending_count(self._h)
+
+
+def pred_run(dots, clocks, dep_off, deps, process_id=1):
+    """PredecessorsGraph over an arrival stream, draining after every add.
+    Returns (execution order as dots, pending count)."""
+    p = Pred(process_id)
+    out = []
+    deps = np.ascontiguousarray(deps, np.uint64)
+    for i in range(len(dots)):
+        p.add(int(dots[i]), int(clocks[i]), deps[dep_off[i]:dep_off[i + 1]])
+        out.extend(p.drain())
+    return np.asarray(out, dtype=np.uint64), p.pending()
