@@ -8,10 +8,12 @@ from __future__ import annotations
 
 
 class Command:
-    __slots__ = ("rifl", "shard_to_keys")
+    """read_only: every op is a read (Command::read_only, command.rs:65-67)."""
+    __slots__ = ("rifl", "shard_to_keys", "read_only")
 
-    def __init__(self, rifl, keys, shard_of=None):
+    def __init__(self, rifl, keys, shard_of=None, read_only: bool = False):
         self.rifl = rifl
+        self.read_only = read_only
         self.shard_to_keys = {}
         for k in keys:
             s = shard_of(k) if shard_of else 0

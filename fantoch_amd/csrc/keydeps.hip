@@ -75,10 +75,12 @@ __device__ __forceinline__ uint32_t sort_unique_dev(uint64_t *a, uint32_t n) {
   return w;
 }
 
+// scratch slot of command i: dm deps per key (1 sequential, 2 read/write),
+// one noop, its past
 __device__ __forceinline__ uint32_t tmp_base(const uint32_t *key_off, const uint32_t *past_off,
-                                             uint32_t cmd_first, uint32_t i) {
+                                             uint32_t cmd_first, uint32_t i, uint32_t dm) {
   const uint32_t c = cmd_first + i;
-  uint32_t b = (key_off[c] - key_off[cmd_first]) + i;
+  uint32_t b = (key_off[c] - key_off[cmd_first]) * dm + i;
   if (past_off) b += past_off[c] - past_off[cmd_first];
   return b;
 }
@@ -86,15 +88,17 @@ __device__ __forceinline__ uint32_t tmp_base(const uint32_t *key_off, const uint
 __global__ void k_cmd(uint32_t cmd_first, uint32_t ncmd, const uint32_t *__restrict__ key_off,
                       const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot,
                       const uint64_t *__restrict__ elem_dep,
+                      const uint64_t *__restrict__ elem_dep2,
                       const uint8_t *__restrict__ elem_tail, uint64_t noop_latest,
                       const uint32_t *__restrict__ past_off, const uint64_t *__restrict__ past,
                       uint64_t *__restrict__ latest, uint64_t *__restrict__ tmp,
                       uint32_t *__restrict__ cnt) {
   const uint32_t ebase = key_off[cmd_first];
+  const uint32_t dm = elem_dep2 ? 2u : 1u;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ncmd;
        i += gridDim.x * blockDim.x) {
     const uint32_t c = cmd_first + i;
-    uint64_t *t = tmp + tmp_base(key_off, past_off, cmd_first, i);
+    uint64_t *t = tmp + tmp_base(key_off, past_off, cmd_first, i, dm);
     uint32_t n = 0;
     if (past_off) /* sequential.rs:31-34: start from past */
       for (uint32_t p = past_off[c]; p < past_off[c + 1]; p++) t[n++] = past[p];
@@ -102,6 +106,7 @@ __global__ void k_cmd(uint32_t cmd_first, uint32_t ncmd, const uint32_t *__restr
     for (uint32_t e = key_off[c] - ebase; e < key_off[c + 1] - ebase; e++) {
       const uint64_t d = elem_dep[e];
       if (d) t[n++] = d; /* :84-87 */
+      if (elem_dep2 && elem_dep2[e]) t[n++] = elem_dep2[e]; /* locked.rs:111-113 */
       if (elem_tail[e]) latest[key32[e]] = self; /* :88, :90-95 */
     }
     if (noop_latest) t[n++] = noop_latest; /* :100 */
@@ -109,13 +114,71 @@ __global__ void k_cmd(uint32_t cmd_first, uint32_t ncmd, const uint32_t *__restr
   }
 }
 
+// Read/write rules (LockedKeyDeps::do_add_cmd, locked.rs:94-118), per key in
+// arrival order: a read depends on the latest write and becomes the latest
+// read; a write depends on the latest read and the latest write and becomes
+// the latest write (the latest read stays).  Over a key-sorted batch: marks
+// (position + 1) of segment heads, writes and reads, whose exclusive prefix
+// maxima give each element's previous write / read inside its segment.
+__global__ void k_rw_marks(const uint32_t *__restrict__ ks, const uint32_t *__restrict__ vs,
+                           uint32_t m, const uint32_t *__restrict__ cmd_of,
+                           const uint8_t *__restrict__ ro, uint32_t *__restrict__ mh,
+                           uint32_t *__restrict__ mw, uint32_t *__restrict__ mr) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m;
+       j += gridDim.x * blockDim.x) {
+    const bool read = ro[cmd_of[vs[j]]] != 0;
+    mh[j] = (j == 0 || ks[j - 1] != ks[j]) ? j + 1 : 0u;
+    mw[j] = read ? 0u : j + 1;
+    mr[j] = read ? j + 1 : 0u;
+  }
+}
+
+__global__ void k_prev_rw(const uint32_t *__restrict__ ks, const uint32_t *__restrict__ vs,
+                          uint32_t m, const uint32_t *__restrict__ cmd_of,
+                          const uint8_t *__restrict__ ro, const uint64_t *__restrict__ dot,
+                          const uint64_t *__restrict__ latest_w,
+                          const uint64_t *__restrict__ latest_r, const uint32_t *__restrict__ mh,
+                          const uint32_t *__restrict__ sh, const uint32_t *__restrict__ sw,
+                          const uint32_t *__restrict__ sr, uint64_t *__restrict__ elem_dep,
+                          uint64_t *__restrict__ elem_dep2) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t k = ks[j], e = vs[j];
+    const uint32_t seg = max(sh[j], mh[j]);  // segment head position + 1
+    const uint64_t pw = sw[j] >= seg ? dot[cmd_of[vs[sw[j] - 1]]] : latest_w[k];
+    const uint64_t pr = sr[j] >= seg ? dot[cmd_of[vs[sr[j] - 1]]] : latest_r[k];
+    elem_dep[e] = pw;
+    elem_dep2[e] = ro[cmd_of[e]] ? 0ull : pr;
+  }
+}
+
+// segment tails: the last write / read of the key in the batch becomes its
+// latest write / read (after every head has read the tables: own launch)
+__global__ void k_tails_rw(const uint32_t *__restrict__ ks, const uint32_t *__restrict__ vs,
+                           uint32_t m, const uint32_t *__restrict__ cmd_of,
+                           const uint64_t *__restrict__ dot, const uint32_t *__restrict__ mh,
+                           const uint32_t *__restrict__ sh, const uint32_t *__restrict__ mw,
+                           const uint32_t *__restrict__ sw, const uint32_t *__restrict__ mr,
+                           const uint32_t *__restrict__ sr, uint64_t *__restrict__ latest_w,
+                           uint64_t *__restrict__ latest_r) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m;
+       j += gridDim.x * blockDim.x) {
+    if (j + 1 < m && ks[j + 1] == ks[j]) continue;
+    const uint32_t k = ks[j];
+    const uint32_t seg = max(sh[j], mh[j]);
+    const uint32_t lw = max(sw[j], mw[j]), lr = max(sr[j], mr[j]);
+    if (lw >= seg) latest_w[k] = dot[cmd_of[vs[lw - 1]]];
+    if (lr >= seg) latest_r[k] = dot[cmd_of[vs[lr - 1]]];
+  }
+}
+
 __global__ void k_compact(uint32_t cmd_first, uint32_t ncmd, const uint32_t *__restrict__ key_off,
-                          const uint32_t *__restrict__ past_off,
+                          const uint32_t *__restrict__ past_off, uint32_t dm,
                           const uint64_t *__restrict__ tmp, const uint32_t *__restrict__ off,
                           uint64_t *__restrict__ out) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ncmd;
        i += gridDim.x * blockDim.x) {
-    const uint64_t *t = tmp + tmp_base(key_off, past_off, cmd_first, i);
+    const uint64_t *t = tmp + tmp_base(key_off, past_off, cmd_first, i, dm);
     const uint32_t o = off[i], c = off[i + 1] - off[i];
     for (uint32_t j = 0; j < c; j++) out[o + j] = t[j];
   }
@@ -185,14 +248,22 @@ void KeyDepsDevice::check_err(const char *what) {
 
 // Runs the command pipeline for commands [a, b) of the staged batch; appends
 // their CSR to (host) out.  Returns number of deps written.
-size_t KeyDepsDevice::run_segment(uint32_t a, uint32_t b, bool has_past, uint32_t *out_off,
-                                  uint64_t *out_dep, size_t out_base) {
+void KeyDepsDevice::enable_rw() {
+  if (rw) return;
+  latest_r.ensure(key_space);
+  FH_HIP(hipMemsetAsync(latest_r.get(), 0, key_space * sizeof(uint64_t), stream));
+  rw = true;
+}
+
+size_t KeyDepsDevice::run_segment(uint32_t a, uint32_t b, bool has_past, bool has_ro,
+                                  uint32_t *out_off, uint64_t *out_dep, size_t out_base) {
   const uint32_t ncmd = b - a;
   if (ncmd == 0) return 0;
   const uint32_t e0 = h_key_off[a], e1 = h_key_off[b];
   const uint32_t m = e1 - e0;
   const uint32_t p0 = has_past ? h_past_off[a] : 0, p1 = has_past ? h_past_off[b] : 0;
-  const size_t tmp_n = size_t(m) + ncmd + (p1 - p0);
+  const uint32_t dm = has_ro ? 2u : 1u;
+  const size_t tmp_n = size_t(m) * dm + ncmd + (p1 - p0);
   uint32_t *key32 = d_key32.ensure(m);
   uint32_t *cmd_of = d_cmd_of.ensure(m);
   uint64_t *edep = d_elem_dep.ensure(m);
@@ -207,19 +278,40 @@ size_t KeyDepsDevice::run_segment(uint32_t a, uint32_t b, bool has_past, uint32_
   uint32_t *ka = d_sk_a.ensure(m), *kb = d_sk_b.ensure(m);
   uint32_t *va = d_sv_a.ensure(m), *vb = d_sv_b.ensure(m);
   sort_pairs<uint32_t>(key32, nullptr, ka, va, kb, vb, m, key_bits, sort_ws, stream, &ks, &vs);
-  if (m)
+  uint64_t *edep2 = nullptr;
+  if (has_ro) {
+    // LockedKeyDeps read/write rules; tails update both tables in their own
+    // launch, so k_cmd below writes nothing
+    edep2 = d_elem_dep2.ensure(m);
+    FH_HIP(hipMemsetAsync(etail, 0, m, stream));
+    if (m) {
+      uint32_t *mh = d_mh.ensure(m), *mw = d_mw.ensure(m), *mr = d_mr.ensure(m);
+      uint32_t *sh = d_sh.ensure(m + 1), *sw = d_sw.ensure(m + 1), *sr = d_sr.ensure(m + 1);
+      k_rw_marks<<<grid_for(m, B), B, 0, stream>>>(ks, vs, m, cmd_of, d_ro.get(), mh, mw, mr);
+      exclusive_scan_max_u32(mh, sh, m, scan_ws, stream);
+      exclusive_scan_max_u32(mw, sw, m, scan_ws, stream);
+      exclusive_scan_max_u32(mr, sr, m, scan_ws, stream);
+      k_prev_rw<<<grid_for(m, B), B, 0, stream>>>(ks, vs, m, cmd_of, d_ro.get(), d_dot.get(),
+                                                  latest.get(), latest_r.get(), mh, sh, sw, sr,
+                                                  edep, edep2);
+      k_tails_rw<<<grid_for(m, B), B, 0, stream>>>(ks, vs, m, cmd_of, d_dot.get(), mh, sh, mw,
+                                                   sw, mr, sr, latest.get(), latest_r.get());
+    }
+  } else if (m) {
     k_prev<<<grid_for(m, B), B, 0, stream>>>(ks, vs, m, cmd_of, d_dot.get(), latest.get(), edep,
                                              etail);
+  }
   const uint32_t *poff = has_past ? d_past_off.get() : nullptr;
   k_cmd<<<grid_for(ncmd, B), B, 0, stream>>>(a, ncmd, d_key_off.get(), key32, d_dot.get(), edep,
-                                             etail, noop_latest, poff, d_past.get(),
+                                             edep2, etail, noop_latest, poff, d_past.get(),
                                              latest.get(), tmp, cnt);
   exclusive_scan_u32(cnt, off, ncmd, scan_ws, stream);
   uint32_t total = 0;
   FH_HIP(hipMemcpyAsync(&total, off + ncmd, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
   FH_HIP(hipStreamSynchronize(stream));
   uint64_t *dout = d_out.ensure(total ? total : 1);
-  k_compact<<<grid_for(ncmd, B), B, 0, stream>>>(a, ncmd, d_key_off.get(), poff, tmp, off, dout);
+  k_compact<<<grid_for(ncmd, B), B, 0, stream>>>(a, ncmd, d_key_off.get(), poff, dm, tmp, off,
+                                                 dout);
   std::vector<uint32_t> hoff(ncmd + 1);
   FH_HIP(hipMemcpyAsync(hoff.data(), off, (ncmd + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         stream));
@@ -240,14 +332,22 @@ size_t KeyDepsDevice::table_values(uint64_t extra) {
   const uint32_t K = uint32_t(key_space);
   uint32_t *flags = d_cnt.ensure(K);
   uint32_t *pos = d_off.ensure(K + 1);
-  k_nonzero_flags<<<grid_for(K, B), B, 0, stream>>>(latest.get(), K, flags);
-  exclusive_scan_u32(flags, pos, K, scan_ws, stream);
-  uint32_t total = 0;
-  FH_HIP(hipMemcpyAsync(&total, pos + K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-  FH_HIP(hipStreamSynchronize(stream));
+  // the latest (write) table, then the latest reads under read/write rules
+  // (do_noop_deps, locked.rs:156-169)
+  const uint64_t *tables[2] = {latest.get(), rw ? latest_r.get() : nullptr};
+  uint32_t tot[2] = {0, 0};
+  for (int t = 0; t < 2 && tables[t]; t++) {
+    k_nonzero_flags<<<grid_for(K, B), B, 0, stream>>>(tables[t], K, flags);
+    exclusive_scan_u32(flags, pos, K, scan_ws, stream);
+    FH_HIP(hipMemcpyAsync(&tot[t], pos + K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    if (t == 0) d_out.ensure(size_t(tot[0]) + (rw ? K : 0) + 2);
+    k_nonzero_gather<<<grid_for(K, B), B, 0, stream>>>(tables[t], K, pos,
+                                                        d_out.get() + (t ? tot[0] : 0));
+  }
+  const uint32_t total = tot[0] + tot[1];
   const size_t cnt = size_t(total) + (extra ? 1 : 0);
-  uint64_t *vals = d_out.ensure(cnt + 1);
-  k_nonzero_gather<<<grid_for(K, B), B, 0, stream>>>(latest.get(), K, pos, vals);
+  uint64_t *vals = d_out.get();
   if (extra)
     FH_HIP(hipMemcpyAsync(vals + total, &extra, sizeof(uint64_t), hipMemcpyHostToDevice, stream));
   if (cnt > 1) {
@@ -279,16 +379,20 @@ void KeyDepsDevice::add_batch(size_t n, const uint64_t *dot, const uint32_t *key
                               const uint64_t *key_id, const uint8_t *is_noop,
                               const uint32_t *past_off, const uint64_t *past_dot,
                               uint32_t *out_off, uint64_t *out_dep, size_t out_cap,
-                              size_t *out_len) {
+                              size_t *out_len, const uint8_t *read_only) {
   FH_CHECK(out_off && out_len && (n == 0 || (dot && key_off)), FH_EINVAL, "null argument");
   FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "batch too large");
   const bool has_past = past_off != nullptr;
-  // capacity bound (checked before any state change)
+  const bool has_ro = read_only != nullptr;
+  // capacity bound (checked before any state change); read/write rules give
+  // up to two deps per key and noops see both tables
   size_t noops = 0;
   for (size_t i = 0; i < n; i++) noops += (is_noop && is_noop[i]) ? 1 : 0;
   const size_t nkeys = n ? key_off[n] : 0;
-  size_t bound = nkeys + (n - noops) + (has_past ? past_off[n] : 0);
-  if (noops) bound += noops * (std::min<uint64_t>(key_space, seen_ub + nkeys) + 1);
+  const size_t tables = (has_ro || rw) ? 2 : 1;
+  size_t bound = nkeys * (has_ro ? 2 : 1) + (n - noops) + (has_past ? past_off[n] : 0);
+  if (noops)
+    bound += noops * (tables * std::min<uint64_t>(key_space, seen_ub + nkeys) + 1);
   if (out_cap < bound || (bound && !out_dep)) {
     *out_len = bound;
     throw Error(FH_ECAP, "output capacity too small");
@@ -324,12 +428,18 @@ void KeyDepsDevice::add_batch(size_t n, const uint64_t *dot, const uint32_t *key
   } else {
     d_past.ensure(1);
   }
+  if (has_ro) {
+    enable_rw();
+    FH_HIP(hipMemcpyAsync(d_ro.ensure(n), read_only, n, hipMemcpyHostToDevice, stream));
+  }
   size_t written = 0;
   size_t i = 0;
   while (i < n) {
     size_t j = i;
     while (j < n && !(is_noop && is_noop[j])) j++;
-    if (j > i) written += run_segment(uint32_t(i), uint32_t(j), has_past, out_off, out_dep, written);
+    if (j > i)
+      written += run_segment(uint32_t(i), uint32_t(j), has_past, has_ro, out_off, out_dep,
+                             written);
     if (j < n) {
       // noop (do_add_noop :106-123): deps = previous noop + latest of every key
       const uint64_t prev = noop_latest;
@@ -357,6 +467,16 @@ size_t KeyDepsDevice::cmd_deps(size_t nkeys, const uint64_t *key_id, uint64_t *o
     FH_HIP(hipMemcpyAsync(vals.data(), dv, nkeys * sizeof(uint64_t), hipMemcpyDeviceToHost,
                           stream));
     check_err("cmd_deps");
+    if (rw) {  // do_cmd_deps (locked.rs:172-185): latest read and write
+      std::vector<uint64_t> rv(nkeys);
+      k_gather_keys<<<grid_for(nkeys, 256), 256, 0, stream>>>(latest_r.get(), dk,
+                                                              uint32_t(nkeys), key_space, dv,
+                                                              err.get());
+      FH_HIP(hipMemcpyAsync(rv.data(), dv, nkeys * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                            stream));
+      check_err("cmd_deps");
+      vals.insert(vals.end(), rv.begin(), rv.end());
+    }
   }
   if (noop_latest) vals.push_back(noop_latest);
   std::vector<uint64_t> s;
@@ -408,6 +528,19 @@ fh_status fh_keydeps_add_batch(fh_keydeps *h, size_t n, const uint64_t *dot,
   FH_CHECK(h, FH_EINVAL, "null handle");
   h->dev.add_batch(n, dot, key_off, key_id, is_noop, past_off, past_dot, out_dep_off,
                    out_dep_dot, out_cap, out_len);
+  FH_API_END
+}
+
+fh_status fh_keydeps_add_batch_rw(fh_keydeps *h, size_t n, const uint64_t *dot,
+                                  const uint32_t *key_off, const uint64_t *key_id,
+                                  const uint8_t *read_only, const uint8_t *is_noop,
+                                  const uint32_t *past_off, const uint64_t *past_dot,
+                                  uint32_t *out_dep_off, uint64_t *out_dep_dot, size_t out_cap,
+                                  size_t *out_len) {
+  FH_API_BEGIN
+  FH_CHECK(h && (n == 0 || read_only), FH_EINVAL, "null argument");
+  h->dev.add_batch(n, dot, key_off, key_id, is_noop, past_off, past_dot, out_dep_off,
+                   out_dep_dot, out_cap, out_len, n ? read_only : nullptr);
   FH_API_END
 }
 

@@ -1,7 +1,8 @@
-// scan.hip -- exclusive prefix sum for gfx950, reduce-then-scan (see scan.h).
-// Three launches, no inter-workgroup hand-off inside a launch (cross-XCD
-// hand-offs cost microseconds each on MI355X; a chained scan serialises on
-// them).
+// scan.hip -- exclusive prefix sum / prefix max for gfx950, reduce-then-scan
+// (see scan.h).  Three launches, no inter-workgroup hand-off inside a launch
+// (cross-XCD hand-offs cost microseconds each on MI355X; a chained scan
+// serialises on them).  The operator is a template parameter with identity 0
+// (sum, or max over u32).
 #include "scan.h"
 
 namespace fh {
@@ -11,6 +12,14 @@ constexpr int kThreads = 256;
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
 
+struct OpAdd {
+  static __device__ __forceinline__ uint32_t f(uint32_t a, uint32_t b) { return a + b; }
+};
+struct OpMax {
+  static __device__ __forceinline__ uint32_t f(uint32_t a, uint32_t b) { return a > b ? a : b; }
+};
+
+template <class Op>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_tmp,
                                                     uint32_t *total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -18,21 +27,25 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_tmp,
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t t = __shfl_up(x, o, 64);
-    if (lane >= o) x += t;
+    if (lane >= o) x = Op::f(x, t);
   }
+  // exclusive value inside the wave
+  uint32_t ex = __shfl_up(x, 1, 64);
+  if (lane == 0) ex = 0;
   if (lane == 63) s_tmp[w] = x;
   __syncthreads();
   uint32_t pre = 0, tot = 0;
 #pragma unroll
   for (int i = 0; i < kThreads / 64; i++) {
-    if (i < w) pre += s_tmp[i];
-    tot += s_tmp[i];
+    if (i < w) pre = Op::f(pre, s_tmp[i]);
+    tot = Op::f(tot, s_tmp[i]);
   }
   __syncthreads();
   if (total) *total = tot;
-  return pre + x - v;
+  return Op::f(pre, ex);
 }
 
+template <class Op>
 __global__ void __launch_bounds__(kThreads)
     k_scan_reduce(const uint32_t *__restrict__ in, uint32_t n, uint32_t *__restrict__ bsum) {
   __shared__ uint32_t s_tmp[kThreads / 64];
@@ -41,13 +54,14 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + i * kThreads + threadIdx.x;
-    s += idx < n ? in[idx] : 0u;
+    s = Op::f(s, idx < n ? in[idx] : 0u);
   }
   uint32_t tot = 0;
-  block_excl_scan(s, s_tmp, &tot);
+  block_excl_scan<Op>(s, s_tmp, &tot);
   if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
+template <class Op>
 __global__ void __launch_bounds__(kThreads) k_scan_top(uint32_t *__restrict__ bsum, uint32_t nb) {
   __shared__ uint32_t s_tmp[kThreads / 64];
   uint32_t carry = 0;
@@ -55,12 +69,13 @@ __global__ void __launch_bounds__(kThreads) k_scan_top(uint32_t *__restrict__ bs
     const uint32_t b = b0 + threadIdx.x;
     const uint32_t v = b < nb ? bsum[b] : 0u;
     uint32_t tot = 0;
-    const uint32_t ex = block_excl_scan(v, s_tmp, &tot);
-    if (b < nb) bsum[b] = carry + ex;
-    carry += tot;
+    const uint32_t ex = block_excl_scan<Op>(v, s_tmp, &tot);
+    if (b < nb) bsum[b] = Op::f(carry, ex);
+    carry = Op::f(carry, tot);
   }
 }
 
+template <class Op>
 __global__ void __launch_bounds__(kThreads)
     k_scan_down(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint32_t n,
                 const uint32_t *__restrict__ bsum) {
@@ -73,22 +88,20 @@ __global__ void __launch_bounds__(kThreads)
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + i;
     v[i] = idx < n ? in[idx] : 0u;
-    s += v[i];
+    s = Op::f(s, v[i]);
   }
-  uint32_t run = bsum[blockIdx.x] + block_excl_scan(s, s_tmp, nullptr);
+  uint32_t run = Op::f(bsum[blockIdx.x], block_excl_scan<Op>(s, s_tmp, nullptr));
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + i;
     if (idx < n) out[idx] = run;
-    run += v[i];
+    run = Op::f(run, v[i]);
     if (idx + 1 == n) out[n] = run;
   }
 }
 
-}  // namespace
-
-void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
-                        hipStream_t s) {
+template <class Op>
+void scan_impl(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws, hipStream_t s) {
   FH_CHECK(n < (size_t(1) << 31), FH_EINVAL, "scan: too many elements");
   if (n == 0) {
     FH_HIP(hipMemsetAsync(out, 0, sizeof(uint32_t), s));
@@ -96,9 +109,21 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspa
   }
   const uint32_t nb = uint32_t((n + kTile - 1) / kTile);
   uint32_t *bsum = ws.status.ensure(nb + 1);
-  k_scan_reduce<<<nb, kThreads, 0, s>>>(in, uint32_t(n), bsum);
-  k_scan_top<<<1, kThreads, 0, s>>>(bsum, nb);
-  k_scan_down<<<nb, kThreads, 0, s>>>(in, out, uint32_t(n), bsum);
+  k_scan_reduce<Op><<<nb, kThreads, 0, s>>>(in, uint32_t(n), bsum);
+  k_scan_top<Op><<<1, kThreads, 0, s>>>(bsum, nb);
+  k_scan_down<Op><<<nb, kThreads, 0, s>>>(in, out, uint32_t(n), bsum);
+}
+
+}  // namespace
+
+void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
+                        hipStream_t s) {
+  scan_impl<OpAdd>(in, out, n, ws, s);
+}
+
+void exclusive_scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
+                            hipStream_t s) {
+  scan_impl<OpMax>(in, out, n, ws, s);
 }
 
 }  // namespace fh

@@ -60,12 +60,17 @@ def make_config(n=1, f=0, shard_count=1, device=-1, key_space=1 << 20) -> L.fh_c
 
 
 class HipKeyDeps:
-    """KeyDeps implementation over fh_keydeps_* (include/fantoch_hip.h)."""
+    """KeyDeps implementation over fh_keydeps_* (include/fantoch_hip.h).
+
+    read_write=False: SequentialKeyDeps (deps/keys/sequential.rs);
+    read_write=True: LockedKeyDeps' read/write rules (deps/keys/locked.rs:
+    83-169), with Command.read_only selecting the rule per command."""
 
     def __init__(self, shard_id: int = 0, key_space: int = 1 << 20, device: int = -1,
-                 intern: bool = True):
+                 intern: bool = True, read_write: bool = False):
         self._lib = L.load()
         self.shard_id = shard_id
+        self.read_write = read_write
         self.cfg = make_config(device=device, key_space=key_space)
         h = C.c_void_p()
         L.check(self._lib.fh_keydeps_create(shard_id, C.byref(self.cfg), C.byref(h)))
@@ -101,17 +106,19 @@ class HipKeyDeps:
         self._note_shards(dot, cmd)
         past_l = None if past is None else [p.dot if isinstance(p, Dependency) else int(p)
                                             for p in past]
+        ro = [bool(getattr(cmd, "read_only", False))] if self.read_write else None
         off, deps = self.add_batch([dot], [self._key_ids(cmd)], None,
-                                   None if past_l is None else [past_l])
+                                   None if past_l is None else [past_l], read_only=ro)
         return set(int(x) for x in deps[off[0]:off[1]])
 
     def add_noop(self, dot: int) -> set:
-        off, deps = self.add_batch([dot], [[]], [True], None)
+        off, deps = self.add_batch([dot], [[]], [True], None,
+                                   read_only=[False] if self.read_write else None)
         return set(int(x) for x in deps[off[0]:off[1]])
 
     def cmd_deps(self, cmd) -> set:
         k = np.asarray(self._key_ids(cmd), dtype=np.uint64)
-        cap = len(k) + 1
+        cap = 2 * len(k) + 1
         out = np.zeros(cap, dtype=np.uint64)
         n = C.c_size_t(0)
         L.check(self._lib.fh_keydeps_cmd_deps(self._h, len(k), L.ptr(k), L.ptr(out), cap,
@@ -126,11 +133,13 @@ class HipKeyDeps:
         return set(int(x) for x in out[:n.value])
 
     # -- batched form ------------------------------------------------------
-    def add_batch(self, dots, keys, is_noop=None, past=None):
+    def add_batch(self, dots, keys, is_noop=None, past=None, read_only=None):
         """dots: sequence of packed dots; keys: per-command key-id lists (or a
         (key_off, key_ids) pair of arrays); is_noop: optional bools; past:
-        optional per-command dot lists (None = no past for every command).
-        Returns (dep_off[n+1], dep_dots) as numpy arrays."""
+        optional per-command dot lists (None = no past for every command);
+        read_only: optional bools -- LockedKeyDeps' read/write rules
+        (fh_keydeps_add_batch_rw).  Returns (dep_off[n+1], dep_dots) as numpy
+        arrays."""
         n = len(dots)
         dot_a = np.ascontiguousarray(dots, dtype=np.uint64)
         if isinstance(keys, tuple):
@@ -147,15 +156,22 @@ class HipKeyDeps:
             past_off[1:] = np.cumsum([len(p) for p in past]) if n else []
             past_dot = np.asarray([x for p in past for x in p], dtype=np.uint64)
         out_off = np.zeros(n + 1, dtype=np.uint32)
-        cap = int(len(key_ids) + n + (0 if past_dot is None else len(past_dot)) + 1)
+        ro = None if read_only is None else np.ascontiguousarray(read_only, dtype=np.uint8)
+        cap = int(len(key_ids) * (1 if ro is None else 2) + n +
+                  (0 if past_dot is None else len(past_dot)) + 1)
         while True:
             out = np.zeros(cap, dtype=np.uint64)
             ln = C.c_size_t(0)
-            st = self._lib.fh_keydeps_add_batch(
-                self._h, n, L.ptr(dot_a), L.ptr(key_off), L.ptr(key_ids) if len(key_ids) else None,
-                L.ptr(noop), L.ptr(past_off),
-                L.ptr(past_dot) if past_dot is not None and len(past_dot) else None,
-                L.ptr(out_off), L.ptr(out), cap, C.byref(ln))
+            kp = L.ptr(key_ids) if len(key_ids) else None
+            pp = L.ptr(past_dot) if past_dot is not None and len(past_dot) else None
+            if ro is None:
+                st = self._lib.fh_keydeps_add_batch(
+                    self._h, n, L.ptr(dot_a), L.ptr(key_off), kp, L.ptr(noop), L.ptr(past_off),
+                    pp, L.ptr(out_off), L.ptr(out), cap, C.byref(ln))
+            else:
+                st = self._lib.fh_keydeps_add_batch_rw(
+                    self._h, n, L.ptr(dot_a), L.ptr(key_off), kp, L.ptr(ro), L.ptr(noop),
+                    L.ptr(past_off), pp, L.ptr(out_off), L.ptr(out), cap, C.byref(ln))
             if st == L.FH_ECAP:
                 cap = int(ln.value)
                 continue

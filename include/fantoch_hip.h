@@ -100,6 +100,22 @@ fh_status fh_keydeps_add_batch(fh_keydeps *h, size_t n, const uint64_t *dot,
                                uint64_t *out_dep_dot, size_t out_cap,
                                size_t *out_len);
 
+/* fh_keydeps_add_batch with LockedKeyDeps' read/write rules
+ * (deps/keys/locked.rs:83-128): per key, a read-only command
+ * (read_only[i] = Command::read_only, fantoch/src/command.rs:65-67) depends
+ * on the latest write and becomes the latest read; a write depends on the
+ * latest read and the latest write and becomes the latest write.  Noops
+ * (:130-169) depend on every key's latest read and write.  Write-only
+ * batches give SequentialKeyDeps' results.  Upper bound for out_cap:
+ * sum_i(2 keys_i + past_i + 1) for commands, plus (2 distinct keys seen + 1)
+ * per noop. */
+fh_status fh_keydeps_add_batch_rw(fh_keydeps *h, size_t n, const uint64_t *dot,
+                                  const uint32_t *key_off, const uint64_t *key_id,
+                                  const uint8_t *read_only, const uint8_t *is_noop,
+                                  const uint32_t *past_off, const uint64_t *past_dot,
+                                  uint32_t *out_dep_off, uint64_t *out_dep_dot,
+                                  size_t out_cap, size_t *out_len);
+
 /* KeyDeps::cmd_deps (test-only query, keys/mod.rs:54-56;
  * sequential.rs:44-50): latest noop + latest dot of each key, no update. */
 fh_status fh_keydeps_cmd_deps(fh_keydeps *h, size_t nkeys,

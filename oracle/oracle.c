@@ -308,6 +308,107 @@ size_t fo_keydeps_run(uint64_t shard_id, size_t n, const uint64_t *dot,
 }
 
 /* ------------------------------------------------------------------ */
+/* LockedKeyDeps (deps/keys/locked.rs), applied sequentially           */
+/* ------------------------------------------------------------------ */
+struct fo_lkeydeps {
+  u64map w, r;        /* LatestRW{read, write} per key  :10-15 */
+  uint64_t noop_dot;  /* latest_noop (0 == None)        :21 */
+  vec64 scratch;
+};
+
+fo_lkeydeps *fo_lkeydeps_new(uint64_t shard_id) {
+  fo_lkeydeps *kd = (fo_lkeydeps *)calloc(1, sizeof(*kd));
+  (void)shard_id;
+  map_init(&kd->w, 1024);
+  map_init(&kd->r, 1024);
+  return kd;
+}
+void fo_lkeydeps_free(fo_lkeydeps *kd) {
+  if (!kd) return;
+  map_free(&kd->w);
+  map_free(&kd->r);
+  free(kd->scratch.a);
+  free(kd);
+}
+
+/* add_cmd (:34-46) -> do_add_cmd (:83-128) */
+size_t fo_lkeydeps_add_cmd(fo_lkeydeps *kd, uint64_t dot, const uint64_t *keys,
+                           size_t nkeys, int read_only, const uint64_t *past,
+                           size_t npast, int has_past, uint64_t *out, size_t cap) {
+  vec64 *d = &kd->scratch;
+  d->len = 0;
+  if (has_past)
+    for (size_t i = 0; i < npast; i++) vpush(d, past[i]);
+  for (size_t i = 0; i < nkeys; i++) {
+    uint64_t *wd = map_get(&kd->w, keys[i]);
+    if (read_only) { /* :100-106: latest write; become the latest read */
+      if (wd) vpush(d, *wd);
+      map_put(&kd->r, keys[i], dot);
+    } else { /* :107-117: latest read and write; become the latest write */
+      uint64_t *rd = map_get(&kd->r, keys[i]);
+      if (rd) vpush(d, *rd);
+      if (wd) {
+        vpush(d, *wd);
+        *wd = dot;
+      } else {
+        map_put(&kd->w, keys[i], dot);
+      }
+    }
+  }
+  if (kd->noop_dot) vpush(d, kd->noop_dot); /* :124 */
+  size_t n = sort_unique(d->a, d->len);
+  return emit(d->a, n, out, cap);
+}
+
+/* do_noop_deps (:156-169): every key's latest read and write */
+static void lk_noop_deps(const fo_lkeydeps *kd, vec64 *d) {
+  for (size_t i = 0; i < kd->w.cap; i++)
+    if (kd->w.k[i] != EMPTY_KEY) vpush(d, kd->w.v[i]);
+  for (size_t i = 0; i < kd->r.cap; i++)
+    if (kd->r.k[i] != EMPTY_KEY) vpush(d, kd->r.v[i]);
+}
+
+/* add_noop (:48-52) -> do_add_noop (:130-154) */
+size_t fo_lkeydeps_add_noop(fo_lkeydeps *kd, uint64_t dot, uint64_t *out, size_t cap) {
+  vec64 *d = &kd->scratch;
+  d->len = 0;
+  uint64_t prev = kd->noop_dot;
+  kd->noop_dot = dot;
+  if (prev) vpush(d, prev);
+  lk_noop_deps(kd, d);
+  size_t n = sort_unique(d->a, d->len);
+  return emit(d->a, n, out, cap);
+}
+
+/* cmd_deps (:54-60) with do_cmd_deps (:172-185) */
+size_t fo_lkeydeps_cmd_deps(const fo_lkeydeps *kd, const uint64_t *keys, size_t nkeys,
+                            uint64_t *out, size_t cap) {
+  vec64 d = {0};
+  if (kd->noop_dot) vpush(&d, kd->noop_dot);
+  for (size_t i = 0; i < nkeys; i++) {
+    uint64_t *rd = map_get(&kd->r, keys[i]);
+    uint64_t *wd = map_get(&kd->w, keys[i]);
+    if (rd) vpush(&d, *rd);
+    if (wd) vpush(&d, *wd);
+  }
+  size_t n = sort_unique(d.a, d.len);
+  emit(d.a, n, out, cap);
+  free(d.a);
+  return n;
+}
+
+/* noop_deps (:62-68) */
+size_t fo_lkeydeps_noop_deps(const fo_lkeydeps *kd, uint64_t *out, size_t cap) {
+  vec64 d = {0};
+  if (kd->noop_dot) vpush(&d, kd->noop_dot);
+  lk_noop_deps(kd, &d);
+  size_t n = sort_unique(d.a, d.len);
+  emit(d.a, n, out, cap);
+  free(d.a);
+  return n;
+}
+
+/* ------------------------------------------------------------------ */
 /* QuorumDeps (deps/quorum.rs)                                         */
 /* ------------------------------------------------------------------ */
 size_t fo_quorum_deps(size_t fast_quorum_size, size_t nrep,

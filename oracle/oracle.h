@@ -67,6 +67,29 @@ size_t fo_keydeps_run(uint64_t shard_id, size_t n, const uint64_t *dot,
                       uint64_t *out_dep, size_t out_dep_cap);
 
 /* ---------------------------------------------------------------------
+ * LockedKeyDeps (deps/keys/locked.rs:10-186), applied sequentially: per key
+ * a read depends on the latest write and becomes the latest read; a write
+ * depends on the latest read and write and becomes the latest write; noops
+ * see every key's latest read and write.  Parity: the write rules are pinned
+ * by key_deps_flow::<LockedKeyDeps> (keys/mod.rs:86-88, write-only); the
+ * reference has no read-only known-answer test, so the read rules are
+ * restated from locked.rs:100-106 and checked by hand-derived cases
+ * (tests/test_oracle_rw.py).
+ * ------------------------------------------------------------------- */
+typedef struct fo_lkeydeps fo_lkeydeps;
+
+fo_lkeydeps *fo_lkeydeps_new(uint64_t shard_id);
+void fo_lkeydeps_free(fo_lkeydeps *kd);
+size_t fo_lkeydeps_add_cmd(fo_lkeydeps *kd, uint64_t dot, const uint64_t *keys,
+                           size_t nkeys, int read_only, const uint64_t *past,
+                           size_t npast, int has_past, uint64_t *out, size_t cap);
+size_t fo_lkeydeps_add_noop(fo_lkeydeps *kd, uint64_t dot, uint64_t *out,
+                            size_t cap);
+size_t fo_lkeydeps_cmd_deps(const fo_lkeydeps *kd, const uint64_t *keys,
+                            size_t nkeys, uint64_t *out, size_t cap);
+size_t fo_lkeydeps_noop_deps(const fo_lkeydeps *kd, uint64_t *out, size_t cap);
+
+/* ---------------------------------------------------------------------
  * QuorumDeps  (deps/quorum.rs:7-98)
  * reports: nrep dep-sets given as CSR (rep_off[nrep+1], rep_dep).
  * Returns union size, writes sorted union into out; *flag receives the

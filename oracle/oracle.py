@@ -63,6 +63,17 @@ def _load():
     lib.fo_graph_drain.argtypes = [V, V, V, S]
     lib.fo_graph_pending_count.restype = S
     lib.fo_graph_pending_count.argtypes = [V]
+    lib.fo_lkeydeps_new.restype = V
+    lib.fo_lkeydeps_new.argtypes = [C.c_uint64]
+    lib.fo_lkeydeps_free.argtypes = [V]
+    lib.fo_lkeydeps_add_cmd.restype = S
+    lib.fo_lkeydeps_add_cmd.argtypes = [V, C.c_uint64, V, S, C.c_int, V, S, C.c_int, V, S]
+    lib.fo_lkeydeps_add_noop.restype = S
+    lib.fo_lkeydeps_add_noop.argtypes = [V, C.c_uint64, V, S]
+    lib.fo_lkeydeps_cmd_deps.restype = S
+    lib.fo_lkeydeps_cmd_deps.argtypes = [V, V, S, V, S]
+    lib.fo_lkeydeps_noop_deps.restype = S
+    lib.fo_lkeydeps_noop_deps.argtypes = [V, V, S]
     lib.fo_pred_new.restype = V
     lib.fo_pred_new.argtypes = [C.c_uint32]
     lib.fo_pred_free.argtypes = [V]
@@ -149,6 +160,47 @@ class KeyDeps:
         n = lib().fo_keydeps_noop_deps(self._h, None, 0)
         out = np.zeros(max(n, 1), dtype=np.uint64)
         lib().fo_keydeps_noop_deps(self._h, _ptr(out), n)
+        return set(int(x) for x in out[:n])
+
+
+class LockedKeyDeps:
+    """LockedKeyDeps (deps/keys/locked.rs:10-186), applied sequentially."""
+
+    def __init__(self, shard_id: int = 0):
+        self._h = lib().fo_lkeydeps_new(shard_id)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().fo_lkeydeps_free(self._h)
+            self._h = None
+
+    def add_cmd(self, dot_, keys, read_only=False, past=None):
+        k = _arr(keys)
+        p = _arr(past or [])
+        cap = len(p) + 2 * len(k) + 1
+        out = np.zeros(cap, dtype=np.uint64)
+        n = lib().fo_lkeydeps_add_cmd(self._h, dot_, _ptr(k), len(k), 1 if read_only else 0,
+                                      _ptr(p), len(p), 1 if past is not None else 0,
+                                      _ptr(out), cap)
+        return set(int(x) for x in out[:n])
+
+    def add_noop(self, dot_):
+        n = lib().fo_lkeydeps_noop_deps(self._h, None, 0) + 1
+        out = np.zeros(n, dtype=np.uint64)
+        m = lib().fo_lkeydeps_add_noop(self._h, dot_, _ptr(out), n)
+        assert m <= n
+        return set(int(x) for x in out[:m])
+
+    def cmd_deps(self, keys):
+        k = _arr(keys)
+        out = np.zeros(2 * len(k) + 1, dtype=np.uint64)
+        n = lib().fo_lkeydeps_cmd_deps(self._h, _ptr(k), len(k), _ptr(out), len(out))
+        return set(int(x) for x in out[:n])
+
+    def noop_deps(self):
+        n = lib().fo_lkeydeps_noop_deps(self._h, None, 0)
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        lib().fo_lkeydeps_noop_deps(self._h, _ptr(out), n)
         return set(int(x) for x in out[:n])
 
 
