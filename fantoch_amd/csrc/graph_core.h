@@ -84,6 +84,7 @@ struct GraphCore {
   DBuf<uint8_t> blocked;
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)
   bool profile = false;
+  uint32_t dbg_rounds = 0, dbg_hprop = 0, dbg_reach = 0;  // FH_GRAPH_DEBUG counters
   // per-kernel timing (engine profiling)
   std::vector<std::pair<const char *, hipEvent_t>> *marks = nullptr;
 
