@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfantoch_hip.so")
 
 FH_OK, FH_EINVAL, FH_EHIP, FH_EOOM, FH_EINVARIANT, FH_ECAP, FH_ENOTIMPL = range(7)
+FH_REPLY_INFO, FH_REPLY_EXECUTED = 0, 1  # RequestReply kinds (include/fantoch_hip.h)
 STATUS_NAMES = ["FH_OK", "FH_EINVAL", "FH_EHIP", "FH_EOOM", "FH_EINVARIANT", "FH_ECAP",
                 "FH_ENOTIMPL"]
 
@@ -67,6 +68,11 @@ SIGNATURES = {
     "fh_graph_set_executed_frontier": (C.c_int, [V, C.c_uint32, C.c_uint64]),
     "fh_graph_pending": (C.c_int, [V, P(S)]),
     "fh_graph_missing": (C.c_int, [V, V, S, P(S)]),
+    "fh_graph_add_batch_sharded": (C.c_int, [V, S, V, V, V, V, V, V, V]),
+    "fh_graph_requests": (C.c_int, [V, V, V, S, P(S)]),
+    "fh_graph_handle_requests": (C.c_int, [V, C.c_uint64, S, V]),
+    "fh_graph_cleanup": (C.c_int, [V]),
+    "fh_graph_request_replies": (C.c_int, [V, S, V, V, V, V, V, S, V, V, P(S), P(S)]),
     "fh_engine_create": (C.c_int, [P(fh_config), P(V)]),
     "fh_engine_destroy": (C.c_int, [V]),
     "fh_engine_reset": (C.c_int, [V]),

@@ -12,6 +12,9 @@
 // host and mirrored to the device per batch.
 #include <algorithm>
 #include <deque>
+#include <map>
+#include <set>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -86,9 +89,23 @@ struct GraphDevice {
   hipStream_t stream = nullptr;
   int key_bits = 1;
   AEClock clock;
-  // carried pending vertices (arrival order)
-  std::vector<uint64_t> p_dot, p_keys, p_deps;
+  // carried pending vertices (arrival order); p_cshard = Command::shards()
+  // bitmask per vertex, p_dshard = Dependency::shards bitmask per dependency
+  std::vector<uint64_t> p_dot, p_keys, p_deps, p_cshard, p_dshard;
   std::vector<uint32_t> p_koff{0}, p_doff{0};
+  // partial replication (graph/mod.rs:139-157, 279-375; index.rs:145-211):
+  // requested = dots already indexed as a missing non-local dependency
+  // (PendingIndex keys that produced a request), out_requests = requests()
+  // not yet taken, buffered = buffered_in_requests, replies = out_request_replies
+  std::unordered_set<uint64_t> requested;
+  std::set<std::pair<uint64_t, uint64_t>> out_requests;  // (target shard, dot)
+  std::map<uint64_t, std::set<uint64_t>> buffered;       // from shard -> dots
+  struct Reply {
+    uint64_t to, dot, cshard;
+    uint8_t kind;  // FH_REPLY_INFO / FH_REPLY_EXECUTED
+    std::vector<uint64_t> deps, dshards;
+  };
+  std::vector<Reply> replies;
   // drain queue
   std::deque<std::pair<uint64_t, uint64_t>> ready;
   std::vector<uint64_t> missing_now;
@@ -119,8 +136,79 @@ struct GraphDevice {
     }
   }
 
+  // PendingIndex::index (index.rs:171-205) as called by index_pending
+  // (mod.rs:527-556) on the first find of each added vertex: a dependency
+  // missing when its child is added (not executed, not a carried vertex, not
+  // an earlier vertex of this batch) and not replicated by this shard is
+  // requested from dep.dot.target_shard(n) the first time it is indexed.  In
+  // partial replication the first find collects every missing dependency of
+  // the reachable set (tarjan.rs:161-169); the reachable vertices' own missing
+  // deps were indexed on their own first finds (missing is monotone: missing
+  // -> present -> executed), so the direct deps of each added vertex suffice.
+  void index_requests(size_t n, const uint64_t *dot, const uint32_t *dep_off,
+                      const uint64_t *dep_dot, const uint64_t *dep_shards) {
+    if (cfg.shard_count <= 1 || !dep_shards || n == 0) return;
+    std::unordered_set<uint64_t> carried(p_dot.begin(), p_dot.end());
+    std::unordered_map<uint64_t, size_t> pos;
+    pos.reserve(n);
+    for (size_t i = 0; i < n; i++) pos.emplace(dot[i], i);
+    const uint32_t nproc = cfg.n ? cfg.n : 1;
+    for (size_t i = 0; i < n; i++) {
+      for (uint32_t e = dep_off[i]; e < dep_off[i + 1]; e++) {
+        const uint64_t d = dep_dot[e];
+        if (d == dot[i] || clock.contains(d) || carried.count(d)) continue;
+        auto it = pos.find(d);
+        if (it != pos.end() && it->second < i) continue;
+        // "shards should be set if it's not a noop" (index.rs:190-194)
+        FH_CHECK(dep_shards[e] != 0, FH_EINVARIANT,
+                 "PendingIndex::index: missing dependency without a shard set");
+        if ((dep_shards[e] >> shard_id) & 1) continue;  // is_mine
+        if (!requested.insert(d).second) continue;     // already indexed
+        const uint64_t target = ((d >> 56) - 1) / nproc;  // Dot::target_shard (id.rs:59-61)
+        out_requests.emplace(target, d);
+      }
+    }
+  }
+
+  // process_requests (mod.rs:297-375): Info for an indexed vertex, Executed
+  // for an executed dot, otherwise buffer until the next cleanup.
+  void process_requests(uint64_t from, const uint64_t *dots, size_t n) {
+    std::unordered_map<uint64_t, size_t> vid;
+    vid.reserve(p_dot.size());
+    for (size_t v = 0; v < p_dot.size(); v++) vid.emplace(p_dot[v], v);
+    for (size_t i = 0; i < n; i++) {
+      const uint64_t d = dots[i];
+      auto it = vid.find(d);
+      if (it != vid.end()) {
+        const size_t v = it->second;
+        // panic if the shard that requested this vertex replicates it (:313-322)
+        FH_CHECK(from >= 64 || !((p_cshard[v] >> from) & 1), FH_EINVARIANT,
+                 "Graph::process_requests: requested dot is replicated by the requesting shard");
+        Reply r{from, d, p_cshard[v], FH_REPLY_INFO, {}, {}};
+        r.deps.assign(p_deps.begin() + p_doff[v], p_deps.begin() + p_doff[v + 1]);
+        r.dshards.assign(p_dshard.begin() + p_doff[v], p_dshard.begin() + p_doff[v + 1]);
+        replies.push_back(std::move(r));
+      } else if (clock.contains(d)) {
+        replies.push_back(Reply{from, d, 0, FH_REPLY_EXECUTED, {}, {}});
+      } else {
+        buffered[from].insert(d);
+      }
+    }
+  }
+
+  // cleanup -> check_pending_requests (mod.rs:168-179, 673-678)
+  void retry_buffered() {
+    auto b = std::move(buffered);
+    buffered.clear();
+    for (auto &kv : b) {
+      std::vector<uint64_t> v(kv.second.begin(), kv.second.end());
+      process_requests(kv.first, v.data(), v.size());
+    }
+  }
+
   void add_batch(size_t n, const uint64_t *dot, const uint32_t *key_off, const uint64_t *key_id,
-                 const uint32_t *dep_off, const uint64_t *dep_dot) {
+                 const uint32_t *dep_off, const uint64_t *dep_dot,
+                 const uint64_t *cmd_shards = nullptr, const uint64_t *dep_shards = nullptr) {
     FH_CHECK(n == 0 || (dot && key_off && dep_off), FH_EINVAL, "null argument");
     FH_HIP(hipSetDevice(device));
     // vertices: carried pending (earlier arrivals) then the batch
@@ -130,7 +218,7 @@ struct GraphDevice {
     std::vector<uint64_t> vdot(p_dot);
     vdot.insert(vdot.end(), dot, dot + n);
     std::vector<uint32_t> koff(p_koff), doff(p_doff);
-    std::vector<uint64_t> keys(p_keys), deps(p_deps);
+    std::vector<uint64_t> keys(p_keys), deps(p_deps), cshard(p_cshard), dshard(p_dshard);
     for (size_t i = 0; i < n; i++) {
       for (uint32_t e = key_off[i]; e < key_off[i + 1]; e++) {
         FH_CHECK(key_id[e] < cfg.key_space, FH_EINVAL, "key id >= key_space");
@@ -139,6 +227,9 @@ struct GraphDevice {
       koff.push_back(uint32_t(keys.size()));
       deps.insert(deps.end(), dep_dot + dep_off[i], dep_dot + dep_off[i + 1]);
       doff.push_back(uint32_t(deps.size()));
+      cshard.push_back(cmd_shards ? cmd_shards[i] : 0);
+      for (uint32_t e = dep_off[i]; e < dep_off[i + 1]; e++)
+        dshard.push_back(dep_shards ? dep_shards[e] : 0);
     }
     if (V == 0) return;
     std::vector<uint32_t> k32(keys.begin(), keys.end());
@@ -188,6 +279,7 @@ struct GraphDevice {
     FH_HIP(hipStreamSynchronize(stream));
     // mod.rs:235-240: indexing an already indexed dot panics
     FH_CHECK(dup == 0, FH_EINVARIANT, "Graph::handle_add tried to index already indexed dot");
+    index_requests(n, dot, dep_off, dep_dot, dep_shards);
     uint32_t *dst = d_dst.ensure(E + 1);
     k_resolve_fill<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), ddot_v, ddo, dd, sd, sv,
                                                       d_frontier.get(), dexc,
@@ -225,6 +317,8 @@ struct GraphDevice {
     p_dot.clear();
     p_keys.clear();
     p_deps.clear();
+    p_cshard.clear();
+    p_dshard.clear();
     p_koff.assign(1, 0);
     p_doff.assign(1, 0);
     std::unordered_set<uint64_t> present;
@@ -238,7 +332,9 @@ struct GraphDevice {
       p_keys.insert(p_keys.end(), keys.begin() + koff[v], keys.begin() + koff[v + 1]);
       p_koff.push_back(uint32_t(p_keys.size()));
       p_deps.insert(p_deps.end(), deps.begin() + doff[v], deps.begin() + doff[v + 1]);
+      p_dshard.insert(p_dshard.end(), dshard.begin() + doff[v], dshard.begin() + doff[v + 1]);
       p_doff.push_back(uint32_t(p_deps.size()));
+      p_cshard.push_back(cshard[v]);
       for (uint32_t e = doff[v]; e < doff[v + 1]; e++) {
         const uint64_t d = deps[e];
         if (d != vdot[v] && !clock.contains(d) && !present.count(d) && seen.insert(d).second)
@@ -289,6 +385,83 @@ fh_status fh_graph_add_batch(fh_graph *h, size_t n, const uint64_t *dot, const u
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
   h->dev.add_batch(n, dot, key_off, key_id, dep_off, dep_dot);
+  FH_API_END
+}
+
+fh_status fh_graph_add_batch_sharded(fh_graph *h, size_t n, const uint64_t *dot,
+                                     const uint32_t *key_off, const uint64_t *key_id,
+                                     const uint32_t *dep_off, const uint64_t *dep_dot,
+                                     const uint64_t *cmd_shards, const uint64_t *dep_shards) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_CHECK(h->dev.shard_id < 64, FH_EINVAL, "shard sets are 64-bit masks: shard_id must be < 64");
+  h->dev.add_batch(n, dot, key_off, key_id, dep_off, dep_dot, cmd_shards, dep_shards);
+  FH_API_END
+}
+
+fh_status fh_graph_requests(fh_graph *h, uint64_t *dot, uint64_t *shard, size_t cap,
+                            size_t *len) {
+  FH_API_BEGIN
+  FH_CHECK(h && len, FH_EINVAL, "null argument");
+  auto &r = h->dev.out_requests;
+  *len = r.size();
+  if (r.empty()) return FH_OK;
+  FH_CHECK(dot && shard && cap >= r.size(), FH_ECAP, "request output capacity too small");
+  size_t i = 0;
+  for (const auto &p : r) {
+    shard[i] = p.first;
+    dot[i] = p.second;
+    i++;
+  }
+  r.clear();
+  FH_API_END
+}
+
+fh_status fh_graph_handle_requests(fh_graph *h, uint64_t from_shard, size_t n,
+                                   const uint64_t *dots) {
+  FH_API_BEGIN
+  FH_CHECK(h && (n == 0 || dots), FH_EINVAL, "null argument");
+  h->dev.process_requests(from_shard, dots, n);
+  FH_API_END
+}
+
+fh_status fh_graph_cleanup(fh_graph *h) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.retry_buffered();
+  FH_API_END
+}
+
+fh_status fh_graph_request_replies(fh_graph *h, size_t cap, uint64_t *to_shard, uint8_t *kind,
+                                   uint64_t *dot, uint64_t *cmd_shards, uint32_t *dep_off,
+                                   size_t dep_cap, uint64_t *dep_dot, uint64_t *dep_shards,
+                                   size_t *n_replies, size_t *n_deps) {
+  FH_API_BEGIN
+  FH_CHECK(h && n_replies && n_deps, FH_EINVAL, "null argument");
+  auto &rs = h->dev.replies;
+  size_t nd = 0;
+  for (const auto &r : rs) nd += r.deps.size();
+  *n_replies = rs.size();
+  *n_deps = nd;
+  if (rs.empty()) return FH_OK;
+  FH_CHECK(cap >= rs.size() && dep_cap >= nd && to_shard && kind && dot && cmd_shards && dep_off &&
+               (nd == 0 || (dep_dot && dep_shards)),
+           FH_ECAP, "reply output capacity too small");
+  size_t e = 0;
+  dep_off[0] = 0;
+  for (size_t i = 0; i < rs.size(); i++) {
+    const auto &r = rs[i];
+    to_shard[i] = r.to;
+    kind[i] = r.kind;
+    dot[i] = r.dot;
+    cmd_shards[i] = r.cshard;
+    for (size_t j = 0; j < r.deps.size(); j++, e++) {
+      dep_dot[e] = r.deps[j];
+      dep_shards[e] = r.dshards[j];
+    }
+    dep_off[i + 1] = uint32_t(e);
+  }
+  rs.clear();
   FH_API_END
 }
 

@@ -10,10 +10,19 @@ fantoch_ps/src/executor/graph/executor.rs:19-197:
     monitor() -> Option<&ExecutionOrderMonitor>    -> monitor() -> {key: [rifl, ...]}
     parallel() -> bool                             -> parallel() (True, like GraphExecutor)
 
-handle() processes one Add at a time (batch of one, API-compatible);
-handle_batch() takes a whole arrival-ordered batch in one device pass.  The
-reference's Request/RequestReply/Executed infos (partial replication) are not
-supported yet; handle() raises for them.
+    cleanup() / to_executors / fetch_requests / fetch_request_replies
+                                                   -> cleanup(), requests(), request_replies()
+
+handle() processes one info at a time (an Add is a batch of one,
+API-compatible); handle_batch() takes a whole arrival-ordered batch of Adds
+in one device pass.  Partial replication (graph/mod.rs:279-408): Add infos
+carry shard sets (Dependency.shards, Command.shards()); a missing dependency
+not replicated here becomes a request to its target shard; Request infos are
+answered with Info / Executed replies or buffered until cleanup();
+RequestReply infos are ingested (Info -> add, Executed -> executed clock +
+pending retry).  One handle plays both executor roles of the shard (the
+reference routes Add/RequestReply to index 0 and Request/Executed to index 1,
+executor.rs:242-262, over a shared VertexIndex).
 """
 from __future__ import annotations
 
@@ -38,6 +47,43 @@ class GraphExecutionInfo:
     @staticmethod
     def add(dot, cmd, deps):
         return GraphExecutionInfo("add", dot, cmd, deps)
+
+    @staticmethod
+    def request(from_shard, dots):
+        """GraphExecutionInfo::Request{from, dots} (executor.rs:215-220)."""
+        return GraphExecutionInfo("request", from_shard, None, list(dots))
+
+    @staticmethod
+    def request_reply(replies):
+        """GraphExecutionInfo::RequestReply{infos} (executor.rs:221-224)."""
+        return GraphExecutionInfo("request_reply", 0, None, list(replies))
+
+    @staticmethod
+    def executed(dots):
+        """GraphExecutionInfo::Executed{dots} (executor.rs:225-227)."""
+        return GraphExecutionInfo("executed", 0, None, list(dots))
+
+
+@dataclass
+class RequestReply:
+    """RequestReply::{Info{dot, cmd, deps}, Executed{dot}} (graph/mod.rs:33-43)."""
+    kind: str          # "info" | "executed"
+    dot: int
+    cmd: object = None
+    deps: object = None  # list[Dependency] for Info
+
+
+def _mask(shards) -> int:
+    m = 0
+    for s in shards:
+        if s >= 64:
+            raise ValueError("shard ids must be < 64")
+        m |= 1 << s
+    return m
+
+
+def _unmask(m: int):
+    return frozenset(s for s in range(64) if (m >> s) & 1)
 
 
 class HipGraphExecutor:
@@ -73,30 +119,127 @@ class HipGraphExecutor:
         return list(cmd.keys(self.shard_id)) if hasattr(cmd, "keys") else list(cmd)
 
     def handle(self, info: GraphExecutionInfo):
-        if info.kind != "add":
-            raise NotImplementedError("partial-replication executor infos (SURVEY §8f rank 2)")
-        self.handle_batch([info])
+        """GraphExecutor::handle (executor.rs:76-100)."""
+        if info.kind == "add":
+            self.handle_batch([info])
+        elif info.kind == "request":
+            self.handle_request(info.dot, info.deps)
+        elif info.kind == "request_reply":
+            self.handle_request_reply(info.deps)
+        elif info.kind == "executed":
+            pass  # handle_executed: the shard's single handle already holds the clock
+        else:
+            raise ValueError(f"unknown GraphExecutionInfo kind {info.kind!r}")
 
     def handle_batch(self, infos):
         n = len(infos)
         dots = np.zeros(n, dtype=np.uint64)
         key_off = np.zeros(n + 1, dtype=np.uint32)
         dep_off = np.zeros(n + 1, dtype=np.uint32)
-        keys, deps = [], []
+        cmd_sh = np.zeros(n, dtype=np.uint64)
+        keys, deps, dep_sh = [], [], []
+        sharded = False
         for i, info in enumerate(infos):
             dots[i] = info.dot
             ks = self._keys_of(info.cmd)
             keys.extend(self.keys(k) for k in ks)
             key_off[i + 1] = len(keys)
-            deps.extend(d.dot if isinstance(d, Dependency) else int(d) for d in info.deps)
+            for d in info.deps:
+                if isinstance(d, Dependency):
+                    deps.append(d.dot)
+                    dep_sh.append(_mask(d.shards) if d.shards is not None else 0)
+                    sharded |= d.shards is not None
+                else:
+                    deps.append(int(d))
+                    dep_sh.append(0)
             dep_off[i + 1] = len(deps)
+            if hasattr(info.cmd, "shards"):
+                cmd_sh[i] = _mask(info.cmd.shards())
             self._cmds[int(info.dot)] = (info.cmd, ks)
         key_a = np.asarray(keys, dtype=np.uint64)
         dep_a = np.asarray(deps, dtype=np.uint64)
-        L.check(self._lib.fh_graph_add_batch(self._h, n, L.ptr(dots), L.ptr(key_off),
-                                             L.ptr(key_a) if len(key_a) else None,
-                                             L.ptr(dep_off), L.ptr(dep_a) if len(dep_a) else None))
+        dsh_a = np.asarray(dep_sh, dtype=np.uint64)
+        if self.cfg.shard_count > 1 and sharded:
+            L.check(self._lib.fh_graph_add_batch_sharded(
+                self._h, n, L.ptr(dots), L.ptr(key_off), L.ptr(key_a) if len(key_a) else None,
+                L.ptr(dep_off), L.ptr(dep_a) if len(dep_a) else None, L.ptr(cmd_sh),
+                L.ptr(dsh_a) if len(dsh_a) else None))
+        else:
+            L.check(self._lib.fh_graph_add_batch(self._h, n, L.ptr(dots), L.ptr(key_off),
+                                                 L.ptr(key_a) if len(key_a) else None,
+                                                 L.ptr(dep_off),
+                                                 L.ptr(dep_a) if len(dep_a) else None))
         self._fetch()
+
+    # -- partial replication (graph/mod.rs:279-408, executor.rs:147-189) -----
+    def handle_request(self, from_shard: int, dots):
+        a = np.asarray(list(dots), dtype=np.uint64)
+        L.check(self._lib.fh_graph_handle_requests(self._h, from_shard, len(a),
+                                                   L.ptr(a) if len(a) else None))
+
+    def handle_request_reply(self, replies):
+        """Info -> handle_add (one batch, in reply order); Executed -> executed
+        clock + pending retry (mod.rs:377-408)."""
+        infos = [GraphExecutionInfo.add(r.dot, r.cmd, r.deps) for r in replies if r.kind == "info"]
+        executed = [r.dot for r in replies if r.kind == "executed"]
+        if executed:
+            self.mark_executed(executed)
+        if infos:
+            self.handle_batch(infos)
+        elif executed:
+            self.handle_batch([])  # retry pending vertices against the new clock
+
+    def cleanup(self):
+        """Executor::cleanup -> check_pending_requests (mod.rs:168-179)."""
+        L.check(self._lib.fh_graph_cleanup(self._h))
+
+    def requests(self):
+        """fetch_requests: {target shard: set(dots)} (mod.rs:147-150)."""
+        n = C.c_size_t(0)
+        st = self._lib.fh_graph_requests(self._h, None, None, 0, C.byref(n))
+        if n.value == 0:
+            return {}
+        if st != L.FH_ECAP:
+            L.check(st)
+        dot = np.zeros(n.value, dtype=np.uint64)
+        sh = np.zeros(n.value, dtype=np.uint64)
+        L.check(self._lib.fh_graph_requests(self._h, L.ptr(dot), L.ptr(sh), n.value, C.byref(n)))
+        out = {}
+        for d, s in zip(dot.tolist(), sh.tolist()):
+            out.setdefault(int(s), set()).add(int(d))
+        return out
+
+    def request_replies(self):
+        """fetch_request_replies: {to shard: [RequestReply]} (mod.rs:152-157)."""
+        nr, nd = C.c_size_t(0), C.c_size_t(0)
+        st = self._lib.fh_graph_request_replies(self._h, 0, None, None, None, None, None, 0,
+                                                None, None, C.byref(nr), C.byref(nd))
+        if nr.value == 0:
+            return {}
+        if st != L.FH_ECAP:
+            L.check(st)
+        r, d = nr.value, max(1, nd.value)
+        to = np.zeros(r, np.uint64)
+        kind = np.zeros(r, np.uint8)
+        dot = np.zeros(r, np.uint64)
+        csh = np.zeros(r, np.uint64)
+        off = np.zeros(r + 1, np.uint32)
+        ddot = np.zeros(d, np.uint64)
+        dsh = np.zeros(d, np.uint64)
+        L.check(self._lib.fh_graph_request_replies(
+            self._h, r, L.ptr(to), L.ptr(kind), L.ptr(dot), L.ptr(csh), L.ptr(off), d,
+            L.ptr(ddot), L.ptr(dsh), C.byref(nr), C.byref(nd)))
+        out = {}
+        for i in range(r):
+            dt = int(dot[i])
+            if kind[i] == L.FH_REPLY_INFO:
+                deps = [Dependency(int(ddot[e]), _unmask(int(dsh[e])) if dsh[e] else None)
+                        for e in range(off[i], off[i + 1])]
+                rep = RequestReply("info", dt, self._cmds.get(dt, (None,))[0], deps)
+            else:
+                rep = RequestReply("executed", dt)
+            out.setdefault(int(to[i]), []).append(rep)
+        return out
 
     def _fetch(self):
         """fetch_commands_to_execute + execute (executor.rs:133-145, 191-196)."""

@@ -181,6 +181,58 @@ fh_status fh_graph_pending(fh_graph *h, size_t *count);
 fh_status fh_graph_missing(fh_graph *h, uint64_t *dots, size_t cap,
                            size_t *len);
 
+/* ---- Partial replication: requests and replies between shards ----------
+ * (graph/mod.rs:139-157, 168-179, 279-408; index.rs:145-211;
+ * GraphExecutor::{cleanup, fetch_requests, fetch_request_replies,
+ * handle(Request/RequestReply)} executor.rs:65-70, 147-189, 242-262).
+ * One fh_graph plays both executor roles of a shard (index 0 adds, index 1
+ * answers requests); they share the vertex index in the reference too
+ * (index.rs:21), and the executed clock the replies consult is the main
+ * executor's (the reference's secondary clock is that clock, delivered by
+ * handle_executed). */
+
+/* fh_graph_add_batch with shard sets, as 64-bit masks (bit s = shard s):
+ * cmd_shards[n] = Command::shards() of each added command (command.rs:103-
+ * 110), dep_shards[dep_off[n]] = Dependency::shards of each dependency
+ * (deps/keys/mod.rs:18-35).  A dependency missing when its command is added
+ * whose shard set excludes this shard is queued as a request to
+ * Dot::target_shard(n) (id.rs:59-61) the first time it is indexed
+ * (PendingIndex::index, index.rs:171-205).  FH_EINVARIANT for a missing
+ * dependency with an empty shard set (a noop: index.rs:190-194). */
+fh_status fh_graph_add_batch_sharded(fh_graph *h, size_t n, const uint64_t *dot,
+                                     const uint32_t *key_off, const uint64_t *key_id,
+                                     const uint32_t *dep_off, const uint64_t *dep_dot,
+                                     const uint64_t *cmd_shards,
+                                     const uint64_t *dep_shards);
+/* DependencyGraph::requests (mod.rs:147-150): take the queued requests,
+ * sorted by (target shard, dot).  FH_ECAP (len = count, nothing taken) if
+ * cap is too small. */
+fh_status fh_graph_requests(fh_graph *h, uint64_t *dot, uint64_t *shard,
+                            size_t cap, size_t *len);
+/* handle_request / process_requests (mod.rs:279-375): per dot, an Info
+ * reply {dot, deps, shard sets} for a pending vertex (FH_EINVARIANT if the
+ * vertex's command is replicated by from_shard, :313-322), an Executed reply
+ * for an executed dot, otherwise buffered until fh_graph_cleanup. */
+fh_status fh_graph_handle_requests(fh_graph *h, uint64_t from_shard, size_t n,
+                                   const uint64_t *dots);
+/* cleanup -> check_pending_requests (mod.rs:168-179, 673-678). */
+fh_status fh_graph_cleanup(fh_graph *h);
+#define FH_REPLY_INFO 0     /* RequestReply::Info{dot, cmd, deps}  mod.rs:33-43 */
+#define FH_REPLY_EXECUTED 1 /* RequestReply::Executed{dot}                      */
+/* DependencyGraph::request_replies (mod.rs:152-157): take the queued
+ * replies.  Reply i goes to to_shard[i]; Info replies carry the vertex's
+ * deps in dep_dot/dep_shards[dep_off[i]..dep_off[i+1]] (the command payload
+ * stays with the caller, keyed by dot).  FH_ECAP (counts set, nothing taken)
+ * if cap < replies or dep_cap < deps.  The receiver applies Info with
+ * fh_graph_add_batch_sharded and Executed with fh_graph_mark_executed
+ * followed by an empty add batch (the pending retry, mod.rs:393-405). */
+fh_status fh_graph_request_replies(fh_graph *h, size_t cap, uint64_t *to_shard,
+                                   uint8_t *kind, uint64_t *dot,
+                                   uint64_t *cmd_shards, uint32_t *dep_off,
+                                   size_t dep_cap, uint64_t *dep_dot,
+                                   uint64_t *dep_shards, size_t *n_replies,
+                                   size_t *n_deps);
+
 /* ======================================================================
  * Caesar's predecessors executor.
  * Replaces PredecessorsExecutor / PredecessorsGraph

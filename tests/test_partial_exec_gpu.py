@@ -1,0 +1,192 @@
+"""Partial-replication executor paths of the HIP GraphExecutor (fh_graph_*):
+requests for missing non-local dependencies, Info / Executed replies,
+buffered requests and cleanup (executor/graph/mod.rs:139-157, 168-179,
+279-408; index.rs:145-211; executor.rs:147-189, 242-262).
+
+The reference has no unit test for these paths (parity via
+`check_monitors` only, protocol/mod.rs:924-1013), so the checks are
+  * hand-derived cases of the rules themselves (which dots are requested, from
+    which shard, and how a request is answered), and
+  * the monitor property on multi-shard streams: every shard executes every
+    command it replicates exactly once, and each key's execution sequence is
+    the key's commands in commit order -- what the oracle's SequentialKeyDeps
+    per shard + union gives for a single view (every dependency is an earlier
+    command, so the per-key order is the stream order).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import D
+from fantoch_amd import _lib as L
+from fantoch_amd.command import Command
+from fantoch_amd.executor import GraphExecutionInfo, HipGraphExecutor, RequestReply
+from fantoch_amd.keydeps import Dependency
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def dep(pair, shards):
+    return Dependency(D(pair), frozenset(shards))
+
+
+def shard_of_key(k, S):
+    return int(k) % S
+
+
+def test_requests_only_first_missing_nonlocal_dependency():
+    """PendingIndex::index (index.rs:171-205): a missing dependency is
+    requested from Dot::target_shard(n) = (source-1)/n the first time it is
+    indexed, and only if its shard set excludes this shard."""
+    n = 2
+    ex = HipGraphExecutor(process_id=1, shard_id=0, n=n, f=0, shard_count=3, key_space=16)
+    cmd = Command(D([1, 1]), ["a"], shard_of=lambda k: 0)
+    # (3,1) lives on shard 1 ((3-1)//2 = 1), (5,7) on shard 2, (2,4) is ours
+    ex.handle(GraphExecutionInfo.add(D([1, 1]), cmd,
+                                     [dep([3, 1], [1]), dep([5, 7], [2, 1]), dep([2, 4], [0, 1])]))
+    assert ex.pending() == 1
+    assert ex.requests() == {1: {D([3, 1])}, 2: {D([5, 7])}}
+    assert ex.requests() == {}, "requests() takes the queue"
+    # a second child of the same missing dots: already indexed, no new request
+    ex.handle(GraphExecutionInfo.add(D([1, 2]), Command(D([1, 2]), ["a"]),
+                                     [dep([3, 1], [1]), dep([1, 1], [0]), dep([6, 1], [2])]))
+    assert ex.requests() == {2: {D([6, 1])}}
+    # a dependency executed (or present) when its child arrives is not missing
+    ex.mark_executed([D([4, 1])])
+    ex.handle(GraphExecutionInfo.add(D([1, 3]), Command(D([1, 3]), ["a"]),
+                                     [dep([4, 1], [1]), dep([1, 2], [0])]))
+    assert ex.requests() == {}
+    # Executed replies release the children (mod.rs:393-405)
+    ex.handle(GraphExecutionInfo.request_reply(
+        [RequestReply("executed", D(p)) for p in ([3, 1], [5, 7], [6, 1], [2, 4])]))
+    assert ex.pending() == 0
+    order = []
+    while (r := ex.to_clients()) is not None:
+        order.append(r[0])
+    assert order == [D([1, 1]), D([1, 2]), D([1, 3])]
+
+
+def test_noop_missing_dependency_is_an_invariant_violation():
+    ex = HipGraphExecutor(process_id=1, shard_id=0, n=1, f=0, shard_count=2, key_space=16)
+    with pytest.raises(L.FhError) as e:
+        ex.handle(GraphExecutionInfo.add(D([1, 1]), Command(D([1, 1]), ["a"]),
+                                         [dep([2, 1], [1]), Dependency(D([2, 2]), None)]))
+    assert e.value.status == L.FH_EINVARIANT
+
+
+def test_process_requests_info_executed_buffered():
+    """process_requests (mod.rs:297-375) + check_pending_requests (:673-678)."""
+    ex = HipGraphExecutor(process_id=2, shard_id=1, n=1, f=0, shard_count=2, key_space=16)
+    sh = lambda k: 1  # noqa: E731  every key of this test lives on shard 1
+    # (2,1) pending here (waits on a missing local dep (2,9)), (2,2) executes
+    ex.handle(GraphExecutionInfo.add(D([2, 1]), Command(D([2, 1]), ["x"], sh),
+                                     [dep([2, 9], [1]), dep([1, 5], [0, 1])]))
+    ex.handle(GraphExecutionInfo.add(D([2, 2]), Command(D([2, 2]), ["y"], sh), []))
+    ex.handle(GraphExecutionInfo.request(0, [D([2, 1]), D([2, 2]), D([2, 3])]))
+    rep = ex.request_replies()
+    assert set(rep) == {0}
+    by = {r.dot: r for r in rep[0]}
+    assert by[D([2, 1])].kind == "info"
+    assert {(d.dot, d.shards) for d in by[D([2, 1])].deps} == {
+        (D([2, 9]), frozenset([1])), (D([1, 5]), frozenset([0, 1]))}
+    assert by[D([2, 2])].kind == "executed"
+    assert D([2, 3]) not in by, "unknown dot is buffered"
+    assert ex.request_replies() == {}
+    ex.cleanup()
+    assert ex.request_replies() == {}, "still unknown: stays buffered"
+    ex.handle(GraphExecutionInfo.add(D([2, 3]), Command(D([2, 3]), ["z"], sh), []))
+    ex.cleanup()
+    assert [(r.kind, r.dot) for r in ex.request_replies()[0]] == [("executed", D([2, 3]))]
+
+
+def test_request_from_a_replicating_shard_panics():
+    """mod.rs:313-322: the requester must not replicate the requested command."""
+    ex = HipGraphExecutor(process_id=1, shard_id=0, n=1, f=0, shard_count=2, key_space=16)
+    c = Command(D([1, 1]), ["a", "b"], shard_of=lambda k: 0 if k == "a" else 1)
+    ex.handle(GraphExecutionInfo.add(D([1, 1]), c, [dep([1, 9], [0])]))
+    with pytest.raises(L.FhError) as e:
+        ex.handle(GraphExecutionInfo.request(1, [D([1, 1])]))
+    assert e.value.status == L.FH_EINVARIANT
+
+
+def partial_stream(seed, ncmd, S, n, K, kmax):
+    """Commands with 1..kmax keys over K keys, shard(key) = key mod S; the dot
+    comes from a process of the target shard (first key, workload.rs:172-176;
+    process ids n*s+1..n*s+n, util.rs:115-132).  Committed deps = union over
+    the command's shards of each shard's SequentialKeyDeps over its keys
+    (atlas.rs:559-639) -- computed by the oracle."""
+    rng = random.Random(seed)
+    seq = {}
+    kd = [O.KeyDeps(s) for s in range(S)]
+    cmds = []
+    for i in range(ncmd):
+        nk = rng.randint(1, kmax)
+        keys = rng.sample(range(K), nk)
+        target = shard_of_key(keys[0], S)
+        src = n * target + 1 + rng.randrange(n)
+        seq[src] = seq.get(src, 0) + 1
+        dot = (src << 56) | seq[src]
+        shards = sorted({shard_of_key(k, S) for k in keys})
+        deps = set()
+        for s in shards:
+            deps |= kd[s].add_cmd(dot, [k for k in keys if shard_of_key(k, S) == s])
+        cmds.append((dot, keys, shards, deps))
+    shards_of = {c[0]: c[2] for c in cmds}
+    return cmds, shards_of
+
+
+@pytest.mark.parametrize("seed,S,n,K", [(0, 2, 1, 24), (1, 3, 3, 40), (2, 4, 2, 64)])
+def test_multi_shard_stream_monitors(seed, S, n, K):
+    cmds, shards_of = partial_stream(seed, 1500, S, n, K, kmax=3)
+    rng = random.Random(100 + seed)
+    exs = [HipGraphExecutor(process_id=n * s + 1, shard_id=s, n=n, f=0, shard_count=S,
+                            key_space=K) for s in range(S)]
+    # each shard sees its commands in commit order perturbed by a local delay
+    arrivals = []
+    for s in range(S):
+        mine = [(i + rng.randrange(48), i) for i, c in enumerate(cmds) if s in c[2]]
+        arrivals.append([i for _, i in sorted(mine)])
+    pos = [0] * S
+    nreq = nrep = 0
+    while True:
+        progressed = False
+        for s in range(S):
+            if pos[s] < len(arrivals[s]):
+                b = rng.randint(1, 97)
+                infos = []
+                for i in arrivals[s][pos[s]:pos[s] + b]:
+                    dot, keys, shards, deps = cmds[i]
+                    c = Command(dot, [str(k) for k in keys], shard_of=lambda k: int(k) % S)
+                    infos.append(GraphExecutionInfo.add(
+                        dot, c, [Dependency(d, frozenset(shards_of[d])) for d in sorted(deps)]))
+                pos[s] += b
+                exs[s].handle_batch(infos)
+                progressed = True
+        # message exchange: requests -> replies (executor.rs:147-189)
+        for s in range(S):
+            for t, dots in exs[s].requests().items():
+                assert t != s and all(s not in shards_of[d] for d in dots)
+                assert all(((d >> 56) - 1) // n == t for d in dots)
+                exs[t].handle(GraphExecutionInfo.request(s, dots))
+                nreq += len(dots)
+                progressed = True
+        for t in range(S):
+            exs[t].cleanup()
+            for s, reps in exs[t].request_replies().items():
+                exs[s].handle(GraphExecutionInfo.request_reply(reps))
+                nrep += len(reps)
+                progressed = True
+        if not progressed:
+            break
+    assert nreq > 0 and nrep > 0, "the stream must exercise cross-shard requests"
+    for s in range(S):
+        assert exs[s].pending() == 0, f"shard {s} left commands pending"
+        mon = exs[s].monitor()
+        want = {}
+        for dot, keys, shards, deps in cmds:
+            for k in keys:
+                if shard_of_key(k, S) == s:
+                    want.setdefault(str(k), []).append(dot)
+        assert mon == want, f"shard {s}: per-key execution order differs"
