@@ -13,6 +13,8 @@ LIB_PATH = os.path.join(HERE, "libfantoch_hip.so")
 
 FH_OK, FH_EINVAL, FH_EHIP, FH_EOOM, FH_EINVARIANT, FH_ECAP, FH_ENOTIMPL = range(7)
 FH_REPLY_INFO, FH_REPLY_EXECUTED = 0, 1  # RequestReply kinds (include/fantoch_hip.h)
+# execution-log event kinds (include/fantoch_hip.h)
+FH_LOG_ADD, FH_LOG_REQUEST, FH_LOG_REPLY_INFO, FH_LOG_REPLY_EXECUTED, FH_LOG_EXECUTED = range(5)
 STATUS_NAMES = ["FH_OK", "FH_EINVAL", "FH_EHIP", "FH_EOOM", "FH_EINVARIANT", "FH_ECAP",
                 "FH_ENOTIMPL"]
 
@@ -73,6 +75,12 @@ SIGNATURES = {
     "fh_graph_handle_requests": (C.c_int, [V, C.c_uint64, S, V]),
     "fh_graph_cleanup": (C.c_int, [V]),
     "fh_graph_request_replies": (C.c_int, [V, S, V, V, V, V, V, S, V, V, P(S), P(S)]),
+    "fh_execlog_parse": (C.c_int, [V, S, C.c_uint64, P(V)]),
+    "fh_execlog_destroy": (C.c_int, [V]),
+    "fh_execlog_sizes": (C.c_int, [V, P(S), P(S), P(S), P(S), P(S)]),
+    "fh_execlog_events": (C.c_int, [V, V, V, V, V, V, V, V, V, V, V, V]),
+    "fh_execlog_key": (C.c_int, [V, C.c_uint64, V, S, P(S)]),
+    "fh_execlog_replay": (C.c_int, [V, V, S, P(S)]),
     "fh_engine_create": (C.c_int, [P(fh_config), P(V)]),
     "fh_engine_destroy": (C.c_int, [V]),
     "fh_engine_reset": (C.c_int, [V]),

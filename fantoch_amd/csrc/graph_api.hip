@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "dotindex.h"
+#include "execlog.h"
 #include "graph_core.h"
 
 namespace fh {
@@ -500,6 +501,53 @@ fh_status fh_graph_missing(fh_graph *h, uint64_t *dots, size_t cap, size_t *len)
   const auto &m = h->dev.missing_now;
   *len = m.size();
   for (size_t i = 0; i < m.size() && i < cap && dots; i++) dots[i] = m[i];
+  FH_API_END
+}
+
+}  // extern "C"
+
+extern "C" {
+
+fh_status fh_execlog_replay(const fh_execlog *h, fh_graph *g, size_t batch, size_t *executed) {
+  FH_API_BEGIN
+  FH_CHECK(h && g, FH_EINVAL, "null argument");
+  FH_CHECK(g->dev.shard_id < 64, FH_EINVAL, "shard sets are 64-bit masks: shard_id must be < 64");
+  const fh::ExecLog &L = fh::execlog_of(h);
+  auto &dev = g->dev;
+  const size_t ready0 = dev.ready.size();
+  const size_t E = L.kind.size();
+  const size_t cap = batch ? batch : E + 1;
+  std::vector<uint32_t> koff, doff;
+  size_t i = 0;
+  while (i < E) {
+    const uint8_t k = L.kind[i];
+    if (k == FH_LOG_ADD || k == FH_LOG_REPLY_INFO) {
+      // a run of adds: event arrays are already CSR; rebase the offsets
+      size_t j = i;
+      while (j < E && j - i < cap && (L.kind[j] == FH_LOG_ADD || L.kind[j] == FH_LOG_REPLY_INFO))
+        j++;
+      koff.assign(L.key_off.begin() + i, L.key_off.begin() + j + 1);
+      doff.assign(L.dep_off.begin() + i, L.dep_off.begin() + j + 1);
+      for (auto &o : koff) o -= L.key_off[i];
+      for (auto &o : doff) o -= L.dep_off[i];
+      dev.add_batch(j - i, L.dot.data() + i, koff.data(), L.key_id.data() + L.key_off[i],
+                    doff.data(), L.dep_dot.data() + L.dep_off[i], L.shards.data() + i,
+                    L.dep_shards.data() + L.dep_off[i]);
+      i = j;
+    } else if (k == FH_LOG_REQUEST) {
+      dev.process_requests(L.shards[i], L.dep_dot.data() + L.dep_off[i],
+                           L.dep_off[i + 1] - L.dep_off[i]);
+      i++;
+    } else if (k == FH_LOG_REPLY_EXECUTED) {
+      size_t j = i;
+      while (j < E && L.kind[j] == FH_LOG_REPLY_EXECUTED) dev.clock.add(L.dot[j++]);
+      dev.add_batch(0, nullptr, nullptr, nullptr, nullptr, nullptr);  // pending retry
+      i = j;
+    } else {
+      i++;  // Executed: handle_executed on the shared clock is a no-op here
+    }
+  }
+  if (executed) *executed = dev.ready.size() - ready0;
   FH_API_END
 }
 

@@ -233,6 +233,54 @@ fh_status fh_graph_request_replies(fh_graph *h, size_t cap, uint64_t *to_shard,
                                    uint64_t *dep_shards, size_t *n_replies,
                                    size_t *n_deps);
 
+/* ---- Execution-log ingest and replay ---------------
+ * The runner's execution log (run/task/execution_logger.rs:11-55): frames of
+ * a 4-byte big-endian length (tokio LengthDelimitedCodec defaults,
+ * run/rw/mod.rs:20-36) holding a bincode-1.3 GraphExecutionInfo
+ * (executor/graph/executor.rs:204-222; run/rw/mod.rs:87-100).  Replaces the
+ * replay binary's loop (fantoch_ps/src/bin/graph_executor_replay.rs:13-38).
+ * Host-only parsing: no device is needed to parse. */
+typedef struct fh_execlog fh_execlog;
+#define FH_LOG_ADD 0            /* GraphExecutionInfo::Add{dot, cmd, deps}  */
+#define FH_LOG_REQUEST 1        /* ::Request{from, dots}                    */
+#define FH_LOG_REPLY_INFO 2     /* ::RequestReply -> RequestReply::Info     */
+#define FH_LOG_REPLY_EXECUTED 3 /* ::RequestReply -> RequestReply::Executed */
+#define FH_LOG_EXECUTED 4       /* ::Executed{dots}                         */
+/* Parse a whole log; Command::keys(shard_id) become each event's keys
+ * (interned in first-seen order).  FH_EINVAL names the frame and byte of
+ * malformed input (bad variant / tag, truncation, trailing bytes). */
+fh_status fh_execlog_parse(const uint8_t *buf, size_t len, uint64_t shard_id,
+                           fh_execlog **out);
+fh_status fh_execlog_destroy(fh_execlog *h);
+/* Sizes for fh_execlog_events: frames, events, keys (sum over events),
+ * deps (sum over events), distinct keys.  Any pointer may be NULL. */
+fh_status fh_execlog_sizes(const fh_execlog *h, size_t *frames, size_t *events,
+                           size_t *keys, size_t *deps, size_t *distinct_keys);
+/* Event arrays (any pointer may be NULL): kind[events], dot[events] (packed),
+ * rifl_client/rifl_seq[events], shards[events] (Command::shards() mask, or
+ * the requesting shard of a Request), read_only[events],
+ * key_off[events+1] / key_id[keys], dep_off[events+1] / dep_dot[deps] /
+ * dep_shards[deps] (Dependency::shards mask, 0 = None; the dots of a
+ * Request / Executed). */
+fh_status fh_execlog_events(const fh_execlog *h, uint8_t *kind, uint64_t *dot,
+                            uint64_t *rifl_client, uint64_t *rifl_seq,
+                            uint64_t *shards, uint8_t *read_only,
+                            uint32_t *key_off, uint64_t *key_id,
+                            uint32_t *dep_off, uint64_t *dep_dot,
+                            uint64_t *dep_shards);
+/* Name of interned key `id` (FH_ECAP with *len = size if cap is short). */
+fh_status fh_execlog_key(const fh_execlog *h, uint64_t id, char *buf,
+                         size_t cap, size_t *len);
+/* Feed the log to an executor as GraphExecutor::handle would
+ * (executor.rs:76-100): runs of Add / RequestReply::Info events go in
+ * batches of up to `batch` (0 = unbounded) to fh_graph_add_batch_sharded,
+ * Request -> fh_graph_handle_requests, RequestReply::Executed ->
+ * fh_graph_mark_executed + pending retry, Executed -> nothing (one handle
+ * holds the clock).  *executed (may be NULL) = commands that became ready;
+ * drain them with fh_graph_drain. */
+fh_status fh_execlog_replay(const fh_execlog *h, fh_graph *g, size_t batch,
+                            size_t *executed);
+
 /* ======================================================================
  * Caesar's predecessors executor.
  * Replaces PredecessorsExecutor / PredecessorsGraph
