@@ -80,11 +80,14 @@ struct GraphCore {
   SortWorkspace sort_ws;
   ScanWorkspace scan_ws;
   DBuf<uint32_t> rep, cnt, pos, order, rank, tmp32a, tmp32b, tmp32c, tmp32d, flags;
+  DBuf<uint32_t> kraise;  // [V] last kappa iteration that raised kap[rep]
   DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c;
   DBuf<uint8_t> blocked;
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)
   bool profile = false;
   uint32_t dbg_rounds = 0, dbg_hprop = 0, dbg_reach = 0;  // FH_GRAPH_DEBUG counters
+  uint32_t dbg_cand = 0, dbg_restricted = 0, dbg_sync_n = 0;
+  double dbg_sync_us = 0;
   // per-kernel timing (engine profiling)
   std::vector<std::pair<const char *, hipEvent_t>> *marks = nullptr;
 
@@ -96,8 +99,10 @@ struct GraphCore {
   void pending_closure(const GraphInput &in, GraphOutput &out);
   uint64_t count_forward(const GraphInput &in);
   void find_sccs(const GraphInput &in);
-  bool order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters);
-  void coloring_fallback(const GraphInput &in);
+  bool order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters,
+                   bool give_up_early = false);
+  // false: restricted candidates too many, nothing done
+  bool coloring_fallback(const GraphInput &in, uint32_t recent_iter);
   void build_orders(const GraphInput &in, GraphOutput &out);
 };
 

@@ -1,4 +1,5 @@
 // graph_core.hip -- batch SCC + execution order (see graph_core.h).
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -255,7 +256,8 @@ __global__ void k_kap_init(uint32_t V, const uint8_t *__restrict__ blocked,
 
 __global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
                             const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
-                            const uint32_t *__restrict__ rep, uint64_t *kap, uint32_t *changed) {
+                            const uint32_t *__restrict__ rep, uint64_t *kap, uint32_t *changed,
+                            uint32_t *kraise, uint32_t iter) {
   WAVE_STRIDE(v, V) {
     const bool act = v < V && !blocked[v];
     const uint32_t r = act ? rep[v] : 0u;
@@ -269,8 +271,29 @@ __global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32
         }
       }
     }
-    if (agg_max<unsigned long long>((unsigned long long *)kap, r, best, act && best != 0))
-      *changed = 1;
+    const bool raised =
+        agg_max<unsigned long long>((unsigned long long *)kap, r, best, act && best != 0);
+    if (raised) __hip_atomic_store(&kraise[r], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // raises per iteration, over 8 counters (one per XCD under round-robin
+    // placement): the give-up rule watches whether they shrink
+    const uint64_t m = __ballot(raised);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&changed[blockIdx.x & 7], uint32_t(__popcll(m)));
+  }
+}
+
+// Candidates of the restricted fallback: a cycle the windows missed keeps
+// raising the kappa of its SCC's representatives on every iteration, so
+// vertices whose representative was not raised recently start out `done`
+// (excluded).  Vertices on long forward chains are included too; that only
+// costs work.  The result is certified by the next kappa run.
+__global__ void k_fb_candidates(uint32_t V, const uint8_t *__restrict__ blocked,
+                                const uint32_t *__restrict__ rep,
+                                const uint32_t *__restrict__ kraise, uint32_t recent,
+                                uint8_t *__restrict__ done, uint32_t *__restrict__ fl) {
+  GRID_STRIDE(v, V) {
+    const bool cand = !blocked[v] && kraise[rep[v]] >= recent;
+    done[v] = cand ? 0 : 1;
+    fl[v] = cand ? 1u : 0u;
   }
 }
 
@@ -279,23 +302,36 @@ __global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32
 // H[S] = max arrival position reachable from S (among active SCCs); each
 // class {S : H[S] = t} is reached from its root rep(t), and the members the
 // root reaches form one SCC with it.
-__global__ void k_fb_init(uint32_t V, const uint8_t *__restrict__ blocked,
+// The fallback kernels run over every vertex (list == null) or over a
+// vertex list (the candidates of the restricted fallback): v = list[j].
+#define FB_VID(j) (list ? list[j] : (j))
+
+__global__ void k_fb_hreset(uint32_t n, const uint32_t *__restrict__ list,
+                            const uint32_t *__restrict__ rep, uint32_t *H) {
+  GRID_STRIDE(j, n) H[rep[FB_VID(j)]] = 0;
+}
+
+__global__ void k_fb_init(uint32_t n, const uint32_t *__restrict__ list,
+                          const uint8_t *__restrict__ blocked,
                           const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                           uint32_t *H, uint8_t *reached) {
-  WAVE_STRIDE(v, V) {
-    const uint32_t r = v < V ? rep[v] : 0u;
-    if (v < V && r == v) reached[v] = 0;
-    const bool act = v < V && !blocked[v] && !done[v];
+  WAVE_STRIDE(j, n) {
+    const uint32_t v = j < n ? FB_VID(j) : 0u;
+    const uint32_t r = j < n ? rep[v] : 0u;
+    if (j < n && r == v) reached[v] = 0;
+    const bool act = j < n && !blocked[v] && !done[v];
     agg_max<uint32_t>(H, r, v, act);
   }
 }
 
-__global__ void k_fb_hprop(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+__global__ void k_fb_hprop(uint32_t n, const uint32_t *__restrict__ list,
+                           const uint32_t *__restrict__ off, uint32_t stride,
                            const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            uint32_t *H, uint32_t *changed) {
-  WAVE_STRIDE(v, V) {
-    const bool act = v < V && !blocked[v] && !done[v];
+  WAVE_STRIDE(j, n) {
+    const uint32_t v = j < n ? FB_VID(j) : 0u;
+    const bool act = j < n && !blocked[v] && !done[v];
     const uint32_t r = act ? rep[v] : 0u;
     uint32_t best = 0;
     if (act) {
@@ -312,20 +348,24 @@ __global__ void k_fb_hprop(uint32_t V, const uint32_t *__restrict__ off, uint32_
   }
 }
 
-__global__ void k_fb_roots(uint32_t V, const uint8_t *__restrict__ blocked,
+__global__ void k_fb_roots(uint32_t n, const uint32_t *__restrict__ list,
+                           const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            const uint32_t *__restrict__ H, uint8_t *reached) {
-  GRID_STRIDE(v, V) {
+  GRID_STRIDE(j, n) {
+    const uint32_t v = FB_VID(j);
     if (blocked[v] || done[v]) continue;
     if (H[rep[v]] == v) reached[rep[v]] = 1;  // v is the class maximum: its SCC is the root
   }
 }
 
-__global__ void k_fb_reach(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+__global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
+                           const uint32_t *__restrict__ off, uint32_t stride,
                            const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            const uint32_t *__restrict__ H, uint8_t *reached, uint32_t *changed) {
-  GRID_STRIDE(v, V) {
+  GRID_STRIDE(j, n) {
+    const uint32_t v = FB_VID(j);
     if (blocked[v] || done[v]) continue;
     const uint32_t r = rep[v];
     if (!__hip_atomic_load(&reached[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
@@ -342,11 +382,13 @@ __global__ void k_fb_reach(uint32_t V, const uint32_t *__restrict__ off, uint32_
   }
 }
 
-__global__ void k_fb_merge(uint32_t V, const uint8_t *__restrict__ blocked, uint8_t *done,
+__global__ void k_fb_merge(uint32_t n, const uint32_t *__restrict__ list,
+                           const uint8_t *__restrict__ blocked, uint8_t *done,
                            const uint32_t *__restrict__ rep, const uint32_t *__restrict__ H,
                            const uint8_t *__restrict__ reached, uint32_t *parent,
                            uint32_t *remaining) {
-  GRID_STRIDE(v, V) {
+  GRID_STRIDE(j, n) {
+    const uint32_t v = FB_VID(j);
     if (blocked[v] || done[v]) continue;
     const uint32_t r = rep[v];
     if (reached[r]) {
@@ -355,6 +397,28 @@ __global__ void k_fb_merge(uint32_t V, const uint8_t *__restrict__ blocked, uint
     } else {
       *remaining = 1;
     }
+  }
+}
+
+__global__ void k_fb_compress(uint32_t n, const uint32_t *__restrict__ list, uint32_t *parent) {
+  GRID_STRIDE(j, n) {
+    const uint32_t v = FB_VID(j);
+    parent[v] = uf_find(parent, v);
+  }
+}
+
+__global__ void k_fb_copy(uint32_t n, const uint32_t *__restrict__ list,
+                          const uint32_t *__restrict__ src, uint32_t *__restrict__ dst) {
+  GRID_STRIDE(j, n) {
+    const uint32_t v = FB_VID(j);
+    dst[v] = src[v];
+  }
+}
+
+__global__ void k_compact(uint32_t V, const uint32_t *__restrict__ fl,
+                          const uint32_t *__restrict__ pos, uint32_t *__restrict__ list) {
+  GRID_STRIDE(v, V) {
+    if (fl[v]) list[pos[v]] = v;
   }
 }
 
@@ -457,10 +521,16 @@ void GraphCore::mark(const char *name) {
 }
 
 uint32_t GraphCore::read_scalar(int i) {
-  uint32_t v = 0;
-  FH_HIP(hipMemcpyAsync(&v, scalars.get() + i, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-  FH_HIP(hipStreamSynchronize(stream));
-  return v;
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Acc {
+    GraphCore *g;
+    std::chrono::steady_clock::time_point t0;
+    ~Acc() {
+      g->dbg_sync_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      g->dbg_sync_n++;
+    }
+  } acc{this, t0};
+  return fetch_u32(scalars.get() + i, stream);
 }
 
 void GraphCore::pending_closure(const GraphInput &in, GraphOutput &out) {
@@ -498,60 +568,112 @@ void GraphCore::find_sccs(const GraphInput &in) {
   mark("scc_compress");
 }
 
-bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters) {
+bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters,
+                            bool give_up_early) {
   const uint32_t V = in.V;
   FH_HIP(hipMemsetAsync(kap.get(), 0, size_t(V) * sizeof(uint64_t), stream));
+  FH_HIP(hipMemsetAsync(kraise.ensure(V + 1), 0, size_t(V) * sizeof(uint32_t), stream));
   k_kap_init<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get());
+  // raises of the last iterations; a cycle the windows missed keeps raising
+  // its members forever, a converging run raises fewer and fewer vertices
+  uint64_t r1 = 0, r2 = 0;
   for (uint32_t it = 0; it < max_iters; it++) {
-    FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
+    FH_HIP(hipMemsetAsync(scalars.get() + 16, 0, 8 * sizeof(uint32_t), stream));
     k_kap_relax<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), rep.get(),
-                                                   kap.get(), scalars.get());
+                                                   kap.get(), scalars.get() + 16, kraise.get(), it + 1);
     iters = it + 1;
-    if (!read_scalar(0)) {
+    uint32_t c[8];
+    fetch_u32(scalars.get() + 16, c, 8, stream);
+    uint64_t raised = 0;
+    for (int i = 0; i < 8; i++) raised += c[i];
+    if (!raised) {
       mark("kappa");
       return true;
     }
+    // give up early (bounded runs only) when the raises stopped shrinking:
+    // fewer than 10 % less than two iterations ago
+    if (give_up_early && iters >= 5 && raised * 10 > r2 * 9) break;
+    r2 = r1;
+    r1 = raised;
   }
   mark("kappa");
   return false;
 }
 
-void GraphCore::coloring_fallback(const GraphInput &in) {
+// recent_iter > 0: restricted to the vertices whose representative's kappa
+// was raised at iteration >= recent_iter (k_fb_candidates); 0: every vertex.
+bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
   const uint32_t V = in.V;
   uint8_t *done = reinterpret_cast<uint8_t *>(tmp32d.ensure((V + 3) / 4 + 1));
   uint8_t *reached = reinterpret_cast<uint8_t *>(flags.ensure((V + 3) / 4 + 1));
   uint32_t *H = tmp32c.ensure(V);
-  FH_HIP(hipMemsetAsync(done, 0, V, stream));
+  uint32_t *parent = tmp32a.ensure(V);
+  const uint32_t *list = nullptr;
+  uint32_t n = V;
+  if (recent_iter) {
+    // candidates -> done flags + a compacted vertex list
+    uint32_t *fl = cnt.ensure(V);
+    uint32_t *ps = pos.ensure(V + 1);
+    k_fb_candidates<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), kraise.get(),
+                                                       recent_iter, done, fl);
+    exclusive_scan_u32(fl, ps, V, scan_ws, stream);
+    FH_HIP(hipMemcpyAsync(&n, ps + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    uint32_t *lst = order.ensure(V + 1);
+    k_compact<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, lst);
+    FH_HIP(hipStreamSynchronize(stream));
+    list = lst;
+    dbg_cand = n;
+    // most of the graph: the exact pass over every vertex is as cheap
+    if (n > V / 4) return false;
+    dbg_restricted++;
+    if (n == 0) {
+      mark("scc_fallback");
+      return true;
+    }
+  } else {
+    FH_HIP(hipMemsetAsync(done, 0, V, stream));
+  }
+  const unsigned G = grid_for(n, B);
   for (;;) {
-    FH_HIP(hipMemsetAsync(H, 0, size_t(V) * sizeof(uint32_t), stream));
-    k_fb_init<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), done, rep.get(), H, reached);
+    if (list)
+      k_fb_hreset<<<G, B, 0, stream>>>(n, list, rep.get(), H);
+    else
+      FH_HIP(hipMemsetAsync(H, 0, size_t(V) * sizeof(uint32_t), stream));
+    k_fb_init<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
     dbg_rounds++;
     do {
       dbg_hprop++;
       FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
-      k_fb_hprop<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), done,
-                                                    rep.get(), H, scalars.get());
+      k_fb_hprop<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, blocked.get(), done,
+                                       rep.get(), H, scalars.get());
     } while (read_scalar(0));
-    k_fb_roots<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), done, rep.get(), H, reached);
+    k_fb_roots<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
     do {
       dbg_reach++;
       FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
-      k_fb_reach<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), done,
-                                                    rep.get(), H, reached, scalars.get());
+      k_fb_reach<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, blocked.get(), done,
+                                       rep.get(), H, reached, scalars.get());
     } while (read_scalar(0));
     FH_HIP(hipMemsetAsync(scalars.get() + 1, 0, sizeof(uint32_t), stream));
     // unions go to a separate parent array so rep[] stays stable while read
-    uint32_t *parent = tmp32a.ensure(V);
-    FH_HIP(hipMemcpyAsync(parent, rep.get(), size_t(V) * sizeof(uint32_t),
-                          hipMemcpyDeviceToDevice, stream));
-    k_fb_merge<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), done, rep.get(), H, reached,
-                                                  parent, scalars.get() + 1);
-    k_uf_compress<<<grid_for(V, B), B, 0, stream>>>(V, parent);
-    FH_HIP(hipMemcpyAsync(rep.get(), parent, size_t(V) * sizeof(uint32_t),
-                          hipMemcpyDeviceToDevice, stream));
+    // (only the processed vertices' entries are read or written)
+    if (list)
+      k_fb_copy<<<G, B, 0, stream>>>(n, list, rep.get(), parent);
+    else
+      FH_HIP(hipMemcpyAsync(parent, rep.get(), size_t(V) * sizeof(uint32_t),
+                            hipMemcpyDeviceToDevice, stream));
+    k_fb_merge<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached, parent,
+                                     scalars.get() + 1);
+    k_fb_compress<<<G, B, 0, stream>>>(n, list, parent);
+    if (list)
+      k_fb_copy<<<G, B, 0, stream>>>(n, list, parent, rep.get());
+    else
+      FH_HIP(hipMemcpyAsync(rep.get(), parent, size_t(V) * sizeof(uint32_t),
+                            hipMemcpyDeviceToDevice, stream));
     if (!read_scalar(1)) break;
   }
   mark("scc_fallback");
+  return true;
 }
 
 void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
@@ -677,25 +799,36 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
   }
   uint32_t iters = 0, iters1 = 0;
-  dbg_rounds = dbg_hprop = dbg_reach = 0;
+  dbg_rounds = dbg_hprop = dbg_reach = dbg_sync_n = 0;
+  dbg_sync_us = 0;
   // a cycle the windows missed makes kappa grow forever: give up early and let
   // the exact coloring complete the partition (an exact partition converges in
   // a handful of rounds on every measured stream: C1 2, C4 4, C5 9)
-  bool ok = order_kappa(in, nfwd ? 12 : 4, iters);
+  const uint32_t give_up = nfwd ? 12 : 4;
+  bool ok = order_kappa(in, give_up, iters, true);
   iters1 = iters;
+  dbg_cand = dbg_restricted = 0;
   if (!ok) {
-    coloring_fallback(in);
     out.fallback_used = true;
-    ok = order_kappa(in, 1u << 30, iters);
+    // first the vertices still being raised (the missed cycles are among
+    // them), certified by a bounded kappa run; if a cycle is left, the exact
+    // coloring over every vertex
+    static const bool full_only = getenv("FH_FB_FULL") != nullptr;
+    if (!full_only && coloring_fallback(in, 1)) ok = order_kappa(in, give_up, iters, true);
+    if (!ok) {
+      coloring_fallback(in, 0);
+      ok = order_kappa(in, 1u << 30, iters);
+    }
   }
   out.kappa_iters = iters;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   if (debug)
     fprintf(stderr,
-            "fh graph: V=%u forward=%llu kappa=%u fallback=%d (rounds %u, hprop %u, reach %u) "
-            "kappa2=%u\n",
-            V, (unsigned long long)nfwd, iters1, int(out.fallback_used), dbg_rounds, dbg_hprop,
-            dbg_reach, out.fallback_used ? iters : 0u);
+            "fh graph: V=%u forward=%llu kappa=%u fallback=%d (candidates %u, restricted %u, "
+            "rounds %u, hprop %u, reach %u) kappa2=%u syncs %u %.0f us\n",
+            V, (unsigned long long)nfwd, iters1, int(out.fallback_used), dbg_cand,
+            dbg_restricted, dbg_rounds, dbg_hprop, dbg_reach, out.fallback_used ? iters : 0u,
+            dbg_sync_n, dbg_sync_us);
   build_orders(in, out);
 }
 

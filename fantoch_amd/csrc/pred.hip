@@ -145,12 +145,7 @@ struct PredDevice {
     }
   }
 
-  uint32_t read_u32(const uint32_t *p) {
-    uint32_t v = 0;
-    FH_HIP(hipMemcpyAsync(&v, p, sizeof(v), hipMemcpyDeviceToHost, stream));
-    FH_HIP(hipStreamSynchronize(stream));
-    return v;
-  }
+  uint32_t read_u32(const uint32_t *p) { return fetch_u32(p, stream); }
 
   void add_batch(size_t n, const uint64_t *dot, const uint64_t *clock, const uint32_t *dep_off,
                  const uint64_t *dep_dot) {

@@ -17,4 +17,18 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspa
 void exclusive_scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
                             hipStream_t s);
 
+// Low-latency read-back of n <= 14 device u32 words (fixpoint flags,
+// totals) into host memory: a one-wave kernel stores them into pinned,
+// device-mapped host memory followed by a sequence number (system-scope
+// release), and the host polls the sequence number (with hipStreamQuery, so
+// a failed launch surfaces as an error instead of a hang).  A pageable
+// hipMemcpyAsync + hipStreamSynchronize round trip measured ~150-180 us on
+// the GPU box; the graph's fixpoint loops take one per iteration.
+void fetch_u32(const uint32_t *dev, uint32_t *host, int n, hipStream_t s);
+inline uint32_t fetch_u32(const uint32_t *dev, hipStream_t s) {
+  uint32_t v = 0;
+  fetch_u32(dev, &v, 1, s);
+  return v;
+}
+
 }  // namespace fh

@@ -3,6 +3,8 @@
 // (cross-XCD hand-offs cost microseconds each on MI355X; a chained scan
 // serialises on them).  The operator is a template parameter with identity 0
 // (sum, or max over u32).
+#include <cstdlib>
+
 #include "scan.h"
 
 namespace fh {
@@ -124,6 +126,69 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspa
 void exclusive_scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
                             hipStream_t s) {
   scan_impl<OpMax>(in, out, n, ws, s);
+}
+
+namespace {
+
+__global__ void k_fetch_u32(const uint32_t *__restrict__ src, uint32_t *dst, int n,
+                            uint32_t seq) {
+  if (threadIdx.x != 0) return;
+  for (int t = 0; t < n; t++)
+    __hip_atomic_store(&dst[2 + t], src[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&dst[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct Mailbox {
+  uint32_t *host = nullptr;  // [0] sequence, [2..16) words
+  uint32_t *dev = nullptr;
+  uint32_t seq = 0;
+  int device = -1;
+  ~Mailbox() {
+    if (host) (void)hipHostFree(host);
+  }
+};
+
+}  // namespace
+
+void fetch_u32(const uint32_t *dev, uint32_t *host, int n, hipStream_t s) {
+  FH_CHECK(n >= 0 && n <= 14, FH_EINVAL, "fetch_u32: at most 14 words");
+  static const char *ab = getenv("FH_FETCH_MEMCPY");  // A/B measurement
+  static const bool use_memcpy = ab && *ab && *ab != '0';
+  if (use_memcpy) {
+    FH_HIP(hipMemcpyAsync(host, dev, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    FH_HIP(hipStreamSynchronize(s));
+    return;
+  }
+  // one mailbox per thread and device (handles are single-threaded)
+  thread_local Mailbox mb[16];
+  int d = 0;
+  FH_HIP(hipGetDevice(&d));
+  Mailbox &m = mb[d & 15];
+  if (!m.host || m.device != d) {
+    if (m.host) (void)hipHostFree(m.host);
+    m.host = nullptr;
+    FH_HIP(hipHostMalloc(reinterpret_cast<void **>(&m.host), 64,
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    FH_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&m.dev), m.host, 0));
+    m.device = d;
+    m.seq = 0;
+    __atomic_store_n(&m.host[0], 0u, __ATOMIC_RELEASE);
+  }
+  const uint32_t seq = ++m.seq;
+  k_fetch_u32<<<1, 1, 0, s>>>(dev, m.dev, n, seq);
+  FH_HIP(hipGetLastError());
+  for (;;) {
+    if (__atomic_load_n(&m.host[0], __ATOMIC_ACQUIRE) == seq) break;
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) {
+      // the stream drained: the store must be visible now
+      FH_CHECK(__atomic_load_n(&m.host[0], __ATOMIC_ACQUIRE) == seq, FH_EHIP,
+               "fetch_u32: mailbox not written");
+      break;
+    }
+    if (e != hipErrorNotReady) throw Error(FH_EHIP, std::string("fetch_u32: ") + hipGetErrorString(e));
+  }
+  for (int i = 0; i < n; i++) host[i] = __atomic_load_n(&m.host[2 + i], __ATOMIC_RELAXED);
 }
 
 }  // namespace fh
