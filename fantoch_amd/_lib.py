@@ -56,6 +56,7 @@ SIGNATURES = {
     "fh_keydeps_cmd_deps": (C.c_int, [V, S, V, V, S, P(S)]),
     "fh_keydeps_noop_deps": (C.c_int, [V, V, S, P(S)]),
     "fh_dep_union": (C.c_int, [C.c_int, S, S, V, V, V, V, P(S), V]),
+    "fh_keydeps_add_batch_device": (C.c_int, [V, S, S, V, V, V, V, V, S, P(S), V]),
     "fh_keydeps_add_batch_rw": (C.c_int, [V, S, V, V, V, V, V, V, V, V, V, S, P(S)]),
     "fh_pred_create": (C.c_int, [C.c_uint32, C.c_uint64, P(fh_config), P(V)]),
     "fh_pred_destroy": (C.c_int, [V]),

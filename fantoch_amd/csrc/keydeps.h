@@ -41,12 +41,17 @@ struct KeyDepsDevice {
                  const uint8_t *is_noop, const uint32_t *past_off, const uint64_t *past_dot,
                  uint32_t *out_off, uint64_t *out_dep, size_t out_cap, size_t *out_len,
                  const uint8_t *read_only = nullptr);
+  // device-resident batch (no noops, no past): inputs and outputs are device
+  // pointers on this handle's device
+  void add_batch_device(size_t n, size_t nkeys, const uint64_t *dot, const uint32_t *key_off,
+                        const uint64_t *key_id, uint32_t *out_off, uint64_t *out_dep,
+                        size_t out_cap, size_t *out_len, hipStream_t user);
   size_t cmd_deps(size_t nkeys, const uint64_t *key_id, uint64_t *out, size_t cap);
   size_t noop_deps(uint64_t *out, size_t cap);
 
  private:
   size_t run_segment(uint32_t a, uint32_t b, bool has_past, bool has_ro, uint32_t *out_off,
-                     uint64_t *out_dep, size_t out_base);
+                     uint64_t *out_dep, size_t out_base, bool dev_out = false);
   void enable_rw();
   size_t table_values(uint64_t extra);
   size_t download_unique(size_t cnt, uint64_t *out, size_t cap);

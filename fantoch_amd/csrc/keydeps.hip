@@ -256,7 +256,8 @@ void KeyDepsDevice::enable_rw() {
 }
 
 size_t KeyDepsDevice::run_segment(uint32_t a, uint32_t b, bool has_past, bool has_ro,
-                                  uint32_t *out_off, uint64_t *out_dep, size_t out_base) {
+                                  uint32_t *out_off, uint64_t *out_dep, size_t out_base,
+                                  bool dev_out) {
   const uint32_t ncmd = b - a;
   if (ncmd == 0) return 0;
   const uint32_t e0 = h_key_off[a], e1 = h_key_off[b];
@@ -312,14 +313,24 @@ size_t KeyDepsDevice::run_segment(uint32_t a, uint32_t b, bool has_past, bool ha
   uint64_t *dout = d_out.ensure(total ? total : 1);
   k_compact<<<grid_for(ncmd, B), B, 0, stream>>>(a, ncmd, d_key_off.get(), poff, dm, tmp, off,
                                                  dout);
-  std::vector<uint32_t> hoff(ncmd + 1);
-  FH_HIP(hipMemcpyAsync(hoff.data(), off, (ncmd + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        stream));
-  if (total)
-    FH_HIP(hipMemcpyAsync(out_dep + out_base, dout, size_t(total) * sizeof(uint64_t),
+  if (dev_out) {
+    // device-resident caller (one segment: a = 0, out_base = 0)
+    FH_HIP(hipMemcpyAsync(out_off, off, (ncmd + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                          stream));
+    if (total)
+      FH_HIP(hipMemcpyAsync(out_dep, dout, size_t(total) * sizeof(uint64_t),
+                            hipMemcpyDeviceToDevice, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+  } else {
+    std::vector<uint32_t> hoff(ncmd + 1);
+    FH_HIP(hipMemcpyAsync(hoff.data(), off, (ncmd + 1) * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, stream));
-  FH_HIP(hipStreamSynchronize(stream));
-  for (uint32_t i = 0; i <= ncmd; i++) out_off[a + i] = uint32_t(out_base + hoff[i]);
+    if (total)
+      FH_HIP(hipMemcpyAsync(out_dep + out_base, dout, size_t(total) * sizeof(uint64_t),
+                            hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    for (uint32_t i = 0; i <= ncmd; i++) out_off[a + i] = uint32_t(out_base + hoff[i]);
+  }
   check_err("add_batch");
   seen_ub = std::min<uint64_t>(key_space, seen_ub + m);
   return total;
@@ -455,6 +466,46 @@ void KeyDepsDevice::add_batch(size_t n, const uint64_t *dot, const uint32_t *key
   *out_len = written;
 }
 
+void KeyDepsDevice::add_batch_device(size_t n, size_t nkeys, const uint64_t *dot,
+                                     const uint32_t *key_off, const uint64_t *key_id,
+                                     uint32_t *out_off, uint64_t *out_dep, size_t out_cap,
+                                     size_t *out_len, hipStream_t user) {
+  FH_CHECK(out_off && out_len && (n == 0 || (dot && key_off && (nkeys == 0 || key_id))),
+           FH_EINVAL, "null argument");
+  FH_CHECK(n < (size_t(1) << 30) && nkeys < (size_t(1) << 31), FH_EINVAL, "batch too large");
+  FH_CHECK(!rw, FH_EINVAL, "add_batch_device: handle uses read/write rules");
+  // every command: one dep per key + the latest noop (sequential.rs:72-104)
+  const size_t bound = nkeys + n;
+  if (out_cap < bound || (bound && !out_dep)) {
+    *out_len = bound;
+    throw Error(FH_ECAP, "output capacity too small");
+  }
+  FH_HIP(hipSetDevice(device));
+  // the caller's stream produced the inputs; this handle's stream reads them
+  FH_HIP(hipStreamSynchronize(user));
+  if (n == 0) {
+    const uint32_t z = 0;
+    FH_HIP(hipMemcpyAsync(out_off, &z, sizeof(z), hipMemcpyHostToDevice, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    *out_len = 0;
+    return;
+  }
+  FH_HIP(hipMemcpyAsync(d_dot.ensure(n), dot, n * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                        stream));
+  FH_HIP(hipMemcpyAsync(d_key_off.ensure(n + 1), key_off, (n + 1) * sizeof(uint32_t),
+                        hipMemcpyDeviceToDevice, stream));
+  if (nkeys)
+    FH_HIP(hipMemcpyAsync(d_key64.ensure(nkeys), key_id, nkeys * sizeof(uint64_t),
+                          hipMemcpyDeviceToDevice, stream));
+  else
+    d_key64.ensure(1);
+  d_past.ensure(1);
+  // run_segment reads the segment's element bounds on the host
+  h_key_off.assign(n + 1, 0);
+  h_key_off[n] = uint32_t(nkeys);
+  *out_len = run_segment(0, uint32_t(n), false, false, out_off, out_dep, 0, true);
+}
+
 size_t KeyDepsDevice::cmd_deps(size_t nkeys, const uint64_t *key_id, uint64_t *out, size_t cap) {
   FH_HIP(hipSetDevice(device));
   std::vector<uint64_t> vals(nkeys);
@@ -528,6 +579,18 @@ fh_status fh_keydeps_add_batch(fh_keydeps *h, size_t n, const uint64_t *dot,
   FH_CHECK(h, FH_EINVAL, "null handle");
   h->dev.add_batch(n, dot, key_off, key_id, is_noop, past_off, past_dot, out_dep_off,
                    out_dep_dot, out_cap, out_len);
+  FH_API_END
+}
+
+fh_status fh_keydeps_add_batch_device(fh_keydeps *h, size_t n, size_t nkeys,
+                                      const uint64_t *dot_dev, const uint32_t *key_off_dev,
+                                      const uint64_t *key_id_dev, uint32_t *out_off_dev,
+                                      uint64_t *out_dep_dev, size_t out_cap, size_t *out_len,
+                                      void *stream) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.add_batch_device(n, nkeys, dot_dev, key_off_dev, key_id_dev, out_off_dev, out_dep_dev,
+                          out_cap, out_len, reinterpret_cast<hipStream_t>(stream));
   FH_API_END
 }
 

@@ -78,6 +78,74 @@ def hip_union(device: int = -1):
     return run
 
 
+# ------------------------------------------------------ device-resident path
+# The same three stages with every array in HBM (torch tensors on the rank's
+# GPU): local_view with torch ops, fh_keydeps_add_batch_device, the record
+# build, all_to_all_single over RCCL and fh_dep_union on device pointers.
+# Nothing crosses PCIe but the few scalars the stages size their outputs with.
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr())
+
+
+def device_local_deps(kd, dots, keys, rank: int, world: int):
+    """The shard's KeyDeps over its owned keys of a batch (dots[n] int64,
+    keys[n, k] int64 on the GPU) -> (record command index, record dep) on the
+    GPU: one record per dependency its KeyDeps reports for an owned-key
+    command (fh_keydeps_add_batch_device)."""
+    import torch
+
+    lib = L.load()
+    mine = keys % world == rank
+    cnt = mine.sum(dim=1)
+    cmds = torch.nonzero(cnt, as_tuple=True)[0]
+    key_off = torch.zeros(len(cmds) + 1, dtype=torch.int32, device=keys.device)
+    key_off[1:] = torch.cumsum(cnt[cmds], 0)
+    key_ids = torch.div(keys[cmds][mine[cmds]], world, rounding_mode="floor").contiguous()
+    sel_dots = dots[cmds].contiguous()
+    n, nkeys = len(cmds), len(key_ids)
+    out_off = torch.empty(n + 1, dtype=torch.int32, device=keys.device)
+    out_dep = torch.empty(max(1, n + nkeys), dtype=torch.int64, device=keys.device)
+    ln = C.c_size_t(0)
+    stream = torch.cuda.current_stream(keys.device).cuda_stream
+    L.check(lib.fh_keydeps_add_batch_device(
+        kd._h, n, nkeys, _ptr(sel_dots), _ptr(key_off), _ptr(key_ids) if nkeys else None,
+        _ptr(out_off), _ptr(out_dep), len(out_dep), C.byref(ln), C.c_void_p(stream)))
+    per = (out_off[1:] - out_off[:-1]).to(torch.int64)
+    rec_cmd = torch.repeat_interleave(cmds, per)
+    return rec_cmd, out_dep[:ln.value]
+
+
+def device_union(n_cmd: int, cmd, dep):
+    """records (owner-local command index int64, dep int64) on the GPU ->
+    (dep_off int32[n_cmd+1], deps int64) through fh_dep_union."""
+    import torch
+
+    lib = L.load()
+    dev = dep.device
+    c32 = cmd.to(torch.int32).contiguous()
+    d64 = dep.contiguous()
+    off = torch.empty(n_cmd + 1, dtype=torch.int32, device=dev)
+    out = torch.empty(max(1, len(d64)), dtype=torch.int64, device=dev)
+    ln = C.c_size_t(0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    L.check(lib.fh_dep_union(dev.index, n_cmd, len(d64), _ptr(c32), _ptr(d64), _ptr(off),
+                             _ptr(out), C.byref(ln), C.c_void_p(stream)))
+    return off, out[:ln.value]
+
+
+def device_route(keys, rec_cmd, rec_dep, world: int):
+    """Records sorted by destination (the owner of their command) and the
+    per-destination counts, for all_to_all_single."""
+    import torch
+
+    owner = keys[:, 0] % world
+    dest = owner[rec_cmd]
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=world)
+    return rec_cmd[order], rec_dep[order], counts, owner
+
+
 class PartialShard:
     """One shard (one process, one GPU) of the partial-replication engine.
 
@@ -120,6 +188,28 @@ class PartialShard:
                                input_split_sizes=send.tolist(), group=self.group)
         out = out.cpu().numpy()
         return out[:, 0], out[:, 1].view(np.uint64)
+
+    def step_device(self, dots, keys):
+        """step() with the batch and every stage in HBM (dots[n], keys[n, k]:
+        int64 tensors on this rank's GPU): the HIP KeyDeps, the records, one
+        RCCL all-to-all (counts, then the records), the HIP union.  Returns
+        (owned command indices, dep_off, deps) as GPU tensors."""
+        import torch
+        import torch.distributed as dist
+
+        rec_cmd, rec_dep = device_local_deps(self._kd, dots, keys, self.rank, self.world)
+        rec_cmd, rec_dep, send, owner = device_route(keys, rec_cmd, rec_dep, self.world)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self.group)
+        sc, rc = send.tolist(), recv.tolist()
+        payload = torch.stack([rec_cmd, rec_dep], 1)
+        got = torch.empty((sum(rc), 2), dtype=torch.int64, device=keys.device)
+        dist.all_to_all_single(got, payload, output_split_sizes=rc, input_split_sizes=sc,
+                               group=self.group)
+        owned = torch.nonzero(owner == self.rank, as_tuple=True)[0]
+        pos = torch.searchsorted(owned, got[:, 0].contiguous())
+        dep_off, deps = device_union(len(owned), pos, got[:, 1])
+        return owned, dep_off, deps
 
     def step(self, dots: np.ndarray, keys: np.ndarray):
         """One batch of the global stream (dots[n], keys[n, k]).  Returns the

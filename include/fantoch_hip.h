@@ -116,6 +116,23 @@ fh_status fh_keydeps_add_batch_rw(fh_keydeps *h, size_t n, const uint64_t *dot,
                                   uint32_t *out_dep_off, uint64_t *out_dep_dot,
                                   size_t out_cap, size_t *out_len);
 
+/* fh_keydeps_add_batch on device-resident buffers (the multi-GPU partial-
+ * replication path): commands only (no noops, no past), every
+ * pointer a device pointer on the handle's device.  key_off_dev[n+1] with
+ * key_off_dev[n] == nkeys (given on the host).  The call waits for `stream`
+ * (hipStream_t of the caller that produced the inputs, NULL = null stream),
+ * runs on the handle's stream and returns when out_off_dev[n+1] and
+ * out_dep_dev[*out_len] are written.  out_cap >= nkeys + n, else FH_ECAP with
+ * *out_len = that bound and no state change.  FH_EINVAL (after the batch ran)
+ * for a key id >= key_space. */
+fh_status fh_keydeps_add_batch_device(fh_keydeps *h, size_t n, size_t nkeys,
+                                      const uint64_t *dot_dev,
+                                      const uint32_t *key_off_dev,
+                                      const uint64_t *key_id_dev,
+                                      uint32_t *out_off_dev, uint64_t *out_dep_dev,
+                                      size_t out_cap, size_t *out_len,
+                                      void *stream);
+
 /* KeyDeps::cmd_deps (test-only query, keys/mod.rs:54-56;
  * sequential.rs:44-50): latest noop + latest dot of each key, no update. */
 fh_status fh_keydeps_cmd_deps(fh_keydeps *h, size_t nkeys,
