@@ -347,8 +347,27 @@ __global__ void k_identity_labels(uint32_t n, const uint64_t *__restrict__ dot,
   }
 }
 
+// Key histogram of the per-key sequence.  Its keys come in runs (each key's
+// elements are contiguous), so one atomic per run within a wave: the run's
+// head lane adds the run length (C3's 20M elements on 17 keys took 125 ms
+// with one atomic per element).
 __global__ void k_key_hist(uint32_t m, const uint32_t *__restrict__ keys, uint32_t *__restrict__ h) {
-  GRID_STRIDE(j, m) atomicAdd(&h[keys[j]], 1u);
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t b = blockIdx.x * blockDim.x; b < m; b += gridDim.x * blockDim.x) {
+    const uint32_t j = b + threadIdx.x;
+    const bool valid = j < m;
+    const uint32_t k = valid ? keys[j] : ~0u;
+    const uint32_t kp = __shfl_up(k, 1, 64);
+    const bool head = valid && (lane == 0 || kp != k);
+    const uint64_t heads = __ballot(head);
+    const uint64_t vmask = __ballot(valid);
+    if (head) {
+      const uint64_t later = lane == 63 ? 0ull : heads >> (lane + 1);
+      const uint32_t nvalid = uint32_t(__popcll(vmask));  // valid lanes are a prefix
+      const uint32_t end = later ? lane + 1 + uint32_t(__ffsll((long long)later) - 1) : nvalid;
+      atomicAdd(&h[k], end - lane);
+    }
+  }
 }
 
 __global__ void k_compact_deps(uint32_t n, uint32_t S, const uint64_t *__restrict__ dd,

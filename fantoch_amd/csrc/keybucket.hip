@@ -258,10 +258,12 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
   match_n<kItems>(mb, bkt, vld, peers);
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
+#ifndef FH_ABL_NOCLOCK  // diagnostic builds only: partition without the clock
     if (vld[i]) {
       atomicMax(&s_mx[d[i] >> 56], (unsigned long long)(d[i] & 0x00FFFFFFFFFFFFFFull));
       atomicAdd(&s_nc[d[i] >> 56], 1u);
     }
+#endif
     const uint32_t b0 = vld[i] ? s_wh[w][bkt[i]] : 0u;
     if (vld[i] && (peers[i] & lt) == 0) s_wh[w][bkt[i]] = b0 + uint32_t(__popcll(peers[i]));
     rank[i] = b0 + uint32_t(__popcll(peers[i] & lt));
