@@ -47,8 +47,8 @@ def parse():
     ap.add_argument("--zipf", type=float, default=0.7)
     ap.add_argument("--seed", type=int, default=0xFA170C4000000002)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=4_000_000,
-                    help="commands in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=40_000_000,
+                    help="commands in the CPU-baseline sample (~10 s of one host core)")
     ap.add_argument("--probe", default="kb_step,kb_partition,kb_order",
                     help="kernels whose launches are timed (comma-separated); the roofline "
                          "entry reports the one with the most device time")
