@@ -99,7 +99,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
                              const uint64_t *__restrict__ frontier,
                              uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ dep_cnt,
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
-                             uint32_t *nblocked) {
+                             uint32_t *nblocked, uint32_t *__restrict__ nv_out) {
   const uint32_t S = fq * k;
   GRID_STRIDE(i, n) {
     uint64_t *dd = dep_dot + size_t(i) * S;
@@ -133,6 +133,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
       }
     }
     for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
+    if (nv_out) nv_out[i] = nv;
     const uint32_t m = S == 1 ? nd : sort_unique_u64(dd, nd);
     for (uint32_t q = m; q < S; q++) dd[q] = 0;
     dep_cnt[i] = m;
@@ -370,6 +371,16 @@ __global__ void k_key_hist(uint32_t m, const uint32_t *__restrict__ keys, uint32
   }
 }
 
+// fixed-stride in-batch edges (S slots, the first cnt[i] real) -> CSR: the
+// graph's fixpoint passes then read only real edges (C5: 6.3 of 12 slots)
+__global__ void k_edges_csr(uint32_t n, uint32_t S, const uint32_t *__restrict__ ds,
+                            const uint32_t *__restrict__ off, uint32_t *__restrict__ out) {
+  GRID_STRIDE(i, n) {
+    const uint32_t o = off[i], c = off[i + 1] - o;
+    for (uint32_t q = 0; q < c; q++) out[o + q] = ds[size_t(i) * S + q];
+  }
+}
+
 __global__ void k_compact_deps(uint32_t n, uint32_t S, const uint64_t *__restrict__ dd,
                                const uint32_t *__restrict__ off, uint64_t *__restrict__ out) {
   GRID_STRIDE(i, n) {
@@ -418,6 +429,7 @@ struct EngineDevice {
   // scratch / outputs
   DBuf<uint64_t> vkeys, sk64a, sk64b, dep_ext, dep_dot, seq_dot, lab;
   DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_vid, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
+  DBuf<uint32_t> edge_cnt, edge_off, edge_csr;  // replica views: in-batch edges as CSR
   DBuf<uint8_t> tail, blocked0;
   DBuf<uint32_t> scal;
   DBuf<unsigned long long> srcstats;
@@ -748,14 +760,24 @@ struct EngineDevice {
         n, k, fq, key_space, bkey, bproc, bdot, dvid, dext, tl,
         views ? views_latest() : latest.get(), views ? 1ull : uint64_t(lmul),
         views ? ~0ull : uint64_t(lmask), (const uint64_t *)dot.get(), bbase, frontier.get(), ddot,
-        dcnt, dd, nullptr, scal.get());
+        dcnt, dd, nullptr, scal.get(), views && S >= 8 ? edge_cnt.ensure(n + 1) : nullptr);
     mark("keydeps_union");
+    const uint32_t *gdst = dd, *goff = nullptr;
+    if (views && S >= 8) {  // measured: a win at S = 12 (C5), flat or worse at 3 and 6
+      uint32_t *eo = edge_off.ensure(n + 1);
+      exclusive_scan_u32(edge_cnt.get(), eo, n, scan_ws, stream);
+      uint32_t *ec = edge_csr.ensure(size_t(n) * S + 1);
+      k_edges_csr<<<grid_for(n, B), B, 0, stream>>>(n, S, dd, eo, ec);
+      gdst = ec;
+      goff = eo;
+      mark("edges_csr");
+    }
     // graph stage
     GraphInput gin;
     gin.V = n;
-    gin.off = nullptr;
-    gin.stride = S;
-    gin.dst = dd;
+    gin.off = goff;
+    gin.stride = goff ? 0 : S;
+    gin.dst = gdst;
     gin.blocked0 = nullptr;  // see k_cmd_engine: no pending carried by the fused engine
     gin.dot = bdot;
     gin.k = k;
