@@ -86,6 +86,98 @@ __device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
   return w;
 }
 
+// k_cmd_engine for rows of at most kRegSlots slots, in registers: every slot
+// is read into a fixed register position (absent = all ones), a bitonic
+// network sorts the 16 dots, and the unique ones stream out.  (The general
+// path's insertion sort runs on the global row: a dependent load/store chain
+// per step; C5's 12-slot rows spent 15 ms there.)  A dot is never all ones
+// (ProcessId 255 with sequence 2^56 - 1), so the sentinel cannot collide.
+constexpr uint32_t kRegSlots = 16;
+__device__ __forceinline__ void cmd_union_regs(
+    uint32_t i, uint32_t S, uint32_t k, uint32_t fq, uint64_t K, const uint32_t *__restrict__ key32,
+    const uint8_t *__restrict__ fq_proc, const uint64_t *__restrict__ dot,
+    const uint32_t *__restrict__ dep_vid, const uint64_t *__restrict__ dep_ext,
+    const uint8_t *__restrict__ tail, uint64_t *__restrict__ latest, uint64_t lmul,
+    uint64_t lmask, const uint64_t *__restrict__ dlog, uint64_t log_base,
+    const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
+    uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
+    uint32_t *nblocked, uint32_t *__restrict__ nv_out) {
+  uint64_t r[kRegSlots];
+  uint32_t vv[kRegSlots];
+  bool missing = false;
+  const uint64_t self = dot[i];
+#pragma unroll
+  for (uint32_t t = 0; t < kRegSlots; t++) {
+    r[t] = ~0ull;
+    vv[t] = ~0u;
+    if (t < S) {
+      const uint32_t e = i * S + t;
+      const uint32_t v = dep_vid[e];
+      if (v != ~0u) {
+        vv[t] = v;
+        r[t] = dot[v];
+      } else {
+        uint64_t x = dep_ext[e];
+        if (is_log_ref(x)) x = dlog[x - kLogFlag];  // single view: command-log reference
+        if (x) {
+          r[t] = x;
+          if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
+        }
+      }
+      if (tail[e]) {
+        const uint32_t j = t / k, s = t % k;
+        const uint64_t slot = fq_proc ? uint64_t(fq_proc[i * fq + j]) * K + key32[i * k + s]
+                                      : (uint64_t(key32[i * k + s]) * lmul) & lmask;
+        latest[slot] = fq_proc ? self : (kLogFlag | (log_base + i));
+      }
+    }
+  }
+  // bitonic sort of the 16 register slots, ascending
+#pragma unroll
+  for (uint32_t kk = 2; kk <= kRegSlots; kk <<= 1) {
+#pragma unroll
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (uint32_t a = 0; a < kRegSlots; a++) {
+        const uint32_t b = a ^ j;
+        if (b > a) {
+          const uint64_t x = r[a], y = r[b];
+          const bool sw = (a & kk) == 0 ? x > y : x < y;
+          r[a] = sw ? y : x;
+          r[b] = sw ? x : y;
+        }
+      }
+    }
+  }
+  uint64_t *dd = dep_dot + size_t(i) * S;
+  uint32_t m = 0;
+  uint64_t prev = 0;  // dots are never 0
+#pragma unroll
+  for (uint32_t t = 0; t < kRegSlots; t++) {
+    if (r[t] != ~0ull && r[t] != prev) {
+      dd[m++] = r[t];
+      prev = r[t];
+    }
+  }
+  for (uint32_t q = m; q < S; q++) dd[q] = 0;
+  uint32_t *ds = dst + size_t(i) * S;
+  uint32_t nv = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < kRegSlots; t++) {
+    if (vv[t] != ~0u) {
+      bool dup = false;
+#pragma unroll
+      for (uint32_t q = 0; q < t; q++) dup |= vv[q] == vv[t];
+      if (!dup) ds[nv++] = vv[t];
+    }
+  }
+  for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
+  if (nv_out) nv_out[i] = nv;
+  dep_cnt[i] = m;
+  if (blocked0) blocked0[i] = missing;
+  if (missing) atomicAdd(nblocked, 1u);
+}
+
 // Per command: union of its fast-quorum members' element deps (vids and
 // external dots), committed dep dots (sorted, fixed stride S), graph edges
 // (vids, padded with the vertex itself), latest-table update at tails and the
@@ -101,6 +193,14 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out) {
   const uint32_t S = fq * k;
+  if (S <= kRegSlots) {  // uniform: the register path
+    GRID_STRIDE(i, n) {
+      cmd_union_regs(i, S, k, fq, K, key32, fq_proc, dot, dep_vid, dep_ext, tail, latest, lmul,
+                     lmask, dlog, log_base, frontier, dep_dot, dep_cnt, dst, blocked0, nblocked,
+                     nv_out);
+    }
+    return;
+  }
   GRID_STRIDE(i, n) {
     uint64_t *dd = dep_dot + size_t(i) * S;
     uint32_t *ds = dst + size_t(i) * S;
