@@ -44,30 +44,49 @@ __global__ void k_view_keys(uint32_t M, uint32_t k, uint32_t fq, uint64_t K,
   }
 }
 
-// Element dependency = previous element of its segment (in-batch vid) or the
-// persistent latest entry of the segment (external dot) at the head.
+// Element dependency code (one u64 per element, command-major position e):
+// 0 = none, in-batch vid + 1 (< 2^48) for the previous element of its
+// segment, else the persistent latest entry of the segment at the head (a
+// dot, >= 2^56, or a command-log reference, [2^48, 2^56)).
 template <class KT>
 __global__ void k_prev_engine(uint32_t M, const KT *__restrict__ ks, const uint32_t *__restrict__ vs,
                               int tb, uint32_t per_cmd, const uint64_t *__restrict__ latest,
-                              uint64_t lmul, uint64_t lmask, uint32_t *__restrict__ dep_vid,
-                              uint64_t *__restrict__ dep_ext, uint8_t *__restrict__ tail,
+                              uint64_t lmul, uint64_t lmask, uint64_t *__restrict__ dep_code,
                               uint32_t *__restrict__ sorted_vid) {
   GRID_STRIDE(j, M) {
     const uint32_t e = vs[j];
     const KT seg = ks[j] >> tb;
     const bool head = j == 0 || (ks[j - 1] >> tb) != seg;
-    const bool is_tail = j + 1 == M || (ks[j + 1] >> tb) != seg;
-    if (head) {
-      // the segment id is the latest-table slot: key, or replica * K + key
-      dep_vid[e] = ~0u;
-      dep_ext[e] = latest[(uint64_t(seg) * lmul) & lmask];
-    } else {
-      dep_vid[e] = vs[j - 1] / per_cmd;
-      dep_ext[e] = 0;
-    }
-    tail[e] = is_tail;
+    // the segment id is the latest-table slot: key, or replica * K + key
+    dep_code[e] = head ? latest[(uint64_t(seg) * lmul) & lmask] : uint64_t(vs[j - 1] / per_cmd) + 1;
     if (sorted_vid) sorted_vid[j] = e / per_cmd;
   }
+}
+
+// Segment tails become the latest entries (sequential.rs:88-95), in a launch
+// of their own so that every head of k_prev_engine has read the old value:
+// the command's dot (replica views) or its command-log reference.
+template <class KT>
+__global__ void k_tail_engine(uint32_t M, const KT *__restrict__ ks, const uint32_t *__restrict__ vs,
+                              int tb, uint32_t per_cmd, uint64_t *__restrict__ latest,
+                              uint64_t lmul, uint64_t lmask, const uint64_t *__restrict__ bdot,
+                              uint64_t log_base) {
+  GRID_STRIDE(j, M) {
+    const KT seg = ks[j] >> tb;
+    if (j + 1 == M || (ks[j + 1] >> tb) != seg) {
+      const uint32_t cmd = vs[j] / per_cmd;
+      latest[(uint64_t(seg) * lmul) & lmask] = bdot ? bdot[cmd] : (kLogFlag | (log_base + cmd));
+    }
+  }
+}
+
+// decode an element's dependency code: in-batch vid (true) or external value
+__device__ __forceinline__ bool dep_in_batch(uint64_t c, uint32_t *v) {
+  if (c != 0 && c < kLogFlag) {
+    *v = uint32_t(c - 1);
+    return true;
+  }
+  return false;
 }
 
 __device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
@@ -94,41 +113,30 @@ __device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
 // (ProcessId 255 with sequence 2^56 - 1), so the sentinel cannot collide.
 constexpr uint32_t kRegSlots = 16;
 __device__ __forceinline__ void cmd_union_regs(
-    uint32_t i, uint32_t S, uint32_t k, uint32_t fq, uint64_t K, const uint32_t *__restrict__ key32,
-    const uint8_t *__restrict__ fq_proc, const uint64_t *__restrict__ dot,
-    const uint32_t *__restrict__ dep_vid, const uint64_t *__restrict__ dep_ext,
-    const uint8_t *__restrict__ tail, uint64_t *__restrict__ latest, uint64_t lmul,
-    uint64_t lmask, const uint64_t *__restrict__ dlog, uint64_t log_base,
+    uint32_t i, uint32_t S, const uint64_t *__restrict__ dot,
+    const uint64_t *__restrict__ dep_code, const uint64_t *__restrict__ dlog,
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
-  const uint64_t self = dot[i];
 #pragma unroll
   for (uint32_t t = 0; t < kRegSlots; t++) {
     r[t] = ~0ull;
     vv[t] = ~0u;
     if (t < S) {
-      const uint32_t e = i * S + t;
-      const uint32_t v = dep_vid[e];
-      if (v != ~0u) {
+      uint64_t x = dep_code[size_t(i) * S + t];
+      uint32_t v;
+      if (dep_in_batch(x, &v)) {
         vv[t] = v;
         r[t] = dot[v];
       } else {
-        uint64_t x = dep_ext[e];
         if (is_log_ref(x)) x = dlog[x - kLogFlag];  // single view: command-log reference
         if (x) {
           r[t] = x;
           if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
         }
-      }
-      if (tail[e]) {
-        const uint32_t j = t / k, s = t % k;
-        const uint64_t slot = fq_proc ? uint64_t(fq_proc[i * fq + j]) * K + key32[i * k + s]
-                                      : (uint64_t(key32[i * k + s]) * lmul) & lmask;
-        latest[slot] = fq_proc ? self : (kLogFlag | (log_base + i));
       }
     }
   }
@@ -182,22 +190,17 @@ __device__ __forceinline__ void cmd_union_regs(
 // external dots), committed dep dots (sorted, fixed stride S), graph edges
 // (vids, padded with the vertex itself), latest-table update at tails and the
 // missing-dependency flag for external deps that are not executed.
-__global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
-                             const uint32_t *__restrict__ key32, const uint8_t *__restrict__ fq_proc,
-                             const uint64_t *__restrict__ dot, const uint32_t *__restrict__ dep_vid,
-                             const uint64_t *__restrict__ dep_ext, const uint8_t *__restrict__ tail,
-                             uint64_t *__restrict__ latest, uint64_t lmul, uint64_t lmask,
-                             const uint64_t *__restrict__ dlog, uint64_t log_base,
+__global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict__ dot,
+                             const uint64_t *__restrict__ dep_code,
+                             const uint64_t *__restrict__ dlog,
                              const uint64_t *__restrict__ frontier,
                              uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ dep_cnt,
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out) {
-  const uint32_t S = fq * k;
   if (S <= kRegSlots) {  // uniform: the register path
     GRID_STRIDE(i, n) {
-      cmd_union_regs(i, S, k, fq, K, key32, fq_proc, dot, dep_vid, dep_ext, tail, latest, lmul,
-                     lmask, dlog, log_base, frontier, dep_dot, dep_cnt, dst, blocked0, nblocked,
-                     nv_out);
+      cmd_union_regs(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
+                     nblocked, nv_out);
     }
     return;
   }
@@ -206,17 +209,15 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
     uint32_t *ds = dst + size_t(i) * S;
     uint32_t nv = 0, nd = 0;
     bool missing = false;
-    const uint64_t self = dot[i];
     for (uint32_t t = 0; t < S; t++) {
-      const uint32_t e = i * S + t;
-      const uint32_t v = dep_vid[e];
-      if (v != ~0u) {
+      uint64_t x = dep_code[size_t(i) * S + t];
+      uint32_t v;
+      if (dep_in_batch(x, &v)) {
         bool dup = false;
         for (uint32_t q = 0; q < nv; q++) dup |= ds[q] == v;
         if (!dup) ds[nv++] = v;
         dd[nd++] = dot[v];
       } else {
-        uint64_t x = dep_ext[e];
         if (is_log_ref(x)) x = dlog[x - kLogFlag];  // single view: command-log reference
         if (x) {
           dd[nd++] = x;
@@ -224,12 +225,6 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t k, uint32_t fq, uint64_t K,
           // fused engine: every earlier batch executed completely)
           if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
         }
-      }
-      if (tail[e]) {
-        const uint32_t j = t / k, s = t % k;
-        const uint64_t slot = fq_proc ? uint64_t(fq_proc[i * fq + j]) * K + key32[i * k + s]
-                                      : (uint64_t(key32[i * k + s]) * lmul) & lmask;
-        latest[slot] = fq_proc ? self : (kLogFlag | (log_base + i));
       }
     }
     for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
@@ -528,9 +523,9 @@ struct EngineDevice {
   DBuf<uint8_t> fq_proc;
   // scratch / outputs
   DBuf<uint64_t> vkeys, sk64a, sk64b, dep_ext, dep_dot, seq_dot, lab;
-  DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_vid, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
+  DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
   DBuf<uint32_t> edge_cnt, edge_off, edge_csr;  // replica views: in-batch edges as CSR
-  DBuf<uint8_t> tail, blocked0;
+  DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
   DBuf<unsigned long long> srcstats;
   SortWorkspace sort_ws;
@@ -740,9 +735,7 @@ struct EngineDevice {
       ~ProbeGuard() { t_probe = nullptr; }
     } probe_guard(probe.slots.empty() ? nullptr : &probe);
     uint32_t *vs = nullptr;
-    uint32_t *dvid = dep_vid.ensure(M + 1);
-    uint64_t *dext = dep_ext.ensure(M + 1);
-    uint8_t *tl = tail.ensure(M + 1);
+    uint64_t *dext = dep_ext.ensure(M + 1);  // per-element dependency codes
     uint32_t *svid = sorted_vid.ensure(M + 1);
     sorted_keys32 = nullptr;
     if (!views && k == 1) {
@@ -818,8 +811,10 @@ struct EngineDevice {
                            &ks, &vs);
       mark("keydeps_sort");
       k_prev_engine<uint32_t><<<grid_for(M, B), B, 0, stream>>>(
-          M, ks, vs, 0, S, latest.get(), uint64_t(lmul), uint64_t(lmask), dvid, dext, tl,
+          M, ks, vs, 0, S, latest.get(), uint64_t(lmul), uint64_t(lmask), dext,
           k == 1 ? nullptr : svid);
+      k_tail_engine<uint32_t><<<grid_for(M, B), B, 0, stream>>>(
+          M, ks, vs, 0, S, latest.get(), uint64_t(lmul), uint64_t(lmask), nullptr, bbase);
       sorted_keys32 = ks;
     } else {
       sv_fused = false;
@@ -833,7 +828,9 @@ struct EngineDevice {
                            &vs);
       mark("keydeps_sort");
       k_prev_engine<uint64_t><<<grid_for(M, B), B, 0, stream>>>(
-          M, ks, vs, tbits, S, views_latest(), 1ull, ~0ull, dvid, dext, tl, nullptr);
+          M, ks, vs, tbits, S, views_latest(), 1ull, ~0ull, dext, nullptr);
+      k_tail_engine<uint64_t><<<grid_for(M, B), B, 0, stream>>>(
+          M, ks, vs, tbits, S, views_latest(), 1ull, ~0ull, bdot, 0);
     }
     if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bproc, bdot, bbase);
     if (ms || profile) FH_HIP(hipEventRecord(ev1, stream));
@@ -847,9 +844,7 @@ struct EngineDevice {
   void run_general(uint32_t n, uint32_t k, uint32_t fq, uint32_t S, uint32_t M, bool views,
                    const uint32_t *bkey, const uint8_t *bproc, const uint64_t *bdot,
                    uint64_t bbase) {
-    uint32_t *dvid = dep_vid.get();
-    uint64_t *dext = dep_ext.get();
-    uint8_t *tl = tail.get();
+    const uint64_t *dcode = dep_ext.get();
     uint32_t *svid = sorted_vid.get();
     mark("keydeps_prev");
     uint64_t *ddot = dep_dot.ensure(M + 1);
@@ -857,10 +852,8 @@ struct EngineDevice {
     uint32_t *dd = dst.ensure(M + 1);
     FH_HIP(hipMemsetAsync(scal.get(), 0, sizeof(uint32_t), stream));
     k_cmd_engine<<<grid_for(n, B), B, 0, stream>>>(
-        n, k, fq, key_space, bkey, bproc, bdot, dvid, dext, tl,
-        views ? views_latest() : latest.get(), views ? 1ull : uint64_t(lmul),
-        views ? ~0ull : uint64_t(lmask), (const uint64_t *)dot.get(), bbase, frontier.get(), ddot,
-        dcnt, dd, nullptr, scal.get(), views && S >= 8 ? edge_cnt.ensure(n + 1) : nullptr);
+        n, S, bdot, dcode, (const uint64_t *)dot.get(), frontier.get(), ddot, dcnt, dd, nullptr,
+        scal.get(), views && S >= 8 ? edge_cnt.ensure(n + 1) : nullptr);
     mark("keydeps_union");
     const uint32_t *gdst = dd, *goff = nullptr;
     if (views && S >= 8) {  // measured: a win at S = 12 (C5), flat or worse at 3 and 6
