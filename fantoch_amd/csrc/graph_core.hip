@@ -592,7 +592,7 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
     }
     // give up early (bounded runs only) when the raises stopped shrinking:
     // fewer than 10 % less than two iterations ago
-    if (give_up_early && iters >= 5 && raised * 10 > r2 * 9) break;
+    if (give_up_early && iters >= 3 && raised * 10 > r2 * 9) break;
     r2 = r1;
     r1 = raised;
   }
