@@ -81,6 +81,8 @@ struct GraphCore {
   ScanWorkspace scan_ws;
   DBuf<uint32_t> rep, cnt, pos, order, rank, tmp32a, tmp32b, tmp32c, tmp32d, flags;
   DBuf<uint32_t> kraise;  // [V] last kappa iteration that raised kap[rep]
+  DBuf<uint32_t> erep;    // [E] rep[dst[e]] (refresh_edge_rep)
+  uint64_t nedges = 0;
   DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c;
   DBuf<uint8_t> blocked;
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)
@@ -99,6 +101,7 @@ struct GraphCore {
   void pending_closure(const GraphInput &in, GraphOutput &out);
   uint64_t count_forward(const GraphInput &in);
   void find_sccs(const GraphInput &in);
+  void refresh_edge_rep(const GraphInput &in);
   bool order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters,
                    bool give_up_early = false);
   // false: restricted candidates too many, nothing done

@@ -254,8 +254,18 @@ __global__ void k_kap_init(uint32_t V, const uint8_t *__restrict__ blocked,
   }
 }
 
+// erep[e] = rep[dst[e]]: the representative of every edge's target, refreshed
+// whenever rep changes, so the iterative kernels read it coalesced alongside
+// the edge instead of gathering rep[] per edge on every iteration
+__global__ void k_edge_rep(uint64_t E, const uint32_t *__restrict__ dst,
+                           const uint32_t *__restrict__ rep, uint32_t *__restrict__ erep) {
+  for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E;
+       e += uint64_t(gridDim.x) * blockDim.x)
+    erep[e] = rep[dst[e]];
+}
+
 __global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
-                            const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
+                            const uint32_t *__restrict__ erep, const uint8_t *__restrict__ blocked,
                             const uint32_t *__restrict__ rep, uint64_t *kap, uint32_t *changed,
                             uint32_t *kraise, uint32_t iter) {
   WAVE_STRIDE(v, V) {
@@ -264,7 +274,7 @@ __global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32
     uint64_t best = 0;
     if (act) {
       for (uint32_t e = EB(v); e < EE(v); e++) {
-        const uint32_t ru = rep[dst[e]];
+        const uint32_t ru = erep[e];
         if (ru != r) {
           const uint64_t c = ld_u64(&kap[ru]) + 1;
           best = c > best ? c : best;
@@ -326,7 +336,8 @@ __global__ void k_fb_init(uint32_t n, const uint32_t *__restrict__ list,
 
 __global__ void k_fb_hprop(uint32_t n, const uint32_t *__restrict__ list,
                            const uint32_t *__restrict__ off, uint32_t stride,
-                           const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
+                           const uint32_t *__restrict__ dst, const uint32_t *__restrict__ erep,
+                           const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            uint32_t *H, uint32_t *changed) {
   WAVE_STRIDE(j, n) {
@@ -336,9 +347,10 @@ __global__ void k_fb_hprop(uint32_t n, const uint32_t *__restrict__ list,
     uint32_t best = 0;
     if (act) {
       for (uint32_t e = EB(v); e < EE(v); e++) {
-        const uint32_t u = dst[e];
-        const uint32_t ru = rep[u];
-        if (ru != r && !done[u]) {
+        // done is uniform over a representative's class (members share
+        // reached[r]; blocked is closed under cycles), so done[ru] == done[u]
+        const uint32_t ru = erep ? erep[e] : rep[dst[e]];
+        if (ru != r && !done[erep ? ru : dst[e]]) {
           const uint32_t h = ld_u32(&H[ru]);
           best = h > best ? h : best;
         }
@@ -361,7 +373,8 @@ __global__ void k_fb_roots(uint32_t n, const uint32_t *__restrict__ list,
 
 __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
                            const uint32_t *__restrict__ off, uint32_t stride,
-                           const uint32_t *__restrict__ dst, const uint8_t *__restrict__ blocked,
+                           const uint32_t *__restrict__ dst, const uint32_t *__restrict__ erep,
+                           const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            const uint32_t *__restrict__ H, uint8_t *reached, uint32_t *changed) {
   GRID_STRIDE(j, n) {
@@ -371,9 +384,8 @@ __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
     if (!__hip_atomic_load(&reached[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
     const uint32_t hr = H[r];
     for (uint32_t e = EB(v); e < EE(v); e++) {
-      const uint32_t u = dst[e];
-      const uint32_t ru = rep[u];
-      if (ru != r && !done[u] && H[ru] == hr &&
+      const uint32_t ru = erep ? erep[e] : rep[dst[e]];
+      if (ru != r && !done[erep ? ru : dst[e]] && H[ru] == hr &&
           !__hip_atomic_load(&reached[ru], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         __hip_atomic_store(&reached[ru], uint8_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *changed = 1;
@@ -568,18 +580,26 @@ void GraphCore::find_sccs(const GraphInput &in) {
   mark("scc_compress");
 }
 
+void GraphCore::refresh_edge_rep(const GraphInput &in) {
+  if (nedges == 0) return;
+  uint32_t *er = erep.ensure(nedges);
+  const uint64_t blocks = (nedges + B - 1) / B;
+  k_edge_rep<<<unsigned(blocks < 65536 ? blocks : 65536), B, 0, stream>>>(nedges, in.dst, rep.get(), er);
+}
+
 bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters,
                             bool give_up_early) {
   const uint32_t V = in.V;
   FH_HIP(hipMemsetAsync(kap.get(), 0, size_t(V) * sizeof(uint64_t), stream));
   FH_HIP(hipMemsetAsync(kraise.ensure(V + 1), 0, size_t(V) * sizeof(uint32_t), stream));
   k_kap_init<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get());
+  refresh_edge_rep(in);
   // raises of the last iterations; a cycle the windows missed keeps raising
   // its members forever, a converging run raises fewer and fewer vertices
   uint64_t r1 = 0, r2 = 0;
   for (uint32_t it = 0; it < max_iters; it++) {
     FH_HIP(hipMemsetAsync(scalars.get() + 16, 0, 8 * sizeof(uint32_t), stream));
-    k_kap_relax<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), rep.get(),
+    k_kap_relax<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(), rep.get(),
                                                    kap.get(), scalars.get() + 16, kraise.get(), it + 1);
     iters = it + 1;
     uint32_t c[8];
@@ -634,7 +654,11 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     FH_HIP(hipMemsetAsync(done, 0, V, stream));
   }
   const unsigned G = grid_for(n, B);
+  // the full pass reads edge targets' representatives from erep (rep changes
+  // once per round, at the merge); the restricted pass touches few edges
   for (;;) {
+    if (!list) refresh_edge_rep(in);
+    const uint32_t *er = list ? nullptr : erep.get();
     if (list)
       k_fb_hreset<<<G, B, 0, stream>>>(n, list, rep.get(), H);
     else
@@ -644,14 +668,14 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     do {
       dbg_hprop++;
       FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
-      k_fb_hprop<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, blocked.get(), done,
+      k_fb_hprop<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
                                        rep.get(), H, scalars.get());
     } while (read_scalar(0));
     k_fb_roots<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
     do {
       dbg_reach++;
       FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
-      k_fb_reach<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, blocked.get(), done,
+      k_fb_reach<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
                                        rep.get(), H, reached, scalars.get());
     } while (read_scalar(0));
     FH_HIP(hipMemsetAsync(scalars.get() + 1, 0, sizeof(uint32_t), stream));
@@ -763,6 +787,13 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   if (V == 0) {
     out.trivial = true;
     return;
+  }
+  nedges = uint64_t(V) * in.stride;
+  if (in.off) {
+    uint32_t e = 0;
+    FH_HIP(hipMemcpyAsync(&e, in.off + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    nedges = e;
   }
   pending_closure(in, out);
   // trivial: nothing pending and every edge points to an earlier arrival ->
