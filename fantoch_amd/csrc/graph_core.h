@@ -88,7 +88,7 @@ struct GraphCore {
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)
   bool profile = false;
   uint32_t dbg_rounds = 0, dbg_hprop = 0, dbg_reach = 0;  // FH_GRAPH_DEBUG counters
-  uint32_t dbg_cand = 0, dbg_restricted = 0, dbg_sync_n = 0;
+  uint32_t dbg_cand = 0, dbg_restricted = 0, dbg_sync_n = 0, dbg_left = 0;
   double dbg_sync_us = 0;
   // per-kernel timing (engine profiling)
   std::vector<std::pair<const char *, hipEvent_t>> *marks = nullptr;

@@ -334,6 +334,20 @@ __global__ void k_fb_init(uint32_t n, const uint32_t *__restrict__ list,
   }
 }
 
+// first full round: the high half of kappa (ready time) is the maximum
+// arrival position its bounded run reached from the class, a lower bound of
+// the propagation's fixpoint H, so starting from it converges to the same H
+// in fewer iterations
+__global__ void k_fb_seed(uint32_t V, const uint8_t *__restrict__ blocked,
+                          const uint32_t *__restrict__ rep, const uint64_t *__restrict__ kap,
+                          uint32_t *H) {
+  GRID_STRIDE(v, V) {
+    if (blocked[v] || rep[v] != v) continue;
+    const uint32_t h = uint32_t(kap[v] >> 32);
+    if (h > H[v]) H[v] = h;
+  }
+}
+
 __global__ void k_fb_hprop(uint32_t n, const uint32_t *__restrict__ list,
                            const uint32_t *__restrict__ off, uint32_t stride,
                            const uint32_t *__restrict__ dst, const uint32_t *__restrict__ erep,
@@ -425,6 +439,11 @@ __global__ void k_fb_copy(uint32_t n, const uint32_t *__restrict__ list,
     const uint32_t v = FB_VID(j);
     dst[v] = src[v];
   }
+}
+
+__global__ void k_fb_left(uint32_t V, const uint8_t *__restrict__ blocked,
+                          const uint8_t *__restrict__ done, uint32_t *__restrict__ fl) {
+  GRID_STRIDE(v, V) fl[v] = (!blocked[v] && !done[v]) ? 1u : 0u;
 }
 
 __global__ void k_compact(uint32_t V, const uint32_t *__restrict__ fl,
@@ -653,17 +672,25 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
   } else {
     FH_HIP(hipMemsetAsync(done, 0, V, stream));
   }
-  const unsigned G = grid_for(n, B);
-  // the full pass reads edge targets' representatives from erep (rep changes
-  // once per round, at the merge); the restricted pass touches few edges
+  unsigned G = grid_for(n, B);
+  // the full pass reads edge targets' representatives from erep.  A round only
+  // merges classes it marks done, so the representative of every vertex not
+  // yet done is unchanged and erep stays valid for the edges still followed;
+  // done[old rep] == done[u] since a class is marked done as a whole.  After
+  // the first round the pass runs over a compacted list of the vertices left.
+  const bool full = list == nullptr;
+  const uint32_t *er = nullptr;
+  if (full) {
+    refresh_edge_rep(in);
+    er = erep.get();
+  }
   for (;;) {
-    if (!list) refresh_edge_rep(in);
-    const uint32_t *er = list ? nullptr : erep.get();
     if (list)
       k_fb_hreset<<<G, B, 0, stream>>>(n, list, rep.get(), H);
     else
       FH_HIP(hipMemsetAsync(H, 0, size_t(V) * sizeof(uint32_t), stream));
     k_fb_init<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
+    if (full && !list) k_fb_seed<<<G, B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get(), H);
     dbg_rounds++;
     do {
       dbg_hprop++;
@@ -695,6 +722,21 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
       FH_HIP(hipMemcpyAsync(rep.get(), parent, size_t(V) * sizeof(uint32_t),
                             hipMemcpyDeviceToDevice, stream));
     if (!read_scalar(1)) break;
+    if (full) {
+      // vertices left for the next round -> list (the restricted pass's path)
+      uint32_t *fl = cnt.ensure(V);
+      uint32_t *ps = pos.ensure(V + 1);
+      uint32_t *lst = order.ensure(V + 1);
+      k_fb_left<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), done, fl);
+      exclusive_scan_u32(fl, ps, V, scan_ws, stream);
+      k_compact<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, lst);
+      FH_HIP(hipMemcpyAsync(&n, ps + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      FH_HIP(hipStreamSynchronize(stream));
+      if (n == 0) break;
+      list = lst;
+      G = grid_for(n, B);
+      dbg_left += n;
+    }
   }
   mark("scc_fallback");
   return true;
@@ -830,7 +872,7 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
   }
   uint32_t iters = 0, iters1 = 0;
-  dbg_rounds = dbg_hprop = dbg_reach = dbg_sync_n = 0;
+  dbg_rounds = dbg_hprop = dbg_reach = dbg_sync_n = dbg_left = 0;
   dbg_sync_us = 0;
   // a cycle the windows missed makes kappa grow forever: give up early and let
   // the exact coloring complete the partition (an exact partition converges in
@@ -856,9 +898,9 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   if (debug)
     fprintf(stderr,
             "fh graph: V=%u forward=%llu kappa=%u fallback=%d (candidates %u, restricted %u, "
-            "rounds %u, hprop %u, reach %u) kappa2=%u syncs %u %.0f us\n",
+            "rounds %u, hprop %u, reach %u, left %u) kappa2=%u syncs %u %.0f us\n",
             V, (unsigned long long)nfwd, iters1, int(out.fallback_used), dbg_cand,
-            dbg_restricted, dbg_rounds, dbg_hprop, dbg_reach, out.fallback_used ? iters : 0u,
+            dbg_restricted, dbg_rounds, dbg_hprop, dbg_reach, dbg_left, out.fallback_used ? iters : 0u,
             dbg_sync_n, dbg_sync_us);
   build_orders(in, out);
 }
