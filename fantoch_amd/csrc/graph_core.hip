@@ -273,12 +273,17 @@ __global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32
     const uint32_t r = act ? rep[v] : 0u;
     uint64_t best = 0;
     if (act) {
-      for (uint32_t e = EB(v); e < EE(v); e++) {
-        const uint32_t ru = erep[e];
-        if (ru != r) {
-          const uint64_t c = ld_u64(&kap[ru]) + 1;
-          best = c > best ? c : best;
-        }
+      // four edges per trip, every gather issued before the first is used
+      const uint32_t eb = EB(v), ee = EE(v);
+      for (uint32_t e = eb; e < ee; e += 4) {
+        uint32_t ru[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
+        uint64_t c[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) c[j] = ru[j] != r ? ld_u64(&kap[ru[j]]) + 1 : 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) best = c[j] > best ? c[j] : best;
       }
     }
     const bool raised =
@@ -360,13 +365,34 @@ __global__ void k_fb_hprop(uint32_t n, const uint32_t *__restrict__ list,
     const uint32_t r = act ? rep[v] : 0u;
     uint32_t best = 0;
     if (act) {
-      for (uint32_t e = EB(v); e < EE(v); e++) {
-        // done is uniform over a representative's class (members share
-        // reached[r]; blocked is closed under cycles), so done[ru] == done[u]
-        const uint32_t ru = erep ? erep[e] : rep[dst[e]];
-        if (ru != r && !done[erep ? ru : dst[e]]) {
-          const uint32_t h = ld_u32(&H[ru]);
-          best = h > best ? h : best;
+      // done is uniform over a representative's class (members share
+      // reached[r]; blocked is closed under cycles), so done[ru] == done[u]
+      const uint32_t eb = EB(v), ee = EE(v);
+      if (erep) {
+        // four edges per trip, every gather issued before the first is used
+        for (uint32_t e = eb; e < ee; e += 4) {
+          uint32_t ru[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
+          uint8_t dn[4];
+          uint32_t h[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            dn[j] = ru[j] != r ? done[ru[j]] : 1;
+            h[j] = ru[j] != r ? ld_u32(&H[ru[j]]) : 0;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (!dn[j]) best = h[j] > best ? h[j] : best;
+        }
+      } else {
+        for (uint32_t e = eb; e < ee; e++) {
+          const uint32_t u = dst[e];
+          const uint32_t ru = rep[u];
+          if (ru != r && !done[u]) {
+            const uint32_t h = ld_u32(&H[ru]);
+            best = h > best ? h : best;
+          }
         }
       }
     }
