@@ -423,12 +423,31 @@ __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
     const uint32_t r = rep[v];
     if (!__hip_atomic_load(&reached[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
     const uint32_t hr = H[r];
-    for (uint32_t e = EB(v); e < EE(v); e++) {
-      const uint32_t ru = erep ? erep[e] : rep[dst[e]];
-      if (ru != r && !done[erep ? ru : dst[e]] && H[ru] == hr &&
-          !__hip_atomic_load(&reached[ru], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        __hip_atomic_store(&reached[ru], uint8_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *changed = 1;
+    const uint32_t eb = EB(v), ee = EE(v);
+    if (erep) {
+      // four edges per trip, every gather issued before the first is used
+      for (uint32_t e = eb; e < ee; e += 4) {
+        uint32_t ru[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
+        bool cand[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) cand[j] = ru[j] != r && !done[ru[j]] && H[ru[j]] == hr;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (cand[j] && !__hip_atomic_load(&reached[ru[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            __hip_atomic_store(&reached[ru[j]], uint8_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *changed = 1;
+          }
+      }
+    } else {
+      for (uint32_t e = eb; e < ee; e++) {
+        const uint32_t ru = rep[dst[e]];
+        if (ru != r && !done[dst[e]] && H[ru] == hr &&
+            !__hip_atomic_load(&reached[ru], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          __hip_atomic_store(&reached[ru], uint8_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *changed = 1;
+        }
       }
     }
   }
