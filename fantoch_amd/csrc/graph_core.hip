@@ -247,8 +247,12 @@ __global__ void __launch_bounds__(256)
 // ---------------------------------------------------------------- kappa
 __global__ void k_kap_init(uint32_t V, const uint8_t *__restrict__ blocked,
                            const uint32_t *__restrict__ rep, uint64_t *kap) {
-  WAVE_STRIDE(v, V) {
-    const bool act = v < V && !blocked[v];
+  // highest vertex first: a class's maximum lands early and the later
+  // (smaller) members' waves see it and skip the atomic (one large SCC would
+  // otherwise serialise every wave on its representative's word)
+  WAVE_STRIDE(i, V) {
+    const uint32_t v = i < V ? V - 1 - i : 0u;
+    const bool act = i < V && !blocked[v];
     agg_max<unsigned long long>((unsigned long long *)kap, act ? rep[v] : 0u,
                                 (unsigned long long)v << 32, act);
   }
@@ -330,11 +334,13 @@ __global__ void k_fb_init(uint32_t n, const uint32_t *__restrict__ list,
                           const uint8_t *__restrict__ blocked,
                           const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                           uint32_t *H, uint8_t *reached) {
-  WAVE_STRIDE(j, n) {
-    const uint32_t v = j < n ? FB_VID(j) : 0u;
-    const uint32_t r = j < n ? rep[v] : 0u;
-    if (j < n && r == v) reached[v] = 0;
-    const bool act = j < n && !blocked[v] && !done[v];
+  // highest vertex first (lists are ascending), as in k_kap_init
+  WAVE_STRIDE(i, n) {
+    const uint32_t j = i < n ? n - 1 - i : 0u;
+    const uint32_t v = i < n ? FB_VID(j) : 0u;
+    const uint32_t r = i < n ? rep[v] : 0u;
+    if (i < n && r == v) reached[v] = 0;
+    const bool act = i < n && !blocked[v] && !done[v];
     agg_max<uint32_t>(H, r, v, act);
   }
 }
