@@ -1,24 +1,32 @@
 #!/usr/bin/env python
-"""bench.py -- commands ordered per second (deps + SCC + order) on MI355X.
+"""bench.py -- commands ordered per second (deps+SCC+order) on MI355X.
 
-Workload (BASELINE.json configs[1], "C2"): Zipf s=0.7 over 1M keys, 1 key per
-command, one replica view, batches of 1M commands.  A step is one pass of the
-fused engine over the next batch of the committed stream (inputs resident in
-HBM, KeyDeps / executed-clock state carried from the previous batch): radix
-sort -> per-key predecessor deps -> dependency graph certified acyclic ->
-execution order -> per-key execution sequence -> executed-clock advance.
+Headline workload (BASELINE.json configs[3], "C4"): Atlas n=5 f=1 (fast quorum
+3), 100M commands, Zipf s=0.99 over 2^20 keys, 1 key per command, replica
+views (each replica's KeyDeps sees its commands in its own arrival order,
+reorder window W=64).  One step orders the whole 100M-command stream from a
+clean state, inputs resident in HBM:
+  per-replica KeyDeps (sort by (replica, key) + previous element of each
+  segment) -> QuorumDeps union -> dependency graph -> SCCs -> execution
+  order -> per-key execution sequences,
+and every output is materialised on the device inside the step: committed
+deps as CSR of dots, SCC labels (min dot), execution ranks, per-key offsets
+and per-key dot sequences (fh_engine_run).  Between steps fh_engine_rewind
+clears the latest tables and executed clock on the engine stream.
 
 Multi-GPU (`--gpus N`, one process per GPU under torch.distributed.run): the
-stream is key-sharded (owner = key mod N); with one key per
-command a shard's commands depend only on that shard, so there is no data-path
-collective (weak scaling: every rank orders ~1M commands per step).  Each
-shard sequences its own dots, as fantoch's per-shard DotGen does
-(fantoch/src/util.rs:115-122).
+stream is key-sharded (owner = key mod N).  With one key per
+command every dependency joins two commands of one key, so a shard's graph is
+closed: each rank orders its shard of the same global stream (global dots)
+with no data-path collective; torch.distributed (RCCL) carries only the
+barrier and the max-over-ranks time.  Total work is fixed: "scaling":
+"strong", value = 100M x steps / max-over-ranks time.
 
-Output: one JSON line (rank 0) with the metric, the roofline of the dominant
-kernel (HIP events around it inside the timed steps) and the CPU baseline
-(the oracle restatement of SequentialKeyDeps + GraphExecutor on a bounded
-sample, rank 0 at N=1 only).
+The JSON line also carries the roofline of the dominant kernel (HIP events on
+the engine stream around its launches in a probe pass), the CPU baseline (the
+oracle restatement of the reference's per-replica SequentialKeyDeps +
+QuorumDeps + incremental GraphExecutor on a bounded prefix, rank 0 at N=1)
+and, as `secondary`, the C2 line (single-view KeyDeps, 1M-command batches).
 """
 from __future__ import annotations
 
@@ -35,6 +43,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 METRIC = "commands ordered/sec (deps+SCC+order) at 1/2/4/8 GPUs; % HBM roofline"
+C4_SEED = 0xFA170C4000000004
+C2_SEED = 0xFA170C4000000002
 
 
 def parse():
@@ -42,54 +52,136 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--commands", type=int, default=100_000_000, help="C4 stream length")
     ap.add_argument("--keys", type=int, default=1 << 20)
-    ap.add_argument("--zipf", type=float, default=0.7)
-    ap.add_argument("--seed", type=int, default=0xFA170C4000000002)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=40_000_000,
-                    help="commands in the CPU-baseline sample (~10 s of one host core)")
-    ap.add_argument("--probe", default="kb_step,kb_partition,kb_order",
-                    help="kernels whose launches are timed (comma-separated); the roofline "
-                         "entry reports the one with the most device time")
+    ap.add_argument("--cpu-sample", type=int, default=4_000_000,
+                    help="C4 commands in the CPU-baseline prefix (~10 s of one host core)")
+    ap.add_argument("--probe", default="sort_scatter,graph_tile,prev_engine,cmd_union,log_keys",
+                    help="kernels whose launches are timed in the probe pass")
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase profile pass")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the secondary C2 line")
     return ap.parse_args()
-
-
-def shard_batches(args, rank, world, nbatches):
-    """The rank's key shard of the global C2 stream (fantoch_amd/shard.py)."""
-    from fantoch_amd.shard import shard_batches as sb
-    from fantoch_amd.workload import Workload
-    w = Workload.zipf(args.zipf, args.keys, k=1, seed=args.seed, n=5)
-    return sb(w, rank, world, args.batch, nbatches)
 
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, written by tools/collect_pmc.py from
-    separate FETCH_SIZE / WRITE_SIZE passes of this same command), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    (profiles/pmc_traffic.json, tools/collect_pmc.py), or None."""
     try:
-        with open(path) as fh:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
             return json.load(fh).get(kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
 
-def cpu_baseline(batch_stream, sample):
-    """Oracle (C restatement of the reference CPU path) on `sample` commands,
-    single-threaded; returns cmds/s."""
-    from oracle import oracle as O
+def c4_workload(keys):
     from fantoch_amd.workload import Workload
-    s = batch_stream
-    dots, keys = s.dots[:sample], s.keys[:sample].reshape(-1)
-    key_off = np.arange(len(dots) + 1, dtype=np.uint32)
+    return Workload.zipf(0.99, keys, k=1, views=3, window=64, seed=C4_SEED, n=5)
+
+
+def cpu_baseline_c4(w, sample):
+    """Oracle (C restatement of the reference CPU path: per-replica
+    SequentialKeyDeps, QuorumDeps union, incremental GraphExecutor) on the
+    first `sample` commands of the same stream, one thread; cmds/s."""
+    from oracle import oracle as O
+    s = w.generate(sample)
+    key_off = s.key_off()
+    keys = s.keys.reshape(-1)
     t0 = time.perf_counter()
-    dep_off, deps = O.keydeps_run(dots, key_off, keys)
-    ex, lab, kso, ks = O.graph_run(dots, key_off, keys, dep_off, deps, s.key_space)
+    off, deps = O.views_run(0, 5, s.dots, key_off, keys, s.fq_proc, s.fq_time)
+    ex, lab, kso, ks = O.graph_run(s.dots, key_off, keys, off, deps, s.key_space)
     dt = time.perf_counter() - t0
-    assert len(ex) == len(dots)
-    return len(dots) / dt, dt
+    assert len(ex) == s.n
+    return s.n / dt, dt
+
+
+def timed_steps(eng, steps, barrier, rewind=True):
+    import torch
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if rewind:
+            eng.rewind()
+        eng.run(sync=False)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    return t1 - t0
+
+
+def probe_pass(eng, names, steps, rewind=True):
+    import torch
+    eng.set_probe(names)
+    for _ in range(steps):
+        if rewind:
+            eng.rewind()
+        eng.run(sync=False)
+    torch.cuda.synchronize()
+    probes = {}
+    for name in [x for x in names.split(",") if x]:
+        ms_, nl_, by_ = eng.probe_stats(name)
+        if nl_:
+            probes[name] = {"avg_launch_us": ms_ * 1e3, "launches": nl_,
+                            "algorithmic_bytes_per_launch": by_,
+                            "achieved_GBs": by_ / (ms_ * 1e-3) / 1e9 if ms_ > 0 else 0.0,
+                            "traffic": pmc_traffic(name)}
+    eng.set_probe(None)
+    return probes
+
+
+def roofline(probes, fallback):
+    if not probes:
+        return {"bound": "hbm", "kernel": fallback, "achieved": 0.0, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": 0.0, "traffic": None}
+    # dominant kernel: the most device time over the pass
+    dom = max(probes, key=lambda k: probes[k]["avg_launch_us"] * probes[k]["launches"])
+    p = probes[dom]
+    ach = p["achieved_GBs"]
+    return {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": p["traffic"], "launches": p["launches"],
+            "avg_launch_us": p["avg_launch_us"],
+            "algorithmic_bytes_per_launch": p["algorithmic_bytes_per_launch"]}
+
+
+def phases_of(eng, rewind=True):
+    eng.set_profiling(True)
+    acc = {}
+    for _ in range(3):
+        if rewind:
+            eng.rewind()
+        eng.run(sync=True)
+        for name, ms in eng.kernel_times():
+            acc.setdefault(name, []).append(ms)
+    eng.set_profiling(False)
+    return {k: round(float(np.median(v[1:] if len(v) > 1 else v)), 4) for k, v in acc.items()}
+
+
+def secondary_c2(args, local):
+    """C2: single-view KeyDeps + GraphExecutor, Zipf 0.7 over 1M keys, 1M-command
+    batches of one continuing stream (state carried across batches)."""
+    import torch
+    from fantoch_amd.engine import Engine
+    from fantoch_amd.workload import Workload
+    batch, steps, warm = 1_000_000, 20, 5
+    w = Workload.zipf(0.7, 1 << 20, k=1, seed=C2_SEED, n=5)
+    s = w.generate(batch * (warm + steps))
+    eng = Engine(s.key_space, n=5, device=local)
+    from fantoch_amd.workload import Stream
+    eng.stage_many([Stream(s.dots[i * batch:(i + 1) * batch], s.keys[i * batch:(i + 1) * batch],
+                           None, None, s.key_space) for i in range(warm + steps)])
+    for _ in range(warm):
+        eng.run(sync=False)
+    torch.cuda.synchronize()
+    el = timed_steps(eng, steps, lambda: None, rewind=False)
+    r = eng.results()
+    eng.close()
+    return {"metric": METRIC, "value": batch * steps / el, "unit": "commands/s",
+            "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warm,
+            "config": {"workload": "C2: Zipf s=0.7 over 2^20 keys, 1 key/cmd, single replica view, "
+                                   "1M-command batches of one stream, every output materialised",
+                       "batch": batch},
+            "deps_last_batch": int(r["dep_off"][-1])}
 
 
 def main():
@@ -98,85 +190,59 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    import torch
     if world > 1 or "RANK" in os.environ:
-        import torch
         import torch.distributed as dist_mod
         dist = dist_mod
         torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl")
-    import torch
 
     from fantoch_amd.engine import Engine
-
-    # warmup + the timed steps + a probe pass of the same length (per-launch
-    # HIP events cost ~3 us of stream time each, so they stay out of the
-    # timed region)
-    nb = args.warmup + 2 * args.steps
-    batches = shard_batches(args, rank, world, nb)
-    key_space = batches[0].key_space
-    eng = Engine(key_space, n=5, device=local)
-    eng.stage_many(batches)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
+    w = c4_workload(args.keys)
+    t_gen = time.perf_counter()
+    if world == 1:
+        s = w.generate(args.commands, logs=True, times=False)
+    else:
+        s = w.generate_shard(args.commands, world, rank)
+    t_gen = time.perf_counter() - t_gen
+    eng = Engine(s.key_space, n=5, device=local)
+    eng.stage(s)
     for _ in range(args.warmup):
+        eng.rewind()
         eng.run(sync=False)
     torch.cuda.synchronize()
-
-    # timed region: exactly `steps` batches, no instrumentation
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.run(sync=False)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    # probe pass: the next `steps` batches with HIP events on the stream of
-    # every launch of the probed kernels (their own dispatch begin/end)
-    eng.set_probe(args.probe)
-    for _ in range(args.steps):
-        eng.run(sync=False)
-    torch.cuda.synchronize()
-    probes = {}
-    for name in [x for x in args.probe.split(",") if x]:
-        ms_, nl_, by_ = eng.probe_stats(name)
-        if nl_:
-            probes[name] = {"avg_launch_us": ms_ * 1e3, "launches": nl_,
-                            "algorithmic_bytes_per_launch": by_,
-                            "achieved_GBs": by_ / (ms_ * 1e-3) / 1e9 if ms_ > 0 else 0.0}
-    eng.set_probe(None)
-    # dominant kernel: most device time over the pass (average x launches)
-    dominant = (max(probes, key=lambda k: probes[k]["avg_launch_us"] * probes[k]["launches"])
-                if probes else args.probe)
-    pd = probes.get(dominant, {"avg_launch_us": 0.0, "launches": 0,
-                               "algorithmic_bytes_per_launch": 0.0})
-    probe_ms, probe_launches = pd["avg_launch_us"] * 1e-3, pd["launches"]
-    probe_bytes = pd["algorithmic_bytes_per_launch"]
-    elapsed = t1 - t0
+    elapsed = timed_steps(eng, args.steps, barrier)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_cmds = args.batch * args.steps * world
-    value = total_cmds / elapsed
+    value = args.commands * args.steps / elapsed
 
-    # per-phase device times (separate profiled pass over a re-staged batch)
-    phases = None
-    if rank == 0 and not args.no_phases:
-        eng2 = Engine(key_space, n=5, device=local)
-        eng2.stage_many(batches[:4])
-        eng2.set_profiling(True)
-        acc = {}
-        for _ in range(4):
-            eng2.run(sync=True)
-            for name, ms in eng2.kernel_times():
-                acc.setdefault(name, []).append(ms)
-        phases = {k: float(np.median(v[1:])) for k, v in acc.items()}
-        eng2.close()
+    # outputs of the last run (read back outside the timed region)
+    r = eng.results()
+    n_local = s.n
+    deps_total = int(r["dep_off"][-1])
+    _, scc_sizes = np.unique(r["scc_label"], return_counts=True)
+    probes = probe_pass(eng, args.probe, min(args.steps, 10))
+    phases = None if (args.no_phases or rank != 0) else phases_of(eng)
+    eng.close()
 
+    d = deps_total / max(1, n_local)
+    k, views = 1, 3
+    # SURVEY §8d algorithmic bytes per command with replica views: KeyDeps per
+    # view (read dot + key ids, write offset + deps; d_v <= k), the union of
+    # the views' reports into d committed deps, the executor (CSR as vertex
+    # ids, dot for the tie-break, SCC id + exec rank) and the per-key order.
+    b_deps = views * (8 * (1 + k) + 4 + 8 * k)
+    b_union = views * (4 + 8 * k) + 4 + 8 * d
+    b_exec = 4 + 4 * d + 8 + 4 + 4
+    b_order = 8 + 8 * k
+    bpc = b_deps + b_union + b_exec + b_order
     result = {
         "metric": METRIC,
         "value": value,
@@ -186,45 +252,37 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
-        "config": {"workload": "C2: batched KeyDeps+GraphExecutor, Zipf s=0.7 over 1M keys, "
-                               "1 key/cmd, single replica view, 1M-command batches per GPU, "
-                               "key-sharded across GPUs",
-                   "batch_per_gpu": args.batch, "keys": args.keys, "zipf_s": args.zipf,
+        "config": {"workload": "C4: Atlas n=5 f=1 (fast quorum 3) replica views, 100M commands, "
+                               "Zipf s=0.99 over 2^20 keys, 1 key/cmd, reorder window 64; one step "
+                               "orders the whole stream, every output materialised on the device",
+                   "commands": args.commands, "keys": args.keys, "zipf_s": 0.99, "views": views,
                    "parallelism": f"key-shard x{world}"},
+        "roofline": roofline(probes, "sort_scatter"),
+        "kernels": probes,
+        "path_roofline": {"bytes_per_cmd": bpc,
+                          "achieved_GBs": value * bpc / 1e9 / world,
+                          "frac": value * bpc / 1e9 / world / HBM_PEAK_GBS},
+        "stream": {"commands_this_rank": n_local, "deps_per_cmd": d, "sccs": int(len(scc_sizes)),
+                   "largest_scc": int(scc_sizes.max()) if len(scc_sizes) else 0,
+                   "generate_s": round(t_gen, 2)},
     }
-    achieved = probe_bytes / (probe_ms * 1e-3) / 1e9 if probe_ms > 0 else 0.0
-    result["roofline"] = {"bound": "hbm", "kernel": dominant, "achieved": achieved,
-                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                          "traffic": pmc_traffic(dominant), "launches": probe_launches,
-                          "avg_launch_us": probe_ms * 1e3,
-                          "algorithmic_bytes_per_launch": probe_bytes}
-    for name, pr in probes.items():
-        pr["traffic"] = pmc_traffic(name)
-    result["kernels"] = probes
-    # whole path against SURVEY §8d's 68 B/command (single view, k = 1)
-    result["path_roofline"] = {"bytes_per_cmd": 68.0,
-                               "achieved_GBs": value * 68.0 / 1e9 / world,
-                               "frac": value * 68.0 / 1e9 / world / HBM_PEAK_GBS}
     if phases is not None:
         result["phases_ms"] = phases
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sample = min(args.cpu_sample, args.batch * nb)
-        big = batches[0]
-        if sample > big.n:
-            from fantoch_amd.workload import Stream
-            big = Stream(np.concatenate([b.dots for b in batches]),
-                         np.concatenate([b.keys for b in batches]), None, None, key_space)
-        v, dt = cpu_baseline(big, sample)
+        sample = min(args.cpu_sample, args.commands)
+        v, dt = cpu_baseline_c4(w, sample)
         result["cpu_baseline"] = {"value": v, "unit": "commands/s", "cores": 1, "kind": "port",
-                                  "sample": f"first {sample} commands of the same C2 stream, "
-                                            f"oracle SequentialKeyDeps + incremental "
-                                            f"GraphExecutor, 1 thread, {dt:.2f}s"}
+                                  "sample": f"first {sample} commands of the same C4 stream: oracle "
+                                            f"per-replica SequentialKeyDeps + QuorumDeps union + "
+                                            f"incremental GraphExecutor, 1 thread, {dt:.2f}s"}
+    if rank == 0 and world == 1 and not args.no_secondary:
+        result["secondary"] = secondary_c2(args, local)
     if rank == 0:
-        print(json.dumps(result))
+        print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

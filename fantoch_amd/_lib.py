@@ -87,6 +87,7 @@ SIGNATURES = {
     "fh_engine_reset": (C.c_int, [V]),
     "fh_engine_stage": (C.c_int, [V, P(fh_stream_desc), V, V, V, V]),
     "fh_engine_stage_many": (C.c_int, [V, P(fh_stream_desc), S, V, V, V, V]),
+    "fh_engine_stage_logs": (C.c_int, [V, P(fh_stream_desc), S, V, V, V, V]),
     "fh_engine_run": (C.c_int, [V, P(C.c_float)]),
     "fh_engine_results": (C.c_int, [V, V, V, S, P(S), V, V, V, V]),
     "fh_engine_kernel_times": (C.c_int, [V, P(C.c_char_p), P(C.c_float), S, P(S)]),
@@ -96,6 +97,10 @@ SIGNATURES = {
     "fh_engine_probe_stats_for": (C.c_int, [V, C.c_char_p, P(C.c_float), P(S), P(C.c_double)]),
     "fh_workload_key_space": (C.c_uint64, [P(fh_workload)]),
     "fh_workload_generate": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V, V, V]),
+    "fh_workload_generate_logs": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V]),
+    "fh_workload_generate_shard": (C.c_int, [P(fh_workload), C.c_uint64, S, C.c_uint32,
+                                             C.c_uint32, P(S), V, V, V, V]),
+    "fh_engine_rewind": (C.c_int, [V]),
 }
 
 _lib = None

@@ -16,8 +16,10 @@
 // arrival order is already topological and the per-key order is the key-sorted
 // element order: the graph stage certifies that and reuses it.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "graph_core.h"
@@ -30,17 +32,33 @@ constexpr unsigned B = 256;
 #define GRID_STRIDE(i, n) \
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
 
-// composite sort key for replica views: ((replica * K + key) << tb) | time
-__global__ void k_view_keys(uint32_t M, uint32_t k, uint32_t fq, uint64_t K,
-                            const uint32_t *__restrict__ key32, const uint8_t *__restrict__ fq_proc,
-                            const uint64_t *__restrict__ fq_time, uint64_t tmin, int tb,
-                            uint64_t *__restrict__ out) {
-  GRID_STRIDE(e, M) {
-    const uint32_t s = e % k;
-    const uint32_t ij = e / k;  // i * fq + j
-    const uint32_t i = ij / fq;
-    const uint64_t seg = uint64_t(fq_proc[ij]) * K + key32[i * k + s];
-    out[e] = (seg << tb) | (fq_time[ij] - tmin);
+// Replica views as per-replica arrival logs: replica r's SequentialKeyDeps
+// sees the commands of log r in log order (its add_cmd calls, atlas.rs:236,
+// :303-309).  Element x = q·k + s is key slot s of log entry q; entries are
+// concatenated replica by replica, so element order is (replica, arrival,
+// slot) and a stable sort by the segment id (r + 1)·K + key yields every
+// (replica, key) segment in arrival order.  The value is the element's
+// command-major position (c·fq + j)·k + s, where the union reads it.
+// One chunk of the logs: replica r contributes its entries
+// [first[r], first[r] + count[r]) (chunk-local element order = replica, then
+// arrival, then slot); cum[r] = elements of the replicas before r.
+constexpr int kMaxLogs = 16;
+struct LogChunk {
+  uint32_t first[kMaxLogs];
+  uint32_t cum[kMaxLogs + 1];
+};
+
+__global__ void k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, LogChunk ch,
+                           const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
+                           uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  GRID_STRIDE(x, M) {
+    uint32_t r = 0;
+    while (r + 1 < nlog && x >= ch.cum[r + 1]) r++;
+    const uint32_t y = x - ch.cum[r];
+    const uint32_t q = ch.first[r] + y / k, s = y % k;
+    const uint32_t e = ent[q];
+    keys[x] = (r + 1) * K + key32[(e / fq) * k + s];
+    vals[x] = e * k + s;
   }
 }
 
@@ -81,9 +99,16 @@ __global__ void k_tail_engine(uint32_t M, const KT *__restrict__ ks, const uint3
 }
 
 // decode an element's dependency code: in-batch vid (true) or external value
-__device__ __forceinline__ bool dep_in_batch(uint64_t c, uint32_t *v) {
+// (a log reference to a command of the batch itself, written by an earlier
+// chunk of the batch's replica logs, is in batch too)
+__device__ __forceinline__ bool dep_in_batch(uint64_t c, uint32_t *v, uint64_t bbase,
+                                             uint32_t n) {
   if (c != 0 && c < kLogFlag) {
     *v = uint32_t(c - 1);
+    return true;
+  }
+  if (is_log_ref(c) && c - kLogFlag >= bbase && c - kLogFlag < bbase + n) {
+    *v = uint32_t(c - kLogFlag - bbase);
     return true;
   }
   return false;
@@ -117,7 +142,7 @@ __device__ __forceinline__ void cmd_union_regs(
     const uint64_t *__restrict__ dep_code, const uint64_t *__restrict__ dlog,
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
-    uint32_t *nblocked, uint32_t *__restrict__ nv_out) {
+    uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
@@ -128,7 +153,7 @@ __device__ __forceinline__ void cmd_union_regs(
     if (t < S) {
       uint64_t x = dep_code[size_t(i) * S + t];
       uint32_t v;
-      if (dep_in_batch(x, &v)) {
+      if (dep_in_batch(x, &v, bbase, n)) {
         vv[t] = v;
         r[t] = dot[v];
       } else {
@@ -196,11 +221,12 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              const uint64_t *__restrict__ frontier,
                              uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ dep_cnt,
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
-                             uint32_t *nblocked, uint32_t *__restrict__ nv_out) {
+                             uint32_t *nblocked, uint32_t *__restrict__ nv_out,
+                             uint64_t bbase) {
   if (S <= kRegSlots) {  // uniform: the register path
     GRID_STRIDE(i, n) {
       cmd_union_regs(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                     nblocked, nv_out);
+                     nblocked, nv_out, bbase, n);
     }
     return;
   }
@@ -212,7 +238,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     for (uint32_t t = 0; t < S; t++) {
       uint64_t x = dep_code[size_t(i) * S + t];
       uint32_t v;
-      if (dep_in_batch(x, &v)) {
+      if (dep_in_batch(x, &v, bbase, n)) {
         bool dup = false;
         for (uint32_t q = 0; q < nv; q++) dup |= ds[q] == v;
         if (!dup) ds[nv++] = v;
@@ -398,18 +424,20 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-__global__ void k_frontier_update(const unsigned long long *__restrict__ mn,
-                                  const unsigned long long *__restrict__ mx,
+// The fused engine's executed clock: per source the highest executed
+// sequence and the number of executed dots.  Every batch executes completely
+// (no pending vertex is carried), and a dependency from an earlier batch can
+// only come from the latest tables, which hold executed dots; so the
+// `seq <= frontier[source]` test k_cmd_engine applies to external
+// dependencies is exact for the engine's own streams, including key shards
+// of a global stream whose executed sets are not contiguous per source.
+__global__ void k_frontier_update(const unsigned long long *__restrict__ mx,
                                   const unsigned int *__restrict__ cnt, uint64_t *frontier,
-                                  unsigned long long *excount, uint32_t *err) {
+                                  unsigned long long *excount) {
   const uint32_t s = threadIdx.x;
   if (s >= 256 || cnt[s] == 0) return;
-  if (mn[s] == frontier[s] + 1 && mx[s] - mn[s] + 1 == cnt[s]) {
-    frontier[s] = mx[s];
-    excount[s] += cnt[s];
-  } else {
-    atomicOr(err, 1u);  // non-contiguous executed set: needs exceptions
-  }
+  if (mx[s] > frontier[s]) frontier[s] = mx[s];
+  excount[s] += cnt[s];
 }
 
 // per-key sequence in key-grouped (not key-ascending) order -> ascending
@@ -513,17 +541,23 @@ struct EngineDevice {
   fh_stream_desc desc{};
   bool staged = false;
   size_t nbatches = 0, cursor = 0, last = 0;
-  std::vector<uint64_t> tmins;
-  uint64_t tmin = 0;
-  int tbits = 0;
-  DBuf<uint64_t> dot, fq_time;  // dot: the command log (every staged batch, appended)
-  size_t log_len = 0;            // dots in the log
-  size_t stage_base = 0;         // log position of the first staged batch
+  DBuf<uint64_t> dot;     // the command log (every staged batch, appended)
+  size_t log_len = 0;     // dots in the log
+  size_t stage_base = 0;  // log position of the first staged batch
   DBuf<uint32_t> key32;
-  DBuf<uint8_t> fq_proc;
-  // scratch / outputs
-  DBuf<uint64_t> vkeys, sk64a, sk64b, dep_ext, dep_dot, seq_dot, lab;
+  // replica views: per batch, the replicas' arrival logs concatenated
+  // (entries c·fq + j), and each batch's nproc + 1 log offsets
+  DBuf<uint32_t> lent, loff;
+  std::vector<uint32_t> h_loff;  // host copy of loff
+  // scratch
+  DBuf<uint64_t> dep_ext, dep_dot, seq_dot, lab;
   DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
+  // outputs of the last run (materialised inside run(), copied by results())
+  DBuf<uint32_t> o_dep_off;
+  DBuf<uint64_t> o_dep;
+  const uint64_t *o_label = nullptr;  // [n] min dot of each command's SCC
+  const uint32_t *o_rank = nullptr;   // [n] position in the execution order
+  uint32_t o_nelem = 0;               // per-key sequence length (key_offs, seq_dot)
   DBuf<uint32_t> edge_cnt, edge_off, edge_csr;  // replica views: in-batch edges as CSR
   DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
@@ -643,16 +677,99 @@ struct EngineDevice {
     staged = false;
   }
 
+  // fq_proc / fq_time -> per-replica arrival logs: replica r processes the
+  // commands it is a member for in (time, command index) order.
+  static void views_to_logs(const fh_stream_desc &d, size_t nb, const uint8_t *h_proc,
+                            const uint64_t *h_time, std::vector<uint64_t> &off,
+                            std::vector<uint32_t> &cmd) {
+    const size_t n = d.n, fq = d.views, np = d.nproc;
+    off.assign(nb * np + 1, 0);
+    cmd.assign(n * fq * nb, 0);
+    std::vector<size_t> cnt(nb * np, 0);
+    for (size_t b = 0; b < nb; b++)
+      for (size_t i = 0; i < n * fq; i++) {
+        const uint8_t p = h_proc[b * n * fq + i];
+        FH_CHECK(p >= 1 && p <= np, FH_EINVAL, "fq_proc out of range");
+        cnt[b * np + p - 1]++;
+      }
+    for (size_t x = 0; x < nb * np; x++) off[x + 1] = off[x] + cnt[x];
+    std::vector<size_t> fill(off.begin(), off.end() - 1);
+    for (size_t b = 0; b < nb; b++)
+      for (size_t i = 0; i < n * fq; i++) {
+        const uint8_t p = h_proc[b * n * fq + i];
+        cmd[fill[b * np + p - 1]++] = uint32_t(i / fq);
+      }
+    const size_t logs = nb * np;
+    auto work = [&](size_t lo, size_t hi) {
+      std::vector<std::pair<uint64_t, uint32_t>> tmp;
+      for (size_t x = lo; x < hi; x++) {
+        const size_t b = x / np;
+        tmp.clear();
+        for (size_t q = off[x]; q < off[x + 1]; q++) {
+          const uint32_t c = cmd[q];
+          // this command's member on replica (x % np) + 1
+          uint64_t t = 0;
+          for (size_t j = 0; j < fq; j++)
+            if (h_proc[(b * n + c) * fq + j] == x % np + 1) t = h_time[(b * n + c) * fq + j];
+          tmp.push_back({t, c});
+        }
+        std::sort(tmp.begin(), tmp.end());
+        for (size_t q = 0; q < tmp.size(); q++) cmd[off[x] + q] = tmp[q].second;
+      }
+    };
+    const size_t nt = std::min<size_t>(logs, 16);
+    std::vector<std::thread> ts;
+    for (size_t t = 0; t < nt; t++)
+      ts.emplace_back(work, logs * t / nt, logs * (t + 1) / nt);
+    for (auto &t : ts) t.join();
+  }
+
+  // Replay the staged batches from a clean state: latest tables and executed
+  // clock cleared on the engine stream (no host synchronisation), cursor back
+  // to the first staged batch.  The command log keeps its staged dots.
+  void rewind() {
+    FH_CHECK(staged, FH_EINVAL, "rewind: nothing staged");
+    FH_HIP(hipSetDevice(device));
+    if (kb_next_part != ~size_t(0) && kb_clk.get())
+      FH_HIP(hipMemsetAsync(kb_clk.get() + (kb_next_part & 1) * kKeyBucketClockWords, 0,
+                            kKeyBucketClockWords * sizeof(unsigned long long), stream));
+    kb_next_part = ~size_t(0);
+    FH_HIP(hipMemsetAsync(latest.get(), 0, latest_words(latest_slots) * sizeof(uint64_t), stream));
+    FH_HIP(hipMemsetAsync(frontier.get(), 0, 256 * sizeof(uint64_t), stream));
+    FH_HIP(hipMemsetAsync(excount_ptr(), 0, 256 * sizeof(unsigned long long), stream));
+    cursor = 0;
+  }
+
   void stage(const fh_stream_desc &d, size_t nb, const uint64_t *h_dot, const uint64_t *h_key,
              const uint8_t *h_proc, const uint64_t *h_time) {
+    if (!d.views) {
+      stage_logs(d, nb, h_dot, h_key, nullptr, nullptr);
+      return;
+    }
+    FH_CHECK(h_proc && h_time && d.nproc >= 1 && d.nproc <= 255, FH_EINVAL,
+             "replica views need fq_proc, fq_time and nproc");
+    FH_CHECK(d.views <= 16, FH_EINVAL, "views <= 16");
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> cmd;
+    views_to_logs(d, nb, h_proc, h_time, off, cmd);
+    stage_logs(d, nb, h_dot, h_key, off.data(), cmd.data());
+  }
+
+  // log_off[nb·nproc + 1] (global offsets into log_cmd), log_cmd[] batch-local
+  // command indices; every command appears in exactly `views` logs, at most
+  // once per log
+  void stage_logs(const fh_stream_desc &d, size_t nb, const uint64_t *h_dot,
+                  const uint64_t *h_key, const uint64_t *h_off, const uint32_t *h_cmd) {
     FH_CHECK(h_dot && h_key && nb >= 1, FH_EINVAL, "null argument");
     FH_CHECK(d.keys_per_cmd >= 1 && d.keys_per_cmd <= 8, FH_EINVAL, "keys_per_cmd in [1, 8]");
     const uint32_t fq = d.views ? d.views : 1;
     FH_CHECK(fq <= 16, FH_EINVAL, "views <= 16");
     FH_CHECK(size_t(d.n) * fq * d.keys_per_cmd < (size_t(1) << 30), FH_EINVAL,
              "batch too large (elements >= 2^30)");
-    FH_CHECK(!d.views || (h_proc && h_time && d.nproc >= 1 && d.nproc <= 255), FH_EINVAL,
-             "replica views need fq_proc, fq_time and nproc");
+    FH_CHECK(!d.views || (h_off && h_cmd && d.nproc >= 1 && d.nproc <= 255), FH_EINVAL,
+             "replica views need per-replica logs and nproc");
+    FH_CHECK(!d.views || uint64_t(d.nproc + 1) * key_space <= 0xFFFFFFFFull, FH_ENOTIMPL,
+             "replica views: (nproc + 1) * key_space must fit 32 bits");
     FH_HIP(hipSetDevice(device));
     sync_all();
     const size_t n = d.n, nk = n * d.keys_per_cmd;
@@ -660,6 +777,41 @@ struct EngineDevice {
     for (size_t e = 0; e < nk * nb; e++) {
       FH_CHECK(h_key[e] < key_space, FH_EINVAL, "stage: key id >= key_space");
       k32[e] = uint32_t(h_key[e]);
+    }
+    std::vector<uint32_t> ent, lo;
+    if (d.views) {
+      const size_t np = d.nproc;
+      FH_CHECK(h_off[0] == 0 && h_off[nb * np] == n * fq * nb, FH_EINVAL,
+               "logs: every command must appear in exactly `views` replica logs");
+      ent.resize(n * fq * nb);
+      lo.resize(nb * (np + 1));
+      std::vector<uint8_t> seen(n);
+      std::vector<int16_t> last_r(n);
+      for (size_t b = 0; b < nb; b++) {
+        std::fill(seen.begin(), seen.end(), 0);
+        std::fill(last_r.begin(), last_r.end(), -1);
+        const uint64_t base = h_off[b * np];
+        FH_CHECK(h_off[(b + 1) * np] - base == n * fq, FH_EINVAL,
+                 "logs: a batch's logs must hold n * views entries");
+        for (size_t r = 0; r < np; r++) {
+          lo[b * (np + 1) + r] = uint32_t(h_off[b * np + r] - base);
+          FH_CHECK(h_off[b * np + r + 1] >= h_off[b * np + r], FH_EINVAL, "logs: offsets");
+          for (uint64_t q = h_off[b * np + r]; q < h_off[b * np + r + 1]; q++) {
+            const uint32_t c = h_cmd[q];
+            FH_CHECK(c < n, FH_EINVAL, "logs: command index >= n");
+            FH_CHECK(last_r[c] != int16_t(r), FH_EINVAL,
+                     "logs: a replica processes a command once");
+            FH_CHECK(seen[c] < fq, FH_EINVAL,
+                     "logs: every command must appear in exactly `views` replica logs");
+            last_r[c] = int16_t(r);
+            ent[q] = uint32_t(c * fq + seen[c]++);
+          }
+        }
+        lo[b * (np + 1) + np] = uint32_t(n * fq);
+        for (size_t c = 0; c < n; c++)
+          FH_CHECK(seen[c] == fq, FH_EINVAL,
+                   "logs: every command must appear in exactly `views` replica logs");
+      }
     }
     // append the batches' dots to the command log (grown by doubling, old
     // entries kept: earlier batches stay referenced by the latest table)
@@ -680,25 +832,11 @@ struct EngineDevice {
     log_len += n * nb;
     FH_HIP(hipMemcpyAsync(key32.ensure(nk * nb + 1), k32.data(), nk * nb * sizeof(uint32_t),
                           hipMemcpyHostToDevice, stream));
-    tmins.assign(nb, 0);
-    tbits = 0;
     if (d.views) {
-      const size_t nv = n * fq;
-      for (size_t b = 0; b < nb; b++) {
-        uint64_t lo = ~0ull, hi = 0;
-        for (size_t i = b * nv; i < (b + 1) * nv; i++) {
-          FH_CHECK(h_proc[i] >= 1 && h_proc[i] <= d.nproc, FH_EINVAL, "fq_proc out of range");
-          lo = std::min(lo, h_time[i]);
-          hi = std::max(hi, h_time[i]);
-        }
-        tmins[b] = n ? lo : 0;
-        tbits = std::max(tbits, bits_for(n ? hi - lo + 1 : 1));
-      }
-      FH_CHECK(bits_for(uint64_t(d.nproc + 1) * key_space) + tbits <= 64, FH_ENOTIMPL,
-               "replica-view sort key wider than 64 bits");
-      FH_HIP(hipMemcpyAsync(fq_proc.ensure(nv * nb + 1), h_proc, nv * nb, hipMemcpyHostToDevice,
-                            stream));
-      FH_HIP(hipMemcpyAsync(fq_time.ensure(nv * nb + 1), h_time, nv * nb * sizeof(uint64_t),
+      FH_HIP(hipMemcpyAsync(lent.ensure(ent.size() + 1), ent.data(), ent.size() * sizeof(uint32_t),
+                            hipMemcpyHostToDevice, stream));
+      h_loff = lo;
+      FH_HIP(hipMemcpyAsync(loff.ensure(lo.size() + 1), lo.data(), lo.size() * sizeof(uint32_t),
                             hipMemcpyHostToDevice, stream));
       ensure_latest(d.nproc + 1);
     }
@@ -725,9 +863,6 @@ struct EngineDevice {
     const uint64_t bbase = stage_base + b * n;  // log position of this batch
     const uint64_t *bdot = dot.get() + bbase;
     const uint32_t *bkey = key32.get() + b * size_t(n) * k;
-    const uint8_t *bproc = views ? fq_proc.get() + b * size_t(n) * fq : nullptr;
-    const uint64_t *btime = views ? fq_time.get() + b * size_t(n) * fq : nullptr;
-    tmin = tmins[b];
     if (ms || profile) FH_HIP(hipEventRecord(ev0, stream));
     mark("start");
     struct ProbeGuard {
@@ -818,21 +953,52 @@ struct EngineDevice {
       sorted_keys32 = ks;
     } else {
       sv_fused = false;
-      uint64_t *vk = vkeys.ensure(M + 1);
-      k_view_keys<<<grid_for(M, B), B, 0, stream>>>(M, k, fq, key_space, bkey, bproc, btime, tmin,
-                                                     tbits, vk);
-      uint64_t *ks = nullptr;
-      const int bits = bits_for(uint64_t(desc.nproc + 1) * key_space) + tbits;
-      sort_pairs<uint64_t>(vk, nullptr, sk64a.ensure(M + 1), sva.ensure(M + 1),
-                           sk64b.ensure(M + 1), svb.ensure(M + 1), M, bits, sort_ws, stream, &ks,
-                           &vs);
-      mark("keydeps_sort");
-      k_prev_engine<uint64_t><<<grid_for(M, B), B, 0, stream>>>(
-          M, ks, vs, tbits, S, views_latest(), 1ull, ~0ull, dext, nullptr);
-      k_tail_engine<uint64_t><<<grid_for(M, B), B, 0, stream>>>(
-          M, ks, vs, tbits, S, views_latest(), 1ull, ~0ull, bdot, 0);
+      // every replica's KeyDeps over its arrival log, in chunks: chunk c
+      // takes the c-th slice of each log (a replica's slices stay in arrival
+      // order, so the latest table carries each (replica, key) segment across
+      // chunks exactly as one sequential pass).  A chunk's commands sit in a
+      // window of the stream, so its dependency scatter stays in a cache-
+      // sized slice of the dependency array.
+      const uint32_t np = desc.nproc;
+      FH_CHECK(np <= uint32_t(kMaxLogs), FH_ENOTIMPL, "replica views: nproc <= 16");
+      const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
+      static const size_t chunk_elems = [] {
+        const char *e = getenv("FH_VIEW_CHUNK");
+        return e ? size_t(std::max(1L, atol(e))) : size_t(12) << 20;
+      }();
+      const uint32_t nch = uint32_t(std::max<size_t>(1, (size_t(M) + chunk_elems - 1) / chunk_elems));
+      const int bits = bits_for(uint64_t(np + 1) * key_space);
+      const uint32_t *bent = lent.get() + b * size_t(n) * fq;
+      for (uint32_t c = 0; c < nch; c++) {
+        LogChunk lc;
+        lc.cum[0] = 0;
+        for (uint32_t r = 0; r < np; r++) {
+          const uint64_t len = bl[r + 1] - bl[r];
+          const uint32_t q0 = uint32_t(len * c / nch), q1 = uint32_t(len * (c + 1) / nch);
+          lc.first[r] = bl[r] + q0;
+          lc.cum[r + 1] = lc.cum[r] + (q1 - q0) * k;
+        }
+        const uint32_t Mc = lc.cum[np];
+        uint32_t *lk = sk32a.ensure(Mc + 1), *lv = sva.ensure(Mc + 1);
+        probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys,
+                      dim3(grid_for(Mc, B)), dim3(B), stream, Mc, k, fq, np, lc, bent, bkey,
+                      uint32_t(key_space), lk, lv);
+        uint32_t *ks = nullptr;
+        sort_pairs<uint32_t>(lk, lv, lk, lv, sk32b.ensure(Mc + 1), svb.ensure(Mc + 1), Mc, bits,
+                             sort_ws, stream, &ks, &vs);
+        // heads read the latest table, tails then make the chunk's last
+        // commands the latest (command-log references)
+        probed_launch("prev_engine", double(Mc) * (4.0 + 4.0 + 8.0), k_prev_engine<uint32_t>,
+                      dim3(grid_for(Mc, B)), dim3(B), stream, Mc, (const uint32_t *)ks,
+                      (const uint32_t *)vs, 0, S, (const uint64_t *)views_latest(), 1ull, ~0ull,
+                      dext, (uint32_t *)nullptr);
+        k_tail_engine<uint32_t><<<grid_for(Mc, B), B, 0, stream>>>(
+            Mc, ks, vs, 0, S, views_latest(), 1ull, ~0ull, nullptr, bbase);
+      }
+      mark("keydeps_views");
     }
-    if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bproc, bdot, bbase);
+    if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bdot, bbase);
+    materialize(n, S, bdot);
     if (ms || profile) FH_HIP(hipEventRecord(ev1, stream));
     if (ms) {
       FH_HIP(hipEventSynchronize(ev1));
@@ -842,8 +1008,7 @@ struct EngineDevice {
   }
 
   void run_general(uint32_t n, uint32_t k, uint32_t fq, uint32_t S, uint32_t M, bool views,
-                   const uint32_t *bkey, const uint8_t *bproc, const uint64_t *bdot,
-                   uint64_t bbase) {
+                   const uint32_t *bkey, const uint64_t *bdot, uint64_t bbase) {
     const uint64_t *dcode = dep_ext.get();
     uint32_t *svid = sorted_vid.get();
     mark("keydeps_prev");
@@ -851,9 +1016,11 @@ struct EngineDevice {
     uint32_t *dcnt = dep_cnt.ensure(n + 1);
     uint32_t *dd = dst.ensure(M + 1);
     FH_HIP(hipMemsetAsync(scal.get(), 0, sizeof(uint32_t), stream));
-    k_cmd_engine<<<grid_for(n, B), B, 0, stream>>>(
-        n, S, bdot, dcode, (const uint64_t *)dot.get(), frontier.get(), ddot, dcnt, dd, nullptr,
-        scal.get(), views && S >= 8 ? edge_cnt.ensure(n + 1) : nullptr);
+    probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0), k_cmd_engine,
+                  dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot, dcode,
+                  (const uint64_t *)dot.get(), (const uint64_t *)frontier.get(), ddot, dcnt, dd,
+                  (uint8_t *)nullptr, scal.get(),
+                  views && S >= 8 ? edge_cnt.ensure(n + 1) : (uint32_t *)nullptr, bbase);
     mark("keydeps_union");
     const uint32_t *gdst = dd, *goff = nullptr;
     if (views && S >= 8) {  // measured: a win at S = 12 (C5), flat or worse at 3 and 6
@@ -893,10 +1060,58 @@ struct EngineDevice {
     FH_HIP(hipMemsetAsync(st + 256, 0, 512 * sizeof(unsigned long long), stream));
     k_src_stats<<<grid_for(n, B, 512), B, 0, stream>>>(n, bdot, st, st + 256,
                                                    reinterpret_cast<unsigned int *>(st + 512));
-    k_frontier_update<<<1, 256, 0, stream>>>(st, st + 256,
-                                             reinterpret_cast<unsigned int *>(st + 512),
-                                             frontier.get(), excount_ptr(), err.get());
+    k_frontier_update<<<1, 256, 0, stream>>>(st + 256, reinterpret_cast<unsigned int *>(st + 512),
+                                             frontier.get(), excount_ptr());
     mark("executed_clock");
+  }
+
+  // The run's outputs, materialised on the device before run() returns:
+  // committed deps as CSR of dots (o_dep_off, o_dep), SCC labels and
+  // execution ranks (o_label, o_rank), per-key offsets over the key space
+  // (key_offs) and the per-key execution sequences of dots (seq_dot).
+  // results() only copies them to the host.
+  void materialize(uint32_t n, uint32_t S, const uint64_t *bdot) {
+    uint32_t *off = o_dep_off.ensure(n + 1);
+    if (sv_fused) {
+      // one dependency slot per command: decode, count = slot used
+      S = 1;
+      k_sv_unpermute<<<grid_for(n, B), B, 0, stream>>>(n, sv_vs, dep_ext.get(), bdot, dot.get(),
+                                                        dep_dot.ensure(n + 1));
+      k_cnt_nonzero<<<grid_for(n, B), B, 0, stream>>>(n, dep_dot.get(), dep_cnt.ensure(n + 1));
+    }
+    exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
+    k_compact_deps<<<grid_for(n, B), B, 0, stream>>>(n, S, dep_dot.get(), off,
+                                                      o_dep.ensure(size_t(n) * S + 1));
+    mark("out_deps");
+    if (gout.trivial) {
+      // singleton SCCs in arrival order: label = own dot, rank = position
+      uint64_t *lb = lab.ensure(n + 1);
+      uint32_t *rk = rank_tmp.ensure(n + 1);
+      k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, bdot, lb, rk);
+      o_label = lb;
+      o_rank = rk;
+    } else {
+      o_label = gout.scc_label;
+      o_rank = gout.exec_rank;
+    }
+    // per-key offsets over the ascending key space (histogram + scan)
+    o_nelem = gout.nelem;
+    uint32_t *h = key_hist.ensure(key_space + 1);
+    uint32_t *o = key_offs.ensure(key_space + 2);
+    FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
+    k_key_hist<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, h);
+    exclusive_scan_u32(h, o, key_space, scan_ws, stream);
+    uint64_t *sq = seq_dot.ensure(o_nelem + 1);
+    if (sv_fused && bucket_order) {
+      // key-grouped runs -> ascending keys
+      uint32_t *hp = headpos.ensure(key_space + 1);
+      k_run_heads<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
+      k_run_scatter<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, gout.pk_vid, hp,
+                                                             o, bdot, sq);
+    } else if (sv_fused) {  // (sorted keys, sorted vids): gather the dots
+      k_seq_dots<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_vid, bdot, sq);
+    }  // else: run_general wrote seq_dot
+    mark("out_per_key");
   }
 
   void collect_times() {
@@ -909,95 +1124,39 @@ struct EngineDevice {
     }
   }
 
-  void check_err() {
-    uint32_t e = 0;
-    FH_HIP(hipMemcpyAsync(&e, err.get(), sizeof(e), hipMemcpyDeviceToHost, stream));
-    if (excount.get()) {
-      uint64_t f[256], c[256];
-      FH_HIP(hipMemcpyAsync(f, frontier.get(), sizeof(f), hipMemcpyDeviceToHost, stream));
-      FH_HIP(hipMemcpyAsync(c, excount.get(), sizeof(c), hipMemcpyDeviceToHost, stream));
-      FH_HIP(hipStreamSynchronize(stream));
-      for (int s = 0; s < 256; s++)
-        if (c[s] != f[s]) e = 1;  // executed set not contiguous from 1
-    }
-    FH_HIP(hipStreamSynchronize(stream));
-    FH_CHECK(e == 0, FH_ENOTIMPL,
-             "executed clock: non-contiguous executed dots per process (exceptions not supported "
-             "by the fused engine)");
-  }
-
+  // results of the last run (materialised by run()): device -> host copies
   void results(uint32_t *dep_off, uint64_t *dep_out, size_t dep_cap, size_t *dep_len,
                uint64_t *scc_label, uint32_t *exec_rank, uint32_t *key_off, uint64_t *key_seq) {
     FH_HIP(hipSetDevice(device));
+    FH_CHECK(staged && cursor > 0, FH_EINVAL, "no run to read results from");
     FH_HIP(hipStreamSynchronize(stream));
-    check_err();
-    const uint32_t n = uint32_t(desc.n), k = desc.keys_per_cmd;
-    const uint32_t S = (desc.views ? desc.views : 1) * k;
+    const uint32_t n = uint32_t(desc.n);
     if (dep_off || dep_out || dep_len) {
-      uint32_t *off = u32tmp.ensure(n + 1);
-      if (sv_fused) {  // one dependency slot per command: decode, count = slot used
-        k_sv_unpermute<<<grid_for(n, B), B, 0, stream>>>(n, sv_vs, dep_ext.get(),
-                                                          dot.get() + stage_base + last * n,
-                                                          dot.get(), dep_dot.ensure(n + 1));
-        k_cnt_nonzero<<<grid_for(n, B), B, 0, stream>>>(n, dep_dot.get(), dep_cnt.ensure(n + 1));
-      }
-      exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
       uint32_t total = 0;
-      FH_HIP(hipMemcpyAsync(&total, off + n, sizeof(total), hipMemcpyDeviceToHost, stream));
+      FH_HIP(hipMemcpyAsync(&total, o_dep_off.get() + n, sizeof(total), hipMemcpyDeviceToHost,
+                            stream));
       FH_HIP(hipStreamSynchronize(stream));
       if (dep_len) *dep_len = total;
+      if (dep_out) FH_CHECK(dep_cap >= total, FH_ECAP, "dep output capacity too small");
       if (dep_off)
-        FH_HIP(hipMemcpyAsync(dep_off, off, (n + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                              stream));
-      if (dep_out) {
-        FH_CHECK(dep_cap >= total, FH_ECAP, "dep output capacity too small");
-        uint64_t *c = sk64a.ensure(total + 1);
-        k_compact_deps<<<grid_for(n, B), B, 0, stream>>>(n, S, dep_dot.get(), off, c);
-        FH_HIP(hipMemcpyAsync(dep_out, c, size_t(total) * sizeof(uint64_t),
+        FH_HIP(hipMemcpyAsync(dep_off, o_dep_off.get(), (n + 1) * sizeof(uint32_t),
                               hipMemcpyDeviceToHost, stream));
-      }
-    }
-    if (scc_label || exec_rank) {
-      uint64_t *lb = gout.scc_label;
-      uint32_t *rk = gout.exec_rank;
-      if (gout.trivial) {
-        lb = lab.ensure(n + 1);
-        rk = rank_tmp.ensure(n + 1);
-        k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, dot.get() + stage_base + last * n, lb, rk);
-      }
-      if (scc_label)
-        FH_HIP(hipMemcpyAsync(scc_label, lb, size_t(n) * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                              stream));
-      if (exec_rank)
-        FH_HIP(hipMemcpyAsync(exec_rank, rk, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                              stream));
-    }
-    if (key_off || key_seq) {
-      // per-key offsets over the ascending key space (histogram + scan)
-      uint32_t *h = key_hist.ensure(key_space + 1);
-      uint32_t *o = key_offs.ensure(key_space + 2);
-      FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
-      k_key_hist<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_key, h);
-      exclusive_scan_u32(h, o, key_space, scan_ws, stream);
-      if (key_off)
-        FH_HIP(hipMemcpyAsync(key_off, o, (key_space + 1) * sizeof(uint32_t),
+      if (dep_out)
+        FH_HIP(hipMemcpyAsync(dep_out, o_dep.get(), size_t(total) * sizeof(uint64_t),
                               hipMemcpyDeviceToHost, stream));
-      if (key_seq) {
-        uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
-        const uint64_t *bd = dot.get() + stage_base + last * n;
-        if (sv_fused && bucket_order) {
-          // key-grouped runs -> ascending keys
-          uint32_t *hp = headpos.ensure(key_space + 1);
-          k_run_heads<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_key, hp);
-          k_run_scatter<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_key,
-                                                                    gout.pk_vid, hp, o, bd, sq);
-        } else if (sv_fused) {  // (sorted keys, sorted vids): gather the dots
-          k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, bd, sq);
-        }
-        FH_HIP(hipMemcpyAsync(key_seq, sq, size_t(gout.nelem) * sizeof(uint64_t),
-                              hipMemcpyDeviceToHost, stream));
-      }
     }
+    if (scc_label)
+      FH_HIP(hipMemcpyAsync(scc_label, o_label, size_t(n) * sizeof(uint64_t),
+                            hipMemcpyDeviceToHost, stream));
+    if (exec_rank)
+      FH_HIP(hipMemcpyAsync(exec_rank, o_rank, size_t(n) * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost, stream));
+    if (key_off)
+      FH_HIP(hipMemcpyAsync(key_off, key_offs.get(), (key_space + 1) * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost, stream));
+    if (key_seq)
+      FH_HIP(hipMemcpyAsync(key_seq, seq_dot.get(), size_t(o_nelem) * sizeof(uint64_t),
+                            hipMemcpyDeviceToHost, stream));
     FH_HIP(hipStreamSynchronize(stream));
   }
 };
@@ -1045,6 +1204,23 @@ fh_status fh_engine_stage_many(fh_engine *h, const fh_stream_desc *desc, size_t 
   FH_API_BEGIN
   FH_CHECK(h && desc, FH_EINVAL, "null argument");
   h->dev.stage(*desc, nbatches, dot, key_id, fq_proc, fq_time);
+  FH_API_END
+}
+
+fh_status fh_engine_stage_logs(fh_engine *h, const fh_stream_desc *desc, size_t nbatches,
+                               const uint64_t *dot, const uint64_t *key_id,
+                               const uint64_t *log_off, const uint32_t *log_cmd) {
+  FH_API_BEGIN
+  FH_CHECK(h && desc, FH_EINVAL, "null argument");
+  FH_CHECK(desc->views >= 1, FH_EINVAL, "stage_logs: views must be >= 1");
+  h->dev.stage_logs(*desc, nbatches, dot, key_id, log_off, log_cmd);
+  FH_API_END
+}
+
+fh_status fh_engine_rewind(fh_engine *h) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.rewind();
   FH_API_END
 }
 

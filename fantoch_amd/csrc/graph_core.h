@@ -85,6 +85,9 @@ struct GraphCore {
   uint64_t nedges = 0;
   DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c;
   DBuf<uint8_t> blocked;
+  DBuf<uint32_t> t_h, t_rank, t_cnt, t_start;
+  DBuf<uint64_t> t_prof;  // tile path: ready time, group rank/count/start
+  uint32_t dbg_tile_fail = 0, dbg_tile_ok = 0;
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)
   bool profile = false;
   uint32_t dbg_rounds = 0, dbg_hprop = 0, dbg_reach = 0;  // FH_GRAPH_DEBUG counters
@@ -107,6 +110,11 @@ struct GraphCore {
   // false: restricted candidates too many, nothing done
   bool coloring_fallback(const GraphInput &in, uint32_t recent_iter);
   void build_orders(const GraphInput &in, GraphOutput &out);
+  void build_labels(const GraphInput &in, GraphOutput &out);
+  void build_per_key(const GraphInput &in, GraphOutput &out);
+  // tile-local path (graph_tile.hip): false = certificate failed, nothing set
+  bool tiles_eligible(const GraphInput &in) const;
+  bool run_tiles(const GraphInput &in, GraphOutput &out);
 };
 
 }  // namespace fh

@@ -793,10 +793,9 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
   return true;
 }
 
-void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
+// SCC labels: min dot of each SCC (rep = any common member per SCC)
+void GraphCore::build_labels(const GraphInput &in, GraphOutput &out) {
   const uint32_t V = in.V;
-  const int bv = bits_for(uint64_t(V) + 1);
-  // SCC labels: min dot of each SCC
   uint64_t *lab = label.ensure(V);
   uint64_t *lab_out = tmp64c.ensure(V);
   k_label_init<<<grid_for(V, B), B, 0, stream>>>(V, lab);
@@ -804,6 +803,12 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   k_label_bcast<<<grid_for(V, B), B, 0, stream>>>(V, rep.get(), lab, lab_out);
   out.scc_label = lab_out;
   mark("scc_label");
+}
+
+void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
+  const uint32_t V = in.V;
+  const int bv = bits_for(uint64_t(V) + 1);
+  build_labels(in, out);
   // dot rank (intra-SCC order is dot order)
   uint64_t *ka = tmp64a.ensure(V), *kb = tmp64b.ensure(V);
   uint32_t *va = tmp32a.ensure(V), *vb = tmp32b.ensure(V);
@@ -846,8 +851,14 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   out.nexec = nexec;
   out.npending = V - nexec;
   mark("exec_order");
+  build_per_key(in, out);
+}
+
+// per-key sequence: elements in exec order, stable-sorted by key
+void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
   if (!in.want_per_key) return;
-  // per-key sequence: elements in exec order, stable-sorted by key
+  const uint32_t nexec = out.nexec;
+  const uint32_t *ord = out.exec_order;
   uint32_t *ec = cnt.ensure(nexec + 1);
   uint32_t *ep = pos.ensure(nexec + 1);
   k_elem_counts<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, in.k, in.key_off, ec);
@@ -887,6 +898,16 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     FH_HIP(hipMemcpyAsync(&e, in.off + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     FH_HIP(hipStreamSynchronize(stream));
     nedges = e;
+  }
+  // replica views with a bounded reorder window: everything in tile-local LDS
+  // passes, certified (graph_tile.hip); else the global path below
+  if (!in.no_forward_hint && tiles_eligible(in)) {
+    if (run_tiles(in, out)) {
+      dbg_tile_ok++;
+      build_labels(in, out);
+      build_per_key(in, out);
+      return;
+    }
   }
   pending_closure(in, out);
   // trivial: nothing pending and every edge points to an earlier arrival ->

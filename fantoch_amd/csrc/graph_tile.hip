@@ -1,0 +1,548 @@
+// graph_tile.hip -- tile-local SCC + execution order for graphs whose
+// structure is position-local (replica views with a bounded reorder window).
+//
+// Reference semantics (graph_core.h): the incremental DependencyGraph +
+// TarjanSCCFinder (fantoch_ps/src/executor/graph/mod.rs:215-644,
+// tarjan.rs:98-319) executes SCC S when the last vertex it reaches arrives:
+// its ready time H(S) = the maximum arrival position reachable from S.  SCCs
+// that become ready together run deps first (Tarjan pops them in reverse
+// topological order), members of an SCC in dot order (tarjan.rs:14-15).  The
+// execution order is therefore sorted by (H, depth, tie, dot) where depth is
+// the longest dependency path to the group's root SCC among the SCCs sharing
+// H, and tie separates unconnected SCCs (min member vid).
+//
+// Locality certificate.  Let excess(v) = H(v) - v.  If every vertex has
+// excess < R0 and every forward edge (a dependency that arrived later) spans
+// fewer than L - R0 positions, with L = 2·R0, then for a tile core [a, b) and
+// its context [a - L, b + L):
+//  * a path from any vertex of [a - R0, b + R0) that leaves the context
+//    below can never climb back (that would need a climb > L - R0 >= R0),
+//    and one cannot leave above (H(v) < v + R0 <= b + L);
+//  * so H, the SCCs, the depths and the ready groups G_t = {v : H(v) = t}
+//    of every group with a member in the core (G_t lies in [t - R0, t]) are
+//    the same in the context subgraph as in the whole graph.
+// Conversely if some vertex has excess >= R0, take a shortest path climbing
+// >= R0: it stays in [x, x + R0 + span) and x's own tile sees it (or a long
+// forward edge).  Each tile checks both conditions for its core vertices; any
+// failure sends the batch to the global path (graph_core.hip).
+//
+// Per tile, in LDS (1024 threads, context <= 8192 vertices, u16 local ids):
+//  1. context edges (in-batch deps with both ends in the context);
+//  2. H by max-propagation sweeps to the fixpoint;
+//  3. certificate for the core;
+//  4. SCCs: round 1 = the members of each group reachable from its root t
+//     (H(t) = t) inside the group; later rounds recompute H over the vertices
+//     left and repeat (a group holds few SCCs: the measured C4 maximum is 4);
+//  5. SCC slot = min member; depth by max-propagation over same-group edges;
+//  6. ready groups: count of each core root's group, and each core vertex's
+//     rank in its group by (depth, min member, dot), scanning the compacted
+//     list of raised vertices (H(v) > v) of the group's window.
+// Global epilogue (graph_core.hip): exclusive scan of the group counts gives
+// each group's first execution position, exec_rank = start[H] + rank.
+#include <cstdio>
+#include <cstdlib>
+
+#include "graph_core.h"
+
+namespace fh {
+namespace {
+
+constexpr int kTileThreads = 1024;
+constexpr int kTileC = 10240;  // max context vertices (LDS: 15 B per vertex)
+constexpr uint16_t kNone = 0xFFFF;
+
+// exclusive scan of one value per thread over the 1024-thread block
+__device__ __forceinline__ uint32_t tile_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kTileThreads / 64; i++) {
+    const uint32_t c = s_w[i];
+    if (i < w) pre += c;
+    tot += c;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+// 16-bit LDS min / max through a CAS on the aligned 32-bit word
+__device__ __forceinline__ void lds_min_u16(uint16_t *p, uint16_t v) {
+  uint32_t *w = reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
+  const int sh = int(reinterpret_cast<uintptr_t>(p) & 2) * 8;
+  uint32_t old = *w;
+  for (;;) {
+    if (uint16_t(old >> sh) <= v) return;
+    const uint32_t nw = (old & ~(0xFFFFu << sh)) | (uint32_t(v) << sh);
+    const uint32_t prev = atomicCAS(w, old, nw);
+    if (prev == old) return;
+    old = prev;
+  }
+}
+__device__ __forceinline__ bool lds_max_u16(uint16_t *p, uint16_t v) {
+  uint32_t *w = reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
+  const int sh = int(reinterpret_cast<uintptr_t>(p) & 2) * 8;
+  uint32_t old = *w;
+  for (;;) {
+    if (uint16_t(old >> sh) >= v) return false;
+    const uint32_t nw = (old & ~(0xFFFFu << sh)) | (uint32_t(v) << sh);
+    const uint32_t prev = atomicCAS(w, old, nw);
+    if (prev == old) return true;
+    old = prev;
+  }
+}
+
+__device__ __forceinline__ uint16_t lds_xchg_u16(uint16_t *p, uint16_t v) {
+  uint32_t *w = reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
+  const int sh = int(reinterpret_cast<uintptr_t>(p) & 2) * 8;
+  uint32_t old = *w;
+  for (;;) {
+    const uint32_t nw = (old & ~(0xFFFFu << sh)) | (uint32_t(v) << sh);
+    const uint32_t prev = atomicCAS(w, old, nw);
+    if (prev == old) return uint16_t(old >> sh);
+    old = prev;
+  }
+}
+
+struct TileOut {
+  uint32_t *rep;     // [V] global vid of the SCC's min member
+  uint32_t *hgrp;    // [V] ready time H (a vertex position)
+  uint32_t *grank;   // [V] rank inside the ready group
+  uint32_t *gcount;  // [V] size of the group rooted at v (0 if H(v) != v)
+  uint32_t *stat;    // [0] failed tiles, [1] max core local excess,
+                     // [2] core vertices over R0, [3] long forward edges,
+                     // [4] max H sweeps, [5] max SCC rounds
+  const uint8_t *redo;  // [tiles] or null: only tiles with redo[t] run
+  unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
+};
+
+// One tile: core [a, a + T), context [a - L, a + T + L) with L = 2·R0 and
+// T + 2L <= kTileC.
+template <int S, int R0, int T>
+__global__ void __launch_bounds__(kTileThreads)
+    k_graph_tile(uint32_t V, const uint32_t *__restrict__ dst, const uint64_t *__restrict__ dot,
+                 TileOut out) {
+  constexpr int L = 2 * R0;
+  static_assert(T + 2 * L <= kTileC, "tile context exceeds LDS");
+  if (out.redo && !out.redo[blockIdx.x]) return;
+  __shared__ uint16_t eL[S][kTileC];
+  __shared__ uint16_t sH[kTileC];
+  __shared__ uint16_t sR[kTileC];
+  __shared__ uint8_t sF[kTileC];
+  __shared__ uint16_t W1[kTileC];
+  __shared__ uint16_t W2[kTileC];
+  __shared__ uint32_t s_w[kTileThreads / 64];
+  __shared__ uint32_t s_ch[3];
+  __shared__ uint32_t s_fail, s_maxex, s_over, s_long;
+
+  const int tid = threadIdx.x;
+  uint64_t t_last = wall_clock64();
+  auto phase = [&](int i) {  // after a barrier: thread 0 accounts the phase
+    if (out.prof && tid == 0) {
+      const uint64_t now = wall_clock64();
+      atomicAdd(&out.prof[i], (unsigned long long)(now - t_last));
+      t_last = now;
+    }
+  };
+  const uint32_t a = blockIdx.x * uint32_t(T);
+  const uint32_t b = min(V, a + uint32_t(T));
+  const uint32_t lo = a > uint32_t(L) ? a - L : 0u;
+  const uint32_t hi = min(V, b + uint32_t(L));
+  const int C = int(hi - lo);
+  const int ca = int(a - lo), cb = int(b - lo);  // core, local
+  if (tid < 3) s_ch[tid] = 0;
+  if (tid == 0) s_fail = s_maxex = s_over = s_long = 0;
+
+  // 1. context edges; certificate part 2: forward spans of core vertices
+  uint32_t nlong = 0;
+  for (int x = tid; x < C; x += kTileThreads) {
+    const uint32_t v = lo + x;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint32_t u = dst[size_t(v) * S + s];
+      uint16_t l = kNone;
+      if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
+      if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
+      eL[s][x] = l;
+    }
+    sH[x] = uint16_t(x);
+  }
+  __syncthreads();
+  phase(0);
+  if (nlong) atomicAdd(&s_long, nlong);
+
+  // sweep helper: body(x) returns true if it changed something; loops until
+  // a sweep changes nothing (rotating flags: one barrier per sweep)
+  auto sweeps = [&](auto body, int n, const uint16_t *list) {
+    int it = 0;
+    for (;; it++) {
+      bool ch = false;
+      for (int i = tid; i < n; i += kTileThreads) ch |= body(list ? int(list[i]) : i);
+      if (ch) s_ch[it % 3] = 1;
+      if (tid == 0) s_ch[(it + 1) % 3] = 0;
+      __syncthreads();
+      if (!s_ch[it % 3]) break;
+    }
+    __syncthreads();
+    if (tid < 3) s_ch[tid] = 0;
+    __syncthreads();
+    return it + 1;
+  };
+
+  // 2. H: max arrival position reachable (context subgraph).  H(x) is a
+  // vertex x reaches, so H(H(x)) is reachable too: pointer jumping collapses
+  // chains of forward dependencies in logarithmically many sweeps.
+  const int hs = sweeps(
+      [&](int x) {
+        uint32_t h = sH[x];
+        const uint32_t h0 = h;
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+          const uint16_t y = eL[s][x];
+          if (y != kNone) h = max(h, uint32_t(sH[y]));
+        }
+        h = max(h, uint32_t(sH[h]));
+        if (h > h0) {
+          sH[x] = uint16_t(h);
+          return true;
+        }
+        return false;
+      },
+      C, nullptr);
+  phase(1);
+
+  // 3. certificate part 1: core excess < R0
+  {
+    uint32_t mx = 0, over = 0;
+    for (int x = ca + tid; x < cb; x += kTileThreads) {
+      const uint32_t ex = uint32_t(sH[x]) - uint32_t(x);
+      mx = max(mx, ex);
+      over += ex >= uint32_t(R0);
+    }
+    if (mx) atomicMax(&s_maxex, mx);
+    if (over) atomicAdd(&s_over, over);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    atomicMax(&out.stat[1], s_maxex);
+    if (s_over) atomicAdd(&out.stat[2], s_over);
+    if (s_long) atomicAdd(&out.stat[3], s_long);
+    atomicMax(&out.stat[4], uint32_t(hs));
+    if (s_over || s_long) atomicAdd(&out.stat[0], 1u);
+  }
+  if (s_over || s_long) return;
+
+  // 4. raised vertices (H(v) > v), ascending, into W2 (an ordered
+  // compaction: each thread takes consecutive positions).  Every vertex of a
+  // multi-vertex ready group except its root is raised, so the later phases
+  // work on this list only.  sF bits: 1 reached, 2 processed, 4 the group
+  // rooted here has raised members.
+  constexpr int kPer = kTileC / kTileThreads;
+  uint32_t nraised = 0;
+  for (int x = tid; x < C; x += kTileThreads) {
+    sF[x] = 0;
+    sR[x] = kNone;
+  }
+  __syncthreads();
+  {
+    uint32_t mine = 0;
+    const int x0 = tid * kPer;
+    for (int x = x0; x < x0 + kPer && x < C; x++) mine += sH[x] > x;
+    uint32_t o = tile_scan(mine, s_w, &nraised);
+    for (int x = x0; x < x0 + kPer && x < C; x++)
+      if (sH[x] > x) W2[o++] = uint16_t(x);
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < nraised; i += kTileThreads) sF[sH[W2[i]]] = 4;
+  __syncthreads();
+  phase(2);
+
+  // 5. SCCs.  Round 1: the members of each ready group reachable from its
+  // root t (H(t) = t) inside the group are t's SCC.  Roots push once; then
+  // the raised vertices reached push until nothing new is reached.
+  for (int x = tid; x < C; x += kTileThreads) {
+    if (sH[x] != x) continue;
+    sF[x] |= 3;
+    sR[x] = uint16_t(x);
+    if (!(sF[x] & 4)) continue;  // no raised member: a singleton group
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint16_t y = eL[s][x];
+      if (y != kNone && sH[y] == x) sF[y] |= 1;
+    }
+  }
+  __syncthreads();
+  auto reach = [&](const uint16_t *grp) {
+    // grp: the group label array (sH in round 1, W1 later); only unassigned
+    // (sR == kNone) raised vertices take part
+    sweeps(
+        [&](int i) {
+          const uint16_t x = W2[i];
+          const uint8_t f = sF[x];
+          if ((f & 3) != 1 || sR[x] != kNone) return false;
+          sF[x] = f | 2;
+          const uint16_t g = grp[x];
+#pragma unroll
+          for (int s = 0; s < S; s++) {
+            const uint16_t y = eL[s][x];
+            if (y != kNone && sR[y] == kNone && grp[y] == g) sF[y] |= 1;
+          }
+          return true;
+        },
+        int(nraised), nullptr);
+  };
+  reach(sH);
+  // assign round 1; count the raised vertices left
+  uint32_t left = 0;
+  {
+    uint32_t mine = 0;
+    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+      const uint16_t x = W2[i];
+      if (sF[x] & 1)
+        sR[x] = sH[x];
+      else
+        mine++;
+    }
+    tile_scan(mine, s_w, &left);
+  }
+  phase(3);
+  // later rounds over the raised vertices left: H' over the unassigned
+  // subgraph (W1, pointer jumping), roots H'(x) = x, reach inside the H'
+  // group, assign
+  int round = 0;
+  for (; left; round++) {
+    if (round >= 64) {  // adversarial nesting: leave it to the global path
+      if (tid == 0) atomicAdd(&out.stat[0], 1u);
+      return;
+    }
+    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+      const uint16_t x = W2[i];
+      if (sR[x] == kNone) {
+        W1[x] = x;
+        sF[x] &= 4;
+      }
+    }
+    __syncthreads();
+    sweeps(
+        [&](int i) {
+          const uint16_t x = W2[i];
+          if (sR[x] != kNone) return false;
+          uint32_t h = W1[x];
+          const uint32_t h0 = h;
+#pragma unroll
+          for (int s = 0; s < S; s++) {
+            const uint16_t y = eL[s][x];
+            if (y != kNone && sR[y] == kNone) h = max(h, uint32_t(W1[y]));
+          }
+          h = max(h, uint32_t(W1[h]));
+          if (h > h0) {
+            W1[x] = uint16_t(h);
+            return true;
+          }
+          return false;
+        },
+        int(nraised), nullptr);
+    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+      const uint16_t x = W2[i];
+      if (sR[x] == kNone && W1[x] == x) sF[x] |= 1;
+    }
+    __syncthreads();
+    reach(W1);
+    uint32_t mine = 0;
+    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+      const uint16_t x = W2[i];
+      if (sR[x] != kNone) continue;
+      if (sF[x] & 1)
+        sR[x] = W1[x];  // (W1[x] is unassigned until this pass ends)
+      else
+        mine++;
+    }
+    __syncthreads();
+    tile_scan(mine, s_w, &left);
+  }
+  if (tid == 0 && round) atomicMax(&out.stat[5], uint32_t(round));
+
+  // 6. SCC slot = min member; depth over same-group edges (W1, per slot).
+  // Only raised vertices can have an edge to another SCC of their group (a
+  // root's same-group dependencies reach it back), so the sweeps run over W2.
+  for (int x = tid; x < C; x += kTileThreads) W1[x] = kNone;
+  __syncthreads();
+  for (int x = tid; x < C; x += kTileThreads) lds_min_u16(&W1[sR[x]], uint16_t(x));
+  __syncthreads();
+  for (int x = tid; x < C; x += kTileThreads) sR[x] = W1[sR[x]];
+  __syncthreads();
+  for (int x = tid; x < C; x += kTileThreads) W1[x] = 0;
+  __syncthreads();
+  sweeps(
+      [&](int i) {
+        const uint16_t x = W2[i];
+        const uint16_t r = sR[x], hx = sH[x];
+        uint32_t best = 0;
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+          const uint16_t y = eL[s][x];
+          if (y != kNone && sH[y] == hx) {
+            const uint16_t r2 = sR[y];
+            if (r2 != r) best = max(best, uint32_t(W1[r2]) + 1);
+          }
+        }
+        return best > W1[r] && lds_max_u16(&W1[r], uint16_t(best));
+      },
+      int(nraised), nullptr);
+  phase(4);
+
+  // 7. ready groups: member lists of the groups with raised members (head in
+  // eL[0], next in eL[1]: the edges are no longer needed), then each core
+  // vertex's rank in its group by (depth, min member, dot) and each core
+  // root's group size
+  uint16_t *head = eL[0], *next = eL[1];
+  for (int x = tid; x < C; x += kTileThreads) head[x] = kNone;
+  __syncthreads();
+  for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+    const uint16_t y = W2[i];
+    next[y] = lds_xchg_u16(&head[sH[y]], y);
+  }
+  __syncthreads();
+  for (int x = ca + tid; x < cb; x += kTileThreads) {
+    const uint32_t v = lo + x;
+    const uint16_t t = sH[x];
+    uint32_t cnt = 0, rk = 0;
+    if (sF[t] & 4) {
+      const uint32_t dx = W1[sR[x]], mx = sR[x];
+      uint64_t dotx = 0;
+      bool have_dot = false;
+      auto cmp = [&](uint32_t y) {
+        const uint32_t dy = W1[sR[y]], my = sR[y];
+        if (dy != dx) return dy < dx;
+        if (my != mx) return my < mx;
+        if (!have_dot) {
+          dotx = dot[v];
+          have_dot = true;
+        }
+        return dot[lo + y] < dotx;
+      };
+      if (t != uint32_t(x)) rk += cmp(t);
+      for (uint16_t y = head[t]; y != kNone; y = next[y]) {
+        cnt++;
+        if (y != uint32_t(x)) rk += cmp(y);
+      }
+    }
+    out.rep[v] = lo + sR[x];
+    out.hgrp[v] = lo + t;
+    out.grank[v] = rk;
+    out.gcount[v] = t == uint32_t(x) ? cnt + 1 : 0u;
+  }
+  __syncthreads();
+  phase(5);
+}
+
+__global__ void k_exec_from_groups(uint32_t V, const uint32_t *__restrict__ hgrp,
+                                   const uint32_t *__restrict__ grank,
+                                   const uint32_t *__restrict__ gstart, uint32_t *__restrict__ rank,
+                                   uint32_t *__restrict__ order) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) {
+    const uint32_t r = gstart[hgrp[v]] + grank[v];
+    rank[v] = r;
+    order[r] = v;
+  }
+}
+
+}  // namespace
+
+template <int R0, int T>
+static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint64_t *dot,
+                         const TileOut &to, hipStream_t stream) {
+  const uint32_t tiles = (V + T - 1) / T;
+  // algorithmic bytes: read the vertex's S edge slots and write rep, H, rank
+  // and group count (the context halo re-reads are overhead, not algorithmic)
+  const double bytes = double(V) * (4.0 * S + 16.0);
+  switch (S) {
+    case 2:
+      probed_launch("graph_tile", bytes, k_graph_tile<2, R0, T>, dim3(tiles), dim3(kTileThreads),
+                    stream, V, dst, dot, to);
+      break;
+    default:
+      probed_launch("graph_tile", bytes, k_graph_tile<3, R0, T>, dim3(tiles), dim3(kTileThreads),
+                    stream, V, dst, dot, to);
+      break;
+  }
+}
+
+bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
+  const uint32_t V = in.V;
+  uint32_t *stat = scalars.get() + 24;
+  TileOut to;
+  to.rep = rep.ensure(V + 1);
+  to.hgrp = t_h.ensure(V + 1);
+  to.grank = t_rank.ensure(V + 1);
+  to.gcount = t_cnt.ensure(V + 1);
+  to.stat = stat;
+  to.redo = nullptr;
+  static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
+  to.prof = nullptr;
+  if (debug) {
+    to.prof = reinterpret_cast<unsigned long long *>(t_prof.ensure(16));
+    FH_HIP(hipMemsetAsync(to.prof, 0, 8 * sizeof(unsigned long long), stream));
+  }
+  // certified reach bounds, tried in order: R0 = 1536 with 4096-vertex cores,
+  // then R0 = 2048 with 2048-vertex cores (each a context of <= 10240)
+  bool ok = false;
+  for (int level = 0; level < 2 && !ok; level++) {
+    FH_HIP(hipMemsetAsync(stat, 0, 6 * sizeof(uint32_t), stream));
+    if (level == 0)
+      launch_tiles<1536, 4096>(V, in.stride, in.dst, in.dot, to, stream);
+    else
+      launch_tiles<2048, 2048>(V, in.stride, in.dst, in.dot, to, stream);
+    uint32_t st[6];
+    fetch_u32(stat, st, 6, stream);
+    ok = st[0] == 0;
+    if (debug)
+      fprintf(stderr,
+              "fh graph_tile: V=%u level=%d failed_tiles=%u max_excess=%u over=%u long_fwd=%u "
+              "max_sweeps=%u max_rounds=%u\n",
+              V, level, st[0], st[1], st[2], st[3], st[4], st[5]);
+  }
+  if (debug) {
+    unsigned long long pr[8];
+    FH_HIP(hipMemcpyAsync(pr, to.prof, sizeof(pr), hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    // wall_clock64 runs at 100 MHz on gfx9: ticks * 10 ns, per tile average
+    const double tiles = double((V + 4095) / 4096);
+    fprintf(stderr, "fh graph_tile phases (us per tile): load %.1f H %.1f raised %.1f reach1 %.1f "
+            "rounds+depth %.1f rank %.1f\n", pr[0] * 0.01 / tiles, pr[1] * 0.01 / tiles,
+            pr[2] * 0.01 / tiles, pr[3] * 0.01 / tiles, pr[4] * 0.01 / tiles, pr[5] * 0.01 / tiles);
+  }
+  mark("graph_tile");
+  if (!ok) {
+    dbg_tile_fail++;
+    return false;
+  }
+  // execution order: groups in ready-time order, ranks inside a group
+  uint32_t *gs = t_start.ensure(V + 1);
+  exclusive_scan_u32(t_cnt.get(), gs, V, scan_ws, stream);
+  uint32_t *er = tmp32d.ensure(V + 1);
+  uint32_t *ord = order.ensure(V + 1);
+  k_exec_from_groups<<<grid_for(V, 256), 256, 0, stream>>>(V, t_h.get(), t_rank.get(), gs, er, ord);
+  out.exec_order = ord;
+  out.exec_rank = er;
+  out.nexec = V;
+  out.npending = 0;
+  out.rep = rep.get();
+  mark("exec_order");
+  return true;
+}
+
+bool GraphCore::tiles_eligible(const GraphInput &in) const {
+  return !in.off && !in.blocked0 && in.stride >= 2 && in.stride <= 3 && in.V >= 1 &&
+         !getenv("FH_NO_TILES");
+}
+
+}  // namespace fh

@@ -179,10 +179,160 @@ void gen_range(const fh_workload &w, const Alias *za, uint64_t first, size_t lo,
   }
 }
 
+// Replica `r` (process r + 1) sees member j of command i with
+// j = (r - (p_i - 1)) mod n when j < views, at time (i + d)·W + d (gen_range).
+// Its arrival order is (T = i + d, d) ascending: a counting sort over the
+// bucket T, filled in decreasing i so that within a bucket d ascends.
+uint32_t member_delay(const fh_workload &w, uint64_t i, uint32_t j) {
+  const uint64_t W = w.window ? w.window : 1;
+  return j == 0 ? 0u : uint32_t(rnd(w.seed, i, 1000 + j) % W);
+}
+
+// `keep` (may be null): batch-local index of each command in the output, or
+// ~0u for commands left out (a key shard of the stream)
+void gen_log(const fh_workload &w, uint64_t first, size_t count, uint32_t r, uint32_t *out,
+             size_t cap, const uint32_t *keep = nullptr) {
+  const uint64_t W = w.window ? w.window : 1;
+  std::vector<uint32_t> cnt(count + W + 1, 0);
+  auto member = [&](size_t c, uint32_t *j) {
+    if (keep && keep[c] == ~0u) return false;
+    const uint64_t i = first + c;
+    const uint32_t p = uint32_t(i % w.n);  // p_i - 1
+    *j = (r + w.n - p) % w.n;
+    return *j < w.views;
+  };
+  for (size_t c = 0; c < count; c++) {
+    uint32_t j;
+    if (member(c, &j)) cnt[c + member_delay(w, first + c, j) + 1]++;
+  }
+  for (size_t t = 1; t < cnt.size(); t++) cnt[t] += cnt[t - 1];
+  FH_CHECK(cnt.back() <= cap, FH_EINVARIANT, "log capacity");
+  for (size_t c = count; c-- > 0;) {
+    uint32_t j;
+    if (member(c, &j)) out[cnt[c + member_delay(w, first + c, j)]++] = keep ? keep[c] : uint32_t(c);
+  }
+}
+
+template <class F>
+void parallel_chunks(size_t count, F f) {
+  size_t threads = std::min<size_t>(16, std::max<size_t>(1, count / (1 << 16)));
+  unsigned hc = std::thread::hardware_concurrency();
+  if (hc) threads = std::min<size_t>(threads, hc);
+  std::vector<std::thread> ts;
+  const size_t chunk = (count + threads - 1) / threads;
+  for (size_t t = 0; t < threads; t++) {
+    const size_t lo = t * chunk, hi = std::min(count, lo + chunk);
+    if (lo >= hi) break;
+    ts.emplace_back(f, t, lo, hi);
+  }
+  for (auto &t : ts) t.join();
+}
+
 }  // namespace
 }  // namespace fh
 
 extern "C" {
+
+fh_status fh_workload_generate_shard(const fh_workload *w, uint64_t first, size_t count,
+                                     uint32_t nshards, uint32_t shard, size_t *n_out,
+                                     uint64_t *dot, uint64_t *key_id, uint64_t *log_off,
+                                     uint32_t *log_cmd) {
+  FH_API_BEGIN
+  FH_CHECK(w && n_out, FH_EINVAL, "null argument");
+  fh::validate(*w);
+  FH_CHECK(nshards >= 1 && shard < nshards, FH_EINVAL, "workload: shard must be < nshards");
+  FH_CHECK(count < (size_t(1) << 32), FH_EINVAL, "workload: count must be < 2^32");
+  const fh::Alias *za = w->kind == 0 ? &fh::zipf_alias(w->zipf_s, w->key_count) : nullptr;
+  const uint32_t k = w->keys_per_cmd;
+  // pass 1: membership (owner of the command's first key) and per-chunk counts
+  std::vector<uint32_t> keep(count);
+  std::vector<size_t> per(17, 0);
+  fh::parallel_chunks(count, [&](size_t t, size_t lo, size_t hi) {
+    std::vector<uint64_t> ks(k);
+    size_t m = 0;
+    for (size_t c = lo; c < hi; c++) {
+      fh::gen_range(*w, za, first + c, 0, 1, nullptr, ks.data(), nullptr, nullptr);
+      const bool mine = ks[0] % nshards == shard;
+      keep[c] = mine ? 1u : ~0u;
+      m += mine;
+    }
+    per[t + 1] = m;
+  });
+  for (size_t t = 1; t < per.size(); t++) per[t] += per[t - 1];
+  *n_out = per.back();
+  if (!dot && !key_id && !log_off && !log_cmd) return FH_OK;  // size query
+  FH_CHECK(dot && key_id, FH_EINVAL, "null argument");
+  // pass 2: the shard's commands, global dots and keys, in stream order
+  fh::parallel_chunks(count, [&](size_t t, size_t lo, size_t hi) {
+    size_t o = per[t];
+    for (size_t c = lo; c < hi; c++) {
+      if (keep[c] == ~0u) continue;
+      keep[c] = uint32_t(o);
+      fh::gen_range(*w, za, first + c, 0, 1, dot + o, key_id + o * k, nullptr, nullptr);
+      o++;
+    }
+  });
+  if (!log_off && !log_cmd) return FH_OK;
+  FH_CHECK(log_off && log_cmd && w->views >= 1, FH_EINVAL, "logs need views and both arrays");
+  // replicas' logs restricted to the shard's commands
+  std::vector<size_t> lp(w->n, 0);
+  for (size_t c = 0; c < count; c++) {
+    if (keep[c] == ~0u) continue;
+    const uint32_t p = uint32_t((first + c) % w->n);
+    for (uint32_t j = 0; j < w->views; j++) lp[(p + j) % w->n]++;
+  }
+  log_off[0] = 0;
+  for (uint32_t r = 0; r < w->n; r++) log_off[r + 1] = log_off[r] + lp[r];
+  std::vector<std::thread> ts;
+  std::vector<std::string> errs(w->n);
+  for (uint32_t r = 0; r < w->n; r++)
+    ts.emplace_back([&, r] {
+      try {
+        fh::gen_log(*w, first, count, r, log_cmd + log_off[r], lp[r], keep.data());
+      } catch (const std::exception &e) {
+        errs[r] = e.what();
+      }
+    });
+  for (auto &t : ts) t.join();
+  for (auto &e : errs) FH_CHECK(e.empty(), FH_EINVARIANT, e);
+  FH_API_END
+}
+
+fh_status fh_workload_generate_logs(const fh_workload *w, uint64_t first, size_t count,
+                                    uint64_t *log_off, uint32_t *log_cmd) {
+  FH_API_BEGIN
+  FH_CHECK(w && log_off && log_cmd, FH_EINVAL, "null argument");
+  fh::validate(*w);
+  FH_CHECK(w->views >= 1, FH_EINVAL, "workload: logs need replica views (views >= 1)");
+  FH_CHECK(count < (size_t(1) << 32), FH_EINVAL, "workload: count must be < 2^32");
+  // replica r holds exactly the commands whose fast quorum includes r + 1
+  std::vector<size_t> per(w->n, 0);
+  for (uint32_t r = 0; r < w->n; r++) {
+    // commands i with (r - (i mod n)) mod n < views
+    for (uint32_t j = 0; j < w->views; j++) {
+      const uint32_t p = (r + w->n - j) % w->n;  // p_i - 1 for member j
+      // count of i in [first, first + count) with i mod n == p
+      const uint64_t lo = first, hi = first + count;
+      auto upto = [&](uint64_t x) { return x / w->n + (x % w->n > p ? 1 : 0); };
+      per[r] += size_t(upto(hi) - upto(lo));
+    }
+  }
+  log_off[0] = 0;
+  for (uint32_t r = 0; r < w->n; r++) log_off[r + 1] = log_off[r] + per[r];
+  std::vector<std::thread> ts;
+  std::vector<std::string> errs(w->n);
+  for (uint32_t r = 0; r < w->n; r++)
+    ts.emplace_back([&, r] {
+      try {
+        fh::gen_log(*w, first, count, r, log_cmd + log_off[r], per[r]);
+      } catch (const std::exception &e) {
+        errs[r] = e.what();
+      }
+    });
+  for (auto &t : ts) t.join();
+  for (auto &e : errs) FH_CHECK(e.empty(), FH_EINVARIANT, e);
+  FH_API_END
+}
 
 uint64_t fh_workload_key_space(const fh_workload *w) { return w ? fh::key_space_of(*w) : 0; }
 

@@ -34,11 +34,19 @@ class Engine:
     def reset(self):
         L.check(self._lib.fh_engine_reset(self._h))
 
+    def rewind(self):
+        """Replay the staged batches from a clean state (on the engine stream,
+        no host synchronisation)."""
+        L.check(self._lib.fh_engine_rewind(self._h))
+
     def set_profiling(self, on: bool):
         L.check(self._lib.fh_engine_set_profiling(self._h, 1 if on else 0))
 
     def stage(self, stream, nproc: int = 5):
-        """stream: fantoch_amd.workload.Stream (views taken from it)."""
+        """stream: fantoch_amd.workload.Stream (views taken from it; its
+        per-replica logs if generated, else fq_proc / fq_time)."""
+        if stream.log_cmd is not None:
+            return self.stage_logs([stream], nproc)
         views = 0 if stream.fq_proc is None else stream.fq_proc.shape[1]
         d = L.fh_stream_desc(n=stream.n, keys_per_cmd=stream.k, views=views,
                              nproc=nproc if views else 0, pad=0)
@@ -65,6 +73,30 @@ class Engine:
             tim = np.ascontiguousarray(np.concatenate([b.fq_time for b in batches]), np.uint64)
         L.check(self._lib.fh_engine_stage_many(self._h, C.byref(d), len(batches), L.ptr(dots),
                                                L.ptr(keys), L.ptr(proc), L.ptr(tim)))
+        self.n, self.k = first.n, first.k
+
+    def stage_logs(self, batches, nproc: int = 5):
+        """Stage Streams that carry per-replica arrival logs (equal sizes);
+        each run() processes the next."""
+        first = batches[0]
+        views = first.views
+        assert views >= 1 and all(b.n == first.n and b.k == first.k for b in batches)
+        d = L.fh_stream_desc(n=first.n, keys_per_cmd=first.k, views=views, nproc=nproc, pad=0)
+        one = len(batches) == 1
+        dots = np.ascontiguousarray(first.dots if one else np.concatenate([b.dots for b in batches]),
+                                    dtype=np.uint64)
+        keys = np.ascontiguousarray(first.keys if one else np.concatenate([b.keys for b in batches]),
+                                    dtype=np.uint64)
+        offs, base = [np.zeros(1, dtype=np.uint64)], 0
+        for b in batches:
+            assert len(b.log_off) == nproc + 1
+            offs.append(b.log_off[1:].astype(np.uint64) + np.uint64(base))
+            base += int(b.log_off[-1])
+        off = np.concatenate(offs)
+        cmd = first.log_cmd if one else np.concatenate([b.log_cmd for b in batches])
+        cmd = np.ascontiguousarray(cmd, dtype=np.uint32)
+        L.check(self._lib.fh_engine_stage_logs(self._h, C.byref(d), len(batches), L.ptr(dots),
+                                               L.ptr(keys), L.ptr(off), L.ptr(cmd)))
         self.n, self.k = first.n, first.k
 
     def run(self, sync: bool = True) -> float:

@@ -23,6 +23,11 @@ class Stream:
     fq_proc: np.ndarray       # u8[n, views] or None
     fq_time: np.ndarray       # u64[n, views] or None
     key_space: int
+    # replica views as per-replica arrival logs (fh_engine_stage_logs layout):
+    # log_off u64[nproc+1], log_cmd u32[n*views]; None if not generated
+    log_off: np.ndarray = None
+    log_cmd: np.ndarray = None
+    views_n: int = 0          # fast-quorum size when only the logs are held
 
     @property
     def n(self):
@@ -31,6 +36,12 @@ class Stream:
     @property
     def k(self):
         return self.keys.shape[1]
+
+    @property
+    def views(self):
+        if self.fq_proc is not None:
+            return self.fq_proc.shape[1]
+        return self.views_n
 
     def key_off(self):
         return (np.arange(self.n + 1, dtype=np.uint64) * self.k).astype(np.uint32)
@@ -72,15 +83,49 @@ class Workload:
         w = self._c()
         return int(L.load().fh_workload_key_space(C.byref(w)))
 
-    def generate(self, count: int, first: int = 0) -> Stream:
+    def generate(self, count: int, first: int = 0, logs: bool = False,
+                 times: bool = True) -> Stream:
+        """Commands [first, first + count).  With views: fq_proc / fq_time if
+        `times`, the per-replica arrival logs if `logs` (the same arrivals)."""
         lib = L.load()
         w = self._c()
         dots = np.zeros(count, dtype=np.uint64)
         keys = np.zeros((count, self.keys_per_cmd), dtype=np.uint64)
         fq_proc = fq_time = None
-        if self.views:
+        if self.views and times:
             fq_proc = np.zeros((count, self.views), dtype=np.uint8)
             fq_time = np.zeros((count, self.views), dtype=np.uint64)
         L.check(lib.fh_workload_generate(C.byref(w), first, count, L.ptr(dots), L.ptr(keys),
                                          L.ptr(fq_proc), L.ptr(fq_time)))
-        return Stream(dots, keys, fq_proc, fq_time, self.key_space())
+        s = Stream(dots, keys, fq_proc, fq_time, self.key_space(), views_n=self.views)
+        if self.views and logs:
+            s.log_off = np.zeros(self.n + 1, dtype=np.uint64)
+            s.log_cmd = np.zeros(count * self.views, dtype=np.uint32)
+            L.check(lib.fh_workload_generate_logs(C.byref(w), first, count, L.ptr(s.log_off),
+                                                  L.ptr(s.log_cmd)))
+        return s
+
+    def generate_shard(self, count: int, nshards: int, shard: int, first: int = 0,
+                       logs: bool = True) -> Stream:
+        """Key shard `shard` of `nshards` (owner of the first key = key %
+        nshards) of commands [first, first + count), global dots, with the
+        replicas' logs restricted to it (fh_workload_generate_shard)."""
+        lib = L.load()
+        w = self._c()
+        n = C.c_size_t(0)
+        L.check(lib.fh_workload_generate_shard(C.byref(w), first, count, nshards, shard,
+                                               C.byref(n), None, None, None, None))
+        m = n.value
+        dots = np.zeros(m, dtype=np.uint64)
+        keys = np.zeros((m, self.keys_per_cmd), dtype=np.uint64)
+        lo = lc = None
+        if self.views and logs:
+            lo = np.zeros(self.n + 1, dtype=np.uint64)
+            lc = np.zeros(max(1, m * self.views), dtype=np.uint32)
+        L.check(lib.fh_workload_generate_shard(C.byref(w), first, count, nshards, shard,
+                                               C.byref(n), L.ptr(dots), L.ptr(keys), L.ptr(lo),
+                                               L.ptr(lc)))
+        s = Stream(dots, keys, None, None, self.key_space(), views_n=self.views)
+        if lo is not None:
+            s.log_off, s.log_cmd = lo, lc[:m * self.views]
+        return s

@@ -364,11 +364,30 @@ fh_status fh_engine_stage_many(fh_engine *h, const fh_stream_desc *desc,
                                size_t nbatches, const uint64_t *dot,
                                const uint64_t *key_id, const uint8_t *fq_proc,
                                const uint64_t *fq_time);
+/* Stage replica views as the replicas' own arrival logs (views >= 1): the
+ * commands replica r + 1's KeyDeps processes, in the order it processes them
+ * (its add_cmd calls: coordinator, atlas.rs:236 / epaxos.rs:208, and fast-
+ * quorum member, atlas.rs:303-309 / epaxos.rs:275-281).  For batch b and
+ * replica r (0 <= r < nproc) the log is log_cmd[log_off[b*nproc + r] ..
+ * log_off[b*nproc + r + 1]), batch-local command indices; every command of a
+ * batch appears in exactly `views` logs, at most once per log
+ * (log_off[nbatches*nproc] == nbatches * n * views).  fh_engine_stage with
+ * fq_proc / fq_time builds these logs on the host (members process commands
+ * in (time, index) order). */
+fh_status fh_engine_stage_logs(fh_engine *h, const fh_stream_desc *desc,
+                               size_t nbatches, const uint64_t *dot,
+                               const uint64_t *key_id, const uint64_t *log_off,
+                               const uint32_t *log_cmd);
+/* Replay the staged batches from a clean state (latest tables and executed
+ * clock cleared on the engine's stream, no host synchronisation; the next
+ * run processes the first staged batch again). */
+fh_status fh_engine_rewind(fh_engine *h);
 /* Run the next staged batch on the device (inputs already resident).  If
  * device_ms is non-NULL the stream is synchronised and the device time of
  * the run (HIP events on the engine's stream) is returned. */
 fh_status fh_engine_run(fh_engine *h, float *device_ms);
-/* Copy results back (each pointer may be NULL):
+/* Copy the last run's results back; run() materialises them on the device
+ * (each pointer may be NULL):
  *   dep_off[n+1], dep_dot[cap]   committed deps per command (ascending)
  *   scc_label[n]                 min dot of each command's SCC
  *   exec_rank[n]                 position of each command in exec order
@@ -422,6 +441,24 @@ uint64_t fh_workload_key_space(const fh_workload *w);
 fh_status fh_workload_generate(const fh_workload *w, uint64_t first,
                                size_t count, uint64_t *dot, uint64_t *key_id,
                                uint8_t *fq_proc, uint64_t *fq_time);
+/* The same commands' replica views as per-replica arrival logs (the
+ * fh_engine_stage_logs layout for one batch): log_off[n+1] (n = processes),
+ * log_cmd[count*views] batch-local command indices; replica r lists the
+ * commands it is a member for in (fq_time, index) order. */
+fh_status fh_workload_generate_logs(const fh_workload *w, uint64_t first,
+                                    size_t count, uint64_t *log_off,
+                                    uint32_t *log_cmd);
+/* Key shard `shard` of nshards of commands [first, first+count): the
+ * commands whose first key k0 has k0 % nshards == shard (the key's owner,
+ * SURVEY §8e), in stream order with their global dots; *n_out = how many.
+ * All output pointers NULL = size query.  log_off[n+1] / log_cmd[*n_out *
+ * views] (both NULL = no logs): the replicas' arrival logs restricted to the
+ * shard, as shard-local command indices. */
+fh_status fh_workload_generate_shard(const fh_workload *w, uint64_t first,
+                                     size_t count, uint32_t nshards,
+                                     uint32_t shard, size_t *n_out,
+                                     uint64_t *dot, uint64_t *key_id,
+                                     uint64_t *log_off, uint32_t *log_cmd);
 
 #ifdef __cplusplus
 }

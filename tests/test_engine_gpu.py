@@ -169,3 +169,96 @@ def test_c2_full_size():
     assert np.array_equal(r["deps"], deps)
     assert np.array_equal(r["key_off"], kso)
     assert np.array_equal(r["key_seq"], ks)
+
+
+def test_c4_like_views_many_tiles():
+    """C4 shape across many 4096-vertex tiles of the tile-local graph path."""
+    s = Workload.zipf(0.99, 1 << 20, k=1, views=3, window=64, seed=0xFA170C4000000004).generate(
+        150_000)
+    check_engine(s)
+
+
+def test_c1_full_views_conflict_rate():
+    """C1 at its full size through the logs API (generator logs, not fq times)."""
+    w = Workload.conflict_rate_(10, k=1, views=3, window=64, seed=2)
+    s = w.generate(10_000, logs=True)
+    eng = Engine(s.key_space, n=5)
+    eng.stage_logs([s])
+    eng.run()
+    r = eng.results()
+    dep_off, deps, ex, lab, kso, ks = oracle_pipeline(s)
+    assert np.array_equal(r["dep_off"], dep_off) and np.array_equal(r["deps"], deps)
+    assert dict(zip(s.dots.tolist(), r["scc_label"].tolist())) == dict(zip(ex.tolist(),
+                                                                         lab.tolist()))
+    assert np.array_equal(r["key_off"], kso) and np.array_equal(r["key_seq"], ks)
+
+
+def test_views_wide_window_takes_global_path():
+    """A reorder window far beyond the tile certificate (forward spans >= 1024)
+    must fall back to the global SCC path and still match the oracle."""
+    s = Workload.zipf(0.99, 1 << 12, k=1, views=3, window=3000, seed=8).generate(12_000)
+    check_engine(s)
+
+
+def test_rewind_replays_identically():
+    s = Workload.zipf(0.99, 1 << 14, k=1, views=3, window=64, seed=4).generate(30_000, logs=True)
+    eng = Engine(s.key_space, n=5)
+    eng.stage(s)
+    eng.run()
+    r1 = eng.results()
+    for _ in range(2):
+        eng.rewind()
+        eng.run()
+    r2 = eng.results()
+    for k in r1:
+        assert np.array_equal(r1[k], r2[k]), k
+
+
+@pytest.mark.parametrize("k,chunk", [(1, None), (1, "7000"), (2, "5000")])
+def test_views_streaming_batches_and_chunks(k, chunk, monkeypatch):
+    """Replica views fed as several batches of per-replica logs (each
+    replica's batch b precedes its batch b + 1), state carried across batches;
+    FH_VIEW_CHUNK splits each batch's logs into many KeyDeps chunks.  The
+    oracle sees the same arrivals (times offset per batch)."""
+    if chunk:
+        monkeypatch.setenv("FH_VIEW_CHUNK", chunk)
+    import subprocess, sys, json, os
+    # the chunk size is read once per process: run in a child
+    code = f"""
+import numpy as np, sys
+sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+from fantoch_amd.engine import Engine
+from fantoch_amd.workload import Workload, Stream
+from oracle import oracle as O
+w = Workload.zipf(0.99, 1 << 12, k={k}, views=3, window=64, seed=31)
+nb, m = 4, 9000
+parts = [w.generate(m, first=i * m, logs=True) for i in range(nb)]
+eng = Engine(w.key_space(), n=5)
+eng.stage_logs(parts)
+dots = np.concatenate([p.dots for p in parts]); keys = np.concatenate([p.keys for p in parts])
+proc = np.concatenate([p.fq_proc for p in parts])
+tim = np.concatenate([p.fq_time + np.uint64(i) * np.uint64(1 << 40) for i, p in enumerate(parts)])
+s = Stream(dots, keys, proc, tim, w.key_space())
+key_off = s.key_off(); kk = s.keys.reshape(-1)
+off, deps = O.views_run(0, 5, s.dots, key_off, kk, s.fq_proc, s.fq_time)
+ex, lab, kso, ks = O.graph_run(s.dots, key_off, kk, off, deps, s.key_space)
+lab_of = dict(zip(ex.tolist(), lab.tolist()))
+got_off, got_deps, got_seq = [np.zeros(1, dtype=np.int64)], [], {{}}
+base = 0
+for i in range(nb):
+    eng.run()
+    r = eng.results()
+    got_off.append(r["dep_off"][1:].astype(np.int64) + base); got_deps.append(r["deps"]); base += len(r["deps"])
+    for d, l in zip(parts[i].dots.tolist(), r["scc_label"].tolist()):
+        assert lab_of[d] == l
+    ko = r["key_off"]
+    for key in np.nonzero(np.diff(ko))[0]:
+        got_seq.setdefault(int(key), []).append(r["key_seq"][ko[key]:ko[key + 1]])
+assert np.array_equal(np.concatenate(got_off), off.astype(np.int64))
+assert np.array_equal(np.concatenate(got_deps), deps)
+for key in np.nonzero(np.diff(kso))[0]:
+    assert np.array_equal(np.concatenate(got_seq[int(key)]), ks[kso[key]:kso[key + 1]])
+print("ok")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
