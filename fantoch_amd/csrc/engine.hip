@@ -99,19 +99,70 @@ __global__ void k_tail_engine(uint32_t M, const KT *__restrict__ ks, const uint3
 }
 
 // decode an element's dependency code: in-batch vid (true) or external value
-// (a log reference to a command of the batch itself, written by an earlier
-// chunk of the batch's replica logs, is in batch too)
-__device__ __forceinline__ bool dep_in_batch(uint64_t c, uint32_t *v, uint64_t bbase,
-                                             uint32_t n) {
-  if (c != 0 && c < kLogFlag) {
+// Element dependency codes, decoded by the union:
+//  u64 (single view, k > 1): 0 none, in-batch vid + 1 (< 2^48), else the
+//      segment head's latest entry: a dot (>= 2^56) or a command-log
+//      reference (kLogFlag | position, [2^48, 2^56));
+//  u32 (replica views): 0 none, vid + 1 (< 2^31), else 0x80000000 | the log
+//      position of the head's latest entry (views' latest tables hold log
+//      references only).
+// A log reference into the batch itself (written by an earlier chunk of the
+// batch's replica logs) is an in-batch dependency.  Returns 1 = in batch
+// (*v), 2 = external dot (*x), 0 = none.
+__device__ __forceinline__ int decode_dep(uint64_t c, uint32_t *v, uint64_t *x,
+                                          const uint64_t *__restrict__ dlog, uint64_t bbase,
+                                          uint32_t n) {
+  if (c == 0) return 0;
+  if (c < kLogFlag) {
     *v = uint32_t(c - 1);
-    return true;
+    return 1;
   }
-  if (is_log_ref(c) && c - kLogFlag >= bbase && c - kLogFlag < bbase + n) {
-    *v = uint32_t(c - kLogFlag - bbase);
-    return true;
+  if (is_log_ref(c)) {
+    const uint64_t pos = c - kLogFlag;
+    if (pos >= bbase && pos < bbase + n) {
+      *v = uint32_t(pos - bbase);
+      return 1;
+    }
+    *x = dlog[pos];
+    return 2;
   }
-  return false;
+  *x = c;
+  return 2;
+}
+__device__ __forceinline__ int decode_dep(uint32_t c, uint32_t *v, uint64_t *x,
+                                          const uint64_t *__restrict__ dlog, uint64_t bbase,
+                                          uint32_t n) {
+  if (c == 0) return 0;
+  if (!(c & 0x80000000u)) {
+    *v = c - 1;
+    return 1;
+  }
+  const uint64_t pos = c & 0x7FFFFFFFu;
+  if (pos >= bbase && pos < bbase + n) {
+    *v = uint32_t(pos - bbase);
+    return 1;
+  }
+  *x = dlog[pos];
+  return 2;
+}
+
+// replica views: segment heads take the latest entry as a 32-bit log code,
+// the rest the previous element's command
+__global__ void k_prev_views(uint32_t M, const uint32_t *__restrict__ ks,
+                             const uint32_t *__restrict__ vs, uint32_t per_cmd,
+                             const uint64_t *__restrict__ latest, uint32_t *__restrict__ code) {
+  GRID_STRIDE(j, M) {
+    const uint32_t e = vs[j];
+    const uint32_t seg = ks[j];
+    uint32_t c;
+    if (j == 0 || ks[j - 1] != seg) {
+      const uint64_t x = latest[seg];
+      c = x ? (0x80000000u | uint32_t(x - kLogFlag)) : 0u;
+    } else {
+      c = vs[j - 1] / per_cmd + 1;
+    }
+    code[e] = c;
+  }
 }
 
 __device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
@@ -137,9 +188,10 @@ __device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
 // per step; C5's 12-slot rows spent 15 ms there.)  A dot is never all ones
 // (ProcessId 255 with sequence 2^56 - 1), so the sentinel cannot collide.
 constexpr uint32_t kRegSlots = 16;
+template <uint32_t kRegSlots, class CT>
 __device__ __forceinline__ void cmd_union_regs(
     uint32_t i, uint32_t S, const uint64_t *__restrict__ dot,
-    const uint64_t *__restrict__ dep_code, const uint64_t *__restrict__ dlog,
+    const CT *__restrict__ dep_code, const uint64_t *__restrict__ dlog,
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n) {
@@ -151,17 +203,15 @@ __device__ __forceinline__ void cmd_union_regs(
     r[t] = ~0ull;
     vv[t] = ~0u;
     if (t < S) {
-      uint64_t x = dep_code[size_t(i) * S + t];
-      uint32_t v;
-      if (dep_in_batch(x, &v, bbase, n)) {
+      uint64_t x = 0;
+      uint32_t v = 0;
+      const int kind = decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
+      if (kind == 1) {
         vv[t] = v;
         r[t] = dot[v];
-      } else {
-        if (is_log_ref(x)) x = dlog[x - kLogFlag];  // single view: command-log reference
-        if (x) {
-          r[t] = x;
-          if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
-        }
+      } else if (kind == 2) {
+        r[t] = x;
+        if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
       }
     }
   }
@@ -215,18 +265,34 @@ __device__ __forceinline__ void cmd_union_regs(
 // external dots), committed dep dots (sorted, fixed stride S), graph edges
 // (vids, padded with the vertex itself), latest-table update at tails and the
 // missing-dependency flag for external deps that are not executed.
+template <class CT>
 __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict__ dot,
-                             const uint64_t *__restrict__ dep_code,
+                             const CT *__restrict__ dep_code,
                              const uint64_t *__restrict__ dlog,
                              const uint64_t *__restrict__ frontier,
                              uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ dep_cnt,
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
                              uint64_t bbase) {
-  if (S <= kRegSlots) {  // uniform: the register path
+  // uniform: the register path, with a sorting network sized to the row
+  if (S <= 4) {
     GRID_STRIDE(i, n) {
-      cmd_union_regs(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                     nblocked, nv_out, bbase, n);
+      cmd_union_regs<4>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
+                        nblocked, nv_out, bbase, n);
+    }
+    return;
+  }
+  if (S <= 8) {
+    GRID_STRIDE(i, n) {
+      cmd_union_regs<8>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
+                        nblocked, nv_out, bbase, n);
+    }
+    return;
+  }
+  if (S <= kRegSlots) {
+    GRID_STRIDE(i, n) {
+      cmd_union_regs<kRegSlots>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
+                                blocked0, nblocked, nv_out, bbase, n);
     }
     return;
   }
@@ -236,16 +302,16 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     uint32_t nv = 0, nd = 0;
     bool missing = false;
     for (uint32_t t = 0; t < S; t++) {
-      uint64_t x = dep_code[size_t(i) * S + t];
-      uint32_t v;
-      if (dep_in_batch(x, &v, bbase, n)) {
+      uint64_t x = 0;
+      uint32_t v = 0;
+      const int kind = decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
+      if (kind == 1) {
         bool dup = false;
         for (uint32_t q = 0; q < nv; q++) dup |= ds[q] == v;
         if (!dup) ds[nv++] = v;
         dd[nd++] = dot[v];
-      } else {
-        if (is_log_ref(x)) x = dlog[x - kLogFlag];  // single view: command-log reference
-        if (x) {
+      } else if (kind == 2) {
+        {
           dd[nd++] = x;
           // executed? (AEClock frontier; exceptions are not carried by the
           // fused engine: every earlier batch executed completely)
@@ -440,13 +506,6 @@ __global__ void k_frontier_update(const unsigned long long *__restrict__ mx,
   excount[s] += cnt[s];
 }
 
-// per-key sequence in key-grouped (not key-ascending) order -> ascending
-// layout: the first position of each key's run, then every element moves to
-// off[key] + (its position - the run's first position)
-__global__ void k_run_heads(uint32_t m, const uint32_t *__restrict__ keys, uint32_t *__restrict__ hp) {
-  GRID_STRIDE(j, m) if (j == 0 || keys[j - 1] != keys[j]) hp[keys[j]] = j;
-}
-
 __global__ void k_run_scatter(uint32_t m, const uint32_t *__restrict__ keys,
                               const uint32_t *__restrict__ vids, const uint32_t *__restrict__ hp,
                               const uint32_t *__restrict__ off, const uint64_t *__restrict__ dot,
@@ -471,26 +530,19 @@ __global__ void k_identity_labels(uint32_t n, const uint64_t *__restrict__ dot,
   }
 }
 
-// Key histogram of the per-key sequence.  Its keys come in runs (each key's
-// elements are contiguous), so one atomic per run within a wave: the run's
-// head lane adds the run length (C3's 20M elements on 17 keys took 125 ms
-// with one atomic per element).
-__global__ void k_key_hist(uint32_t m, const uint32_t *__restrict__ keys, uint32_t *__restrict__ h) {
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t b = blockIdx.x * blockDim.x; b < m; b += gridDim.x * blockDim.x) {
-    const uint32_t j = b + threadIdx.x;
-    const bool valid = j < m;
-    const uint32_t k = valid ? keys[j] : ~0u;
-    const uint32_t kp = __shfl_up(k, 1, 64);
-    const bool head = valid && (lane == 0 || kp != k);
-    const uint64_t heads = __ballot(head);
-    const uint64_t vmask = __ballot(valid);
-    if (head) {
-      const uint64_t later = lane == 63 ? 0ull : heads >> (lane + 1);
-      const uint32_t nvalid = uint32_t(__popcll(vmask));  // valid lanes are a prefix
-      const uint32_t end = later ? lane + 1 + uint32_t(__ffsll((long long)later) - 1) : nvalid;
-      atomicAdd(&h[k], end - lane);
-    }
+// Per-key element counts of a key-grouped sequence (every key's elements
+// contiguous): a run's head records its start, its tail the count.  One
+// write per distinct key -- an atomic histogram serialises on Zipf-hot keys
+// (key 0 of C4 holds 6.5% of the stream: 4 ms of same-address atomics).
+__global__ void k_run_start(uint32_t m, const uint32_t *__restrict__ keys,
+                            uint32_t *__restrict__ start) {
+  GRID_STRIDE(j, m) if (j == 0 || keys[j - 1] != keys[j]) start[keys[j]] = j;
+}
+__global__ void k_run_count(uint32_t m, const uint32_t *__restrict__ keys,
+                            const uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
+  GRID_STRIDE(j, m) {
+    const uint32_t k = keys[j];
+    if (j + 1 == m || keys[j + 1] != k) cnt[k] = j + 1 - start[k];
   }
 }
 
@@ -551,6 +603,7 @@ struct EngineDevice {
   std::vector<uint32_t> h_loff;  // host copy of loff
   // scratch
   DBuf<uint64_t> dep_ext, dep_dot, seq_dot, lab;
+  DBuf<uint32_t> dep32;  // replica views: 32-bit element dependency codes
   DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
   // outputs of the last run (materialised inside run(), copied by results())
   DBuf<uint32_t> o_dep_off;
@@ -826,6 +879,8 @@ struct EngineDevice {
       dot.swap(grown);
     }
     FH_CHECK(log_len + n * nb < kLogFlag, FH_ENOTIMPL, "command log exceeds 2^48 commands");
+    FH_CHECK(!d.views || log_len + n * nb < (size_t(1) << 31), FH_ENOTIMPL,
+             "replica views: command log exceeds 2^31 commands (32-bit dependency codes)");
     FH_HIP(hipMemcpyAsync(dot.get() + log_len, h_dot, n * nb * sizeof(uint64_t),
                           hipMemcpyHostToDevice, stream));
     stage_base = log_len;
@@ -988,10 +1043,10 @@ struct EngineDevice {
                              sort_ws, stream, &ks, &vs);
         // heads read the latest table, tails then make the chunk's last
         // commands the latest (command-log references)
-        probed_launch("prev_engine", double(Mc) * (4.0 + 4.0 + 8.0), k_prev_engine<uint32_t>,
+        probed_launch("prev_engine", double(Mc) * (4.0 + 4.0 + 4.0), k_prev_views,
                       dim3(grid_for(Mc, B)), dim3(B), stream, Mc, (const uint32_t *)ks,
-                      (const uint32_t *)vs, 0, S, (const uint64_t *)views_latest(), 1ull, ~0ull,
-                      dext, (uint32_t *)nullptr);
+                      (const uint32_t *)vs, S, (const uint64_t *)views_latest(),
+                      dep32.ensure(M + 1));
         k_tail_engine<uint32_t><<<grid_for(Mc, B), B, 0, stream>>>(
             Mc, ks, vs, 0, S, views_latest(), 1ull, ~0ull, nullptr, bbase);
       }
@@ -1009,18 +1064,25 @@ struct EngineDevice {
 
   void run_general(uint32_t n, uint32_t k, uint32_t fq, uint32_t S, uint32_t M, bool views,
                    const uint32_t *bkey, const uint64_t *bdot, uint64_t bbase) {
-    const uint64_t *dcode = dep_ext.get();
     uint32_t *svid = sorted_vid.get();
     mark("keydeps_prev");
     uint64_t *ddot = dep_dot.ensure(M + 1);
     uint32_t *dcnt = dep_cnt.ensure(n + 1);
     uint32_t *dd = dst.ensure(M + 1);
     FH_HIP(hipMemsetAsync(scal.get(), 0, sizeof(uint32_t), stream));
-    probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0), k_cmd_engine,
-                  dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot, dcode,
-                  (const uint64_t *)dot.get(), (const uint64_t *)frontier.get(), ddot, dcnt, dd,
-                  (uint8_t *)nullptr, scal.get(),
-                  views && S >= 8 ? edge_cnt.ensure(n + 1) : (uint32_t *)nullptr, bbase);
+    uint32_t *ecnt = views && S >= 8 ? edge_cnt.ensure(n + 1) : (uint32_t *)nullptr;
+    if (views)
+      probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
+                    k_cmd_engine<uint32_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
+                    (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
+                    (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
+                    scal.get(), ecnt, bbase);
+    else
+      probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
+                    k_cmd_engine<uint64_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
+                    (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
+                    (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
+                    scal.get(), ecnt, bbase);
     mark("keydeps_union");
     const uint32_t *gdst = dd, *goff = nullptr;
     if (views && S >= 8) {  // measured: a win at S = 12 (C5), flat or worse at 3 and 6
@@ -1098,14 +1160,14 @@ struct EngineDevice {
     o_nelem = gout.nelem;
     uint32_t *h = key_hist.ensure(key_space + 1);
     uint32_t *o = key_offs.ensure(key_space + 2);
+    uint32_t *hp = headpos.ensure(key_space + 1);
     FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
-    k_key_hist<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, h);
+    k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
+    k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
     exclusive_scan_u32(h, o, key_space, scan_ws, stream);
     uint64_t *sq = seq_dot.ensure(o_nelem + 1);
     if (sv_fused && bucket_order) {
-      // key-grouped runs -> ascending keys
-      uint32_t *hp = headpos.ensure(key_space + 1);
-      k_run_heads<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
+      // key-grouped runs -> ascending keys (hp holds each run's start)
       k_run_scatter<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, gout.pk_vid, hp,
                                                              o, bdot, sq);
     } else if (sv_fused) {  // (sorted keys, sorted vids): gather the dots

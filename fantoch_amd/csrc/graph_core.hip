@@ -902,9 +902,8 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   // replica views with a bounded reorder window: everything in tile-local LDS
   // passes, certified (graph_tile.hip); else the global path below
   if (!in.no_forward_hint && tiles_eligible(in)) {
-    if (run_tiles(in, out)) {
+    if (run_tiles(in, out)) {  // (labels come from the tiles)
       dbg_tile_ok++;
-      build_labels(in, out);
       build_per_key(in, out);
       return;
     }

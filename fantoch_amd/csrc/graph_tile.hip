@@ -100,6 +100,14 @@ __device__ __forceinline__ bool lds_max_u16(uint16_t *p, uint16_t v) {
   }
 }
 
+__device__ __forceinline__ uint16_t lds_add_u16(uint16_t *p, uint16_t v) {
+  uint32_t *w = reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
+  const int sh = int(reinterpret_cast<uintptr_t>(p) & 2) * 8;
+  // a 32-bit add of v << sh: the low half never carries into the high half
+  // because every count stays below 2^16
+  return uint16_t(atomicAdd(w, uint32_t(v) << sh) >> sh);
+}
+
 __device__ __forceinline__ uint16_t lds_xchg_u16(uint16_t *p, uint16_t v) {
   uint32_t *w = reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
   const int sh = int(reinterpret_cast<uintptr_t>(p) & 2) * 8;
@@ -114,12 +122,13 @@ __device__ __forceinline__ uint16_t lds_xchg_u16(uint16_t *p, uint16_t v) {
 
 struct TileOut {
   uint32_t *rep;     // [V] global vid of the SCC's min member
+  uint64_t *label;   // [V] min dot of the SCC
   uint32_t *hgrp;    // [V] ready time H (a vertex position)
   uint32_t *grank;   // [V] rank inside the ready group
   uint32_t *gcount;  // [V] size of the group rooted at v (0 if H(v) != v)
   uint32_t *stat;    // [0] failed tiles, [1] max core local excess,
                      // [2] core vertices over R0, [3] long forward edges,
-                     // [4] max H sweeps, [5] max SCC rounds
+                     // [4] max H sweeps, [5] max SCC rounds, [6] max group
   const uint8_t *redo;  // [tiles] or null: only tiles with redo[t] run
   unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
 };
@@ -399,23 +408,42 @@ __global__ void __launch_bounds__(kTileThreads)
       int(nraised), nullptr);
   phase(4);
 
-  // 7. ready groups: member lists of the groups with raised members (head in
-  // eL[0], next in eL[1]: the edges are no longer needed), then each core
-  // vertex's rank in its group by (depth, min member, dot) and each core
-  // root's group size
-  uint16_t *head = eL[0], *next = eL[1];
-  for (int x = tid; x < C; x += kTileThreads) head[x] = kNone;
+  // 7. ready groups: the raised vertices counting-sorted by group root into
+  // eL[1] (group t's members at [end(t-1), end(t)), ends in eL[0]; the edges
+  // are no longer needed), then each core vertex's rank in its group by
+  // (depth, min member, dot) and each core root's group size
+  uint16_t *gend = eL[0], *gmem = eL[1];
+  for (int x = tid; x < C; x += kTileThreads) gend[x] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < nraised; i += kTileThreads) lds_add_u16(&gend[sH[W2[i]]], 1);
+  __syncthreads();
+  {
+    const int x0 = tid * kPer;
+    uint32_t sum = 0;
+    for (int x = x0; x < x0 + kPer && x < C; x++) sum += gend[x];
+    uint32_t tot = 0;
+    uint32_t base = tile_scan(sum, s_w, &tot);
+    for (int x = x0; x < x0 + kPer && x < C; x++) {
+      const uint32_t c = gend[x];
+      gend[x] = uint16_t(base);
+      base += c;
+    }
+  }
   __syncthreads();
   for (uint32_t i = tid; i < nraised; i += kTileThreads) {
     const uint16_t y = W2[i];
-    next[y] = lds_xchg_u16(&head[sH[y]], y);
+    gmem[lds_add_u16(&gend[sH[y]], 1)] = y;
   }
   __syncthreads();
+  uint32_t gmax = 0;
   for (int x = ca + tid; x < cb; x += kTileThreads) {
     const uint32_t v = lo + x;
     const uint16_t t = sH[x];
     uint32_t cnt = 0, rk = 0;
+    uint64_t lab = 0;  // min dot of x's SCC (0 = x's own: a singleton group)
     if (sF[t] & 4) {
+      const uint32_t b0 = t ? gend[t - 1] : 0u, b1 = gend[t];
+      cnt = b1 - b0;
       const uint32_t dx = W1[sR[x]], mx = sR[x];
       uint64_t dotx = 0;
       bool have_dot = false;
@@ -430,16 +458,52 @@ __global__ void __launch_bounds__(kTileThreads)
         return dot[lo + y] < dotx;
       };
       if (t != uint32_t(x)) rk += cmp(t);
-      for (uint16_t y = head[t]; y != kNone; y = next[y]) {
-        cnt++;
-        if (y != uint32_t(x)) rk += cmp(y);
+      // members 8 at a time: (depth, min member) from LDS, and the dots of
+      // same-SCC members loaded together (independent L2 loads in flight)
+      for (uint32_t j = b0; j < b1; j += 8) {
+        uint32_t ys[8];
+        int st[8];  // -1 before x, 1 after x, 0 tie on the SCC (dot decides)
+        uint64_t dy[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          ys[u] = j + u < b1 ? gmem[j + u] : uint32_t(x);
+          const uint32_t d2 = W1[sR[ys[u]]], m2 = sR[ys[u]];
+          st[u] = ys[u] == uint32_t(x) ? 1 : d2 != dx ? (d2 < dx ? -1 : 1)
+                                       : m2 != mx ? (m2 < mx ? -1 : 1) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) dy[u] = st[u] == 0 ? dot[lo + ys[u]] : 0ull;
+        bool any_tie = false;
+#pragma unroll
+        for (int u = 0; u < 8; u++) any_tie |= st[u] == 0;
+        if (any_tie && !have_dot) {
+          dotx = dot[v];
+          have_dot = true;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          rk += st[u] < 0 || (st[u] == 0 && dy[u] < dotx);
+          if (st[u] == 0 && (lab == 0 || dy[u] < lab)) lab = dy[u];
+        }
       }
+      // the root t is in x's SCC iff it shares the SCC slot (cmp(t) above
+      // compared it; its dot was not kept)
+      if (t != uint32_t(x) && sR[t] == mx) {
+        const uint64_t dt = dot[lo + t];
+        if (lab == 0 || dt < lab) lab = dt;
+      }
+      gmax = max(gmax, cnt + 1);
+    }
+    {
+      const uint64_t own = dot[v];
+      out.label[v] = (lab == 0 || own < lab) ? own : lab;
     }
     out.rep[v] = lo + sR[x];
     out.hgrp[v] = lo + t;
     out.grank[v] = rk;
     out.gcount[v] = t == uint32_t(x) ? cnt + 1 : 0u;
   }
+  if (gmax) atomicMax(&out.stat[6], gmax);
   __syncthreads();
   phase(5);
 }
@@ -481,6 +545,7 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   uint32_t *stat = scalars.get() + 24;
   TileOut to;
   to.rep = rep.ensure(V + 1);
+  to.label = tmp64c.ensure(V + 1);
   to.hgrp = t_h.ensure(V + 1);
   to.grank = t_rank.ensure(V + 1);
   to.gcount = t_cnt.ensure(V + 1);
@@ -496,19 +561,19 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   // then R0 = 2048 with 2048-vertex cores (each a context of <= 10240)
   bool ok = false;
   for (int level = 0; level < 2 && !ok; level++) {
-    FH_HIP(hipMemsetAsync(stat, 0, 6 * sizeof(uint32_t), stream));
+    FH_HIP(hipMemsetAsync(stat, 0, 7 * sizeof(uint32_t), stream));
     if (level == 0)
       launch_tiles<1536, 4096>(V, in.stride, in.dst, in.dot, to, stream);
     else
       launch_tiles<2048, 2048>(V, in.stride, in.dst, in.dot, to, stream);
-    uint32_t st[6];
-    fetch_u32(stat, st, 6, stream);
+    uint32_t st[7];
+    fetch_u32(stat, st, 7, stream);
     ok = st[0] == 0;
     if (debug)
       fprintf(stderr,
               "fh graph_tile: V=%u level=%d failed_tiles=%u max_excess=%u over=%u long_fwd=%u "
-              "max_sweeps=%u max_rounds=%u\n",
-              V, level, st[0], st[1], st[2], st[3], st[4], st[5]);
+              "max_sweeps=%u max_rounds=%u max_group=%u\n",
+              V, level, st[0], st[1], st[2], st[3], st[4], st[5], st[6]);
   }
   if (debug) {
     unsigned long long pr[8];
@@ -536,6 +601,7 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   out.nexec = V;
   out.npending = 0;
   out.rep = rep.get();
+  out.scc_label = tmp64c.get();
   mark("exec_order");
   return true;
 }

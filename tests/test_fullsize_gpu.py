@@ -1,0 +1,90 @@
+"""Full-size parity on the GPU: the engine's outputs on the BASELINE.json
+configurations against the oracle's digests (tests/golden/digests.json, made
+by tests/golden/make_digests.py), and full-size properties where the
+incremental oracle cannot finish (its Tarjan is quadratic on C3's stream-wide
+SCC and C5's million-member SCC).  Streams are regenerated here by the seeded
+counter-based generator (same library, same streams)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fantoch_amd.engine import Engine
+from fullsize import CONFIGS, check_properties, digest_deps, digest_labels, digest_perkey
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "digests.json")
+
+
+def gold(name):
+    with open(GOLD) as fh:
+        d = json.load(fh)
+    if name not in d:
+        pytest.skip(f"no digest for {name} (run tests/golden/make_digests.py)")
+    return d[name]
+
+
+def run_engine(s):
+    eng = Engine(s.key_space, n=5)
+    eng.stage(s)
+    eng.run()
+    r = eng.results()
+    eng.close()
+    return r
+
+
+def check_digests(g, r, what=("deps", "labels", "perkey")):
+    if "deps" in what:
+        assert digest_deps(r["dep_off"], r["deps"]) == g["deps"], "committed deps"
+    if "labels" in what:
+        assert digest_labels(r["scc_label"]) == g["labels"], "SCC partition (min-dot labels)"
+    if "perkey" in what:
+        assert digest_perkey(r["key_off"], r["key_seq"]) == g["perkey"], "per-key sequences"
+
+
+def test_c1_full_digest():
+    g = gold("c1")
+    s = CONFIGS["c1"]["workload"]().generate(g["n"], logs=True, times=False)
+    check_digests(g, run_engine(s))
+
+
+def test_c4_full_100m_digest():
+    """The bench.py headline stream at its full 100M commands."""
+    g = gold("c4")
+    s = CONFIGS["c4"]["workload"]().generate(g["n"], logs=True, times=False)
+    check_digests(g, run_engine(s))
+
+
+def test_c4_key_shard_digest():
+    """Key shard 0 of 8 with global dots (the multi-GPU bench's rank 0)."""
+    g = gold("c4shard")
+    c = CONFIGS["c4shard"]
+    s = c["workload"]().generate_shard(c["total"], c["nshards"], c["shard"])
+    assert s.n == g["n"]
+    check_digests(g, run_engine(s))
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_prefix_digest(name):
+    """C3 / C5: everything against the oracle on the largest prefix it finishes."""
+    g = gold(name)["prefix"]
+    s = CONFIGS[name]["workload"]().generate(g["n"], logs=True, times=False)
+    check_digests(g, run_engine(s))
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_full_size_deps_and_properties(name):
+    """C3 at 10M / C5 at 12.5M: committed deps bit-exact against the oracle's
+    linear-time KeyDeps + QuorumDeps pass, and the SCC / order properties."""
+    g = gold(name)
+    s = CONFIGS[name]["workload"]().generate(g["n"], logs=True, times=False)
+    r = run_engine(s)
+    check_digests(g, r, what=("deps",))
+    check_properties(s, r)
+
+
+def test_c4_full_properties():
+    """Independent checks of the 100M headline output (also pinned by digest)."""
+    s = CONFIGS["c4"]["workload"]().generate(20_000_000, logs=True, times=False)
+    check_properties(s, run_engine(s))

@@ -8,7 +8,7 @@ OUT=gpurun_out
 mkdir -p $OUT
 TESTS=${TESTS:-tests/test_engine_gpu.py}
 if [ "$TESTS" != "none" ]; then
-  timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 240 --timeout-method thread > $OUT/pytest_q.log 2>&1
+  timeout -k 10 1000 python -u -m pytest $TESTS -m gpu -x -q --durations=15 --timeout 400 --timeout-method thread > $OUT/pytest_q.log 2>&1
   rc=$?
   tail -15 $OUT/pytest_q.log
   if [ $rc -ne 0 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
