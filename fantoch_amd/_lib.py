@@ -70,6 +70,10 @@ SIGNATURES = {
     "fh_graph_mark_executed": (C.c_int, [V, S, V]),
     "fh_graph_set_executed_frontier": (C.c_int, [V, C.c_uint32, C.c_uint64]),
     "fh_graph_pending": (C.c_int, [V, P(S)]),
+    "fh_graph_set_time": (C.c_int, [V, C.c_uint64]),
+    "fh_graph_monitor_pending": (C.c_int, [V, C.c_uint64, V, V, V, S, P(S)]),
+    "fh_graph_take_metrics": (C.c_int, [V, V, S, V, S, P(S), P(S)]),
+    "fh_graph_passes": (C.c_int, [V, P(C.c_uint64), P(C.c_uint64)]),
     "fh_graph_missing": (C.c_int, [V, V, S, P(S)]),
     "fh_graph_add_batch_sharded": (C.c_int, [V, S, V, V, V, V, V, V, V]),
     "fh_graph_requests": (C.c_int, [V, V, V, S, P(S)]),
@@ -95,6 +99,13 @@ SIGNATURES = {
     "fh_engine_set_probe": (C.c_int, [V, C.c_char_p]),
     "fh_engine_probe_stats": (C.c_int, [V, P(C.c_float), P(S), P(C.c_double)]),
     "fh_engine_probe_stats_for": (C.c_int, [V, C.c_char_p, P(C.c_float), P(S), P(C.c_double)]),
+    "fh_multi_create": (C.c_int, [P(fh_config), S, V, P(V)]),
+    "fh_multi_destroy": (C.c_int, [V]),
+    "fh_multi_stage_logs": (C.c_int, [V, P(fh_stream_desc), V, V, V, V]),
+    "fh_multi_rewind": (C.c_int, [V]),
+    "fh_multi_run": (C.c_int, [V, P(C.c_float)]),
+    "fh_multi_results": (C.c_int, [V, V, V, S, P(S), V, V, V, V]),
+    "fh_multi_shard_size": (C.c_int, [V, S, P(S)]),
     "fh_workload_key_space": (C.c_uint64, [P(fh_workload)]),
     "fh_workload_generate": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V, V, V]),
     "fh_workload_generate_logs": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V]),

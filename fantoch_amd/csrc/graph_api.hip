@@ -14,6 +14,7 @@
 #include <deque>
 #include <map>
 #include <set>
+#include <string>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -110,6 +111,18 @@ struct GraphDevice {
   // drain queue
   std::deque<std::pair<uint64_t, uint64_t>> ready;
   std::vector<uint64_t> missing_now;
+  // time (SysTime::millis of the caller, fh_graph_set_time): vertices are
+  // stamped when added (Vertex::new, tarjan.rs:335-351); p_time per pending
+  uint64_t now_ms = 0;
+  std::vector<uint64_t> p_time;
+  // executor metrics not yet taken (ExecutorMetricsKind, executor/mod.rs:
+  // 122-129): ChainSize per executed SCC, ExecutionDelay per command
+  // (save_scc, graph/mod.rs:490-525)
+  std::vector<uint64_t> m_chain, m_delay;
+  // the executed clock changed since the last pass (a pending retry with no
+  // new vertex and no missing dependency executed since has nothing to do)
+  bool clock_changed = false;
+  uint64_t passes = 0, skipped = 0;
   // device buffers
   DBuf<uint64_t> d_dot, d_ddot, d_sd, d_sd2, d_frontier, d_exc;
   DBuf<uint32_t> d_koff, d_key32, d_doff, d_cnt, d_off, d_dst, d_sv, d_sv2, d_err;
@@ -212,6 +225,26 @@ struct GraphDevice {
                  const uint64_t *cmd_shards = nullptr, const uint64_t *dep_shards = nullptr) {
     FH_CHECK(n == 0 || (dot && key_off && dep_off), FH_EINVAL, "null argument");
     FH_HIP(hipSetDevice(device));
+    // check_pending (mod.rs:558-644) retries only the children of dots that
+    // were just executed: a retry with no new vertex where none of the
+    // pending set's missing dependencies executed since the last pass
+    // changes nothing
+    if (n == 0) {
+      bool resolved = false;
+      if (clock_changed)
+        for (uint64_t d : missing_now)
+          if (clock.contains(d)) {
+            resolved = true;
+            break;
+          }
+      clock_changed = false;
+      if (!resolved) {
+        skipped++;
+        return;
+      }
+    }
+    passes++;
+    clock_changed = false;
     // vertices: carried pending (earlier arrivals) then the batch
     const size_t P = p_dot.size();
     const size_t V = P + n;
@@ -309,10 +342,17 @@ struct GraphDevice {
                           hipMemcpyDeviceToHost, stream));
     FH_HIP(hipMemcpyAsync(blocked.data(), out.blocked, V, hipMemcpyDeviceToHost, stream));
     FH_HIP(hipStreamSynchronize(stream));
+    std::vector<uint64_t> vtime(p_time);
+    vtime.resize(V, now_ms);
     for (uint32_t j = 0; j < out.nexec; j++) {
       const uint32_t v = order[j];
       ready.emplace_back(vdot[v], label[v]);
       clock.add(vdot[v]);  // executed clock update (tarjan.rs:296)
+      // metrics: one ChainSize per SCC (members are contiguous in the
+      // execution order), one ExecutionDelay per command
+      if (j == 0 || label[order[j - 1]] != label[v]) m_chain.push_back(0);
+      m_chain.back()++;
+      m_delay.push_back(now_ms >= vtime[v] ? now_ms - vtime[v] : 0);
     }
     // carry pending vertices; record their missing dependencies
     p_dot.clear();
@@ -322,6 +362,7 @@ struct GraphDevice {
     p_dshard.clear();
     p_koff.assign(1, 0);
     p_doff.assign(1, 0);
+    p_time.clear();
     std::unordered_set<uint64_t> present;
     for (size_t v = 0; v < V; v++)
       if (blocked[v]) present.insert(vdot[v]);
@@ -336,6 +377,7 @@ struct GraphDevice {
       p_dshard.insert(p_dshard.end(), dshard.begin() + doff[v], dshard.begin() + doff[v + 1]);
       p_doff.push_back(uint32_t(p_deps.size()));
       p_cshard.push_back(cshard[v]);
+      p_time.push_back(vtime[v]);
       for (uint32_t e = doff[v]; e < doff[v + 1]; e++) {
         const uint64_t d = deps[e];
         if (d != vdot[v] && !clock.contains(d) && !present.count(d) && seen.insert(d).second)
@@ -343,6 +385,58 @@ struct GraphDevice {
       }
     }
     std::sort(missing_now.begin(), missing_now.end());
+    // PendingIndex entries go once their parent dot is indexed or executed
+    // (index.rs remove, called from check_pending)
+    for (auto it = requested.begin(); it != requested.end();) {
+      if (clock.contains(*it) || present.count(*it))
+        it = requested.erase(it);
+      else
+        ++it;
+    }
+  }
+
+  // VertexIndex::monitor_pending (index.rs:53-103): pending vertices older
+  // than threshold_ms, longest pending first, with each one's missing
+  // dependencies found through other pending vertices
+  // (missing_dependencies, index.rs:105-142); a pending vertex without any
+  // is a liveness bug: FH_EINVARIANT, where the reference panics.
+  void monitor_pending(uint64_t threshold_ms, std::vector<std::pair<uint64_t, uint64_t>> &old_out,
+                       std::vector<uint64_t> &nmissing) {
+    std::unordered_map<uint64_t, size_t> vid;
+    vid.reserve(p_dot.size());
+    for (size_t v = 0; v < p_dot.size(); v++) vid.emplace(p_dot[v], v);
+    std::vector<size_t> idx;
+    for (size_t v = 0; v < p_dot.size(); v++)
+      if (now_ms >= p_time[v] && now_ms - p_time[v] >= threshold_ms) idx.push_back(v);
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return p_time[a] < p_time[b]; });
+    std::vector<uint64_t> stuck;
+    for (size_t v : idx) {
+      std::unordered_set<uint64_t> visited, missing;
+      std::vector<size_t> stack{v};
+      visited.insert(p_dot[v]);
+      while (!stack.empty()) {
+        const size_t x = stack.back();
+        stack.pop_back();
+        for (uint32_t e = p_doff[x]; e < p_doff[x + 1]; e++) {
+          const uint64_t d = p_deps[e];
+          if (d == p_dot[x] || clock.contains(d)) continue;
+          auto it = vid.find(d);
+          if (it == vid.end())
+            missing.insert(d);
+          else if (visited.insert(d).second)
+            stack.push_back(it->second);
+        }
+      }
+      if (missing.empty()) stuck.push_back(p_dot[v]);
+      old_out.emplace_back(p_dot[v], now_ms - p_time[v]);
+      nmissing.push_back(missing.size());
+    }
+    if (!stuck.empty()) {
+      std::string m = "monitor_pending: commands pending without missing dependencies:";
+      for (uint64_t d : stuck) m += " (" + std::to_string(d >> 56) + "," +
+                                   std::to_string(d & 0x00FFFFFFFFFFFFFFull) + ")";
+      throw Error(FH_EINVARIANT, m);
+    }
   }
 
   size_t drain(uint64_t *dots, uint64_t *labels, size_t cap) {
@@ -477,14 +571,83 @@ fh_status fh_graph_drain(fh_graph *h, uint64_t *exec_dot, uint64_t *scc_label, s
 fh_status fh_graph_mark_executed(fh_graph *h, size_t n, const uint64_t *dot) {
   FH_API_BEGIN
   FH_CHECK(h && (n == 0 || dot), FH_EINVAL, "null argument");
-  for (size_t i = 0; i < n; i++) h->dev.clock.add(dot[i]);
+  for (size_t i = 0; i < n; i++) h->dev.clock_changed |= h->dev.clock.add(dot[i]);
   FH_API_END
 }
 
+// Raise source's contiguous frontier to seq (never lowers it): exceptions at
+// or below it go, and exceptions right above it fold in, as AEClock::add does.
 fh_status fh_graph_set_executed_frontier(fh_graph *h, uint32_t source, uint64_t seq) {
   FH_API_BEGIN
   FH_CHECK(h && source < 256, FH_EINVAL, "bad argument");
-  h->dev.clock.frontier[source] = seq;
+  auto &c = h->dev.clock;
+  FH_CHECK(seq >= c.frontier[source], FH_EINVAL,
+           "set_executed_frontier: the executed frontier cannot move backwards");
+  if (seq == c.frontier[source]) return FH_OK;
+  c.frontier[source] = seq;
+  for (auto it = c.exc.begin(); it != c.exc.end();) {
+    if ((*it >> 56) == source && (*it & 0x00FFFFFFFFFFFFFFull) <= seq)
+      it = c.exc.erase(it);
+    else
+      ++it;
+  }
+  for (;;) {
+    auto it = c.exc.find(fh::make_dot(source, c.frontier[source] + 1));
+    if (it == c.exc.end()) break;
+    c.exc.erase(it);
+    c.frontier[source]++;
+  }
+  h->dev.clock_changed = true;
+  FH_API_END
+}
+
+fh_status fh_graph_set_time(fh_graph *h, uint64_t now_ms) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.now_ms = now_ms;
+  FH_API_END
+}
+
+fh_status fh_graph_monitor_pending(fh_graph *h, uint64_t threshold_ms, uint64_t *dots,
+                                   uint64_t *pending_ms, uint64_t *missing, size_t cap,
+                                   size_t *len) {
+  FH_API_BEGIN
+  FH_CHECK(h && len, FH_EINVAL, "null argument");
+  std::vector<std::pair<uint64_t, uint64_t>> old;
+  std::vector<uint64_t> nm;
+  h->dev.monitor_pending(threshold_ms, old, nm);
+  *len = old.size();
+  for (size_t i = 0; i < old.size() && i < cap; i++) {
+    if (dots) dots[i] = old[i].first;
+    if (pending_ms) pending_ms[i] = old[i].second;
+    if (missing) missing[i] = nm[i];
+  }
+  FH_API_END
+}
+
+fh_status fh_graph_take_metrics(fh_graph *h, uint64_t *chain_size, size_t chain_cap,
+                                uint64_t *exec_delay, size_t delay_cap, size_t *n_chain,
+                                size_t *n_delay) {
+  FH_API_BEGIN
+  FH_CHECK(h && n_chain && n_delay, FH_EINVAL, "null argument");
+  auto &d = h->dev;
+  *n_chain = d.m_chain.size();
+  *n_delay = d.m_delay.size();
+  FH_CHECK((d.m_chain.empty() || (chain_size && chain_cap >= d.m_chain.size())) &&
+               (d.m_delay.empty() || (exec_delay && delay_cap >= d.m_delay.size())),
+           FH_ECAP, "metrics output capacity too small");
+  std::copy(d.m_chain.begin(), d.m_chain.end(), chain_size);
+  std::copy(d.m_delay.begin(), d.m_delay.end(), exec_delay);
+  d.m_chain.clear();
+  d.m_delay.clear();
+  FH_API_END
+}
+
+fh_status fh_graph_passes(fh_graph *h, uint64_t *passes, uint64_t *skipped) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  if (passes) *passes = h->dev.passes;
+  if (skipped) *skipped = h->dev.skipped;
   FH_API_END
 }
 
@@ -540,7 +703,7 @@ fh_status fh_execlog_replay(const fh_execlog *h, fh_graph *g, size_t batch, size
       i++;
     } else if (k == FH_LOG_REPLY_EXECUTED) {
       size_t j = i;
-      while (j < E && L.kind[j] == FH_LOG_REPLY_EXECUTED) dev.clock.add(L.dot[j++]);
+      while (j < E && L.kind[j] == FH_LOG_REPLY_EXECUTED) dev.clock_changed |= dev.clock.add(L.dot[j++]);
       dev.add_batch(0, nullptr, nullptr, nullptr, nullptr, nullptr);  // pending retry
       i = j;
     } else {

@@ -285,7 +285,13 @@ __global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32
         for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
         uint64_t c[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) c[j] = ru[j] != r ? ld_u64(&kap[ru[j]]) + 1 : 0;
+        for (int j = 0; j < 4; j++) {
+          // +1 on the depth half, saturated below 2^32 - 1: an unconverged
+          // run (a cycle the windows missed) must not carry into the ready
+          // time half that k_fb_seed reads
+          const uint64_t k = ru[j] != r ? ld_u64(&kap[ru[j]]) : 0;
+          c[j] = ru[j] == r ? 0 : (uint32_t(k) >= 0xFFFFFFFEu ? k : k + 1);
+        }
 #pragma unroll
         for (int j = 0; j < 4; j++) best = c[j] > best ? c[j] : best;
       }

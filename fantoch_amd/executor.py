@@ -178,16 +178,60 @@ class HipGraphExecutor:
                                                    L.ptr(a) if len(a) else None))
 
     def handle_request_reply(self, replies):
-        """Info -> handle_add (one batch, in reply order); Executed -> executed
-        clock + pending retry (mod.rs:377-408)."""
-        infos = [GraphExecutionInfo.add(r.dot, r.cmd, r.deps) for r in replies if r.kind == "info"]
-        executed = [r.dot for r in replies if r.kind == "executed"]
-        if executed:
-            self.mark_executed(executed)
-        if infos:
-            self.handle_batch(infos)
-        elif executed:
-            self.handle_batch([])  # retry pending vertices against the new clock
+        """In reply order (mod.rs:377-408): each run of consecutive Info
+        replies is one add batch (handle_add per reply), each Executed reply
+        updates the executed clock and retries the pending vertices."""
+        run = []
+        for r in replies:
+            if r.kind == "info":
+                run.append(GraphExecutionInfo.add(r.dot, r.cmd, r.deps))
+                continue
+            if run:
+                self.handle_batch(run)
+                run = []
+            self.mark_executed([r.dot])
+            self.handle_batch([])  # check_pending against the new clock
+        if run:
+            self.handle_batch(run)
+
+    def set_time(self, now_ms: int):
+        """SysTime::millis for the vertices added next (Vertex::new)."""
+        L.check(self._lib.fh_graph_set_time(self._h, int(now_ms)))
+
+    def monitor_pending(self, threshold_ms: int = 1000):
+        """Executor::monitor_pending (index.rs:53-103): [(dot, pending_ms,
+        missing deps)] longest pending first; raises FhError(FH_EINVARIANT)
+        for a pending command without missing dependencies."""
+        n = C.c_size_t(0)
+        L.check(self._lib.fh_graph_monitor_pending(self._h, int(threshold_ms), None, None, None, 0,
+                                                   C.byref(n)))
+        if n.value == 0:
+            return []
+        d = np.zeros(n.value, dtype=np.uint64)
+        t = np.zeros(n.value, dtype=np.uint64)
+        m = np.zeros(n.value, dtype=np.uint64)
+        L.check(self._lib.fh_graph_monitor_pending(self._h, int(threshold_ms), L.ptr(d), L.ptr(t),
+                                                   L.ptr(m), n.value, C.byref(n)))
+        return list(zip(d.tolist(), t.tolist(), m.tolist()))
+
+    def take_metrics(self):
+        """ChainSize / ExecutionDelay values collected since the last call
+        (ExecutorMetricsKind, executor/mod.rs:120-129)."""
+        nc, nd = C.c_size_t(0), C.c_size_t(0)
+        st = self._lib.fh_graph_take_metrics(self._h, None, 0, None, 0, C.byref(nc), C.byref(nd))
+        if nc.value == 0 and nd.value == 0:
+            L.check(st)
+            return [], []
+        ch = np.zeros(max(1, nc.value), dtype=np.uint64)
+        de = np.zeros(max(1, nd.value), dtype=np.uint64)
+        L.check(self._lib.fh_graph_take_metrics(self._h, L.ptr(ch), nc.value, L.ptr(de), nd.value,
+                                                C.byref(nc), C.byref(nd)))
+        return ch[:nc.value].tolist(), de[:nd.value].tolist()
+
+    def passes(self):
+        p, k = C.c_uint64(0), C.c_uint64(0)
+        L.check(self._lib.fh_graph_passes(self._h, C.byref(p), C.byref(k)))
+        return p.value, k.value
 
     def cleanup(self):
         """Executor::cleanup -> check_pending_requests (mod.rs:168-179)."""

@@ -187,10 +187,40 @@ fh_status fh_graph_add_batch(fh_graph *h, size_t n, const uint64_t *dot,
 fh_status fh_graph_drain(fh_graph *h, uint64_t *exec_dot, uint64_t *scc_label,
                          size_t cap, size_t *len);
 
-/* Executed-clock updates (AEClock::add; graph/mod.rs:199-212, 397-405). */
+/* Executed-clock updates (AEClock::add; graph/mod.rs:199-212, 397-405).
+ * set_executed_frontier raises a source's contiguous frontier (FH_EINVAL if
+ * it would move backwards), dropping exceptions at or below it and folding
+ * the ones right above it, as AEClock::add does. */
 fh_status fh_graph_mark_executed(fh_graph *h, size_t n, const uint64_t *dot);
 fh_status fh_graph_set_executed_frontier(fh_graph *h, uint32_t source,
                                          uint64_t seq);
+/* Current time in ms (SysTime::millis of the caller, fantoch/src/time.rs:3-6):
+ * vertices added afterwards are stamped with it (Vertex::new,
+ * graph/tarjan.rs:335-351) and the execution delay of a command is the time
+ * at which it becomes ready minus its stamp (graph/mod.rs:515-520). */
+fh_status fh_graph_set_time(fh_graph *h, uint64_t now_ms);
+/* Executor::monitor_pending -> VertexIndex::monitor_pending
+ * (graph/index.rs:53-103, graph/mod.rs:181-196): the pending vertices
+ * pending for >= threshold_ms (the reference uses 1 s), longest first, with
+ * the number of missing dependencies found through other pending vertices
+ * (missing_dependencies, index.rs:105-142).  FH_EINVARIANT if one of them
+ * has none (the reference panics: a liveness bug).  Any array may be NULL;
+ * *len = count (up to cap entries written). */
+fh_status fh_graph_monitor_pending(fh_graph *h, uint64_t threshold_ms,
+                                   uint64_t *dots, uint64_t *pending_ms,
+                                   uint64_t *missing, size_t cap, size_t *len);
+/* Executor metrics collected since the last call (ExecutorMetricsKind,
+ * fantoch/src/executor/mod.rs:120-129, collected in save_scc,
+ * graph/mod.rs:490-525): chain_size[] = the size of every executed SCC
+ * (ChainSize), exec_delay[] = ms from add to ready of every executed command
+ * (ExecutionDelay).  FH_ECAP (counts set, nothing taken) if a cap is short. */
+fh_status fh_graph_take_metrics(fh_graph *h, uint64_t *chain_size, size_t chain_cap,
+                                uint64_t *exec_delay, size_t delay_cap,
+                                size_t *n_chain, size_t *n_delay);
+/* Graph passes run and pending retries skipped (a retry with no new vertex
+ * where none of the pending set's missing dependencies executed since the
+ * last pass), for tests and tuning. */
+fh_status fh_graph_passes(fh_graph *h, uint64_t *passes, uint64_t *skipped);
 /* Number of pending vertices (VertexIndex size, graph/index.rs:18-51). */
 fh_status fh_graph_pending(fh_graph *h, size_t *count);
 /* Missing dependencies of pending vertices (deps neither executed nor
@@ -413,6 +443,38 @@ fh_status fh_engine_probe_stats_for(fh_engine *h, const char *kernel, float *avg
                                     size_t *launches, double *bytes_per_launch);
 /* Enable/disable per-kernel event timing (adds events between kernels). */
 fh_status fh_engine_set_profiling(fh_engine *h, int on);
+
+/* ======================================================================
+ * Multi-GPU fused engine from one process: one engine
+ * per device over key shards, owner(key) = key mod ndev.  With one key per
+ * command a shard's dependency graph is closed (every dependency joins two
+ * commands of one key), so shards order concurrently with no exchange; each
+ * keeps the global dots and its replicas' logs restricted to its commands.
+ * (Multi-key cross-shard streams go through fh_dep_union and the partial-
+ * replication executor instead: FH_ENOTIMPL for keys_per_cmd > 1.)
+ * ==================================================================== */
+typedef struct fh_multi fh_multi;
+/* devices[ndev] (NULL = 0..ndev-1; a device may repeat). */
+fh_status fh_multi_create(const fh_config *cfg, size_t ndev,
+                          const int32_t *devices, fh_multi **out);
+fh_status fh_multi_destroy(fh_multi *h);
+/* One batch in the fh_engine_stage_logs layout (global command indices). */
+fh_status fh_multi_stage_logs(fh_multi *h, const fh_stream_desc *desc,
+                              const uint64_t *dot, const uint64_t *key_id,
+                              const uint64_t *log_off, const uint32_t *log_cmd);
+fh_status fh_multi_rewind(fh_multi *h);
+/* Every shard on its device concurrently (a host thread per device);
+ * device_ms (may be NULL) = the slowest shard's device time. */
+fh_status fh_multi_run(fh_multi *h, float *device_ms);
+/* Merged in the stream's command order (as fh_engine_results): deps, SCC
+ * labels, exec_rank = the shards' execution orders concatenated (shards
+ * share no dependency), per-key sequences from each key's owner. */
+fh_status fh_multi_results(fh_multi *h, uint32_t *dep_off, uint64_t *dep_dot,
+                           size_t dep_cap, size_t *dep_len, uint64_t *scc_label,
+                           uint32_t *exec_rank, uint32_t *key_off,
+                           uint64_t *key_seq);
+/* Commands staged on shard `shard`. */
+fh_status fh_multi_shard_size(fh_multi *h, size_t shard, size_t *n);
 
 /* ======================================================================
  * Synthetic workload (fantoch/src/client/{workload,key_gen}.rs semantics,

@@ -136,3 +136,74 @@ def test_views_stream_shuffled_arrivals_match_oracle(batch):
     assert got == want
     # SCC partition equals the oracle's
     assert ex.last_labels == dict(zip(ex_o.tolist(), lab_o.tolist()))
+
+
+def _ex():
+    return HipGraphExecutor(process_id=1, shard_id=0, n=3, f=1, key_space=16)
+
+
+def _add(ex, dot, deps, keys=("A",)):
+    ex.handle(GraphExecutionInfo.add(dot, Command(dot, list(keys)), deps))
+
+
+def test_monitor_pending_reports_missing_and_ages():
+    """VertexIndex::monitor_pending (index.rs:53-103): pending commands older
+    than the threshold, longest first, with their missing dependencies (found
+    through other pending vertices)."""
+    ex = _ex()
+    ex.set_time(1000)
+    _add(ex, D((1, 1)), [D((2, 1))])            # waits on (2,1), never added
+    ex.set_time(1500)
+    _add(ex, D((1, 2)), [D((1, 1))])            # waits through (1,1)
+    ex.set_time(2600)
+    got = ex.monitor_pending(1000)
+    assert [(d, t) for d, t, _ in got] == [(D((1, 1)), 1600), (D((1, 2)), 1100)]
+    assert all(m == 1 for _, _, m in got)       # (2,1) in both cases
+    assert ex.monitor_pending(1500) == [(D((1, 1)), 1600, 1)]
+
+
+def test_metrics_chain_size_and_execution_delay():
+    """save_scc (graph/mod.rs:490-525): one ChainSize per SCC, one
+    ExecutionDelay per command (ready time - add time)."""
+    ex = _ex()
+    ex.set_time(10)
+    _add(ex, D((1, 1)), [D((2, 1))])
+    ex.set_time(25)
+    _add(ex, D((2, 1)), [D((1, 1))])            # closes the 2-cycle
+    ex.set_time(30)
+    _add(ex, D((3, 1)), [D((1, 1))])            # a singleton after it
+    chains, delays = ex.take_metrics()
+    assert sorted(chains) == [1, 2]
+    assert sorted(delays) == [0, 0, 15]
+    assert ex.take_metrics() == ([], [])
+
+
+def test_pending_retry_skipped_until_a_missing_dep_executes():
+    """check_pending retries only when a missing dependency executed: an empty
+    retry with nothing resolved runs no graph pass."""
+    ex = _ex()
+    _add(ex, D((1, 1)), [D((3, 7))])
+    p0, s0 = ex.passes()
+    ex.handle_batch([])
+    ex.mark_executed([D((2, 5))])               # unrelated
+    ex.handle_batch([])
+    p1, s1 = ex.passes()
+    assert (p1, s1) == (p0, s0 + 2) and ex.pending() == 1
+    ex.mark_executed([D((3, 7))])
+    ex.handle_batch([])
+    assert ex.passes()[0] == p0 + 1 and ex.pending() == 0
+
+
+def test_executed_frontier_never_moves_back_and_folds_exceptions():
+    ex = _ex()
+    ex.mark_executed([D((2, 3)), D((2, 4)), D((2, 9))])  # exceptions above frontier 0
+    from fantoch_amd import _lib as L
+    L.check(ex._lib.fh_graph_set_executed_frontier(ex._h, 2, 2))
+    # frontier 2 folds 3 and 4 -> 4; (2,9) stays an exception: a dep on (2,5)
+    # is missing, (2,9) and (2,4) are executed
+    _add(ex, D((1, 1)), [D((2, 4)), D((2, 9))])
+    assert ex.pending() == 0
+    _add(ex, D((1, 2)), [D((2, 5))])
+    assert ex.pending() == 1
+    with pytest.raises(L.FhError):
+        L.check(ex._lib.fh_graph_set_executed_frontier(ex._h, 2, 1))
