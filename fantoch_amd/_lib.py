@@ -58,6 +58,14 @@ SIGNATURES = {
     "fh_dep_union": (C.c_int, [C.c_int, S, S, V, V, V, V, P(S), V]),
     "fh_keydeps_add_batch_device": (C.c_int, [V, S, S, V, V, V, V, V, S, P(S), V]),
     "fh_keydeps_add_batch_rw": (C.c_int, [V, S, V, V, V, V, V, V, V, V, V, S, P(S)]),
+    "fh_keyclocks_create": (C.c_int, [C.c_uint32, C.c_uint64, P(fh_config), P(V)]),
+    "fh_keyclocks_destroy": (C.c_int, [V]),
+    "fh_keyclocks_clock_next": (C.c_int, [V, P(C.c_uint64)]),
+    "fh_keyclocks_clock_join": (C.c_int, [V, C.c_uint64]),
+    "fh_keyclocks_add": (C.c_int, [V, S, V, V, V, V]),
+    "fh_keyclocks_remove": (C.c_int, [V, S, V, V, V]),
+    "fh_keyclocks_predecessors": (C.c_int, [V, S, V, V, V, V, V, V, S, P(S), V, V, S, P(S)]),
+    "fh_keyclocks_len": (C.c_int, [V, P(S)]),
     "fh_pred_create": (C.c_int, [C.c_uint32, C.c_uint64, P(fh_config), P(V)]),
     "fh_pred_destroy": (C.c_int, [V]),
     "fh_pred_add_batch": (C.c_int, [V, S, V, V, V, V]),

@@ -357,6 +357,52 @@ fh_status fh_pred_drain(fh_pred *h, uint64_t *exec_dot, size_t cap,
 fh_status fh_pred_pending(fh_pred *h, size_t *count);
 
 /* ======================================================================
+ * Caesar's KeyClocks -- the timestamp-ordered conflict index whose
+ * predecessors become a command's dependencies.
+ * Replaces SequentialKeyClocks
+ * (fantoch_ps/src/protocol/common/pred/clocks/keys/sequential.rs:14-152)
+ * behind the KeyClocks trait (pred/clocks/keys/mod.rs:13-45).  Clocks are
+ * packed (seq << 8) | process_id: the integer order is Clock's derived Ord
+ * (pred/clocks/mod.rs:15-30).  Dependency sets come back in ascending clock
+ * order, without repeats.
+ * ==================================================================== */
+typedef struct fh_keyclocks fh_keyclocks;
+/* KeyClocks::new(process_id, shard_id) (sequential.rs:22-30). */
+fh_status fh_keyclocks_create(uint32_t process_id, uint64_t shard_id,
+                              const fh_config *cfg, fh_keyclocks **out);
+fh_status fh_keyclocks_destroy(fh_keyclocks *h);
+/* clock_next / clock_join (sequential.rs:33-42). */
+fh_status fh_keyclocks_clock_next(fh_keyclocks *h, uint64_t *clock);
+fh_status fh_keyclocks_clock_join(fh_keyclocks *h, uint64_t clock);
+/* A batch of KeyClocks::add(dot, cmd, clock) (sequential.rs:43-56): each
+ * command's keys (key_off[n+1], key_id[], <= 8 per command) get the entry
+ * clock -> dot.  FH_EINVARIANT (no state change) for a timestamp added twice
+ * on a key. */
+fh_status fh_keyclocks_add(fh_keyclocks *h, size_t n, const uint64_t *dot,
+                           const uint32_t *key_off, const uint64_t *key_id,
+                           const uint64_t *clock);
+/* A batch of KeyClocks::remove(cmd, clock) (sequential.rs:58-75).
+ * FH_EINVARIANT (no state change) for a timestamp never added. */
+fh_status fh_keyclocks_remove(fh_keyclocks *h, size_t n, const uint32_t *key_off,
+                              const uint64_t *key_id, const uint64_t *clock);
+/* A batch of KeyClocks::predecessors(dot, cmd, clock, higher)
+ * (sequential.rs:77-119): pred_off[n+1] / pred_dot[] = the dots on the
+ * command's keys with a lower clock; higher_off / higher_dot (all three
+ * higher_* NULL = `higher: None`) = those with a higher clock.  Sizes are
+ * always reported (*pred_len, *higher_len); FH_ECAP if a cap is short
+ * (nothing written there).  FH_EINVARIANT if another command holds the same
+ * timestamp on a key (:108-112). */
+fh_status fh_keyclocks_predecessors(fh_keyclocks *h, size_t n, const uint64_t *dot,
+                                    const uint32_t *key_off, const uint64_t *key_id,
+                                    const uint64_t *clock, uint32_t *pred_off,
+                                    uint64_t *pred_dot, size_t pred_cap,
+                                    size_t *pred_len, uint32_t *higher_off,
+                                    uint64_t *higher_dot, size_t higher_cap,
+                                    size_t *higher_len);
+/* Entries held (sum over keys of CommandsPerKey sizes). */
+fh_status fh_keyclocks_len(fh_keyclocks *h, size_t *entries);
+
+/* ======================================================================
  * Fused engine -- a committed command stream, device resident end to end:
  * KeyDeps (one replica, or the fast-quorum views of Atlas/EPaxos with the
  * QuorumDeps union, quorum.rs:28-98) -> dependency graph -> SCC ->

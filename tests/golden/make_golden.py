@@ -170,8 +170,47 @@ def sccs_found_and_missing_dep():
     }
 
 
+def key_clocks():
+    """clock_test + predecessors_test of SequentialKeyClocks
+    (fantoch_ps/src/protocol/common/pred/clocks/keys/sequential.rs:167-...),
+    transcribed: clocks as [seq, process_id], dots as [source, seq]; each
+    check = (keys, clock) -> (higher/"blocking", predecessors)."""
+    p1, p2 = 1, 2
+    A, B, C, AC = ["A"], ["B"], ["C"], ["A", "C"]
+    dot, dot_1, dot_3 = [p1, 0], [p1, 1], [p1, 3]
+    c = {k: [k, p1] for k in (1, 2, 3, 4)}
+
+    def chk(keys, clock, blocking, preds):
+        return {"op": "check", "dot": dot, "keys": keys, "clock": clock,
+                "blocking": blocking, "predecessors": preds}
+
+    ops = [chk(A, c[2], [], []),
+           {"op": "add", "dot": dot_1, "keys": A, "clock": c[1]},
+           chk(A, c[2], [], [dot_1]), chk(B, c[2], [], []), chk(C, c[2], [], []),
+           chk(AC, c[2], [], [dot_1]),
+           {"op": "add", "dot": dot_3, "keys": AC, "clock": c[3]},
+           chk(A, c[2], [dot_3], [dot_1]), chk(B, c[2], [], []), chk(C, c[2], [dot_3], []),
+           chk(AC, c[2], [dot_3], [dot_1]),
+           chk(A, c[4], [], [dot_1, dot_3]), chk(B, c[4], [], []), chk(C, c[4], [], [dot_3]),
+           chk(AC, c[4], [], [dot_1, dot_3]),
+           {"op": "remove", "keys": A, "clock": c[1]},
+           chk(A, c[2], [dot_3], []), chk(B, c[2], [], []), chk(C, c[2], [dot_3], []),
+           chk(AC, c[2], [dot_3], []),
+           chk(A, c[4], [], [dot_3]), chk(B, c[4], [], []), chk(C, c[4], [], [dot_3]),
+           chk(AC, c[4], [], [dot_3]),
+           {"op": "remove", "keys": AC, "clock": c[3]},
+           chk(A, c[4], [], []), chk(B, c[4], [], []), chk(C, c[4], [], []), chk(AC, c[4], [], [])]
+    clock_ops = [{"op": "next", "expect": [1, p1]}, {"op": "next", "expect": [2, p1]},
+                 {"op": "join", "clock": [1, p2]},
+                 {"op": "next", "expect": [3, p1]}, {"op": "next", "expect": [4, p1]},
+                 {"op": "join", "clock": [10, p2]},
+                 {"op": "next", "expect": [11, p1]}, {"op": "next", "expect": [12, p1]}]
+    return {"process_id": p1, "shard_id": 0, "predecessors_test": ops, "clock_test": clock_ops}
+
+
 def main():
     fixtures = {
+        "key_clocks.json": key_clocks(),
         "key_deps_flow.json": key_deps_flow(),
         "quorum_deps.json": quorum(),
         "graph_simple.json": graph_simple(),
