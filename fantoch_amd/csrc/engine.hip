@@ -194,7 +194,8 @@ __device__ __forceinline__ void cmd_union_regs(
     const CT *__restrict__ dep_code, const uint64_t *__restrict__ dlog,
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
-    uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n) {
+    uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n,
+    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
@@ -232,17 +233,25 @@ __device__ __forceinline__ void cmd_union_regs(
       }
     }
   }
-  uint64_t *dd = dep_dot + size_t(i) * S;
+  // out_off: the committed deps go straight to their CSR row (sized by
+  // k_cmd_count); otherwise to a fixed-stride row, zero padded
+  uint64_t *dd = out_off ? dep_dot + out_off[i] : dep_dot + size_t(i) * S;
+  const uint32_t cap = out_off ? out_off[i + 1] - out_off[i] : S;
   uint32_t m = 0;
   uint64_t prev = 0;  // dots are never 0
 #pragma unroll
   for (uint32_t t = 0; t < kRegSlots; t++) {
     if (r[t] != ~0ull && r[t] != prev) {
-      dd[m++] = r[t];
+      if (m < cap) dd[m] = r[t];
+      m++;
       prev = r[t];
     }
   }
-  for (uint32_t q = m; q < S; q++) dd[q] = 0;
+  if (out_off) {
+    if (m != cap) atomicOr(err, 1u);  // an in-batch dot repeated outside the batch
+  } else {
+    for (uint32_t q = m; q < S; q++) dd[q] = 0;
+  }
   uint32_t *ds = dst + size_t(i) * S;
   uint32_t nv = 0;
 #pragma unroll
@@ -273,26 +282,27 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ dep_cnt,
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
-                             uint64_t bbase) {
+                             uint64_t bbase, const uint32_t *__restrict__ out_off,
+                             uint32_t *__restrict__ err) {
   // uniform: the register path, with a sorting network sized to the row
   if (S <= 4) {
     GRID_STRIDE(i, n) {
       cmd_union_regs<4>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n);
+                        nblocked, nv_out, bbase, n, out_off, err);
     }
     return;
   }
   if (S <= 8) {
     GRID_STRIDE(i, n) {
       cmd_union_regs<8>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n);
+                        nblocked, nv_out, bbase, n, out_off, err);
     }
     return;
   }
   if (S <= kRegSlots) {
     GRID_STRIDE(i, n) {
       cmd_union_regs<kRegSlots>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                                blocked0, nblocked, nv_out, bbase, n);
+                                blocked0, nblocked, nv_out, bbase, n, out_off, err);
     }
     return;
   }
@@ -326,6 +336,50 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     dep_cnt[i] = m;
     if (blocked0) blocked0[i] = missing;
     if (missing) atomicAdd(nblocked, 1u);
+  }
+}
+
+// Committed-dep count per command (rows of at most kRegSlots slots), from
+// the codes alone: in-batch deps dedup by vid, external ones by dot (dots are
+// unique, so this is the union's count).  Its scan places k_cmd_engine's
+// output straight into the CSR: no fixed-stride rows, no compaction pass.
+template <uint32_t kSlots, class CT>
+__device__ __forceinline__ uint32_t cmd_count_regs(uint32_t i, uint32_t S,
+                                                   const CT *__restrict__ dep_code,
+                                                   const uint64_t *__restrict__ dlog,
+                                                   uint64_t bbase, uint32_t n) {
+  uint64_t r[kSlots];
+#pragma unroll
+  for (uint32_t t = 0; t < kSlots; t++) {
+    r[t] = ~0ull;
+    if (t < S) {
+      uint64_t x = 0;
+      uint32_t v = 0;
+      const int kind = decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
+      r[t] = kind == 1 ? uint64_t(v) : kind == 2 ? x : ~0ull;  // dots >= 2^56 > vids
+    }
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < kSlots; t++) {
+    bool dup = r[t] == ~0ull;
+#pragma unroll
+    for (uint32_t q = 0; q < t; q++) dup |= r[q] == r[t];
+    c += dup ? 0u : 1u;
+  }
+  return c;
+}
+
+template <class CT>
+__global__ void k_cmd_count(uint32_t n, uint32_t S, const CT *__restrict__ dep_code,
+                            const uint64_t *__restrict__ dlog, uint64_t bbase,
+                            uint32_t *__restrict__ cnt) {
+  if (S <= 4) {
+    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<4>(i, S, dep_code, dlog, bbase, n);
+  } else if (S <= 8) {
+    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<8>(i, S, dep_code, dlog, bbase, n);
+  } else {
+    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<kRegSlots>(i, S, dep_code, dlog, bbase, n);
   }
 }
 
@@ -606,6 +660,7 @@ struct EngineDevice {
   DBuf<uint32_t> dep32;  // replica views: 32-bit element dependency codes
   DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
   // outputs of the last run (materialised inside run(), copied by results())
+  bool deps_direct = false;  // run_general wrote o_dep_off / o_dep (no compaction)
   DBuf<uint32_t> o_dep_off;
   DBuf<uint64_t> o_dep;
   const uint64_t *o_label = nullptr;  // [n] min dot of each command's SCC
@@ -1066,23 +1121,42 @@ struct EngineDevice {
                    const uint32_t *bkey, const uint64_t *bdot, uint64_t bbase) {
     uint32_t *svid = sorted_vid.get();
     mark("keydeps_prev");
-    uint64_t *ddot = dep_dot.ensure(M + 1);
     uint32_t *dcnt = dep_cnt.ensure(n + 1);
     uint32_t *dd = dst.ensure(M + 1);
-    FH_HIP(hipMemsetAsync(scal.get(), 0, sizeof(uint32_t), stream));
+    FH_HIP(hipMemsetAsync(scal.get(), 0, 2 * sizeof(uint32_t), stream));
     uint32_t *ecnt = views && S >= 8 ? edge_cnt.ensure(n + 1) : (uint32_t *)nullptr;
+    // rows of <= kRegSlots slots: count, scan, and the union writes the
+    // committed-deps CSR directly; wider rows go through fixed-stride rows
+    deps_direct = S <= kRegSlots;
+    uint64_t *ddot = nullptr;
+    const uint32_t *doff = nullptr;
+    if (deps_direct) {
+      if (views)
+        k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, stream>>>(
+            n, S, (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(), bbase, dcnt);
+      else
+        k_cmd_count<uint64_t><<<grid_for(n, B), B, 0, stream>>>(
+            n, S, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(), bbase, dcnt);
+      uint32_t *off = o_dep_off.ensure(n + 1);
+      exclusive_scan_u32(dcnt, off, n, scan_ws, stream);
+      doff = off;
+      ddot = o_dep.ensure(M + 1);
+      mark("keydeps_count");
+    } else {
+      ddot = dep_dot.ensure(M + 1);
+    }
     if (views)
       probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
                     k_cmd_engine<uint32_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
                     (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                    scal.get(), ecnt, bbase);
+                    scal.get(), ecnt, bbase, doff, scal.get() + 1);
     else
       probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
                     k_cmd_engine<uint64_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
                     (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                    scal.get(), ecnt, bbase);
+                    scal.get(), ecnt, bbase, doff, scal.get() + 1);
     mark("keydeps_union");
     const uint32_t *gdst = dd, *goff = nullptr;
     if (views && S >= 8) {  // measured: a win at S = 12 (C5), flat or worse at 3 and 6
@@ -1134,6 +1208,9 @@ struct EngineDevice {
   // results() only copies them to the host.
   void materialize(uint32_t n, uint32_t S, const uint64_t *bdot) {
     uint32_t *off = o_dep_off.ensure(n + 1);
+    if (!sv_fused && deps_direct) {
+      // written by the union (k_cmd_count sized the rows)
+    } else {
     if (sv_fused) {
       // one dependency slot per command: decode, count = slot used
       S = 1;
@@ -1144,6 +1221,7 @@ struct EngineDevice {
     exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
     k_compact_deps<<<grid_for(n, B), B, 0, stream>>>(n, S, dep_dot.get(), off,
                                                       o_dep.ensure(size_t(n) * S + 1));
+    }
     mark("out_deps");
     if (gout.trivial) {
       // singleton SCCs in arrival order: label = own dot, rank = position
@@ -1193,6 +1271,11 @@ struct EngineDevice {
     FH_CHECK(staged && cursor > 0, FH_EINVAL, "no run to read results from");
     FH_HIP(hipStreamSynchronize(stream));
     const uint32_t n = uint32_t(desc.n);
+    if (!sv_fused && deps_direct) {
+      uint32_t bad = 0;
+      FH_HIP(hipMemcpy(&bad, scal.get() + 1, sizeof(bad), hipMemcpyDeviceToHost));
+      FH_CHECK(bad == 0, FH_EINVARIANT, "a dot of the batch repeats a dot of an earlier batch");
+    }
     if (dep_off || dep_out || dep_len) {
       uint32_t total = 0;
       FH_HIP(hipMemcpyAsync(&total, o_dep_off.get() + n, sizeof(total), hipMemcpyDeviceToHost,

@@ -88,6 +88,8 @@ struct GraphCore {
   DBuf<uint32_t> t_h, t_rank, t_cnt, t_start;
   DBuf<uint64_t> t_prof;  // tile path: ready time, group rank/count/start
   uint32_t dbg_tile_fail = 0, dbg_tile_ok = 0;
+  uint32_t tile_r0 = 1536;  // graph_tile: first reach bound to try (set from
+                            // the last run's maximum excess)
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)
   bool profile = false;
   uint32_t dbg_rounds = 0, dbg_hprop = 0, dbg_reach = 0;  // FH_GRAPH_DEBUG counters

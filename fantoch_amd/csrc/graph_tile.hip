@@ -39,6 +39,7 @@
 //     list of raised vertices (H(v) > v) of the group's window.
 // Global epilogue (graph_core.hip): exclusive scan of the group counts gives
 // each group's first execution position, exec_rank = start[H] + rank.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -50,6 +51,10 @@ namespace {
 constexpr int kTileThreads = 1024;
 constexpr int kTileC = 10240;  // max context vertices (LDS: 15 B per vertex)
 constexpr uint16_t kNone = 0xFFFF;
+constexpr int kMaxCore = 8;     // core vertices per thread (T <= 8192)
+
+// R0 rounded up to a multiple of 64 (at least 256)
+static uint32_t round_r0(uint32_t x) { return std::max<uint32_t>(256, (x + 63) & ~63u); }
 
 // exclusive scan of one value per thread over the 1024-thread block
 __device__ __forceinline__ uint32_t tile_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
@@ -131,16 +136,20 @@ struct TileOut {
                      // [4] max H sweeps, [5] max SCC rounds, [6] max group
   const uint8_t *redo;  // [tiles] or null: only tiles with redo[t] run
   unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
+  int r0;      // certified reach bound R0 (L = 2·R0)
+  int core;    // core vertices per tile T (T + 2L <= kTileC, T <= kMaxCore·1024)
+  int hblock;  // H sweeps: 1 = each wave walks a contiguous block in ascending
+               // steps of 64 (updates of a block's earlier vertices are seen by
+               // its later ones in the same sweep), 0 = block-strided
 };
 
 // One tile: core [a, a + T), context [a - L, a + T + L) with L = 2·R0 and
 // T + 2L <= kTileC.
-template <int S, int R0, int T>
+template <int S>
 __global__ void __launch_bounds__(kTileThreads)
     k_graph_tile(uint32_t V, const uint32_t *__restrict__ dst, const uint64_t *__restrict__ dot,
                  TileOut out) {
-  constexpr int L = 2 * R0;
-  static_assert(T + 2 * L <= kTileC, "tile context exceeds LDS");
+  const int R0 = out.r0, T = out.core, L = 2 * R0;  // host: T + 2L <= kTileC
   if (out.redo && !out.redo[blockIdx.x]) return;
   __shared__ uint16_t eL[S][kTileC];
   __shared__ uint16_t sH[kTileC];
@@ -169,6 +178,14 @@ __global__ void __launch_bounds__(kTileThreads)
   const int ca = int(a - lo), cb = int(b - lo);  // core, local
   if (tid < 3) s_ch[tid] = 0;
   if (tid == 0) s_fail = s_maxex = s_over = s_long = 0;
+  // the core vertices' own dots, loaded now and used by the last phase (its
+  // labels and dot tie-breaks): the loads complete behind the LDS phases
+  uint64_t pdot[kMaxCore];
+#pragma unroll
+  for (int j = 0; j < kMaxCore; j++) {
+    const int x = ca + tid + j * kTileThreads;
+    pdot[j] = x < cb ? dot[lo + x] : 0ull;
+  }
 
   // 1. context edges; certificate part 2: forward spans of core vertices
   uint32_t nlong = 0;
@@ -209,8 +226,12 @@ __global__ void __launch_bounds__(kTileThreads)
   // 2. H: max arrival position reachable (context subgraph).  H(x) is a
   // vertex x reaches, so H(H(x)) is reachable too: pointer jumping collapses
   // chains of forward dependencies in logarithmically many sweeps.
+  const int hP = 64 * ((C + kTileThreads - 1) / kTileThreads);  // per-wave block
   const int hs = sweeps(
-      [&](int x) {
+      [&](int i) {
+        const int x = out.hblock ? ((i & (kTileThreads - 1)) >> 6) * hP + (i >> 10) * 64 + (i & 63)
+                                 : i;
+        if (x >= C) return false;
         uint32_t h = sH[x];
         const uint32_t h0 = h;
 #pragma unroll
@@ -225,7 +246,7 @@ __global__ void __launch_bounds__(kTileThreads)
         }
         return false;
       },
-      C, nullptr);
+      out.hblock ? (kTileThreads / 64) * hP : C, nullptr);
   phase(1);
 
   // 3. certificate part 1: core excess < R0
@@ -436,8 +457,12 @@ __global__ void __launch_bounds__(kTileThreads)
   }
   __syncthreads();
   uint32_t gmax = 0;
-  for (int x = ca + tid; x < cb; x += kTileThreads) {
+#pragma unroll
+  for (int j = 0; j < kMaxCore; j++) {
+    const int x = ca + tid + j * kTileThreads;
+    if (x >= cb) break;
     const uint32_t v = lo + x;
+    const uint64_t dotx = pdot[j];
     const uint16_t t = sH[x];
     uint32_t cnt = 0, rk = 0;
     uint64_t lab = 0;  // min dot of x's SCC (0 = x's own: a singleton group)
@@ -445,16 +470,10 @@ __global__ void __launch_bounds__(kTileThreads)
       const uint32_t b0 = t ? gend[t - 1] : 0u, b1 = gend[t];
       cnt = b1 - b0;
       const uint32_t dx = W1[sR[x]], mx = sR[x];
-      uint64_t dotx = 0;
-      bool have_dot = false;
       auto cmp = [&](uint32_t y) {
         const uint32_t dy = W1[sR[y]], my = sR[y];
         if (dy != dx) return dy < dx;
         if (my != mx) return my < mx;
-        if (!have_dot) {
-          dotx = dot[v];
-          have_dot = true;
-        }
         return dot[lo + y] < dotx;
       };
       if (t != uint32_t(x)) rk += cmp(t);
@@ -473,13 +492,6 @@ __global__ void __launch_bounds__(kTileThreads)
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) dy[u] = st[u] == 0 ? dot[lo + ys[u]] : 0ull;
-        bool any_tie = false;
-#pragma unroll
-        for (int u = 0; u < 8; u++) any_tie |= st[u] == 0;
-        if (any_tie && !have_dot) {
-          dotx = dot[v];
-          have_dot = true;
-        }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
           rk += st[u] < 0 || (st[u] == 0 && dy[u] < dotx);
@@ -494,10 +506,7 @@ __global__ void __launch_bounds__(kTileThreads)
       }
       gmax = max(gmax, cnt + 1);
     }
-    {
-      const uint64_t own = dot[v];
-      out.label[v] = (lab == 0 || own < lab) ? own : lab;
-    }
+    out.label[v] = (lab == 0 || dotx < lab) ? dotx : lab;
     out.rep[v] = lo + sR[x];
     out.hgrp[v] = lo + t;
     out.grank[v] = rk;
@@ -521,20 +530,22 @@ __global__ void k_exec_from_groups(uint32_t V, const uint32_t *__restrict__ hgrp
 
 }  // namespace
 
-template <int R0, int T>
 static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint64_t *dot,
                          const TileOut &to, hipStream_t stream) {
-  const uint32_t tiles = (V + T - 1) / T;
+  FH_CHECK(to.core >= 1024 && to.core <= kMaxCore * kTileThreads &&
+               to.core + 4 * to.r0 <= kTileC && to.r0 >= 64,
+           FH_EINVARIANT, "graph_tile: bad tile geometry");
+  const uint32_t tiles = (V + to.core - 1) / to.core;
   // algorithmic bytes: read the vertex's S edge slots and write rep, H, rank
   // and group count (the context halo re-reads are overhead, not algorithmic)
   const double bytes = double(V) * (4.0 * S + 16.0);
   switch (S) {
     case 2:
-      probed_launch("graph_tile", bytes, k_graph_tile<2, R0, T>, dim3(tiles), dim3(kTileThreads),
+      probed_launch("graph_tile", bytes, k_graph_tile<2>, dim3(tiles), dim3(kTileThreads),
                     stream, V, dst, dot, to);
       break;
     default:
-      probed_launch("graph_tile", bytes, k_graph_tile<3, R0, T>, dim3(tiles), dim3(kTileThreads),
+      probed_launch("graph_tile", bytes, k_graph_tile<3>, dim3(tiles), dim3(kTileThreads),
                     stream, V, dst, dot, to);
       break;
   }
@@ -551,39 +562,52 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.gcount = t_cnt.ensure(V + 1);
   to.stat = stat;
   to.redo = nullptr;
+  static const int hblock = getenv("FH_TILE_HBLOCK") ? atoi(getenv("FH_TILE_HBLOCK")) : 1;
+  to.hblock = hblock;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   to.prof = nullptr;
   if (debug) {
     to.prof = reinterpret_cast<unsigned long long *>(t_prof.ensure(16));
     FH_HIP(hipMemsetAsync(to.prof, 0, 8 * sizeof(unsigned long long), stream));
   }
-  // certified reach bounds, tried in order: R0 = 1536 with 4096-vertex cores,
-  // then R0 = 2048 with 2048-vertex cores (each a context of <= 10240)
+  // Certified reach bound R0 and core T = min(kTileC - 4·R0, 8192): a run
+  // starts from the bound the last run's maximum excess calls for (a tighter
+  // R0 = longer cores, less halo per core vertex); a certificate failure
+  // retries with a larger bound (the kernel reports the excess it saw), up to
+  // R0 = 2048, then the global path.
   bool ok = false;
-  for (int level = 0; level < 2 && !ok; level++) {
+  uint32_t st[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t r0 = tile_r0;
+  for (int attempt = 0; attempt < 4 && !ok; attempt++) {
+    to.r0 = int(r0);
+    to.core = std::min(kTileC - 4 * int(r0), kMaxCore * kTileThreads);
     FH_HIP(hipMemsetAsync(stat, 0, 7 * sizeof(uint32_t), stream));
-    if (level == 0)
-      launch_tiles<1536, 4096>(V, in.stride, in.dst, in.dot, to, stream);
-    else
-      launch_tiles<2048, 2048>(V, in.stride, in.dst, in.dot, to, stream);
-    uint32_t st[7];
+    if (to.prof) FH_HIP(hipMemsetAsync(to.prof, 0, 8 * sizeof(unsigned long long), stream));
+    launch_tiles(V, in.stride, in.dst, in.dot, to, stream);
     fetch_u32(stat, st, 7, stream);
     ok = st[0] == 0;
     if (debug)
       fprintf(stderr,
-              "fh graph_tile: V=%u level=%d failed_tiles=%u max_excess=%u over=%u long_fwd=%u "
-              "max_sweeps=%u max_rounds=%u max_group=%u\n",
-              V, level, st[0], st[1], st[2], st[3], st[4], st[5], st[6]);
+              "fh graph_tile: V=%u R0=%u T=%d failed_tiles=%u max_excess=%u over=%u "
+              "long_fwd=%u max_sweeps=%u max_rounds=%u max_group=%u\n",
+              V, r0, to.core, st[0], st[1], st[2], st[3], st[4], st[5], st[6]);
+    if (ok || r0 >= 2048) break;
+    r0 = std::min<uint32_t>(2048, std::max<uint32_t>(r0 + r0 / 4, round_r0(st[1] + st[1] / 8)));
   }
-  if (debug) {
+  // next run: this run's excess with a small margin (a failure there only
+  // costs one retry)
+  tile_r0 = ok ? std::min<uint32_t>(2048, round_r0(st[1] + st[1] / 32 + 16)) : 1536;
+  if (debug && ok) {
     unsigned long long pr[8];
     FH_HIP(hipMemcpyAsync(pr, to.prof, sizeof(pr), hipMemcpyDeviceToHost, stream));
     FH_HIP(hipStreamSynchronize(stream));
     // wall_clock64 runs at 100 MHz on gfx9: ticks * 10 ns, per tile average
-    const double tiles = double((V + 4095) / 4096);
-    fprintf(stderr, "fh graph_tile phases (us per tile): load %.1f H %.1f raised %.1f reach1 %.1f "
-            "rounds+depth %.1f rank %.1f\n", pr[0] * 0.01 / tiles, pr[1] * 0.01 / tiles,
-            pr[2] * 0.01 / tiles, pr[3] * 0.01 / tiles, pr[4] * 0.01 / tiles, pr[5] * 0.01 / tiles);
+    // (the profile sums every launch of this run)
+    const double tiles = double((V + to.core - 1) / to.core);
+    fprintf(stderr, "fh graph_tile phases (us per tile, T=%d): load %.1f H %.1f raised %.1f "
+            "reach1 %.1f rounds+depth %.1f rank %.1f\n", to.core, pr[0] * 0.01 / tiles,
+            pr[1] * 0.01 / tiles, pr[2] * 0.01 / tiles, pr[3] * 0.01 / tiles,
+            pr[4] * 0.01 / tiles, pr[5] * 0.01 / tiles);
   }
   mark("graph_tile");
   if (!ok) {

@@ -122,4 +122,18 @@ def test_caesar_predecessors_feed_the_executor():
         off[j + 1] = len(flat)
     want, pending = O.pred_run(a_dots, a_clk, off, np.asarray(flat, dtype=np.uint64))
     assert pending == 0
-    assert ex.executed_order == [int(x) for x in want]
+    # parity = each key's execution sequence (the interleaving across keys
+    # depends on batching: the reference's is the order commits arrive in)
+    keys_of = {d: ks for d, ks in zip(dots, keys)}
+    clock_of = {d: c for d, c in zip(dots, clocks)}
+
+    def per_key(seq):
+        out = {}
+        for d in seq:
+            for k in keys_of[int(d)]:
+                out.setdefault(k, []).append(int(d))
+        return out
+    got = per_key(ex.executed_order)
+    assert got == per_key(want)
+    for k, seq in got.items():  # Caesar: a key's commands run in clock order
+        assert [clock_of[d] for d in seq] == sorted(clock_of[d] for d in seq)
