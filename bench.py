@@ -96,15 +96,17 @@ def cpu_baseline_c4(w, sample):
 
 
 def timed_steps(eng, steps, barrier, rewind=True):
-    import torch
+    # eng.sync() = hipStreamSynchronize on the engine's stream: the library's
+    # HIP runtime is not torch's, so torch.cuda.synchronize() would not wait
+    # for the engine's kernels
     barrier()
-    torch.cuda.synchronize()
+    eng.sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         if rewind:
             eng.rewind()
         eng.run(sync=False)
-    torch.cuda.synchronize()
+    eng.sync()
     t1 = time.perf_counter()
     barrier()
     return t1 - t0
@@ -117,7 +119,7 @@ def probe_pass(eng, names, steps, rewind=True):
         if rewind:
             eng.rewind()
         eng.run(sync=False)
-    torch.cuda.synchronize()
+    eng.sync()
     probes = {}
     for name in [x for x in names.split(",") if x]:
         ms_, nl_, by_ = eng.probe_stats(name)
@@ -172,7 +174,7 @@ def secondary_c2(args, local):
                            None, None, s.key_space) for i in range(warm + steps)])
     for _ in range(warm):
         eng.run(sync=False)
-    torch.cuda.synchronize()
+    eng.sync()
     el = timed_steps(eng, steps, lambda: None, rewind=False)
     r = eng.results()
     eng.close()
@@ -215,7 +217,7 @@ def main():
     for _ in range(args.warmup):
         eng.rewind()
         eng.run(sync=False)
-    torch.cuda.synchronize()
+    eng.sync()
     elapsed = timed_steps(eng, args.steps, barrier)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")

@@ -111,6 +111,7 @@ SIGNATURES = {
     "fh_multi_destroy": (C.c_int, [V]),
     "fh_multi_stage_logs": (C.c_int, [V, P(fh_stream_desc), V, V, V, V]),
     "fh_multi_rewind": (C.c_int, [V]),
+    "fh_multi_sync": (C.c_int, [V]),
     "fh_multi_run": (C.c_int, [V, P(C.c_float)]),
     "fh_multi_results": (C.c_int, [V, V, V, S, P(S), V, V, V, V]),
     "fh_multi_shard_size": (C.c_int, [V, S, P(S)]),
@@ -120,6 +121,7 @@ SIGNATURES = {
     "fh_workload_generate_shard": (C.c_int, [P(fh_workload), C.c_uint64, S, C.c_uint32,
                                              C.c_uint32, P(S), V, V, V, V]),
     "fh_engine_rewind": (C.c_int, [V]),
+    "fh_engine_sync": (C.c_int, [V]),
 }
 
 _lib = None

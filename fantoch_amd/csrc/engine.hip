@@ -517,28 +517,59 @@ __global__ void k_seq_dots(uint32_t m, const uint32_t *__restrict__ pk_vid,
 }
 
 // executed-clock frontier advance for a fully executed batch: per-source
-// min / max / count of the batch's sequences, reduced in LDS first
+// max / count of the batch's sequences.  Sources 1..kRegSrc accumulate in
+// registers (a batch has few sources: n of the configuration), others in
+// LDS; one wave reduction per source at the end, one global atomic per
+// source per workgroup.  (Per-element LDS atomics serialised on the ~5 hot
+// addresses: 365 us at 100M; a ballot loop per wave was compute bound.)
+constexpr int kRegSrc = 8;
 __global__ void __launch_bounds__(256)
-    k_src_stats(uint32_t n, const uint64_t *__restrict__ dot, unsigned long long *__restrict__ mn,
-                unsigned long long *__restrict__ mx, unsigned int *__restrict__ cnt) {
-  __shared__ unsigned long long s_mn[256], s_mx[256];
+    k_src_stats(uint32_t n, const uint64_t *__restrict__ dot, unsigned long long *__restrict__ mx,
+                unsigned int *__restrict__ cnt) {
+  __shared__ unsigned long long s_mx[256];
   __shared__ unsigned int s_cnt[256];
-  s_mn[threadIdx.x] = ~0ull;
   s_mx[threadIdx.x] = 0;
   s_cnt[threadIdx.x] = 0;
   __syncthreads();
+  uint64_t rmx[kRegSrc];
+  uint32_t rcnt[kRegSrc];
+#pragma unroll
+  for (int q = 0; q < kRegSrc; q++) rmx[q] = 0, rcnt[q] = 0;
   GRID_STRIDE(i, n) {
     const uint64_t d = dot[i];
-    const uint32_t s = uint32_t(d >> 56);
-    const unsigned long long q = d & 0x00FFFFFFFFFFFFFFull;
-    atomicMin(&s_mn[s], q);
-    atomicMax(&s_mx[s], q);
-    atomicAdd(&s_cnt[s], 1u);
+    const uint32_t src = uint32_t(d >> 56);
+    const uint64_t seq = d & 0x00FFFFFFFFFFFFFFull;
+    if (src >= 1 && src <= uint32_t(kRegSrc)) {
+#pragma unroll
+      for (int q = 0; q < kRegSrc; q++)
+        if (src == uint32_t(q + 1)) {
+          rmx[q] = seq > rmx[q] ? seq : rmx[q];
+          rcnt[q]++;
+        }
+    } else {
+      atomicMax(&s_mx[src], (unsigned long long)seq);
+      atomicAdd(&s_cnt[src], 1u);
+    }
+  }
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < kRegSrc; q++) {
+    uint64_t m = rmx[q];
+    uint32_t c = rcnt[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t m2 = __shfl_xor(m, o, 64);
+      m = m2 > m ? m2 : m;
+      c += __shfl_xor(c, o, 64);
+    }
+    if (lane == 0 && c) {
+      atomicMax(&s_mx[q + 1], (unsigned long long)m);
+      atomicAdd(&s_cnt[q + 1], c);
+    }
   }
   __syncthreads();
   const uint32_t s = threadIdx.x;
   if (s_cnt[s]) {
-    atomicMin(&mn[s], s_mn[s]);
     atomicMax(&mx[s], s_mx[s]);
     atomicAdd(&cnt[s], s_cnt[s]);
   }
@@ -665,7 +696,8 @@ struct EngineDevice {
   DBuf<uint64_t> o_dep;
   const uint64_t *o_label = nullptr;  // [n] min dot of each command's SCC
   const uint32_t *o_rank = nullptr;   // [n] position in the execution order
-  uint32_t o_nelem = 0;               // per-key sequence length (key_offs, seq_dot)
+  uint32_t o_nelem = 0;               // per-key sequence length (key_offs, o_seq)
+  const uint64_t *o_seq = nullptr;    // [o_nelem] per-key sequences of dots
   DBuf<uint32_t> edge_cnt, edge_off, edge_csr;  // replica views: in-batch edges as CSR
   DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
@@ -1013,7 +1045,7 @@ struct EngineDevice {
         mark("keydeps_bucket");
         bucket_order = true;
       } else {
-        sort_pairs<uint32_t>(bkey, nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
+        sort_pairs<uint32_t, uint32_t>(bkey, nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
                              sk32b.ensure(M + 1), svb.ensure(M + 1), M, key_bits, sort_ws, stream,
                              &ks, &vs);
         mark("keydeps_sort");
@@ -1051,7 +1083,7 @@ struct EngineDevice {
     } else if (!views) {
       sv_fused = false;
       uint32_t *ks = nullptr;
-      sort_pairs<uint32_t>(bkey, nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
+      sort_pairs<uint32_t, uint32_t>(bkey, nullptr, sk32a.ensure(M + 1), sva.ensure(M + 1),
                            sk32b.ensure(M + 1), svb.ensure(M + 1), M, key_bits, sort_ws, stream,
                            &ks, &vs);
       mark("keydeps_sort");
@@ -1094,7 +1126,7 @@ struct EngineDevice {
                       dim3(grid_for(Mc, B)), dim3(B), stream, Mc, k, fq, np, lc, bent, bkey,
                       uint32_t(key_space), lk, lv);
         uint32_t *ks = nullptr;
-        sort_pairs<uint32_t>(lk, lv, lk, lv, sk32b.ensure(Mc + 1), svb.ensure(Mc + 1), Mc, bits,
+        sort_pairs<uint32_t, uint32_t>(lk, lv, lk, lv, sk32b.ensure(Mc + 1), svb.ensure(Mc + 1), Mc, bits,
                              sort_ws, stream, &ks, &vs);
         // heads read the latest table, tails then make the chunk's last
         // commands the latest (command-log references)
@@ -1184,18 +1216,23 @@ struct EngineDevice {
       gin.sorted_keys = sorted_keys32;
       gin.sorted_vid = svid;
     }
+    gin.per_key_dots = true;
     graph.run(gin, gout);
     FH_CHECK(gout.npending == 0, FH_EINVARIANT, "fused engine batch left pending vertices");
     // per-key sequence of dots (ExecutionOrderMonitor::add order)
-    uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
-    k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, bdot, sq);
-    mark("per_key_dots");
+    if (gout.pk_dot) {
+      o_seq = gout.pk_dot;
+    } else {
+      uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
+      k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, bdot, sq);
+      o_seq = sq;
+      mark("per_key_dots");
+    }
     // executed clock: the whole batch executed
     unsigned long long *st = srcstats.ensure(4 * 256);
-    FH_HIP(hipMemsetAsync(st, 0xFF, 256 * sizeof(unsigned long long), stream));
     FH_HIP(hipMemsetAsync(st + 256, 0, 512 * sizeof(unsigned long long), stream));
-    k_src_stats<<<grid_for(n, B, 512), B, 0, stream>>>(n, bdot, st, st + 256,
-                                                   reinterpret_cast<unsigned int *>(st + 512));
+    k_src_stats<<<grid_for(n, B, 1024), B, 0, stream>>>(n, bdot, st + 256,
+                                                    reinterpret_cast<unsigned int *>(st + 512));
     k_frontier_update<<<1, 256, 0, stream>>>(st + 256, reinterpret_cast<unsigned int *>(st + 512),
                                              frontier.get(), excount_ptr());
     mark("executed_clock");
@@ -1243,14 +1280,17 @@ struct EngineDevice {
     k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
     k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
     exclusive_scan_u32(h, o, key_space, scan_ws, stream);
-    uint64_t *sq = seq_dot.ensure(o_nelem + 1);
-    if (sv_fused && bucket_order) {
-      // key-grouped runs -> ascending keys (hp holds each run's start)
-      k_run_scatter<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, gout.pk_vid, hp,
-                                                             o, bdot, sq);
-    } else if (sv_fused) {  // (sorted keys, sorted vids): gather the dots
-      k_seq_dots<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_vid, bdot, sq);
-    }  // else: run_general wrote seq_dot
+    if (sv_fused) {
+      uint64_t *sq = seq_dot.ensure(o_nelem + 1);
+      if (bucket_order) {
+        // key-grouped runs -> ascending keys (hp holds each run's start)
+        k_run_scatter<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, gout.pk_vid,
+                                                               hp, o, bdot, sq);
+      } else {  // (sorted keys, sorted vids): gather the dots
+        k_seq_dots<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_vid, bdot, sq);
+      }
+      o_seq = sq;
+    }  // else: run_general set o_seq
     mark("out_per_key");
   }
 
@@ -1300,7 +1340,7 @@ struct EngineDevice {
       FH_HIP(hipMemcpyAsync(key_off, key_offs.get(), (key_space + 1) * sizeof(uint32_t),
                             hipMemcpyDeviceToHost, stream));
     if (key_seq)
-      FH_HIP(hipMemcpyAsync(key_seq, seq_dot.get(), size_t(o_nelem) * sizeof(uint64_t),
+      FH_HIP(hipMemcpyAsync(key_seq, o_seq, size_t(o_nelem) * sizeof(uint64_t),
                             hipMemcpyDeviceToHost, stream));
     FH_HIP(hipStreamSynchronize(stream));
   }
@@ -1366,6 +1406,14 @@ fh_status fh_engine_rewind(fh_engine *h) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
   h->dev.rewind();
+  FH_API_END
+}
+
+fh_status fh_engine_sync(fh_engine *h) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_HIP(hipSetDevice(h->dev.device));
+  FH_HIP(hipStreamSynchronize(h->dev.stream));
   FH_API_END
 }
 

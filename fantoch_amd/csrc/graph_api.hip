@@ -296,7 +296,7 @@ struct GraphDevice {
     // dot -> vid index
     uint64_t *sd = nullptr;
     uint32_t *sv = nullptr;
-    sort_pairs<uint64_t>(ddot_v, nullptr, d_sd.ensure(V), d_sv.ensure(V), d_sd2.ensure(V),
+    sort_pairs<uint64_t, uint32_t>(ddot_v, nullptr, d_sd.ensure(V), d_sv.ensure(V), d_sd2.ensure(V),
                          d_sv2.ensure(V), V, 64, sort_ws, stream, &sd, &sv);
     FH_HIP(hipMemsetAsync(d_err.get(), 0, sizeof(uint32_t), stream));
     k_dup_check<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), sd, d_err.get());

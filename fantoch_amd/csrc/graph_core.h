@@ -56,6 +56,7 @@ struct GraphInput {
   const uint32_t *sorted_vid = nullptr;   // [M] vid of each sorted element
   bool no_forward_hint = false;           // edges all point backwards
   bool want_per_key = true;               // build the per-key sequence
+  bool per_key_dots = false;              // ... of dots (pk_dot) instead of vids
 };
 
 struct GraphOutput {
@@ -73,6 +74,7 @@ struct GraphOutput {
   uint32_t nelem = 0;             // per-key sequence length
   uint32_t *pk_key = nullptr;     // [nelem] keys, ascending
   uint32_t *pk_vid = nullptr;     // [nelem] vids in per-key execution order
+  uint64_t *pk_dot = nullptr;     // [nelem] their dots (per_key_dots: pk_vid null)
 };
 
 struct GraphCore {
@@ -83,7 +85,7 @@ struct GraphCore {
   DBuf<uint32_t> kraise;  // [V] last kappa iteration that raised kap[rep]
   DBuf<uint32_t> erep;    // [E] rep[dst[e]] (refresh_edge_rep)
   uint64_t nedges = 0;
-  DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c;
+  DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c, pk_da, pk_db;
   DBuf<uint8_t> blocked;
   DBuf<uint32_t> t_h, t_rank, t_cnt, t_start;
   DBuf<uint64_t> t_prof;  // tile path: ready time, group rank/count/start

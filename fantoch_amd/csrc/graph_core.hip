@@ -594,6 +594,19 @@ __global__ void k_elem_fill(uint32_t n, const uint32_t *__restrict__ order, uint
   }
 }
 
+// one key per command: the element of exec position j is (key, dot) of
+// order[j] (the gather follows the execution order, close to arrival order)
+__global__ void k_elem_fill_dots(uint32_t n, const uint32_t *__restrict__ order,
+                                 const uint32_t *__restrict__ key32,
+                                 const uint64_t *__restrict__ dot, uint32_t *__restrict__ ek,
+                                 uint64_t *__restrict__ ed) {
+  GRID_STRIDE(j, n) {
+    const uint32_t v = order[j];
+    ek[j] = key32[v];
+    ed[j] = dot[v];
+  }
+}
+
 __global__ void k_copy_dot(uint32_t V, const uint64_t *__restrict__ dot, uint64_t *__restrict__ out) {
   GRID_STRIDE(v, V) out[v] = dot[v];
 }
@@ -821,7 +834,7 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   uint64_t *ks = nullptr;
   uint32_t *vs = nullptr;
   uint32_t *dot_rank = rank.ensure(V);
-  sort_pairs<uint64_t>(in.dot, nullptr, ka, va, kb, vb, V, 64, sort_ws, stream, &ks, &vs);
+  sort_pairs<uint64_t, uint32_t>(in.dot, nullptr, ka, va, kb, vb, V, 64, sort_ws, stream, &ks, &vs);
   k_rank_from_sorted<<<grid_for(V, B), B, 0, stream>>>(V, vs, dot_rank);
   mark("dot_rank");
   // SCC order by kappa
@@ -834,7 +847,7 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   k_rep_keys<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, kap.get(), bv, ka, va);
   FH_HIP(hipStreamSynchronize(stream));
   uint32_t *scc_rank = tmp32c.ensure(V);
-  sort_pairs<uint64_t>(ka, va, ka, va, kb, vb, nrep, 2 * bv, sort_ws, stream, &ks, &vs);
+  sort_pairs<uint64_t, uint32_t>(ka, va, ka, va, kb, vb, nrep, 2 * bv, sort_ws, stream, &ks, &vs);
   k_rank_from_sorted<<<grid_for(nrep, B), B, 0, stream>>>(nrep, vs, scc_rank);
   mark("scc_order");
   // vertex order: (scc rank, dot rank)
@@ -845,7 +858,7 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   k_vertex_keys<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, rep.get(), scc_rank, dot_rank, bv,
                                                    ka, va);
   FH_HIP(hipStreamSynchronize(stream));
-  sort_pairs<uint64_t>(ka, va, ka, va, kb, vb, nexec, 2 * bv, sort_ws, stream, &ks, &vs);
+  sort_pairs<uint64_t, uint32_t>(ka, va, ka, va, kb, vb, nexec, 2 * bv, sort_ws, stream, &ks, &vs);
   uint32_t *ord = order.ensure(nexec + 1);
   FH_HIP(hipMemcpyAsync(ord, vs, size_t(nexec) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
                         stream));
@@ -865,6 +878,23 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
   if (!in.want_per_key) return;
   const uint32_t nexec = out.nexec;
   const uint32_t *ord = out.exec_order;
+  if (in.per_key_dots && !in.key_off && in.k == 1) {
+    // (key, dot) pairs in execution order, stable-sorted by key: the per-key
+    // sequences of dots come out of the sort (no gather by vid afterwards)
+    uint32_t *ek = tmp32a.ensure(nexec + 1), *k2 = flags.ensure(nexec + 1);
+    uint64_t *ed = pk_da.ensure(nexec + 1), *d2 = pk_db.ensure(nexec + 1);
+    k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, in.key32, in.dot, ek, ed);
+    uint32_t *ko = nullptr;
+    uint64_t *dout = nullptr;
+    sort_pairs<uint32_t, uint64_t>(ek, ed, k2, d2, ek, ed, nexec, in.key_bits, sort_ws, stream,
+                                   &ko, &dout);
+    out.pk_key = ko;
+    out.pk_vid = nullptr;
+    out.pk_dot = dout;
+    out.nelem = nexec;
+    mark("per_key_order");
+    return;
+  }
   uint32_t *ec = cnt.ensure(nexec + 1);
   uint32_t *ep = pos.ensure(nexec + 1);
   k_elem_counts<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, in.k, in.key_off, ec);
@@ -878,7 +908,7 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
   uint32_t *k2 = flags.ensure(nelem + 1), *v2 = rank.ensure(nelem + 1);
   uint32_t *ko = nullptr, *vo = nullptr;
   // ek/ev are sorted into (k2, v2) or back into (ek, ev)
-  sort_pairs<uint32_t>(ek, ev, k2, v2, ek, ev, nelem, in.key_bits, sort_ws, stream, &ko, &vo);
+  sort_pairs<uint32_t, uint32_t>(ek, ev, k2, v2, ek, ev, nelem, in.key_bits, sort_ws, stream, &ko, &vo);
   out.pk_key = ko;
   out.pk_vid = vo;
   out.nelem = nelem;

@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(kTileThreads)
   __shared__ uint16_t sR[kTileC];
   __shared__ uint8_t sF[kTileC];
   __shared__ uint16_t W1[kTileC];
-  __shared__ uint16_t W2[kTileC];
+  __shared__ __align__(16) uint16_t W2[kTileC];
   __shared__ uint32_t s_w[kTileThreads / 64];
   __shared__ uint32_t s_ch[3];
   __shared__ uint32_t s_fail, s_maxex, s_over, s_long;
@@ -456,6 +456,15 @@ __global__ void __launch_bounds__(kTileThreads)
     gmem[lds_add_u16(&gend[sH[y]], 1)] = y;
   }
   __syncthreads();
+  // the group members' dots, staged once in W2's space (the raised list is
+  // consumed): members of one SCC tie on (depth, min member) and compare
+  // dots, which would otherwise be one round of global loads per 8 members
+  // for every vertex of a large SCC
+  uint64_t *gdot = reinterpret_cast<uint64_t *>(W2);
+  const bool lds_dots = nraised <= uint32_t(kTileC / 4);
+  if (lds_dots)
+    for (uint32_t i = tid; i < nraised; i += kTileThreads) gdot[i] = dot[lo + gmem[i]];
+  __syncthreads();
   uint32_t gmax = 0;
 #pragma unroll
   for (int j = 0; j < kMaxCore; j++) {
@@ -491,7 +500,8 @@ __global__ void __launch_bounds__(kTileThreads)
                                        : m2 != mx ? (m2 < mx ? -1 : 1) : 0;
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) dy[u] = st[u] == 0 ? dot[lo + ys[u]] : 0ull;
+        for (int u = 0; u < 8; u++)
+          dy[u] = st[u] != 0 ? 0ull : lds_dots ? gdot[j + u] : dot[lo + ys[u]];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
           rk += st[u] < 0 || (st[u] == 0 && dy[u] < dotx);

@@ -255,7 +255,7 @@ struct KeyClocksDevice {
                                                 qdot.get(), cb, E, c, d);
     uint64_t *ks = nullptr;
     uint32_t *vs = nullptr;
-    sort_pairs<uint64_t>(c, nullptr, tmpk.ensure(E2 + 1), perm.ensure(E2 + 1),
+    sort_pairs<uint64_t, uint32_t>(c, nullptr, tmpk.ensure(E2 + 1), perm.ensure(E2 + 1),
                          tmpk2.ensure(E2 + 1), perm2.ensure(E2 + 1), E2, kb + cb, sort_ws, stream,
                          &ks, &vs);
     uint64_t *nc = comp.ensure(E2 + 1), *nd = edot.ensure(E2 + 1);
@@ -284,7 +284,7 @@ struct KeyClocksDevice {
                                                 nullptr, cb, 0, r, nullptr);
     uint64_t *rs = nullptr;
     uint32_t *vs = nullptr;
-    sort_pairs<uint64_t>(r, nullptr, tmpk.ensure(m + 1), perm.ensure(m + 1), tmpk2.ensure(m + 1),
+    sort_pairs<uint64_t, uint32_t>(r, nullptr, tmpk.ensure(m + 1), perm.ensure(m + 1), tmpk2.ensure(m + 1),
                          perm2.ensure(m + 1), m, kb + cb, sort_ws, stream, &rs, &vs);
     FH_HIP(hipMemsetAsync(scal.get(), 0, 2 * sizeof(uint32_t), stream));
     k_kc_distinct<<<grid_for(m, B), B, 0, stream>>>(uint32_t(m), rs, scal.get() + 1);

@@ -278,7 +278,7 @@ size_t KeyDepsDevice::run_segment(uint32_t a, uint32_t b, bool has_past, bool ha
   uint32_t *ks = nullptr, *vs = nullptr;
   uint32_t *ka = d_sk_a.ensure(m), *kb = d_sk_b.ensure(m);
   uint32_t *va = d_sv_a.ensure(m), *vb = d_sv_b.ensure(m);
-  sort_pairs<uint32_t>(key32, nullptr, ka, va, kb, vb, m, key_bits, sort_ws, stream, &ks, &vs);
+  sort_pairs<uint32_t, uint32_t>(key32, nullptr, ka, va, kb, vb, m, key_bits, sort_ws, stream, &ks, &vs);
   uint64_t *edep2 = nullptr;
   if (has_ro) {
     // LockedKeyDeps read/write rules; tails update both tables in their own
@@ -367,7 +367,7 @@ size_t KeyDepsDevice::table_values(uint64_t extra) {
     uint32_t *va = d_sv_a.ensure(cnt), *vb = d_sv_b.ensure(cnt);
     uint64_t *ks = nullptr;
     uint32_t *vs = nullptr;
-    sort_pairs<uint64_t>(vals, nullptr, ka, va, kb, vb, cnt, 64, sort_ws, stream, &ks, &vs);
+    sort_pairs<uint64_t, uint32_t>(vals, nullptr, ka, va, kb, vb, cnt, 64, sort_ws, stream, &ks, &vs);
     FH_HIP(hipMemcpyAsync(vals, ks, cnt * sizeof(uint64_t), hipMemcpyDeviceToDevice, stream));
   }
   return cnt;

@@ -156,6 +156,13 @@ fh_status fh_multi_rewind(fh_multi *h) {
   FH_API_END
 }
 
+fh_status fh_multi_sync(fh_multi *h) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  for (auto *e : h->eng) check_status(fh_engine_sync(e));
+  FH_API_END
+}
+
 fh_status fh_multi_run(fh_multi *h, float *device_ms) {
   FH_API_BEGIN
   FH_CHECK(h && h->staged, FH_EINVAL, "nothing staged");

@@ -186,7 +186,7 @@ struct PredDevice {
     // dot -> vid
     uint64_t *sd = nullptr;
     uint32_t *sv = nullptr;
-    sort_pairs<uint64_t>(ddot_v, nullptr, d_sd.ensure(V), d_sv.ensure(V), d_sd2.ensure(V),
+    sort_pairs<uint64_t, uint32_t>(ddot_v, nullptr, d_sd.ensure(V), d_sv.ensure(V), d_sd2.ensure(V),
                          d_sv2.ensure(V), V, 64, sort_ws, stream, &sd, &sv);
     FH_HIP(hipMemsetAsync(d_err.get(), 0, sizeof(uint32_t), stream));
     k_dup_check<<<grid_for(V, kB), kB, 0, stream>>>(uint32_t(V), sd, d_err.get());
@@ -224,7 +224,7 @@ struct PredDevice {
       uint64_t *kc = d_kc.ensure(X), *kco = nullptr;
       uint32_t *kv = d_kv.ensure(X), *kvo = nullptr;
       k_pred_compact<<<grid_for(V, kB), kB, 0, stream>>>(uint32_t(V), blocked, pos, dclk, kc, kv);
-      sort_pairs<uint64_t>(kc, kv, d_kco.ensure(X), d_kv2.ensure(X), d_kc2.ensure(X),
+      sort_pairs<uint64_t, uint32_t>(kc, kv, d_kco.ensure(X), d_kv2.ensure(X), d_kc2.ensure(X),
                            d_kv3.ensure(X), X, 64, sort_ws, stream, &kco, &kvo);
       FH_HIP(hipMemcpyAsync(order.data(), kvo, X * 4, hipMemcpyDeviceToHost, stream));
     }

@@ -1,4 +1,4 @@
-// sort.h -- stable LSD radix sort of (key, u32 value) pairs, reduce-then-scan.
+// sort.h -- stable LSD radix sort of (key, value) pairs, reduce-then-scan.
 //
 // 8-bit digits, per pass: tile digit counts, a two-level scan of the counts
 // (no inter-workgroup hand-off inside any launch), and a stable LDS-staged
@@ -23,10 +23,12 @@ struct SortWorkspace {
 // nullptr means values are the input positions 0..n-1.  Data ping-pongs
 // between (ka, va) and (kb, vb); *kout / *vout point at the sorted result
 // (one of the two).  keys_in/vals_in may alias either pair.  n < 2^30.
-template <class K>
-void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va,
-                K *kb, uint32_t *vb, size_t n, int key_bits, SortWorkspace &ws,
-                hipStream_t s, K **kout, uint32_t **vout);
+// Values are u32 (element ids) or u64 (dots: the per-key sequences carry
+// them through the sort instead of gathering them afterwards).
+template <class K, class VT = uint32_t>
+void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va,
+                K *kb, VT *vb, size_t n, int key_bits, SortWorkspace &ws,
+                hipStream_t s, K **kout, VT **vout);
 
 
 }  // namespace fh

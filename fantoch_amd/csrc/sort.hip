@@ -178,14 +178,14 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
-template <class K, bool IOTA>
+template <class K, class VT, bool IOTA>
 __global__ void __launch_bounds__(kThreads)
-    k_down(const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
-           uint32_t *__restrict__ vout, uint32_t n, int shift,
+    k_down(const K *__restrict__ kin, const VT *__restrict__ vin, K *__restrict__ kout,
+           VT *__restrict__ vout, uint32_t n, int shift,
            const uint32_t *__restrict__ counts, const uint32_t *__restrict__ gsum,
            uint32_t gsize, const uint32_t *__restrict__ dbase) {
   __shared__ K s_k[kTile];
-  __shared__ uint32_t s_v[kTile];
+  __shared__ VT s_v[kTile];
   __shared__ uint32_t s_wh[kWaves][256];
   __shared__ uint32_t s_dex[256];
   __shared__ uint32_t s_gb[256];
@@ -199,13 +199,13 @@ __global__ void __launch_bounds__(kThreads)
   const uint32_t gofs =
       dbase[tid] + gsum[size_t(tile / gsize) * 256 + tid] + counts[size_t(tile) * 256 + tid];
   K key[kItems];
-  uint32_t val[kItems];
+  VT val[kItems];
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = elem_index(base, w, i, lane);
     const bool valid = idx < n;
     key[i] = valid ? kin[idx] : K(0);
-    val[i] = IOTA ? idx : (valid ? vin[idx] : 0u);
+    val[i] = IOTA ? VT(idx) : (valid ? vin[idx] : VT(0));
   }
   __syncthreads();
   const uint64_t lt = (uint64_t(1) << lane) - 1;
@@ -268,10 +268,9 @@ void SortWorkspace::prepare(size_t tiles, int, hipStream_t) {
   meta.ensure((tiles + groups + 1) * 256);
 }
 
-template <class K>
-void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va, K *kb,
-                uint32_t *vb, size_t n, int key_bits, SortWorkspace &ws, hipStream_t s,
-                K **kout, uint32_t **vout) {
+template <class K, class VT>
+void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *vb, size_t n,
+                int key_bits, SortWorkspace &ws, hipStream_t s, K **kout, VT **vout) {
   FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "sort: too many elements (>= 2^30)");
   int passes = (key_bits + 7) / 8;
   if (passes < 1) passes = 1;
@@ -288,12 +287,12 @@ void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va, 
   uint32_t *gsum = counts + size_t(tiles) * 256;
   uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * 256;
   const K *ki = keys_in;
-  const uint32_t *vi = vals_in;
+  const VT *vi = vals_in;
   // never write pass 0 over its own input
   const bool alias_a = (const void *)keys_in == (const void *)ka ||
                        (vals_in && (const void *)vals_in == (const void *)va);
   K *ko = alias_a ? kb : ka;
-  uint32_t *vo = alias_a ? vb : va;
+  VT *vo = alias_a ? vb : va;
   for (int p = 0; p < passes; p++) {
     const int shift = 8 * p;
     k_up<K><<<tiles, kThreads, 0, s>>>(ki, uint32_t(n), shift, counts);
@@ -306,13 +305,13 @@ void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va, 
       k_scan_b<<<1, 256, 0, s>>>(gsum, groups, dbase);
     }
     if (p == 0 && vals_in == nullptr) {
-      k_down<K, true><<<tiles, kThreads, 0, s>>>(ki, nullptr, ko, vo, uint32_t(n), shift, counts,
-                                                  gsum, gsize, dbase);
+      k_down<K, VT, true><<<tiles, kThreads, 0, s>>>(ki, nullptr, ko, vo, uint32_t(n), shift,
+                                                      counts, gsum, gsize, dbase);
     } else {
       // algorithmic traffic of a key+value scatter pass: read and write every
       // pair once
-      probed_launch("sort_scatter", double(n) * 2.0 * (sizeof(K) + sizeof(uint32_t)),
-                    k_down<K, false>, dim3(tiles), dim3(kThreads), s, ki, vi, ko, vo,
+      probed_launch("sort_scatter", double(n) * 2.0 * (sizeof(K) + sizeof(VT)),
+                    k_down<K, VT, false>, dim3(tiles), dim3(kThreads), s, ki, vi, ko, vo,
                     uint32_t(n), shift, (const uint32_t *)counts, (const uint32_t *)gsum, gsize,
                     (const uint32_t *)dbase);
     }
@@ -327,14 +326,20 @@ void sort_pairs(const K *keys_in, const uint32_t *vals_in, K *ka, uint32_t *va, 
     }
   }
   *kout = const_cast<K *>(ki);
-  *vout = const_cast<uint32_t *>(vi);
+  *vout = const_cast<VT *>(vi);
 }
 
-template void sort_pairs<uint32_t>(const uint32_t *, const uint32_t *, uint32_t *,
-                                   uint32_t *, uint32_t *, uint32_t *, size_t, int,
-                                   SortWorkspace &, hipStream_t, uint32_t **, uint32_t **);
-template void sort_pairs<uint64_t>(const uint64_t *, const uint32_t *, uint64_t *,
-                                   uint32_t *, uint64_t *, uint32_t *, size_t, int,
-                                   SortWorkspace &, hipStream_t, uint64_t **, uint32_t **);
+template void sort_pairs<uint32_t, uint32_t>(const uint32_t *, const uint32_t *, uint32_t *,
+                                             uint32_t *, uint32_t *, uint32_t *, size_t, int,
+                                             SortWorkspace &, hipStream_t, uint32_t **,
+                                             uint32_t **);
+template void sort_pairs<uint64_t, uint32_t>(const uint64_t *, const uint32_t *, uint64_t *,
+                                             uint32_t *, uint64_t *, uint32_t *, size_t, int,
+                                             SortWorkspace &, hipStream_t, uint64_t **,
+                                             uint32_t **);
+template void sort_pairs<uint32_t, uint64_t>(const uint32_t *, const uint64_t *, uint32_t *,
+                                             uint64_t *, uint32_t *, uint64_t *, size_t, int,
+                                             SortWorkspace &, hipStream_t, uint32_t **,
+                                             uint64_t **);
 
 }  // namespace fh

@@ -39,6 +39,10 @@ class Engine:
         no host synchronisation)."""
         L.check(self._lib.fh_engine_rewind(self._h))
 
+    def sync(self):
+        """Wait for every run issued on the engine's stream (fh_engine_sync)."""
+        L.check(self._lib.fh_engine_sync(self._h))
+
     def set_profiling(self, on: bool):
         L.check(self._lib.fh_engine_set_profiling(self._h, 1 if on else 0))
 

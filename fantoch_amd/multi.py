@@ -44,6 +44,9 @@ class MultiEngine:
     def rewind(self):
         L.check(self._lib.fh_multi_rewind(self._h))
 
+    def sync(self):
+        L.check(self._lib.fh_multi_sync(self._h))
+
     def run(self, sync: bool = True) -> float:
         ms = C.c_float(0)
         L.check(self._lib.fh_multi_run(self._h, C.byref(ms) if sync else None))

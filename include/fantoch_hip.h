@@ -458,6 +458,11 @@ fh_status fh_engine_stage_logs(fh_engine *h, const fh_stream_desc *desc,
  * clock cleared on the engine's stream, no host synchronisation; the next
  * run processes the first staged batch again). */
 fh_status fh_engine_rewind(fh_engine *h);
+/* Block until every run issued on the engine's stream has finished (what a
+ * timed loop of fh_engine_run(h, NULL) calls brackets itself with: the
+ * library's HIP runtime is not the caller's, so a device-wide synchronise
+ * of another runtime, e.g. torch's, does not wait for it). */
+fh_status fh_engine_sync(fh_engine *h);
 /* Run the next staged batch on the device (inputs already resident).  If
  * device_ms is non-NULL the stream is synchronised and the device time of
  * the run (HIP events on the engine's stream) is returned. */
@@ -509,6 +514,8 @@ fh_status fh_multi_stage_logs(fh_multi *h, const fh_stream_desc *desc,
                               const uint64_t *dot, const uint64_t *key_id,
                               const uint64_t *log_off, const uint32_t *log_cmd);
 fh_status fh_multi_rewind(fh_multi *h);
+/* fh_engine_sync on every shard. */
+fh_status fh_multi_sync(fh_multi *h);
 /* Every shard on its device concurrently (a host thread per device);
  * device_ms (may be NULL) = the slowest shard's device time. */
 fh_status fh_multi_run(fh_multi *h, float *device_ms);

@@ -46,3 +46,17 @@ class Interner:
 @pytest.fixture
 def golden():
     return load_golden
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_runtime_first(request):
+    """torch's wheel bundles its own HIP + HSA runtime (torch/lib), the
+    library links /opt/rocm's; in one process the second runtime to
+    initialise sees no GPU if it is torch's ("No HIP GPUs are available",
+    measured on the GPU box), so a session with GPU tests brings torch's up
+    first.  Only the torch-plumbing tests (device tensors, RCCL) need it."""
+    if any(it.get_closest_marker("gpu") for it in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda")
+    yield
