@@ -24,6 +24,7 @@
 
 #include "graph_core.h"
 #include "keybucket.h"
+#include "srcstats.h"
 
 namespace fh {
 namespace {
@@ -516,63 +517,17 @@ __global__ void k_seq_dots(uint32_t m, const uint32_t *__restrict__ pk_vid,
   GRID_STRIDE(j, m) seq[j] = dot[pk_vid[j]];
 }
 
-// executed-clock frontier advance for a fully executed batch: per-source
-// max / count of the batch's sequences.  Sources 1..kRegSrc accumulate in
-// registers (a batch has few sources: n of the configuration), others in
-// LDS; one wave reduction per source at the end, one global atomic per
-// source per workgroup.  (Per-element LDS atomics serialised on the ~5 hot
-// addresses: 365 us at 100M; a ballot loop per wave was compute bound.)
-constexpr int kRegSrc = 8;
+// executed-clock frontier advance for a fully executed batch (srcstats.h)
 __global__ void __launch_bounds__(256)
     k_src_stats(uint32_t n, const uint64_t *__restrict__ dot, unsigned long long *__restrict__ mx,
                 unsigned int *__restrict__ cnt) {
   __shared__ unsigned long long s_mx[256];
   __shared__ unsigned int s_cnt[256];
-  s_mx[threadIdx.x] = 0;
-  s_cnt[threadIdx.x] = 0;
+  SrcAcc acc;
+  acc.init(s_mx, s_cnt);
   __syncthreads();
-  uint64_t rmx[kRegSrc];
-  uint32_t rcnt[kRegSrc];
-#pragma unroll
-  for (int q = 0; q < kRegSrc; q++) rmx[q] = 0, rcnt[q] = 0;
-  GRID_STRIDE(i, n) {
-    const uint64_t d = dot[i];
-    const uint32_t src = uint32_t(d >> 56);
-    const uint64_t seq = d & 0x00FFFFFFFFFFFFFFull;
-    if (src >= 1 && src <= uint32_t(kRegSrc)) {
-#pragma unroll
-      for (int q = 0; q < kRegSrc; q++)
-        if (src == uint32_t(q + 1)) {
-          rmx[q] = seq > rmx[q] ? seq : rmx[q];
-          rcnt[q]++;
-        }
-    } else {
-      atomicMax(&s_mx[src], (unsigned long long)seq);
-      atomicAdd(&s_cnt[src], 1u);
-    }
-  }
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int q = 0; q < kRegSrc; q++) {
-    uint64_t m = rmx[q];
-    uint32_t c = rcnt[q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const uint64_t m2 = __shfl_xor(m, o, 64);
-      m = m2 > m ? m2 : m;
-      c += __shfl_xor(c, o, 64);
-    }
-    if (lane == 0 && c) {
-      atomicMax(&s_mx[q + 1], (unsigned long long)m);
-      atomicAdd(&s_cnt[q + 1], c);
-    }
-  }
-  __syncthreads();
-  const uint32_t s = threadIdx.x;
-  if (s_cnt[s]) {
-    atomicMax(&mx[s], s_mx[s]);
-    atomicAdd(&cnt[s], s_cnt[s]);
-  }
+  GRID_STRIDE(i, n) acc.add(dot[i]);
+  acc.commit(mx, cnt);
 }
 
 // The fused engine's executed clock: per source the highest executed
@@ -1217,6 +1172,11 @@ struct EngineDevice {
       gin.sorted_vid = svid;
     }
     gin.per_key_dots = true;
+    // the executed-clock stats ride on the per-key pass's dot reads
+    unsigned long long *stt = srcstats.ensure(4 * 256);
+    FH_HIP(hipMemsetAsync(stt + 256, 0, 512 * sizeof(unsigned long long), stream));
+    gin.src_mx = stt + 256;
+    gin.src_cnt = reinterpret_cast<unsigned int *>(stt + 512);
     graph.run(gin, gout);
     FH_CHECK(gout.npending == 0, FH_EINVARIANT, "fused engine batch left pending vertices");
     // per-key sequence of dots (ExecutionOrderMonitor::add order)
@@ -1229,10 +1189,10 @@ struct EngineDevice {
       mark("per_key_dots");
     }
     // executed clock: the whole batch executed
-    unsigned long long *st = srcstats.ensure(4 * 256);
-    FH_HIP(hipMemsetAsync(st + 256, 0, 512 * sizeof(unsigned long long), stream));
-    k_src_stats<<<grid_for(n, B, 1024), B, 0, stream>>>(n, bdot, st + 256,
-                                                    reinterpret_cast<unsigned int *>(st + 512));
+    unsigned long long *st = srcstats.get();
+    if (!gout.src_stats_done)
+      k_src_stats<<<grid_for(n, B, 1024), B, 0, stream>>>(n, bdot, st + 256,
+                                                      reinterpret_cast<unsigned int *>(st + 512));
     k_frontier_update<<<1, 256, 0, stream>>>(st + 256, reinterpret_cast<unsigned int *>(st + 512),
                                              frontier.get(), excount_ptr());
     mark("executed_clock");

@@ -57,6 +57,10 @@ struct GraphInput {
   bool no_forward_hint = false;           // edges all point backwards
   bool want_per_key = true;               // build the per-key sequence
   bool per_key_dots = false;              // ... of dots (pk_dot) instead of vids
+  // optional: per-source (max seq, count) of the executed dots, accumulated
+  // by a pass that reads every dot anyway (GraphOutput::src_stats_done)
+  unsigned long long *src_mx = nullptr;   // [256]
+  unsigned int *src_cnt = nullptr;        // [256]
 };
 
 struct GraphOutput {
@@ -75,6 +79,7 @@ struct GraphOutput {
   uint32_t *pk_key = nullptr;     // [nelem] keys, ascending
   uint32_t *pk_vid = nullptr;     // [nelem] vids in per-key execution order
   uint64_t *pk_dot = nullptr;     // [nelem] their dots (per_key_dots: pk_vid null)
+  bool src_stats_done = false;    // src_mx / src_cnt accumulated
 };
 
 struct GraphCore {

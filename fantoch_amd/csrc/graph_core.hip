@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "graph_core.h"
+#include "srcstats.h"
 
 namespace fh {
 namespace {
@@ -596,15 +597,24 @@ __global__ void k_elem_fill(uint32_t n, const uint32_t *__restrict__ order, uint
 
 // one key per command: the element of exec position j is (key, dot) of
 // order[j] (the gather follows the execution order, close to arrival order)
-__global__ void k_elem_fill_dots(uint32_t n, const uint32_t *__restrict__ order,
-                                 const uint32_t *__restrict__ key32,
-                                 const uint64_t *__restrict__ dot, uint32_t *__restrict__ ek,
-                                 uint64_t *__restrict__ ed) {
+__global__ void __launch_bounds__(256)
+    k_elem_fill_dots(uint32_t n, const uint32_t *__restrict__ order,
+                     const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot,
+                     uint32_t *__restrict__ ek, uint64_t *__restrict__ ed,
+                     unsigned long long *__restrict__ src_mx, unsigned int *__restrict__ src_cnt) {
+  __shared__ unsigned long long s_mx[256];
+  __shared__ unsigned int s_cnt[256];
+  SrcAcc acc;
+  acc.init(s_mx, s_cnt);
+  __syncthreads();
   GRID_STRIDE(j, n) {
     const uint32_t v = order[j];
+    const uint64_t d = dot[v];
     ek[j] = key32[v];
-    ed[j] = dot[v];
+    ed[j] = d;
+    if (src_mx) acc.add(d);
   }
+  if (src_mx) acc.commit(src_mx, src_cnt);  // (src_mx is uniform)
 }
 
 __global__ void k_copy_dot(uint32_t V, const uint64_t *__restrict__ dot, uint64_t *__restrict__ out) {
@@ -883,7 +893,9 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
     // sequences of dots come out of the sort (no gather by vid afterwards)
     uint32_t *ek = tmp32a.ensure(nexec + 1), *k2 = flags.ensure(nexec + 1);
     uint64_t *ed = pk_da.ensure(nexec + 1), *d2 = pk_db.ensure(nexec + 1);
-    k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, in.key32, in.dot, ek, ed);
+    k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, in.key32, in.dot, ek, ed,
+                                                           in.src_mx, in.src_cnt);
+    out.src_stats_done = in.src_mx != nullptr;
     uint32_t *ko = nullptr;
     uint64_t *dout = nullptr;
     sort_pairs<uint32_t, uint64_t>(ek, ed, k2, d2, ek, ed, nexec, in.key_bits, sort_ws, stream,

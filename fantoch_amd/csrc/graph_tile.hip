@@ -140,7 +140,8 @@ struct TileOut {
   int core;    // core vertices per tile T (T + 2L <= kTileC, T <= kMaxCore·1024)
   int hblock;  // H sweeps: 1 = each wave walks a contiguous block in ascending
                // steps of 64 (updates of a block's earlier vertices are seen by
-               // its later ones in the same sweep), 0 = block-strided
+               // its later ones in the same sweep), 2 = the same in batches of
+               // 5 vertices per lane (loads first), 0 = block-strided
 };
 
 // One tile: core [a, a + T), context [a - L, a + T + L) with L = 2·R0 and
@@ -151,12 +152,14 @@ __global__ void __launch_bounds__(kTileThreads)
                  TileOut out) {
   const int R0 = out.r0, T = out.core, L = 2 * R0;  // host: T + 2L <= kTileC
   if (out.redo && !out.redo[blockIdx.x]) return;
-  __shared__ uint16_t eL[S][kTileC];
+  __shared__ __align__(16) uint16_t eL[S][kTileC];
   __shared__ uint16_t sH[kTileC];
   __shared__ uint16_t sR[kTileC];
   __shared__ uint8_t sF[kTileC];
   __shared__ uint16_t W1[kTileC];
   __shared__ __align__(16) uint16_t W2[kTileC];
+  // rank-phase member keys: S = 3 reuses the third edge row, S = 2 has room
+  __shared__ uint32_t gkey_s[S == 3 ? 1 : kTileC / 2];
   __shared__ uint32_t s_w[kTileThreads / 64];
   __shared__ uint32_t s_ch[3];
   __shared__ uint32_t s_fail, s_maxex, s_over, s_long;
@@ -227,7 +230,61 @@ __global__ void __launch_bounds__(kTileThreads)
   // vertex x reaches, so H(H(x)) is reachable too: pointer jumping collapses
   // chains of forward dependencies in logarithmically many sweeps.
   const int hP = 64 * ((C + kTileThreads - 1) / kTileThreads);  // per-wave block
-  const int hs = sweeps(
+  // hblock 2: each wave walks its block kHB vertices per lane at a time, all
+  // loads of a batch issued before any store (one dependent LDS round trip
+  // chain per batch instead of per vertex).  Measured on C4: no faster per
+  // sweep (2.65 vs 2.53 us: the sweep is bound by LDS bank conflicts of the
+  // random sH[y] reads, not by latency) and one sweep more (less in-sweep
+  // propagation), so hblock 1 stays the default.
+  auto h_sweeps_batched = [&]() {
+    constexpr int kHB = 5;
+    const int w = tid >> 6, lane = tid & 63, nk = hP / 64;
+    int it = 0;
+    for (;; it++) {
+      bool ch = false;
+      for (int k0 = 0; k0 < nk; k0 += kHB) {
+        int xs[kHB];
+        uint32_t h[kHB], h0[kHB];
+        uint16_t ys[kHB][S];
+#pragma unroll
+        for (int u = 0; u < kHB; u++) {
+          const int x = w * hP + (k0 + u) * 64 + lane;
+          xs[u] = (k0 + u < nk && x < C) ? x : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kHB; u++) {
+          h0[u] = xs[u] >= 0 ? uint32_t(sH[xs[u]]) : 0u;
+#pragma unroll
+          for (int q = 0; q < S; q++) ys[u][q] = xs[u] >= 0 ? eL[q][xs[u]] : kNone;
+        }
+#pragma unroll
+        for (int u = 0; u < kHB; u++) {
+          h[u] = h0[u];
+#pragma unroll
+          for (int q = 0; q < S; q++)
+            if (ys[u][q] != kNone) h[u] = max(h[u], uint32_t(sH[ys[u][q]]));
+        }
+#pragma unroll
+        for (int u = 0; u < kHB; u++)
+          if (xs[u] >= 0) h[u] = max(h[u], uint32_t(sH[h[u]]));
+#pragma unroll
+        for (int u = 0; u < kHB; u++)
+          if (xs[u] >= 0 && h[u] > h0[u]) {
+            sH[xs[u]] = uint16_t(h[u]);
+            ch = true;
+          }
+      }
+      if (ch) s_ch[it % 3] = 1;
+      if (tid == 0) s_ch[(it + 1) % 3] = 0;
+      __syncthreads();
+      if (!s_ch[it % 3]) break;
+    }
+    __syncthreads();
+    if (tid < 3) s_ch[tid] = 0;
+    __syncthreads();
+    return it + 1;
+  };
+  const int hs = out.hblock == 2 ? h_sweeps_batched() : sweeps(
       [&](int i) {
         const int x = out.hblock ? ((i & (kTileThreads - 1)) >> 6) * hP + (i >> 10) * 64 + (i & 63)
                                  : i;
@@ -460,11 +517,19 @@ __global__ void __launch_bounds__(kTileThreads)
   // consumed): members of one SCC tie on (depth, min member) and compare
   // dots, which would otherwise be one round of global loads per 8 members
   // for every vertex of a large SCC
+  // With them each member's order key (depth << 16 | SCC slot), so the rank
+  // loop reads two independent arrays instead of a gmem -> sR -> W1 chain.
   uint64_t *gdot = reinterpret_cast<uint64_t *>(W2);
+  uint32_t *gkey = S == 3 ? reinterpret_cast<uint32_t *>(&eL[S - 1][0]) : gkey_s;
   const bool lds_dots = nraised <= uint32_t(kTileC / 4);
   if (lds_dots)
-    for (uint32_t i = tid; i < nraised; i += kTileThreads) gdot[i] = dot[lo + gmem[i]];
+    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+      const uint16_t y = gmem[i];
+      gdot[i] = dot[lo + y];
+      gkey[i] = (uint32_t(W1[sR[y]]) << 16) | sR[y];
+    }
   __syncthreads();
+  phase(5);
   uint32_t gmax = 0;
 #pragma unroll
   for (int j = 0; j < kMaxCore; j++) {
@@ -486,6 +551,25 @@ __global__ void __launch_bounds__(kTileThreads)
         return dot[lo + y] < dotx;
       };
       if (t != uint32_t(x)) rk += cmp(t);
+      if (lds_dots) {
+        // x's own entry (if raised) ties with itself on the dot: not before
+        // x, and its dot is x's own in the label minimum
+        const uint32_t kx = (dx << 16) | mx;
+        for (uint32_t j = b0; j < b1; j += 8) {
+          uint32_t kk[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) kk[u] = j + u < b1 ? gkey[j + u] : 0xFFFFFFFFu;
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            rk += kk[u] < kx;
+            if (kk[u] == kx) {
+              const uint64_t dy = gdot[j + u];
+              rk += dy < dotx;
+              if (lab == 0 || dy < lab) lab = dy;
+            }
+          }
+        }
+      } else
       // members 8 at a time: (depth, min member) from LDS, and the dots of
       // same-SCC members loaded together (independent L2 loads in flight)
       for (uint32_t j = b0; j < b1; j += 8) {
@@ -524,7 +608,7 @@ __global__ void __launch_bounds__(kTileThreads)
   }
   if (gmax) atomicMax(&out.stat[6], gmax);
   __syncthreads();
-  phase(5);
+  phase(6);
 }
 
 __global__ void k_exec_from_groups(uint32_t V, const uint32_t *__restrict__ hgrp,
@@ -615,9 +699,10 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
     // (the profile sums every launch of this run)
     const double tiles = double((V + to.core - 1) / to.core);
     fprintf(stderr, "fh graph_tile phases (us per tile, T=%d): load %.1f H %.1f raised %.1f "
-            "reach1 %.1f rounds+depth %.1f rank %.1f\n", to.core, pr[0] * 0.01 / tiles,
-            pr[1] * 0.01 / tiles, pr[2] * 0.01 / tiles, pr[3] * 0.01 / tiles,
-            pr[4] * 0.01 / tiles, pr[5] * 0.01 / tiles);
+            "reach1 %.1f rounds+depth %.1f groups %.1f rank %.1f\n", to.core,
+            pr[0] * 0.01 / tiles, pr[1] * 0.01 / tiles, pr[2] * 0.01 / tiles,
+            pr[3] * 0.01 / tiles, pr[4] * 0.01 / tiles, pr[5] * 0.01 / tiles,
+            pr[6] * 0.01 / tiles);
   }
   mark("graph_tile");
   if (!ok) {

@@ -32,8 +32,17 @@ from collections import defaultdict
 
 # probe name (fh_engine_set_probe) -> kernel-name pattern
 PROBES = {
-    "sort_scatter": r"k_down<unsigned int, false>",
-    "sort_scatter_iota": r"k_down<unsigned int, true>",
+    "sort_scatter": r"k_down<unsigned int, unsigned int, false>",
+    "sort_scatter_iota": r"k_down<unsigned int, unsigned int, true>",
+    "sort_scatter_dots": r"k_down<unsigned int, unsigned long, false>",
+    "graph_tile": r"k_graph_tile<",
+    "prev_engine": r"k_prev_views",
+    "cmd_union": r"k_cmd_engine<unsigned int>",
+    "cmd_count": r"k_cmd_count<unsigned int>",
+    "log_keys": r"k_log_keys",
+    "tail_engine": r"k_tail_engine<unsigned int>",
+    "elem_fill_dots": r"k_elem_fill_dots",
+    "exec_from_groups": r"k_exec_from_groups",
     "sort_up": r"k_up<unsigned int>",
     "sort_scan": r"k_scan_fused",
     "sv_deps": r"k_sv_deps",
@@ -89,10 +98,14 @@ def main():
     fetch = read_counters(os.path.join(a.root, "fetch"), "FETCH_SIZE")
     write = read_counters(os.path.join(a.root, "write"), "WRITE_SIZE")
     rf, wf = cal.get("read4", 1.0), cal.get("write4", 1.0)
-    res = {"_calibration": {"counter_bytes_over_true_bytes": cal,
+    res = {}
+    if os.path.exists(a.out):  # keep the probes this run did not see
+        with open(a.out) as fh:
+            res = {k: v for k, v in json.load(fh).items() if not k.startswith("_")}
+    res.update({"_calibration": {"counter_bytes_over_true_bytes": cal,
                             "note": "1 GiB streams per access width; raw engine counters are "
                                     "divided by read4 / write4"},
-           "_command": a.command}
+           "_command": a.command})
     for probe, pat in PROBES.items():
         fv = [v for k, vs in fetch.items() if pat in k for v in vs]
         wv = [v for k, vs in write.items() if pat in k for v in vs]
