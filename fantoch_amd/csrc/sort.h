@@ -1,7 +1,8 @@
 // sort.h -- stable LSD radix sort of (key, value) pairs, reduce-then-scan.
 //
-// 8-bit digits, per pass: tile digit counts, a two-level scan of the counts
-// (no inter-workgroup hand-off inside any launch), and a stable LDS-staged
+// 8-bit digits (10 or 11 for keys of 17..22 bits: two passes instead of
+// three), per pass: tile digit counts, a two-level scan of the counts (no
+// inter-workgroup hand-off inside any launch), and a stable LDS-staged
 // scatter whose tile ranks come from wave64 ballot matching.
 #pragma once
 
@@ -14,7 +15,7 @@ constexpr int kSortItems = 16;
 constexpr int kSortTile = kSortThreads * kSortItems;  // 4096
 
 struct SortWorkspace {
-  DBuf<uint32_t> meta;  // [tile digit counts: tiles*256][group sums: groups*256]
+  DBuf<uint32_t> meta;  // [tile digit counts: tiles*R][group sums: groups*R], R <= 2048
   size_t meta_words(size_t n, int passes) const;
   void prepare(size_t tiles, int passes, hipStream_t s);
 };

@@ -24,10 +24,11 @@ constexpr int kTile = kSortTile;        // 4096
 constexpr int kWaves = kThreads / 64;
 constexpr int kGroup = 64;              // tiles per scan group
 
+template <int DB>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
   uint64_t peers = __ballot(valid);
 #pragma unroll
-  for (int b = 0; b < 8; b++) {
+  for (int b = 0; b < DB; b++) {
     const bool bit = (d >> b) & 1;
     const uint64_t m = __ballot(bit);
     peers &= bit ? m : ~m;
@@ -61,12 +62,13 @@ __device__ __forceinline__ uint32_t elem_index(uint32_t base, int w, int i, int 
   return base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
 }
 
-template <class K>
+template <class K, int DB>
 __global__ void __launch_bounds__(kThreads)
     k_up(const K *__restrict__ keys, uint32_t n, int shift, uint32_t *__restrict__ counts) {
-  __shared__ uint32_t s_h[kWaves][256];
+  constexpr int R = 1 << DB;
+  __shared__ uint32_t s_h[kWaves][R];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < kWaves * 256; i += kThreads) (&s_h[0][0])[i] = 0;
+  for (int i = tid; i < kWaves * R; i += kThreads) (&s_h[0][0])[i] = 0;
   const uint32_t base = blockIdx.x * kTile;
   K key[kItems];
 #pragma unroll
@@ -80,53 +82,75 @@ __global__ void __launch_bounds__(kThreads)
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = elem_index(base, w, i, lane);
     const bool valid = idx < n;
-    const uint32_t d = uint32_t((key[i] >> shift) & 255);
-    const uint64_t peers = match_digit(d, valid);
+    const uint32_t d = uint32_t((key[i] >> shift) & (R - 1));
+    const uint64_t peers = match_digit<DB>(d, valid);
     if (valid && (peers & lt) == 0) s_h[w][d] += uint32_t(__popcll(peers));  // wave-private
   }
   __syncthreads();
-  uint32_t c = 0;
+  for (int d = tid; d < R; d += kThreads) {
+    uint32_t c = 0;
 #pragma unroll
-  for (int ww = 0; ww < kWaves; ww++) c += s_h[ww][tid];
-  counts[size_t(blockIdx.x) * 256 + tid] = c;
+    for (int ww = 0; ww < kWaves; ww++) c += s_h[ww][d];
+    counts[size_t(blockIdx.x) * R + d] = c;
+  }
 }
 
 // Group g of kGroup tiles: counts[t][d] <- exclusive prefix within the group,
 // gsum[g][d] <- group total.
+template <int DB>
 __global__ void __launch_bounds__(256)
     k_scan_a(uint32_t *__restrict__ counts, uint32_t tiles, uint32_t *__restrict__ gsum) {
-  const uint32_t g = blockIdx.x, d = threadIdx.x;
+  constexpr int R = 1 << DB;
+  const uint32_t g = blockIdx.x;
   const uint32_t t0 = g * kGroup, t1 = min(tiles, t0 + kGroup);
-  uint32_t v[kGroup];
+  for (uint32_t d = threadIdx.x; d < uint32_t(R); d += 256) {
+    uint32_t v[kGroup];
 #pragma unroll
-  for (int i = 0; i < kGroup; i++) v[i] = (t0 + i < t1) ? counts[size_t(t0 + i) * 256 + d] : 0u;
-  uint32_t run = 0;
+    for (int i = 0; i < kGroup; i++) v[i] = (t0 + i < t1) ? counts[size_t(t0 + i) * R + d] : 0u;
+    uint32_t run = 0;
 #pragma unroll
-  for (int i = 0; i < kGroup; i++) {
-    if (t0 + i < t1) counts[size_t(t0 + i) * 256 + d] = run;
-    run += v[i];
+    for (int i = 0; i < kGroup; i++) {
+      if (t0 + i < t1) counts[size_t(t0 + i) * R + d] = run;
+      run += v[i];
+    }
+    gsum[size_t(g) * R + d] = run;
   }
-  gsum[size_t(g) * 256 + d] = run;
 }
 
 // One workgroup: gsum[g][d] <- exclusive prefix over groups, dbase[d] <-
-// exclusive prefix of the digit totals.
+// exclusive prefix of the digit totals.  Thread t owns the Q = R/256
+// consecutive digits [t·Q, (t+1)·Q).
+template <int DB>
 __global__ void __launch_bounds__(256)
     k_scan_b(uint32_t *__restrict__ gsum, uint32_t groups, uint32_t *__restrict__ dbase) {
+  constexpr int R = 1 << DB, Q = R / 256;
   __shared__ uint32_t s_tmp[kWaves];
-  const uint32_t d = threadIdx.x;
-  uint32_t run = 0;
-  for (uint32_t g0 = 0; g0 < groups; g0 += 16) {
-    uint32_t v[16];
+  uint32_t tot[Q];
 #pragma unroll
-    for (int i = 0; i < 16; i++) v[i] = (g0 + i < groups) ? gsum[size_t(g0 + i) * 256 + d] : 0u;
+  for (int q = 0; q < Q; q++) {
+    const uint32_t d = threadIdx.x * Q + q;
+    uint32_t run = 0;
+    for (uint32_t g0 = 0; g0 < groups; g0 += 16) {
+      uint32_t v[16];
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      if (g0 + i < groups) gsum[size_t(g0 + i) * 256 + d] = run;
-      run += v[i];
+      for (int i = 0; i < 16; i++) v[i] = (g0 + i < groups) ? gsum[size_t(g0 + i) * R + d] : 0u;
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        if (g0 + i < groups) gsum[size_t(g0 + i) * R + d] = run;
+        run += v[i];
+      }
     }
+    tot[q] = run;
   }
-  dbase[d] = block_excl_scan(run, s_tmp);
+  uint32_t mine = 0;
+#pragma unroll
+  for (int q = 0; q < Q; q++) mine += tot[q];
+  uint32_t pre = block_excl_scan(mine, s_tmp);
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    dbase[threadIdx.x * Q + q] = pre;
+    pre += tot[q];
+  }
 }
 
 // Small sorts (tiles <= kFusedMaxTiles): one 1024-thread workgroup does both
@@ -178,26 +202,27 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
-template <class K, class VT, bool IOTA>
+template <class K, class VT, bool IOTA, int DB>
 __global__ void __launch_bounds__(kThreads)
     k_down(const K *__restrict__ kin, const VT *__restrict__ vin, K *__restrict__ kout,
            VT *__restrict__ vout, uint32_t n, int shift,
            const uint32_t *__restrict__ counts, const uint32_t *__restrict__ gsum,
            uint32_t gsize, const uint32_t *__restrict__ dbase) {
+  constexpr int R = 1 << DB, Q = R / 256;
   __shared__ K s_k[kTile];
   __shared__ VT s_v[kTile];
-  __shared__ uint32_t s_wh[kWaves][256];
-  __shared__ uint32_t s_dex[256];
-  __shared__ uint32_t s_gb[256];
+  __shared__ uint32_t s_wh[kWaves][R];
+  __shared__ uint32_t s_dex[R];
+  __shared__ uint32_t s_gb[R];
   __shared__ uint32_t s_tmp[kWaves];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t tile = blockIdx.x;
   const uint32_t base = tile * kTile;
-  for (int i = tid; i < kWaves * 256; i += kThreads) (&s_wh[0][0])[i] = 0;
+  for (int i = tid; i < kWaves * R; i += kThreads) (&s_wh[0][0])[i] = 0;
   // global offset of this tile's digit runs (independent of the items)
-  const uint32_t gofs =
-      dbase[tid] + gsum[size_t(tile / gsize) * 256 + tid] + counts[size_t(tile) * 256 + tid];
+  for (int d = tid; d < R; d += kThreads)
+    s_gb[d] = dbase[d] + gsum[size_t(tile / gsize) * R + d] + counts[size_t(tile) * R + d];
   K key[kItems];
   VT val[kItems];
 #pragma unroll
@@ -214,30 +239,45 @@ __global__ void __launch_bounds__(kThreads)
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = elem_index(base, w, i, lane);
     const bool valid = idx < n;
-    const uint32_t d = uint32_t((key[i] >> shift) & 255);
-    const uint64_t peers = match_digit(d, valid);
+    const uint32_t d = uint32_t((key[i] >> shift) & (R - 1));
+    const uint64_t peers = match_digit<DB>(d, valid);
     uint32_t b0 = 0;
     if (valid) b0 = s_wh[w][d];
     if (valid && (peers & lt) == 0) s_wh[w][d] = b0 + uint32_t(__popcll(peers));
     rank[i] = b0 + uint32_t(__popcll(peers & lt));
   }
   __syncthreads();
-  uint32_t cnt = 0;
+  // per digit: the waves' exclusive prefix (stability: wave order = input
+  // order), then the tile-wide exclusive prefix over digits; thread t owns
+  // the Q consecutive digits [t·Q, (t+1)·Q)
+  uint32_t cnt[Q];
 #pragma unroll
-  for (int ww = 0; ww < kWaves; ww++) {
-    const uint32_t c = s_wh[ww][tid];
-    s_wh[ww][tid] = cnt;
-    cnt += c;
+  for (int q = 0; q < Q; q++) {
+    const int d = tid * Q + q;
+    uint32_t c0 = 0;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ww++) {
+      const uint32_t c = s_wh[ww][d];
+      s_wh[ww][d] = c0;
+      c0 += c;
+    }
+    cnt[q] = c0;
   }
-  const uint32_t lpre = block_excl_scan(cnt, s_tmp);
-  s_dex[tid] = lpre;
-  s_gb[tid] = gofs;
+  uint32_t mine = 0;
+#pragma unroll
+  for (int q = 0; q < Q; q++) mine += cnt[q];
+  uint32_t lpre = block_excl_scan(mine, s_tmp);
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    s_dex[tid * Q + q] = lpre;
+    lpre += cnt[q];
+  }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = elem_index(base, w, i, lane);
     if (idx < n) {
-      const uint32_t d = uint32_t((key[i] >> shift) & 255);
+      const uint32_t d = uint32_t((key[i] >> shift) & (R - 1));
       const uint32_t pos = s_dex[d] + s_wh[w][d] + rank[i];
       s_k[pos] = key[i];
       s_v[pos] = val[i];
@@ -248,7 +288,7 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll 4
   for (uint32_t j = tid; j < tile_n; j += kThreads) {
     const K k = s_k[j];
-    const uint32_t d = uint32_t((k >> shift) & 255);
+    const uint32_t d = uint32_t((k >> shift) & (R - 1));
     const uint32_t o = s_gb[d] + (j - s_dex[d]);
     kout[o] = k;
     vout[o] = s_v[j];
@@ -257,24 +297,71 @@ __global__ void __launch_bounds__(kThreads)
 
 }  // namespace
 
+constexpr int kWideMax = 11;  // widest digit (R = 2048)
+
 size_t SortWorkspace::meta_words(size_t n, int) const {
   const size_t tiles = (n + kTile - 1) / kTile;
   const size_t groups = (tiles + kGroup - 1) / kGroup;
-  return (tiles + groups) * 256;
+  return (tiles + groups) * (size_t(1) << kWideMax);
 }
 
 void SortWorkspace::prepare(size_t tiles, int, hipStream_t) {
   const size_t groups = std::max<size_t>((tiles + kGroup - 1) / kGroup, 4);
-  meta.ensure((tiles + groups + 1) * 256);
+  meta.ensure((tiles + groups + 1) * (size_t(1) << kWideMax));
 }
 
+namespace {
+
+// one LSD pass over DB bits at `shift`
+template <class K, class VT, int DB>
+void sort_pass(const K *ki, const VT *vi, K *ko, VT *vo, size_t n, int shift, bool iota,
+               uint32_t tiles, uint32_t groups, uint32_t *counts, uint32_t *gsum,
+               uint32_t *dbase, hipStream_t s) {
+  constexpr int R = 1 << DB;
+  k_up<K, DB><<<tiles, kThreads, 0, s>>>(ki, uint32_t(n), shift, counts);
+  uint32_t gsize = kGroup;
+  if (DB == 8 && tiles <= kFusedMaxTiles) {
+    gsize = (tiles + 3) / 4;
+    k_scan_fused<<<1, 1024, 0, s>>>(counts, tiles, gsize, gsum, dbase);
+  } else {
+    k_scan_a<DB><<<groups, 256, 0, s>>>(counts, tiles, gsum);
+    k_scan_b<DB><<<1, 256, 0, s>>>(gsum, groups, dbase);
+  }
+  if (iota) {
+    k_down<K, VT, true, DB><<<tiles, kThreads, 0, s>>>(ki, nullptr, ko, vo, uint32_t(n), shift,
+                                                        counts, gsum, gsize, dbase);
+  } else {
+    // algorithmic traffic of a key+value scatter pass: read and write every
+    // pair once
+    probed_launch("sort_scatter", double(n) * 2.0 * (sizeof(K) + sizeof(VT)),
+                  k_down<K, VT, false, DB>, dim3(tiles), dim3(kThreads), s, ki, vi, ko, vo,
+                  uint32_t(n), shift, (const uint32_t *)counts, (const uint32_t *)gsum, gsize,
+                  (const uint32_t *)dbase);
+  }
+  (void)R;
+}
+
+}  // namespace
+
+// Digit plan: 8-bit digits.  FH_SORT_WIDE=1 sorts keys of 17..22 bits in two
+// passes of 10 or 11 bits instead of three of 8 (the per-tile count matrix
+// grows 4-8x, one whole read + write of the pairs goes away).  Measured on
+// C4 (20-bit keys): no faster -- KeyDeps 15.75 vs 15.53 ms, per-key 3.40 vs
+// 3.29 ms: the wide k_down holds 57-74 KB of LDS (2 workgroups per CU
+// instead of 4) and matches 10 ballots per item, so a pass costs ~1.5x.
 template <class K, class VT>
 void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *vb, size_t n,
                 int key_bits, SortWorkspace &ws, hipStream_t s, K **kout, VT **vout) {
   FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "sort: too many elements (>= 2^30)");
-  int passes = (key_bits + 7) / 8;
+  static const bool wide = [] {
+    const char *e = getenv("FH_SORT_WIDE");
+    return e && *e && *e != '0';
+  }();
+  int db = 8;
+  if (wide && key_bits > 16 && key_bits <= 2 * kWideMax) db = key_bits <= 20 ? 10 : 11;
+  int passes = (key_bits + db - 1) / db;
   if (passes < 1) passes = 1;
-  if (passes > int(sizeof(K))) passes = int(sizeof(K));
+  if (db == 8 && passes > int(sizeof(K))) passes = int(sizeof(K));
   if (n == 0) {
     *kout = ka;
     *vout = va;
@@ -283,9 +370,10 @@ void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *v
   const uint32_t tiles = uint32_t((n + kTile - 1) / kTile);
   const uint32_t groups = (tiles + kGroup - 1) / kGroup;
   ws.prepare(tiles, passes, s);
+  const uint32_t R = 1u << db;
   uint32_t *counts = ws.meta.get();
-  uint32_t *gsum = counts + size_t(tiles) * 256;
-  uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * 256;
+  uint32_t *gsum = counts + size_t(tiles) * R;
+  uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
   const K *ki = keys_in;
   const VT *vi = vals_in;
   // never write pass 0 over its own input
@@ -294,27 +382,14 @@ void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *v
   K *ko = alias_a ? kb : ka;
   VT *vo = alias_a ? vb : va;
   for (int p = 0; p < passes; p++) {
-    const int shift = 8 * p;
-    k_up<K><<<tiles, kThreads, 0, s>>>(ki, uint32_t(n), shift, counts);
-    uint32_t gsize = kGroup;
-    if (tiles <= kFusedMaxTiles) {
-      gsize = (tiles + 3) / 4;
-      k_scan_fused<<<1, 1024, 0, s>>>(counts, tiles, gsize, gsum, dbase);
-    } else {
-      k_scan_a<<<groups, 256, 0, s>>>(counts, tiles, gsum);
-      k_scan_b<<<1, 256, 0, s>>>(gsum, groups, dbase);
-    }
-    if (p == 0 && vals_in == nullptr) {
-      k_down<K, VT, true><<<tiles, kThreads, 0, s>>>(ki, nullptr, ko, vo, uint32_t(n), shift,
-                                                      counts, gsum, gsize, dbase);
-    } else {
-      // algorithmic traffic of a key+value scatter pass: read and write every
-      // pair once
-      probed_launch("sort_scatter", double(n) * 2.0 * (sizeof(K) + sizeof(VT)),
-                    k_down<K, VT, false>, dim3(tiles), dim3(kThreads), s, ki, vi, ko, vo,
-                    uint32_t(n), shift, (const uint32_t *)counts, (const uint32_t *)gsum, gsize,
-                    (const uint32_t *)dbase);
-    }
+    const int shift = db * p;
+    const bool iota = p == 0 && vals_in == nullptr;
+    if (db == 10)
+      sort_pass<K, VT, 10>(ki, vi, ko, vo, n, shift, iota, tiles, groups, counts, gsum, dbase, s);
+    else if (db == 11)
+      sort_pass<K, VT, 11>(ki, vi, ko, vo, n, shift, iota, tiles, groups, counts, gsum, dbase, s);
+    else
+      sort_pass<K, VT, 8>(ki, vi, ko, vo, n, shift, iota, tiles, groups, counts, gsum, dbase, s);
     ki = ko;
     vi = vo;
     if (ko == ka) {
