@@ -671,7 +671,8 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   // R0 = 2048, then the global path.
   bool ok = false;
   uint32_t st[7] = {0, 0, 0, 0, 0, 0, 0};
-  uint32_t r0 = tile_r0;
+  static const uint32_t r0_env = getenv("FH_TILE_R0") ? uint32_t(atoi(getenv("FH_TILE_R0"))) : 0;
+  uint32_t r0 = r0_env ? round_r0(r0_env) : tile_r0;  // (env: first bound, measurement)
   for (int attempt = 0; attempt < 4 && !ok; attempt++) {
     to.r0 = int(r0);
     to.core = std::min(kTileC - 4 * int(r0), kMaxCore * kTileThreads);
