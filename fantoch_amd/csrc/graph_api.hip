@@ -81,6 +81,93 @@ __global__ void k_resolve_fill(uint32_t V, const uint64_t *__restrict__ dot,
   }
 }
 
+// appended batch rows: offsets rebased past the carried prefix
+__global__ void k_rebase(uint32_t n, uint32_t *__restrict__ koff, uint32_t kbase,
+                         uint32_t *__restrict__ doff, uint32_t dbase) {
+  GRID_STRIDE(i, n) {
+    koff[i] += kbase;
+    doff[i] += dbase;
+  }
+}
+
+// executed vertices in execution order: their dots and SCC labels
+__global__ void k_gather_exec(uint32_t m, const uint32_t *__restrict__ order,
+                              const uint64_t *__restrict__ dot, const uint64_t *__restrict__ label,
+                              uint64_t *__restrict__ odot, uint64_t *__restrict__ olab) {
+  GRID_STRIDE(j, m) {
+    const uint32_t v = order[j];
+    odot[j] = dot[v];
+    olab[j] = label[v];
+  }
+}
+
+// pending compaction: per vertex kept (1), its key and dep counts
+__global__ void k_keep_counts(uint32_t V, const uint8_t *__restrict__ blocked,
+                              const uint32_t *__restrict__ koff, const uint32_t *__restrict__ doff,
+                              uint32_t *__restrict__ kv, uint32_t *__restrict__ kk,
+                              uint32_t *__restrict__ kd) {
+  GRID_STRIDE(v, V) {
+    const bool keep = blocked[v] != 0;
+    kv[v] = keep;
+    kk[v] = keep ? koff[v + 1] - koff[v] : 0u;
+    kd[v] = keep ? doff[v + 1] - doff[v] : 0u;
+  }
+}
+
+__global__ void k_keep_copy(uint32_t V, const uint8_t *__restrict__ blocked,
+                            const uint64_t *__restrict__ dot, const uint32_t *__restrict__ koff,
+                            const uint32_t *__restrict__ key32, const uint32_t *__restrict__ doff,
+                            const uint64_t *__restrict__ ddot, const uint32_t *__restrict__ pv,
+                            const uint32_t *__restrict__ pk, const uint32_t *__restrict__ pd,
+                            uint64_t *__restrict__ ndot, uint32_t *__restrict__ nkoff,
+                            uint32_t *__restrict__ nkey32, uint32_t *__restrict__ ndoff,
+                            uint64_t *__restrict__ nddot) {
+  GRID_STRIDE(v, V) {
+    if (!blocked[v]) continue;
+    const uint32_t o = pv[v];
+    ndot[o] = dot[v];
+    nkoff[o] = pk[v];
+    ndoff[o] = pd[v];
+    for (uint32_t e = koff[v], q = pk[v]; e < koff[v + 1]; e++, q++) nkey32[q] = key32[e];
+    for (uint32_t e = doff[v], q = pd[v]; e < doff[v + 1]; e++, q++) nddot[q] = ddot[e];
+  }
+}
+
+// the missing dependencies (neither executed nor a vertex) of the vertices
+// that have one, appended to a list (order and repeats do not matter)
+__global__ void k_missing_list(uint32_t V, const uint8_t *__restrict__ blocked0,
+                               const uint64_t *__restrict__ dot, const uint32_t *__restrict__ doff,
+                               const uint64_t *__restrict__ ddot, const uint64_t *__restrict__ sd,
+                               const uint32_t *__restrict__ sv,
+                               const uint64_t *__restrict__ frontier,
+                               const uint64_t *__restrict__ exc, uint32_t nexc, uint32_t cap,
+                               uint32_t *__restrict__ n_out, uint64_t *__restrict__ out) {
+  GRID_STRIDE(v, V) {
+    if (!blocked0[v]) continue;
+    const uint64_t self = dot[v];
+    for (uint32_t e = doff[v]; e < doff[v + 1]; e++) {
+      const uint64_t d = ddot[e];
+      if (d == self || executed_dev(d, frontier, exc, nexc) || find_vid(d, sd, sv, V) >= 0)
+        continue;
+      const uint32_t q = atomicAdd(n_out, 1u);
+      if (q < cap) out[q] = d;
+    }
+  }
+}
+
+// DBuf growth that keeps the first `keep` elements (the carried prefix)
+template <class T>
+static T *grow_keep(DBuf<T> &b, size_t need, size_t keep, hipStream_t s) {
+  if (b.get() && need <= b.cap) return b.get();
+  DBuf<T> n;
+  n.ensure(need + need / 2);
+  if (keep && b.get())
+    FH_HIP(hipMemcpyAsync(n.get(), b.get(), keep * sizeof(T), hipMemcpyDeviceToDevice, s));
+  FH_HIP(hipStreamSynchronize(s));
+  b.swap(n);
+  return b.get();
+}
+
 }  // namespace
 
 struct GraphDevice {
@@ -91,10 +178,26 @@ struct GraphDevice {
   hipStream_t stream = nullptr;
   int key_bits = 1;
   AEClock clock;
-  // carried pending vertices (arrival order); p_cshard = Command::shards()
-  // bitmask per vertex, p_dshard = Dependency::shards bitmask per dependency
-  std::vector<uint64_t> p_dot, p_keys, p_deps, p_cshard, p_dshard;
-  std::vector<uint32_t> p_koff{0}, p_doff{0};
+  // Carried pending vertices.  The device keeps them between batches in
+  // arrival order (dots, key lists, dependency lists: set `cur` of two, the
+  // pass compacts the survivors into the other), so a batch uploads only its
+  // own commands.  The host keeps what the control paths need per pending
+  // dot (request replies, the watchdog, metrics): Command::shards() bitmask,
+  // the dependencies with their Dependency::shards bitmasks, the add time and
+  // the arrival sequence.
+  struct PInfo {
+    uint64_t seq, cshard, time;
+    std::vector<uint64_t> deps, dshards;
+  };
+  std::unordered_map<uint64_t, PInfo> pend;
+  std::map<uint64_t, uint64_t> porder;  // arrival seq -> dot
+  uint64_t next_seq = 0;
+  struct DSet {
+    DBuf<uint64_t> dot, ddot;
+    DBuf<uint32_t> koff, key32, doff;
+    uint32_t P = 0, KP = 0, DP = 0;
+  } ds[2];
+  int cur = 0;
   // partial replication (graph/mod.rs:139-157, 279-375; index.rs:145-211):
   // requested = dots already indexed as a missing non-local dependency
   // (PendingIndex keys that produced a request), out_requests = requests()
@@ -112,9 +215,8 @@ struct GraphDevice {
   std::deque<std::pair<uint64_t, uint64_t>> ready;
   std::vector<uint64_t> missing_now;
   // time (SysTime::millis of the caller, fh_graph_set_time): vertices are
-  // stamped when added (Vertex::new, tarjan.rs:335-351); p_time per pending
+  // stamped when added (Vertex::new, tarjan.rs:335-351)
   uint64_t now_ms = 0;
-  std::vector<uint64_t> p_time;
   // executor metrics not yet taken (ExecutorMetricsKind, executor/mod.rs:
   // 122-129): ChainSize per executed SCC, ExecutionDelay per command
   // (save_scc, graph/mod.rs:490-525)
@@ -124,8 +226,8 @@ struct GraphDevice {
   bool clock_changed = false;
   uint64_t passes = 0, skipped = 0;
   // device buffers
-  DBuf<uint64_t> d_dot, d_ddot, d_sd, d_sd2, d_frontier, d_exc;
-  DBuf<uint32_t> d_koff, d_key32, d_doff, d_cnt, d_off, d_dst, d_sv, d_sv2, d_err;
+  DBuf<uint64_t> d_sd, d_sd2, d_frontier, d_exc, d_xdot, d_xlab, d_miss;
+  DBuf<uint32_t> d_cnt, d_off, d_dst, d_sv, d_sv2, d_err, d_kv, d_kk, d_kd, d_pv, d_pk, d_pd;
   DBuf<uint8_t> d_blocked0;
   SortWorkspace sort_ws;
   ScanWorkspace scan_ws;
@@ -141,6 +243,13 @@ struct GraphDevice {
     core.stream = stream;
     d_err.ensure(4);
     d_frontier.ensure(256);
+    for (auto &d : ds) {
+      d.koff.ensure(16);
+      d.doff.ensure(16);
+      FH_HIP(hipMemsetAsync(d.koff.get(), 0, sizeof(uint32_t), stream));
+      FH_HIP(hipMemsetAsync(d.doff.get(), 0, sizeof(uint32_t), stream));
+    }
+    FH_HIP(hipStreamSynchronize(stream));
   }
   ~GraphDevice() {
     (void)hipSetDevice(device);
@@ -162,7 +271,6 @@ struct GraphDevice {
   void index_requests(size_t n, const uint64_t *dot, const uint32_t *dep_off,
                       const uint64_t *dep_dot, const uint64_t *dep_shards) {
     if (cfg.shard_count <= 1 || !dep_shards || n == 0) return;
-    std::unordered_set<uint64_t> carried(p_dot.begin(), p_dot.end());
     std::unordered_map<uint64_t, size_t> pos;
     pos.reserve(n);
     for (size_t i = 0; i < n; i++) pos.emplace(dot[i], i);
@@ -170,7 +278,7 @@ struct GraphDevice {
     for (size_t i = 0; i < n; i++) {
       for (uint32_t e = dep_off[i]; e < dep_off[i + 1]; e++) {
         const uint64_t d = dep_dot[e];
-        if (d == dot[i] || clock.contains(d) || carried.count(d)) continue;
+        if (d == dot[i] || clock.contains(d) || carried(d)) continue;
         auto it = pos.find(d);
         if (it != pos.end() && it->second < i) continue;
         // "shards should be set if it's not a noop" (index.rs:190-194)
@@ -186,21 +294,21 @@ struct GraphDevice {
 
   // process_requests (mod.rs:297-375): Info for an indexed vertex, Executed
   // for an executed dot, otherwise buffer until the next cleanup.
+  // a carried (pending) vertex; batch vertices enter `pend` only after the
+  // pass that indexes them
+  bool carried(uint64_t d) const { return pend.count(d) != 0 && pend.at(d).seq < batch_seq0; }
+  uint64_t batch_seq0 = ~uint64_t(0);
+
   void process_requests(uint64_t from, const uint64_t *dots, size_t n) {
-    std::unordered_map<uint64_t, size_t> vid;
-    vid.reserve(p_dot.size());
-    for (size_t v = 0; v < p_dot.size(); v++) vid.emplace(p_dot[v], v);
     for (size_t i = 0; i < n; i++) {
       const uint64_t d = dots[i];
-      auto it = vid.find(d);
-      if (it != vid.end()) {
-        const size_t v = it->second;
+      auto it = pend.find(d);
+      if (it != pend.end()) {
+        const PInfo &pi = it->second;
         // panic if the shard that requested this vertex replicates it (:313-322)
-        FH_CHECK(from >= 64 || !((p_cshard[v] >> from) & 1), FH_EINVARIANT,
+        FH_CHECK(from >= 64 || !((pi.cshard >> from) & 1), FH_EINVARIANT,
                  "Graph::process_requests: requested dot is replicated by the requesting shard");
-        Reply r{from, d, p_cshard[v], FH_REPLY_INFO, {}, {}};
-        r.deps.assign(p_deps.begin() + p_doff[v], p_deps.begin() + p_doff[v + 1]);
-        r.dshards.assign(p_dshard.begin() + p_doff[v], p_dshard.begin() + p_doff[v + 1]);
+        Reply r{from, d, pi.cshard, FH_REPLY_INFO, pi.deps, pi.dshards};
         replies.push_back(std::move(r));
       } else if (clock.contains(d)) {
         replies.push_back(Reply{from, d, 0, FH_REPLY_EXECUTED, {}, {}});
@@ -245,28 +353,42 @@ struct GraphDevice {
     }
     passes++;
     clock_changed = false;
-    // vertices: carried pending (earlier arrivals) then the batch
-    const size_t P = p_dot.size();
+    // vertices: carried pending (earlier arrivals, already on the device)
+    // then the batch (the only upload)
+    DSet &W = ds[cur];
+    const size_t P = W.P;
     const size_t V = P + n;
     FH_CHECK(V < (size_t(1) << 30), FH_EINVAL, "too many vertices");
-    std::vector<uint64_t> vdot(p_dot);
-    vdot.insert(vdot.end(), dot, dot + n);
-    std::vector<uint32_t> koff(p_koff), doff(p_doff);
-    std::vector<uint64_t> keys(p_keys), deps(p_deps), cshard(p_cshard), dshard(p_dshard);
-    for (size_t i = 0; i < n; i++) {
-      for (uint32_t e = key_off[i]; e < key_off[i + 1]; e++) {
-        FH_CHECK(key_id[e] < cfg.key_space, FH_EINVAL, "key id >= key_space");
-        keys.push_back(key_id[e]);
-      }
-      koff.push_back(uint32_t(keys.size()));
-      deps.insert(deps.end(), dep_dot + dep_off[i], dep_dot + dep_off[i + 1]);
-      doff.push_back(uint32_t(deps.size()));
-      cshard.push_back(cmd_shards ? cmd_shards[i] : 0);
-      for (uint32_t e = dep_off[i]; e < dep_off[i + 1]; e++)
-        dshard.push_back(dep_shards ? dep_shards[e] : 0);
+    FH_CHECK(P == pend.size(), FH_EINVARIANT, "graph: device / host pending sets disagree");
+    const size_t KB = n ? key_off[n] : 0, DB = n ? dep_off[n] : 0;
+    FH_CHECK(size_t(W.KP) + KB < (size_t(1) << 32) && size_t(W.DP) + DB < (size_t(1) << 32),
+             FH_EINVAL, "too many keys / dependencies");
+    std::vector<uint32_t> k32(KB);
+    for (size_t e = 0; e < KB; e++) {
+      FH_CHECK(key_id[e] < cfg.key_space, FH_EINVAL, "key id >= key_space");
+      k32[e] = uint32_t(key_id[e]);
     }
     if (V == 0) return;
-    std::vector<uint32_t> k32(keys.begin(), keys.end());
+    uint64_t *ddot_v = grow_keep(W.dot, V + 1, P, stream);
+    uint32_t *dko = grow_keep(W.koff, V + 2, P + 1, stream);
+    uint32_t *dk = grow_keep(W.key32, W.KP + KB + 1, W.KP, stream);
+    uint32_t *ddo = grow_keep(W.doff, V + 2, P + 1, stream);
+    uint64_t *dd = grow_keep(W.ddot, W.DP + DB + 1, W.DP, stream);
+    if (n) {
+      FH_HIP(hipMemcpyAsync(ddot_v + P, dot, n * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+      FH_HIP(hipMemcpyAsync(dko + P, key_off, (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                            stream));
+      FH_HIP(hipMemcpyAsync(ddo + P, dep_off, (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                            stream));
+      if (KB)
+        FH_HIP(hipMemcpyAsync(dk + W.KP, k32.data(), KB * sizeof(uint32_t), hipMemcpyHostToDevice,
+                              stream));
+      if (DB)
+        FH_HIP(hipMemcpyAsync(dd + W.DP, dep_dot, DB * sizeof(uint64_t), hipMemcpyHostToDevice,
+                              stream));
+      k_rebase<<<grid_for(n + 1, B), B, 0, stream>>>(uint32_t(n + 1), dko + P, W.KP, ddo + P,
+                                                      W.DP);
+    }
     // executed clock mirror
     std::vector<uint64_t> exc(clock.exc.begin(), clock.exc.end());
     std::sort(exc.begin(), exc.end());
@@ -276,29 +398,13 @@ struct GraphDevice {
     if (!exc.empty())
       FH_HIP(hipMemcpyAsync(dexc, exc.data(), exc.size() * sizeof(uint64_t),
                             hipMemcpyHostToDevice, stream));
-    uint64_t *ddot_v = d_dot.ensure(V);
-    FH_HIP(hipMemcpyAsync(ddot_v, vdot.data(), V * sizeof(uint64_t), hipMemcpyHostToDevice,
-                          stream));
-    uint32_t *dko = d_koff.ensure(V + 1);
-    FH_HIP(hipMemcpyAsync(dko, koff.data(), (V + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
-                          stream));
-    uint32_t *dk = d_key32.ensure(k32.size() + 1);
-    if (!k32.empty())
-      FH_HIP(hipMemcpyAsync(dk, k32.data(), k32.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                            stream));
-    uint32_t *ddo = d_doff.ensure(V + 1);
-    FH_HIP(hipMemcpyAsync(ddo, doff.data(), (V + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
-                          stream));
-    uint64_t *dd = d_ddot.ensure(deps.size() + 1);
-    if (!deps.empty())
-      FH_HIP(hipMemcpyAsync(dd, deps.data(), deps.size() * sizeof(uint64_t),
-                            hipMemcpyHostToDevice, stream));
     // dot -> vid index
     uint64_t *sd = nullptr;
     uint32_t *sv = nullptr;
-    sort_pairs<uint64_t, uint32_t>(ddot_v, nullptr, d_sd.ensure(V), d_sv.ensure(V), d_sd2.ensure(V),
-                         d_sv2.ensure(V), V, 64, sort_ws, stream, &sd, &sv);
-    FH_HIP(hipMemsetAsync(d_err.get(), 0, sizeof(uint32_t), stream));
+    sort_pairs<uint64_t, uint32_t>(ddot_v, nullptr, d_sd.ensure(V), d_sv.ensure(V),
+                                   d_sd2.ensure(V), d_sv2.ensure(V), V, 64, sort_ws, stream, &sd,
+                                   &sv);
+    FH_HIP(hipMemsetAsync(d_err.get(), 0, 2 * sizeof(uint32_t), stream));
     k_dup_check<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), sd, d_err.get());
     uint32_t *cnt = d_cnt.ensure(V + 1);
     uint8_t *b0 = d_blocked0.ensure(V + 1);
@@ -311,9 +417,25 @@ struct GraphDevice {
     FH_HIP(hipMemcpyAsync(&E, off + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     FH_HIP(hipMemcpyAsync(&dup, d_err.get(), sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     FH_HIP(hipStreamSynchronize(stream));
-    // mod.rs:235-240: indexing an already indexed dot panics
+    // mod.rs:235-240: indexing an already indexed dot panics (state unchanged:
+    // the carried prefix is untouched, the appended rows are ignored)
     FH_CHECK(dup == 0, FH_EINVARIANT, "Graph::handle_add tried to index already indexed dot");
+    batch_seq0 = next_seq;
     index_requests(n, dot, dep_off, dep_dot, dep_shards);
+    batch_seq0 = ~uint64_t(0);
+    // the batch joins the host's pending metadata (executed ones leave below)
+    for (size_t i = 0; i < n; i++) {
+      PInfo pi;
+      pi.seq = next_seq++;
+      pi.cshard = cmd_shards ? cmd_shards[i] : 0;
+      pi.time = now_ms;
+      pi.deps.assign(dep_dot + dep_off[i], dep_dot + dep_off[i + 1]);
+      pi.dshards.resize(pi.deps.size(), 0);
+      if (dep_shards)
+        std::copy(dep_shards + dep_off[i], dep_shards + dep_off[i + 1], pi.dshards.begin());
+      porder.emplace(pi.seq, dot[i]);
+      pend.emplace(dot[i], std::move(pi));
+    }
     uint32_t *dst = d_dst.ensure(E + 1);
     k_resolve_fill<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), ddot_v, ddo, dd, sd, sv,
                                                       d_frontier.get(), dexc,
@@ -331,64 +453,94 @@ struct GraphDevice {
     gin.want_per_key = false;  // the executor's monitor is fed from the drain order
     GraphOutput out;
     core.run(gin, out);
-    // results to host
-    std::vector<uint32_t> order(out.nexec);
-    std::vector<uint64_t> label(V);
-    std::vector<uint8_t> blocked(V);
-    if (out.nexec)
-      FH_HIP(hipMemcpyAsync(order.data(), out.exec_order, out.nexec * sizeof(uint32_t),
-                            hipMemcpyDeviceToHost, stream));
-    FH_HIP(hipMemcpyAsync(label.data(), out.scc_label, V * sizeof(uint64_t),
-                          hipMemcpyDeviceToHost, stream));
-    FH_HIP(hipMemcpyAsync(blocked.data(), out.blocked, V, hipMemcpyDeviceToHost, stream));
+    // executed vertices to the host: dots and labels in execution order
+    const uint32_t nexec = out.nexec;
+    std::vector<uint64_t> xdot(nexec), xlab(nexec);
+    if (nexec) {
+      uint64_t *xd = d_xdot.ensure(nexec), *xl = d_xlab.ensure(nexec);
+      k_gather_exec<<<grid_for(nexec, B), B, 0, stream>>>(nexec, out.exec_order, ddot_v,
+                                                           out.scc_label, xd, xl);
+      FH_HIP(hipMemcpyAsync(xdot.data(), xd, nexec * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                            stream));
+      FH_HIP(hipMemcpyAsync(xlab.data(), xl, nexec * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                            stream));
+    }
+    // the missing dependencies of the vertices that stay pending
+    const uint32_t P2 = uint32_t(V - nexec);
+    uint32_t nmiss = 0;
+    uint64_t *miss = nullptr;
+    if (P2) {
+      const uint32_t mcap = uint32_t(std::min<size_t>(W.DP + DB, size_t(1) << 30));
+      miss = d_miss.ensure(mcap + 1);
+      k_missing_list<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), b0, ddot_v, ddo, dd, sd, sv,
+                                                        d_frontier.get(), dexc,
+                                                        uint32_t(exc.size()), mcap,
+                                                        d_err.get() + 1, miss);
+      nmiss = fetch_u32(d_err.get() + 1, stream);
+      nmiss = std::min(nmiss, mcap);
+    }
+    std::vector<uint64_t> mlist(nmiss);
+    if (nmiss)
+      FH_HIP(hipMemcpyAsync(mlist.data(), miss, nmiss * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                            stream));
+    // the survivors, compacted in arrival order into the other set
+    DSet &N = ds[1 - cur];
+    if (P2) {
+      uint32_t *kv = d_kv.ensure(V), *kk = d_kk.ensure(V), *kd = d_kd.ensure(V);
+      uint32_t *pv = d_pv.ensure(V + 1), *pk = d_pk.ensure(V + 1), *pd = d_pd.ensure(V + 1);
+      k_keep_counts<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), out.blocked, dko, ddo, kv, kk,
+                                                       kd);
+      exclusive_scan_u32(kv, pv, V, scan_ws, stream);
+      exclusive_scan_u32(kk, pk, V, scan_ws, stream);
+      exclusive_scan_u32(kd, pd, V, scan_ws, stream);
+      uint32_t tot[3];
+      FH_HIP(hipMemcpyAsync(&tot[0], pv + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      FH_HIP(hipMemcpyAsync(&tot[1], pk + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      FH_HIP(hipMemcpyAsync(&tot[2], pd + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      FH_HIP(hipStreamSynchronize(stream));
+      FH_CHECK(tot[0] == P2, FH_EINVARIANT, "graph: pending count disagrees with the pass");
+      uint64_t *ndot = N.dot.ensure(P2 + 1), *nddot = N.ddot.ensure(tot[2] + 1);
+      uint32_t *nkoff = N.koff.ensure(P2 + 2), *nkey = N.key32.ensure(tot[1] + 1);
+      uint32_t *ndoff = N.doff.ensure(P2 + 2);
+      k_keep_copy<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), out.blocked, ddot_v, dko, dk,
+                                                     ddo, dd, pv, pk, pd, ndot, nkoff, nkey,
+                                                     ndoff, nddot);
+      FH_HIP(hipMemcpyAsync(nkoff + P2, &tot[1], sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+      FH_HIP(hipMemcpyAsync(ndoff + P2, &tot[2], sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+      N.KP = tot[1];
+      N.DP = tot[2];
+    } else {
+      N.koff.ensure(16);
+      N.doff.ensure(16);
+      FH_HIP(hipMemsetAsync(N.koff.get(), 0, sizeof(uint32_t), stream));
+      FH_HIP(hipMemsetAsync(N.doff.get(), 0, sizeof(uint32_t), stream));
+      N.KP = N.DP = 0;
+    }
+    N.P = P2;
+    W.P = W.KP = W.DP = 0;
+    cur = 1 - cur;
     FH_HIP(hipStreamSynchronize(stream));
-    std::vector<uint64_t> vtime(p_time);
-    vtime.resize(V, now_ms);
-    for (uint32_t j = 0; j < out.nexec; j++) {
-      const uint32_t v = order[j];
-      ready.emplace_back(vdot[v], label[v]);
-      clock.add(vdot[v]);  // executed clock update (tarjan.rs:296)
+    for (uint32_t j = 0; j < nexec; j++) {
+      const uint64_t d = xdot[j];
+      ready.emplace_back(d, xlab[j]);
+      clock.add(d);  // executed clock update (tarjan.rs:296)
       // metrics: one ChainSize per SCC (members are contiguous in the
       // execution order), one ExecutionDelay per command
-      if (j == 0 || label[order[j - 1]] != label[v]) m_chain.push_back(0);
+      if (j == 0 || xlab[j - 1] != xlab[j]) m_chain.push_back(0);
       m_chain.back()++;
-      m_delay.push_back(now_ms >= vtime[v] ? now_ms - vtime[v] : 0);
+      auto it = pend.find(d);
+      FH_CHECK(it != pend.end(), FH_EINVARIANT, "graph: executed dot was not a vertex");
+      m_delay.push_back(now_ms >= it->second.time ? now_ms - it->second.time : 0);
+      porder.erase(it->second.seq);
+      pend.erase(it);
     }
-    // carry pending vertices; record their missing dependencies
-    p_dot.clear();
-    p_keys.clear();
-    p_deps.clear();
-    p_cshard.clear();
-    p_dshard.clear();
-    p_koff.assign(1, 0);
-    p_doff.assign(1, 0);
-    p_time.clear();
-    std::unordered_set<uint64_t> present;
-    for (size_t v = 0; v < V; v++)
-      if (blocked[v]) present.insert(vdot[v]);
-    missing_now.clear();
-    std::unordered_set<uint64_t> seen;
-    for (size_t v = 0; v < V; v++) {
-      if (!blocked[v]) continue;
-      p_dot.push_back(vdot[v]);
-      p_keys.insert(p_keys.end(), keys.begin() + koff[v], keys.begin() + koff[v + 1]);
-      p_koff.push_back(uint32_t(p_keys.size()));
-      p_deps.insert(p_deps.end(), deps.begin() + doff[v], deps.begin() + doff[v + 1]);
-      p_dshard.insert(p_dshard.end(), dshard.begin() + doff[v], dshard.begin() + doff[v + 1]);
-      p_doff.push_back(uint32_t(p_deps.size()));
-      p_cshard.push_back(cshard[v]);
-      p_time.push_back(vtime[v]);
-      for (uint32_t e = doff[v]; e < doff[v + 1]; e++) {
-        const uint64_t d = deps[e];
-        if (d != vdot[v] && !clock.contains(d) && !present.count(d) && seen.insert(d).second)
-          missing_now.push_back(d);
-      }
-    }
-    std::sort(missing_now.begin(), missing_now.end());
+    std::sort(mlist.begin(), mlist.end());
+    mlist.erase(std::unique(mlist.begin(), mlist.end()), mlist.end());
+    missing_now.swap(mlist);
     // PendingIndex entries go once their parent dot is indexed or executed
     // (index.rs remove, called from check_pending)
     for (auto it = requested.begin(); it != requested.end();) {
-      if (clock.contains(*it) || present.count(*it))
+      if (clock.contains(*it) || pend.count(*it))
         it = requested.erase(it);
       else
         ++it;
@@ -402,33 +554,32 @@ struct GraphDevice {
   // is a liveness bug: FH_EINVARIANT, where the reference panics.
   void monitor_pending(uint64_t threshold_ms, std::vector<std::pair<uint64_t, uint64_t>> &old_out,
                        std::vector<uint64_t> &nmissing) {
-    std::unordered_map<uint64_t, size_t> vid;
-    vid.reserve(p_dot.size());
-    for (size_t v = 0; v < p_dot.size(); v++) vid.emplace(p_dot[v], v);
-    std::vector<size_t> idx;
-    for (size_t v = 0; v < p_dot.size(); v++)
-      if (now_ms >= p_time[v] && now_ms - p_time[v] >= threshold_ms) idx.push_back(v);
-    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return p_time[a] < p_time[b]; });
+    std::vector<std::pair<uint64_t, uint64_t>> idx;  // (time, dot), arrival order
+    for (const auto &so : porder) {
+      const PInfo &pi = pend.at(so.second);
+      if (now_ms >= pi.time && now_ms - pi.time >= threshold_ms) idx.emplace_back(pi.time, so.second);
+    }
+    std::stable_sort(idx.begin(), idx.end(),
+                     [](const auto &a, const auto &b) { return a.first < b.first; });
     std::vector<uint64_t> stuck;
-    for (size_t v : idx) {
+    for (const auto &tv : idx) {
+      const uint64_t v = tv.second;
       std::unordered_set<uint64_t> visited, missing;
-      std::vector<size_t> stack{v};
-      visited.insert(p_dot[v]);
+      std::vector<uint64_t> stack{v};
+      visited.insert(v);
       while (!stack.empty()) {
-        const size_t x = stack.back();
+        const uint64_t x = stack.back();
         stack.pop_back();
-        for (uint32_t e = p_doff[x]; e < p_doff[x + 1]; e++) {
-          const uint64_t d = p_deps[e];
-          if (d == p_dot[x] || clock.contains(d)) continue;
-          auto it = vid.find(d);
-          if (it == vid.end())
+        for (uint64_t d : pend.at(x).deps) {
+          if (d == x || clock.contains(d)) continue;
+          if (!pend.count(d))
             missing.insert(d);
           else if (visited.insert(d).second)
-            stack.push_back(it->second);
+            stack.push_back(d);
         }
       }
-      if (missing.empty()) stuck.push_back(p_dot[v]);
-      old_out.emplace_back(p_dot[v], now_ms - p_time[v]);
+      if (missing.empty()) stuck.push_back(v);
+      old_out.emplace_back(v, now_ms - tv.first);
       nmissing.push_back(missing.size());
     }
     if (!stuck.empty()) {
@@ -654,7 +805,7 @@ fh_status fh_graph_passes(fh_graph *h, uint64_t *passes, uint64_t *skipped) {
 fh_status fh_graph_pending(fh_graph *h, size_t *count) {
   FH_API_BEGIN
   FH_CHECK(h && count, FH_EINVAL, "null argument");
-  *count = h->dev.p_dot.size();
+  *count = h->dev.pend.size();
   FH_API_END
 }
 

@@ -207,3 +207,49 @@ def test_executed_frontier_never_moves_back_and_folds_exceptions():
     assert ex.pending() == 1
     with pytest.raises(L.FhError):
         L.check(ex._lib.fh_graph_set_executed_frontier(ex._h, 2, 1))
+
+
+def test_device_resident_backlog_then_release_matches_oracle():
+    """A command held back until the end leaves most of the stream pending
+    behind it (carried on the device from batch to batch); the missing set is
+    exactly that dot; re-adding a pending dot is rejected without touching the
+    backlog; releasing it executes everything in the oracle's per-key order
+    for the same arrival order."""
+    s = Workload.zipf(0.99, 256, k=2, views=3, window=64, seed=23).generate(6000)
+    key_off = s.key_off()
+    keys = s.keys.reshape(-1)
+    dep_off, deps = O.views_run(0, 5, s.dots, key_off, keys, s.fq_proc, s.fq_time)
+    hold = 40
+    arrival = np.array([i for i in range(s.n) if i != hold] + [hold])
+    a_dots, a_keys = s.dots[arrival], s.keys[arrival]
+    a_key_off = (np.arange(s.n + 1) * s.k).astype(np.uint32)
+    a_dep_off = np.zeros(s.n + 1, dtype=np.uint32)
+    a_deps = []
+    for j, i in enumerate(arrival):
+        a_deps.extend(deps[dep_off[i]:dep_off[i + 1]])
+        a_dep_off[j + 1] = len(a_deps)
+    a_deps = np.asarray(a_deps, dtype=np.uint64)
+    ex_o, lab_o, kso, ks = O.graph_run(a_dots, a_key_off, a_keys.reshape(-1), a_dep_off, a_deps,
+                                       s.key_space)
+    want = {int(k): ks[kso[k]:kso[k + 1]].tolist() for k in np.nonzero(np.diff(kso))[0]}
+    ex = HipGraphExecutor(1, 0, 5, 1, key_space=s.key_space)
+
+    def info(j):
+        return GraphExecutionInfo.add(int(a_dots[j]), [int(x) for x in a_keys[j]],
+                                      a_deps[a_dep_off[j]:a_dep_off[j + 1]].tolist())
+    for b0 in range(0, s.n - 1, 333):
+        ex.handle_batch([info(j) for j in range(b0, min(s.n - 1, b0 + 333))])
+    backlog = ex.pending()
+    assert backlog > s.n // 4
+    assert ex.missing() == [int(s.dots[hold])]
+    from fantoch_amd import _lib as L
+    pend = [d for d, _, _ in ex.monitor_pending(0)]
+    assert len(pend) == backlog
+    j = int(np.nonzero(a_dots == np.uint64(pend[len(pend) // 2]))[0][0])
+    with pytest.raises(L.FhError):
+        ex.handle_batch([info(j)])                   # already pending
+    assert ex.pending() == backlog
+    ex.handle_batch([info(s.n - 1)])                 # the held command
+    assert ex.pending() == 0 and ex.missing() == []
+    assert ex.monitor() == want
+    assert ex.last_labels == dict(zip(ex_o.tolist(), lab_o.tolist()))
