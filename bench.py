@@ -197,7 +197,7 @@ def main():
         import torch.distributed as dist_mod
         dist = dist_mod
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl")
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
     from fantoch_amd.engine import Engine
 

@@ -49,6 +49,7 @@ __global__ void k_dup_check(uint32_t V, const uint64_t *__restrict__ sd, uint32_
 struct AEClock {
   uint64_t frontier[256] = {0};
   std::unordered_set<uint64_t> exc;
+  uint64_t version = 0;  // bumped on every change (device mirrors re-upload)
   bool contains(uint64_t d) const {
     return (d & 0x00FFFFFFFFFFFFFFull) <= frontier[d >> 56] || exc.count(d);
   }
@@ -57,6 +58,7 @@ struct AEClock {
     const uint32_t s = uint32_t(d >> 56);
     const uint64_t q = d & 0x00FFFFFFFFFFFFFFull;
     if (q <= frontier[s]) return false;
+    version++;
     if (q == frontier[s] + 1) {
       frontier[s] = q;
       while (!exc.empty()) {
@@ -67,7 +69,9 @@ struct AEClock {
       }
       return true;
     }
-    return exc.insert(d).second;
+    if (exc.insert(d).second) return true;
+    version--;  // already an exception: unchanged
+    return false;
   }
 };
 

@@ -198,6 +198,8 @@ struct GraphDevice {
     uint32_t P = 0, KP = 0, DP = 0;
   } ds[2];
   int cur = 0;
+  std::vector<uint64_t> exc_sorted;  // the clock's exceptions as on the device
+  uint64_t exc_version = ~uint64_t(0);
   // partial replication (graph/mod.rs:139-157, 279-375; index.rs:145-211):
   // requested = dots already indexed as a missing non-local dependency
   // (PendingIndex keys that produced a request), out_requests = requests()
@@ -389,15 +391,21 @@ struct GraphDevice {
       k_rebase<<<grid_for(n + 1, B), B, 0, stream>>>(uint32_t(n + 1), dko + P, W.KP, ddo + P,
                                                       W.DP);
     }
-    // executed clock mirror
-    std::vector<uint64_t> exc(clock.exc.begin(), clock.exc.end());
-    std::sort(exc.begin(), exc.end());
-    FH_HIP(hipMemcpyAsync(d_frontier.get(), clock.frontier, sizeof(clock.frontier),
-                          hipMemcpyHostToDevice, stream));
-    uint64_t *dexc = d_exc.ensure(exc.size() + 1);
-    if (!exc.empty())
-      FH_HIP(hipMemcpyAsync(dexc, exc.data(), exc.size() * sizeof(uint64_t),
+    // executed clock mirror: re-sorted and re-uploaded only when the clock
+    // changed since the last pass
+    if (clock.version != exc_version) {
+      exc_sorted.assign(clock.exc.begin(), clock.exc.end());
+      std::sort(exc_sorted.begin(), exc_sorted.end());
+      FH_HIP(hipMemcpyAsync(d_frontier.get(), clock.frontier, sizeof(clock.frontier),
                             hipMemcpyHostToDevice, stream));
+      d_exc.ensure(exc_sorted.size() + 1);
+      if (!exc_sorted.empty())
+        FH_HIP(hipMemcpyAsync(d_exc.get(), exc_sorted.data(), exc_sorted.size() * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, stream));
+      exc_version = clock.version;
+    }
+    const std::vector<uint64_t> &exc = exc_sorted;
+    uint64_t *dexc = d_exc.ensure(exc.size() + 1);
     // dot -> vid index
     uint64_t *sd = nullptr;
     uint32_t *sv = nullptr;
@@ -748,6 +756,7 @@ fh_status fh_graph_set_executed_frontier(fh_graph *h, uint32_t source, uint64_t 
     c.exc.erase(it);
     c.frontier[source]++;
   }
+  c.version++;
   h->dev.clock_changed = true;
   FH_API_END
 }

@@ -598,7 +598,7 @@ __global__ void k_elem_fill(uint32_t n, const uint32_t *__restrict__ order, uint
 // one key per command: the element of exec position j is (key, dot) of
 // order[j] (the gather follows the execution order, close to arrival order)
 __global__ void __launch_bounds__(256)
-    k_elem_fill_dots(uint32_t n, const uint32_t *__restrict__ order,
+    k_elem_fill_dots(uint32_t n, uint32_t k, const uint32_t *__restrict__ order,
                      const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot,
                      uint32_t *__restrict__ ek, uint64_t *__restrict__ ed,
                      unsigned long long *__restrict__ src_mx, unsigned int *__restrict__ src_cnt) {
@@ -610,8 +610,10 @@ __global__ void __launch_bounds__(256)
   GRID_STRIDE(j, n) {
     const uint32_t v = order[j];
     const uint64_t d = dot[v];
-    ek[j] = key32[v];
-    ed[j] = d;
+    for (uint32_t s = 0; s < k; s++) {
+      ek[size_t(j) * k + s] = key32[size_t(v) * k + s];
+      ed[size_t(j) * k + s] = d;
+    }
     if (src_mx) acc.add(d);
   }
   if (src_mx) acc.commit(src_mx, src_cnt);  // (src_mx is uniform)
@@ -888,22 +890,24 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
   if (!in.want_per_key) return;
   const uint32_t nexec = out.nexec;
   const uint32_t *ord = out.exec_order;
-  if (in.per_key_dots && !in.key_off && in.k == 1) {
-    // (key, dot) pairs in execution order, stable-sorted by key: the per-key
-    // sequences of dots come out of the sort (no gather by vid afterwards)
-    uint32_t *ek = tmp32a.ensure(nexec + 1), *k2 = flags.ensure(nexec + 1);
-    uint64_t *ed = pk_da.ensure(nexec + 1), *d2 = pk_db.ensure(nexec + 1);
-    k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, in.key32, in.dot, ek, ed,
-                                                           in.src_mx, in.src_cnt);
+  if (in.per_key_dots && !in.key_off && in.k >= 1 && size_t(nexec) * in.k < (size_t(1) << 30)) {
+    // (key, dot) pairs in execution order (k per command), stable-sorted by
+    // key: the per-key sequences of dots come out of the sort (no gather by
+    // vid afterwards)
+    const uint32_t ne = nexec * in.k;
+    uint32_t *ek = tmp32a.ensure(ne + 1), *k2 = flags.ensure(ne + 1);
+    uint64_t *ed = pk_da.ensure(ne + 1), *d2 = pk_db.ensure(ne + 1);
+    k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, in.k, ord, in.key32, in.dot, ek,
+                                                           ed, in.src_mx, in.src_cnt);
     out.src_stats_done = in.src_mx != nullptr;
     uint32_t *ko = nullptr;
     uint64_t *dout = nullptr;
-    sort_pairs<uint32_t, uint64_t>(ek, ed, k2, d2, ek, ed, nexec, in.key_bits, sort_ws, stream,
+    sort_pairs<uint32_t, uint64_t>(ek, ed, k2, d2, ek, ed, ne, in.key_bits, sort_ws, stream,
                                    &ko, &dout);
     out.pk_key = ko;
     out.pk_vid = nullptr;
     out.pk_dot = dout;
-    out.nelem = nexec;
+    out.nelem = ne;
     mark("per_key_order");
     return;
   }
