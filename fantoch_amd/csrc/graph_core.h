@@ -95,6 +95,9 @@ struct GraphCore {
   DBuf<uint32_t> t_h, t_rank, t_cnt, t_start;
   DBuf<uint64_t> t_prof;  // tile path: ready time, group rank/count/start
   uint32_t dbg_tile_fail = 0, dbg_tile_ok = 0;
+  DBuf<uint8_t> fb_pushed;    // coloring reach: vertices that pushed this round
+  bool prefer_full = false;   // the last global-path run needed the full coloring
+  bool kap_seed_ok = true;    // kap holds a bounded run's ready times (k_fb_seed)
   uint32_t tile_r0 = 1536;  // graph_tile: first reach bound to try (set from
                             // the last run's maximum excess)
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)

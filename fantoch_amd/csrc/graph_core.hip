@@ -429,12 +429,17 @@ __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
                            const uint32_t *__restrict__ dst, const uint32_t *__restrict__ erep,
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
-                           const uint32_t *__restrict__ H, uint8_t *reached, uint32_t *changed) {
+                           const uint32_t *__restrict__ H, uint8_t *reached, uint32_t *changed,
+                           uint8_t *__restrict__ pushed) {
   GRID_STRIDE(j, n) {
     const uint32_t v = FB_VID(j);
-    if (blocked[v] || done[v]) continue;
+    // a vertex pushes its edges once, in the launch after its class is
+    // reached (later launches would repeat the same pushes: the reach loop
+    // re-read every edge of every reached class per launch)
+    if (pushed[v] || blocked[v] || done[v]) continue;
     const uint32_t r = rep[v];
     if (!__hip_atomic_load(&reached[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
+    pushed[v] = 1;
     const uint32_t hr = H[r];
     const uint32_t eb = EB(v), ee = EE(v);
     if (erep) {
@@ -727,6 +732,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
   const uint32_t V = in.V;
   uint8_t *done = reinterpret_cast<uint8_t *>(tmp32d.ensure((V + 3) / 4 + 1));
   uint8_t *reached = reinterpret_cast<uint8_t *>(flags.ensure((V + 3) / 4 + 1));
+  uint8_t *pushed = fb_pushed.ensure(V + 1);
   uint32_t *H = tmp32c.ensure(V);
   uint32_t *parent = tmp32a.ensure(V);
   const uint32_t *list = nullptr;
@@ -772,7 +778,8 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     else
       FH_HIP(hipMemsetAsync(H, 0, size_t(V) * sizeof(uint32_t), stream));
     k_fb_init<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
-    if (full && !list) k_fb_seed<<<G, B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get(), H);
+    if (full && !list && kap_seed_ok)
+      k_fb_seed<<<G, B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get(), H);
     dbg_rounds++;
     do {
       dbg_hprop++;
@@ -781,11 +788,12 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
                                        rep.get(), H, scalars.get());
     } while (read_scalar(0));
     k_fb_roots<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
+    FH_HIP(hipMemsetAsync(pushed, 0, V, stream));
     do {
       dbg_reach++;
       FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
       k_fb_reach<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
-                                       rep.get(), H, reached, scalars.get());
+                                       rep.get(), H, reached, scalars.get(), pushed);
     } while (read_scalar(0));
     FH_HIP(hipMemsetAsync(scalars.get() + 1, 0, sizeof(uint32_t), stream));
     // unions go to a separate parent array so rep[] stays stable while read
@@ -1001,9 +1009,26 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   // the exact coloring complete the partition (an exact partition converges in
   // a handful of rounds on every measured stream: C1 2, C4 4, C5 9)
   const uint32_t give_up = nfwd ? 12 : 4;
-  bool ok = order_kappa(in, give_up, iters, true);
-  iters1 = iters;
+  // the last run needed the exact coloring over every vertex: a graph of the
+  // same shape (C5: a 1.2M-member SCC) goes there directly, without the
+  // bounded kappa run and the restricted attempt (their only product here
+  // would be the coloring's seed, worth less than the 3 relax passes)
+  static const char *pf_env = getenv("FH_PREFER_FULL");  // 0 = never, 1 = always
+  const bool direct_full = pf_env ? *pf_env == '1' : prefer_full;
+  bool ok = false;
   dbg_cand = dbg_restricted = 0;
+  if (direct_full) {
+    out.fallback_used = true;
+    kap_seed_ok = false;
+    coloring_fallback(in, 0);
+    kap_seed_ok = true;
+    ok = order_kappa(in, 1u << 30, iters);
+    iters1 = 0;
+  } else {
+    ok = order_kappa(in, give_up, iters, true);
+    iters1 = iters;
+  }
+  bool used_full = direct_full;
   if (!ok) {
     out.fallback_used = true;
     // first the vertices still being raised (the missed cycles are among
@@ -1014,8 +1039,10 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     if (!ok) {
       coloring_fallback(in, 0);
       ok = order_kappa(in, 1u << 30, iters);
+      used_full = true;
     }
   }
+  prefer_full = used_full;
   out.kappa_iters = iters;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   if (debug)

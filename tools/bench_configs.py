@@ -110,14 +110,14 @@ def main():
                 dev_ms.append(ms_)
         r = eng.results()
         _, counts = np.unique(r["scc_label"], return_counts=True)
-        eng2 = Engine(batch.key_space, n=5, device=0)
-        eng2.stage(batch)
-        eng2.set_profiling(True)
-        eng2.run(sync=True)
+        # phases of one more step on the same (warm) engine
+        eng.reset()
+        eng.stage(batch)
+        eng.set_profiling(True)
+        eng.run(sync=True)
         phases = {}
-        for k, v in eng2.kernel_times():
+        for k, v in eng.kernel_times():
             phases[k] = round(phases.get(k, 0.0) + v, 4)
-        eng2.close()
         eng.close()
         ms = float(np.median(wall)) * 1e3
         out = {"config": name, "workload": c["desc"], "cmds_per_step": n, "steps": args.steps,
