@@ -366,7 +366,7 @@ __global__ void k_fb_seed(uint32_t V, const uint8_t *__restrict__ blocked,
   }
 }
 
-__global__ void k_fb_hprop(uint32_t n, const uint32_t *__restrict__ list,
+__global__ void k_fb_hprop(uint32_t V, uint32_t n, const uint32_t *__restrict__ list,
                            const uint32_t *__restrict__ off, uint32_t stride,
                            const uint32_t *__restrict__ dst, const uint32_t *__restrict__ erep,
                            const uint8_t *__restrict__ blocked,
@@ -407,6 +407,15 @@ __global__ void k_fb_hprop(uint32_t n, const uint32_t *__restrict__ list,
             best = h > best ? h : best;
           }
         }
+      }
+      // pointer jump: class r reaches vertex t = H[r], so it reaches all
+      // that t's class reaches (H over the same active subgraph: a lower
+      // bound of the fixpoint, which stays the same); long forward chains
+      // collapse in logarithmically many launches
+      const uint32_t t = max(best, ld_u32(&H[r]));
+      if (t < V && !done[t] && !blocked[t]) {
+        const uint32_t hj = ld_u32(&H[rep[t]]);
+        best = hj > best ? hj : best;
       }
     }
     if (agg_max<uint32_t>(H, r, best, act && best != 0)) *changed = 1;
@@ -784,7 +793,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     do {
       dbg_hprop++;
       FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
-      k_fb_hprop<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
+      k_fb_hprop<<<G, B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
                                        rep.get(), H, scalars.get());
     } while (read_scalar(0));
     k_fb_roots<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
