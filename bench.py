@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--commands", type=int, default=100_000_000, help="C4 stream length")
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=4_000_000,
+    ap.add_argument("--cpu-sample", type=int, default=16_000_000,
                     help="C4 commands in the CPU-baseline prefix (~10 s of one host core)")
     ap.add_argument("--probe", default="sort_scatter,graph_tile,prev_engine,cmd_union,log_keys",
                     help="kernels whose launches are timed in the probe pass")
