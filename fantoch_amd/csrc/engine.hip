@@ -24,6 +24,7 @@
 
 #include "graph_core.h"
 #include "keybucket.h"
+#include "sort_impl.h"
 #include "srcstats.h"
 
 namespace fh {
@@ -47,6 +48,24 @@ constexpr int kMaxLogs = 16;
 struct LogChunk {
   uint32_t first[kMaxLogs];
   uint32_t cum[kMaxLogs + 1];
+};
+
+// the same as a sort source: the first radix pass reads the logs directly
+// (no materialised key/value arrays: one write and one read of 8 B per
+// element saved, opt-in: measured slower, see the chunk loop)
+struct LogSrc {
+  uint32_t k, fq, nlog, K;
+  LogChunk ch;
+  const uint32_t *ent, *key32;
+  __device__ __forceinline__ void get(uint32_t x, uint32_t &key, uint32_t &val) const {
+    uint32_t r = 0;
+    while (r + 1 < nlog && x >= ch.cum[r + 1]) r++;
+    const uint32_t y = x - ch.cum[r];
+    const uint32_t q = ch.first[r] + y / k, s = y % k;
+    const uint32_t e = ent[q];
+    key = (r + 1) * K + key32[(e / fq) * k + s];
+    val = e * k + s;
+  }
 };
 
 __global__ void k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, LogChunk ch,
@@ -1123,12 +1142,23 @@ struct EngineDevice {
         DBuf<uint32_t> &bkb = set ? sk32d : sk32b, &bvb = set ? svd : svb;
         if (pipe && c >= 2) FH_HIP(hipStreamWaitEvent(stream, ev_freed[set], 0));
         uint32_t *lk = bka.ensure(Mc + 1), *lv = bva.ensure(Mc + 1);
-        probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys,
-                      dim3(grid_for(Mc, B)), dim3(B), stream, Mc, k, fq, np, lc, bent, bkey,
-                      uint32_t(key_space), lk, lv);
         uint32_t *ks = nullptr;
-        sort_pairs<uint32_t, uint32_t>(lk, lv, lk, lv, bkb.ensure(Mc + 1), bvb.ensure(Mc + 1), Mc,
-                                       bits, sort_ws, stream, &ks, &vs);
+        // FH_LOG_FUSED=1: pass 0 reads the logs (LogSrc).  Measured on C4:
+        // 16.7 ms against 15.5 materialised -- the divisions and the key
+        // gather move into both pass-0 kernels, which are compute bound
+        static const bool fused = getenv("FH_LOG_FUSED") != nullptr;
+        if (!fused) {
+          probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys,
+                        dim3(grid_for(Mc, B)), dim3(B), stream, Mc, k, fq, np, lc, bent, bkey,
+                        uint32_t(key_space), lk, lv);
+          sort_pairs<uint32_t, uint32_t>(lk, lv, lk, lv, bkb.ensure(Mc + 1), bvb.ensure(Mc + 1),
+                                         Mc, bits, sort_ws, stream, &ks, &vs);
+        } else {
+          const LogSrc src{k, fq, np, uint32_t(key_space), lc, bent, bkey};
+          sort_pairs_src<uint32_t, uint32_t, LogSrc>(src, lk, lv, bkb.ensure(Mc + 1),
+                                                     bvb.ensure(Mc + 1), Mc, bits, sort_ws, stream,
+                                                     &ks, &vs);
+        }
         if (pipe) {
           FH_HIP(hipEventRecord(ev_sorted[set], stream));
           FH_HIP(hipStreamWaitEvent(sp, ev_sorted[set], 0));

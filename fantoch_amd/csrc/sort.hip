@@ -14,290 +14,13 @@
 #include <cstdlib>
 
 #include "sort.h"
+#include "sort_impl.h"
 
 namespace fh {
+
 namespace {
-
-constexpr int kThreads = kSortThreads;  // 256
-constexpr int kItems = kSortItems;      // 16
-constexpr int kTile = kSortTile;        // 4096
-constexpr int kWaves = kThreads / 64;
-constexpr int kGroup = 64;              // tiles per scan group
-
-template <int DB>
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
-  uint64_t peers = __ballot(valid);
-#pragma unroll
-  for (int b = 0; b < DB; b++) {
-    const bool bit = (d >> b) & 1;
-    const uint64_t m = __ballot(bit);
-    peers &= bit ? m : ~m;
-  }
-  return peers;
-}
-
-// Exclusive scan of one value per thread over the 256-thread block.
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_tmp) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = __shfl_up(x, o, 64);
-    if (lane >= o) x += t;
-  }
-  if (lane == 63) s_tmp[w] = x;
-  __syncthreads();
-  uint32_t pre = 0;
-#pragma unroll
-  for (int i = 0; i < kWaves; i++)
-    if (i < w) pre += s_tmp[i];
-  __syncthreads();
-  return pre + x - v;
-}
-
-// Tile element mapping (coalesced): wave w owns a contiguous sub-tile of
-// 64*kItems elements, item i of lane l is element w*64*kItems + i*64 + l.
-// Tile order == (wave, item, lane) lexicographic == input order.
-__device__ __forceinline__ uint32_t elem_index(uint32_t base, int w, int i, int lane) {
-  return base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
-}
-
-template <class K, int DB>
-__global__ void __launch_bounds__(kThreads)
-    k_up(const K *__restrict__ keys, uint32_t n, int shift, uint32_t *__restrict__ counts) {
-  constexpr int R = 1 << DB;
-  __shared__ uint32_t s_h[kWaves][R];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < kWaves * R; i += kThreads) (&s_h[0][0])[i] = 0;
-  const uint32_t base = blockIdx.x * kTile;
-  K key[kItems];
-#pragma unroll
-  for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = elem_index(base, w, i, lane);
-    key[i] = idx < n ? keys[idx] : K(0);
-  }
-  __syncthreads();
-  const uint64_t lt = (uint64_t(1) << lane) - 1;
-#pragma unroll
-  for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = elem_index(base, w, i, lane);
-    const bool valid = idx < n;
-    const uint32_t d = uint32_t((key[i] >> shift) & (R - 1));
-    const uint64_t peers = match_digit<DB>(d, valid);
-    if (valid && (peers & lt) == 0) s_h[w][d] += uint32_t(__popcll(peers));  // wave-private
-  }
-  __syncthreads();
-  for (int d = tid; d < R; d += kThreads) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int ww = 0; ww < kWaves; ww++) c += s_h[ww][d];
-    counts[size_t(blockIdx.x) * R + d] = c;
-  }
-}
-
-// Group g of kGroup tiles: counts[t][d] <- exclusive prefix within the group,
-// gsum[g][d] <- group total.
-template <int DB>
-__global__ void __launch_bounds__(256)
-    k_scan_a(uint32_t *__restrict__ counts, uint32_t tiles, uint32_t *__restrict__ gsum) {
-  constexpr int R = 1 << DB;
-  const uint32_t g = blockIdx.x;
-  const uint32_t t0 = g * kGroup, t1 = min(tiles, t0 + kGroup);
-  for (uint32_t d = threadIdx.x; d < uint32_t(R); d += 256) {
-    uint32_t v[kGroup];
-#pragma unroll
-    for (int i = 0; i < kGroup; i++) v[i] = (t0 + i < t1) ? counts[size_t(t0 + i) * R + d] : 0u;
-    uint32_t run = 0;
-#pragma unroll
-    for (int i = 0; i < kGroup; i++) {
-      if (t0 + i < t1) counts[size_t(t0 + i) * R + d] = run;
-      run += v[i];
-    }
-    gsum[size_t(g) * R + d] = run;
-  }
-}
-
-// One workgroup: gsum[g][d] <- exclusive prefix over groups, dbase[d] <-
-// exclusive prefix of the digit totals.  Thread t owns the Q = R/256
-// consecutive digits [t·Q, (t+1)·Q).
-template <int DB>
-__global__ void __launch_bounds__(256)
-    k_scan_b(uint32_t *__restrict__ gsum, uint32_t groups, uint32_t *__restrict__ dbase) {
-  constexpr int R = 1 << DB, Q = R / 256;
-  __shared__ uint32_t s_tmp[kWaves];
-  uint32_t tot[Q];
-#pragma unroll
-  for (int q = 0; q < Q; q++) {
-    const uint32_t d = threadIdx.x * Q + q;
-    uint32_t run = 0;
-    for (uint32_t g0 = 0; g0 < groups; g0 += 16) {
-      uint32_t v[16];
-#pragma unroll
-      for (int i = 0; i < 16; i++) v[i] = (g0 + i < groups) ? gsum[size_t(g0 + i) * R + d] : 0u;
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        if (g0 + i < groups) gsum[size_t(g0 + i) * R + d] = run;
-        run += v[i];
-      }
-    }
-    tot[q] = run;
-  }
-  uint32_t mine = 0;
-#pragma unroll
-  for (int q = 0; q < Q; q++) mine += tot[q];
-  uint32_t pre = block_excl_scan(mine, s_tmp);
-#pragma unroll
-  for (int q = 0; q < Q; q++) {
-    dbase[threadIdx.x * Q + q] = pre;
-    pre += tot[q];
-  }
-}
-
-// Small sorts (tiles <= kFusedMaxTiles): one 1024-thread workgroup does both
-// scan levels -- 4 threads per digit, each over a contiguous quarter of the
-// tiles (gsum[q][d] <- quarter prefix, dbase[d] <- digit base).
-constexpr int kFusedMaxTiles = 1024;
-__global__ void __launch_bounds__(1024)
-    k_scan_fused(uint32_t *__restrict__ counts, uint32_t tiles, uint32_t per,
-                 uint32_t *__restrict__ gsum, uint32_t *__restrict__ dbase) {
-  __shared__ uint32_t s_part[4][256];
-  __shared__ uint32_t s_tmp[4];
-  const uint32_t d = threadIdx.x & 255, q = threadIdx.x >> 8;
-  const uint32_t t0 = q * per, t1 = min(tiles, t0 + per);
-  uint32_t run = 0;
-  for (uint32_t t = t0; t < t1; t += 16) {
-    uint32_t v[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) v[i] = (t + i < t1) ? counts[size_t(t + i) * 256 + d] : 0u;
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      if (t + i < t1) counts[size_t(t + i) * 256 + d] = run;
-      run += v[i];
-    }
-  }
-  s_part[q][d] = run;
-  __syncthreads();
-  uint32_t qpre = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    if (uint32_t(i) < q) qpre += s_part[i][d];
-    tot += s_part[i][d];
-  }
-  gsum[q * 256 + d] = qpre;
-  // exclusive scan of the digit totals (waves 0..3 hold digits 0..255; every
-  // thread reaches the barrier)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t x = tot;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(x, o, 64);
-    if (lane >= o) x += t;
-  }
-  if (q == 0 && lane == 63) s_tmp[w] = x;
-  __syncthreads();
-  if (q == 0) {
-    uint32_t pre = 0;
-    for (int i = 0; i < w; i++) pre += s_tmp[i];
-    dbase[d] = pre + x - tot;
-  }
-}
-
-template <class K, class VT, bool IOTA, int DB>
-__global__ void __launch_bounds__(kThreads)
-    k_down(const K *__restrict__ kin, const VT *__restrict__ vin, K *__restrict__ kout,
-           VT *__restrict__ vout, uint32_t n, int shift,
-           const uint32_t *__restrict__ counts, const uint32_t *__restrict__ gsum,
-           uint32_t gsize, const uint32_t *__restrict__ dbase) {
-  constexpr int R = 1 << DB, Q = R / 256;
-  __shared__ K s_k[kTile];
-  __shared__ VT s_v[kTile];
-  __shared__ uint32_t s_wh[kWaves][R];
-  __shared__ uint32_t s_dex[R];
-  __shared__ uint32_t s_gb[R];
-  __shared__ uint32_t s_tmp[kWaves];
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t tile = blockIdx.x;
-  const uint32_t base = tile * kTile;
-  for (int i = tid; i < kWaves * R; i += kThreads) (&s_wh[0][0])[i] = 0;
-  // global offset of this tile's digit runs (independent of the items)
-  for (int d = tid; d < R; d += kThreads)
-    s_gb[d] = dbase[d] + gsum[size_t(tile / gsize) * R + d] + counts[size_t(tile) * R + d];
-  K key[kItems];
-  VT val[kItems];
-#pragma unroll
-  for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = elem_index(base, w, i, lane);
-    const bool valid = idx < n;
-    key[i] = valid ? kin[idx] : K(0);
-    val[i] = IOTA ? VT(idx) : (valid ? vin[idx] : VT(0));
-  }
-  __syncthreads();
-  const uint64_t lt = (uint64_t(1) << lane) - 1;
-  uint32_t rank[kItems];
-#pragma unroll
-  for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = elem_index(base, w, i, lane);
-    const bool valid = idx < n;
-    const uint32_t d = uint32_t((key[i] >> shift) & (R - 1));
-    const uint64_t peers = match_digit<DB>(d, valid);
-    uint32_t b0 = 0;
-    if (valid) b0 = s_wh[w][d];
-    if (valid && (peers & lt) == 0) s_wh[w][d] = b0 + uint32_t(__popcll(peers));
-    rank[i] = b0 + uint32_t(__popcll(peers & lt));
-  }
-  __syncthreads();
-  // per digit: the waves' exclusive prefix (stability: wave order = input
-  // order), then the tile-wide exclusive prefix over digits; thread t owns
-  // the Q consecutive digits [t·Q, (t+1)·Q)
-  uint32_t cnt[Q];
-#pragma unroll
-  for (int q = 0; q < Q; q++) {
-    const int d = tid * Q + q;
-    uint32_t c0 = 0;
-#pragma unroll
-    for (int ww = 0; ww < kWaves; ww++) {
-      const uint32_t c = s_wh[ww][d];
-      s_wh[ww][d] = c0;
-      c0 += c;
-    }
-    cnt[q] = c0;
-  }
-  uint32_t mine = 0;
-#pragma unroll
-  for (int q = 0; q < Q; q++) mine += cnt[q];
-  uint32_t lpre = block_excl_scan(mine, s_tmp);
-#pragma unroll
-  for (int q = 0; q < Q; q++) {
-    s_dex[tid * Q + q] = lpre;
-    lpre += cnt[q];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = elem_index(base, w, i, lane);
-    if (idx < n) {
-      const uint32_t d = uint32_t((key[i] >> shift) & (R - 1));
-      const uint32_t pos = s_dex[d] + s_wh[w][d] + rank[i];
-      s_k[pos] = key[i];
-      s_v[pos] = val[i];
-    }
-  }
-  __syncthreads();
-  const uint32_t tile_n = min(uint32_t(kTile), n - base);
-#pragma unroll 4
-  for (uint32_t j = tid; j < tile_n; j += kThreads) {
-    const K k = s_k[j];
-    const uint32_t d = uint32_t((k >> shift) & (R - 1));
-    const uint32_t o = s_gb[d] + (j - s_dex[d]);
-    kout[o] = k;
-    vout[o] = s_v[j];
-  }
-}
-
-}  // namespace
-
 constexpr int kWideMax = 11;  // widest digit (R = 2048)
+}  // namespace
 
 size_t SortWorkspace::meta_words(size_t n, int) const {
   const size_t tiles = (n + kTile - 1) / kTile;
@@ -309,39 +32,6 @@ void SortWorkspace::prepare(size_t tiles, int, hipStream_t) {
   const size_t groups = std::max<size_t>((tiles + kGroup - 1) / kGroup, 4);
   meta.ensure((tiles + groups + 1) * (size_t(1) << kWideMax));
 }
-
-namespace {
-
-// one LSD pass over DB bits at `shift`
-template <class K, class VT, int DB>
-void sort_pass(const K *ki, const VT *vi, K *ko, VT *vo, size_t n, int shift, bool iota,
-               uint32_t tiles, uint32_t groups, uint32_t *counts, uint32_t *gsum,
-               uint32_t *dbase, hipStream_t s) {
-  constexpr int R = 1 << DB;
-  k_up<K, DB><<<tiles, kThreads, 0, s>>>(ki, uint32_t(n), shift, counts);
-  uint32_t gsize = kGroup;
-  if (DB == 8 && tiles <= kFusedMaxTiles) {
-    gsize = (tiles + 3) / 4;
-    k_scan_fused<<<1, 1024, 0, s>>>(counts, tiles, gsize, gsum, dbase);
-  } else {
-    k_scan_a<DB><<<groups, 256, 0, s>>>(counts, tiles, gsum);
-    k_scan_b<DB><<<1, 256, 0, s>>>(gsum, groups, dbase);
-  }
-  if (iota) {
-    k_down<K, VT, true, DB><<<tiles, kThreads, 0, s>>>(ki, nullptr, ko, vo, uint32_t(n), shift,
-                                                        counts, gsum, gsize, dbase);
-  } else {
-    // algorithmic traffic of a key+value scatter pass: read and write every
-    // pair once
-    probed_launch("sort_scatter", double(n) * 2.0 * (sizeof(K) + sizeof(VT)),
-                  k_down<K, VT, false, DB>, dim3(tiles), dim3(kThreads), s, ki, vi, ko, vo,
-                  uint32_t(n), shift, (const uint32_t *)counts, (const uint32_t *)gsum, gsize,
-                  (const uint32_t *)dbase);
-  }
-  (void)R;
-}
-
-}  // namespace
 
 // Digit plan: 8-bit digits.  FH_SORT_WIDE=1 sorts keys of 17..22 bits in two
 // passes of 10 or 11 bits instead of three of 8 (the per-tile count matrix
@@ -367,41 +57,27 @@ void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *v
     *vout = va;
     return;
   }
-  const uint32_t tiles = uint32_t((n + kTile - 1) / kTile);
-  const uint32_t groups = (tiles + kGroup - 1) / kGroup;
-  ws.prepare(tiles, passes, s);
-  const uint32_t R = 1u << db;
-  uint32_t *counts = ws.meta.get();
-  uint32_t *gsum = counts + size_t(tiles) * R;
-  uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
-  const K *ki = keys_in;
-  const VT *vi = vals_in;
   // never write pass 0 over its own input
   const bool alias_a = (const void *)keys_in == (const void *)ka ||
                        (vals_in && (const void *)vals_in == (const void *)va);
-  K *ko = alias_a ? kb : ka;
-  VT *vo = alias_a ? vb : va;
-  for (int p = 0; p < passes; p++) {
-    const int shift = db * p;
-    const bool iota = p == 0 && vals_in == nullptr;
-    if (db == 10)
-      sort_pass<K, VT, 10>(ki, vi, ko, vo, n, shift, iota, tiles, groups, counts, gsum, dbase, s);
-    else if (db == 11)
-      sort_pass<K, VT, 11>(ki, vi, ko, vo, n, shift, iota, tiles, groups, counts, gsum, dbase, s);
-    else
-      sort_pass<K, VT, 8>(ki, vi, ko, vo, n, shift, iota, tiles, groups, counts, gsum, dbase, s);
-    ki = ko;
-    vi = vo;
-    if (ko == ka) {
-      ko = kb;
-      vo = vb;
-    } else {
-      ko = ka;
-      vo = va;
-    }
+  const bool iota = vals_in == nullptr;
+#define FH_SORT_RUN(DBV)                                                                         \
+  if (iota)                                                                                     \
+    sort_passes<K, VT, DBV, ArraySrc<K, VT, true>>(ArraySrc<K, VT, true>{keys_in, nullptr},     \
+                                                   false, ka, va, kb, vb, alias_a, n, passes,  \
+                                                   db, ws, s, kout, vout);                      \
+  else                                                                                          \
+    sort_passes<K, VT, DBV, ArraySrc<K, VT, false>>(ArraySrc<K, VT, false>{keys_in, vals_in},   \
+                                                    true, ka, va, kb, vb, alias_a, n, passes,  \
+                                                    db, ws, s, kout, vout);
+  if (db == 10) {
+    FH_SORT_RUN(10)
+  } else if (db == 11) {
+    FH_SORT_RUN(11)
+  } else {
+    FH_SORT_RUN(8)
   }
-  *kout = const_cast<K *>(ki);
-  *vout = const_cast<VT *>(vi);
+#undef FH_SORT_RUN
 }
 
 template void sort_pairs<uint32_t, uint32_t>(const uint32_t *, const uint32_t *, uint32_t *,
