@@ -32,9 +32,10 @@ from collections import defaultdict
 
 # probe name (fh_engine_set_probe) -> kernel-name pattern
 PROBES = {
-    "sort_scatter": r"k_down<unsigned int, unsigned int, false>",
-    "sort_scatter_iota": r"k_down<unsigned int, unsigned int, true>",
-    "sort_scatter_dots": r"k_down<unsigned int, unsigned long, false>",
+    # k_down<K, VT, DB, Src>: pass 0 of an IOTA sort reads ArraySrc<..., true>
+    "sort_scatter": r"k_down<unsigned int, unsigned int, 8, fh::(anonymous namespace)::ArraySrc<unsigned int, unsigned int, false>",
+    "sort_scatter_iota": r"ArraySrc<unsigned int, unsigned int, true>",
+    "sort_scatter_dots": r"k_down<unsigned int, unsigned long, 8",
     "graph_tile": r"k_graph_tile<",
     "prev_engine": r"k_prev_views",
     "cmd_union": r"k_cmd_engine<unsigned int>",
@@ -43,7 +44,16 @@ PROBES = {
     "tail_engine": r"k_tail_engine<unsigned int>",
     "elem_fill_dots": r"k_elem_fill_dots",
     "exec_from_groups": r"k_exec_from_groups",
-    "sort_up": r"k_up<unsigned int>",
+    # global graph path (C3 / C5 shards: tools/gpu_pmc.sh CFG=c5)
+    "kap_relax": r"k_kap_relax",
+    "kap_init": r"k_kap_init",
+    "fb_hprop": r"k_fb_hprop",
+    "fb_reach": r"k_fb_reach",
+    "fb_init": r"k_fb_init",
+    "windows": r"k_windows",
+    "edge_rep": r"k_edge_rep",
+    "sort_scatter_u64": r"k_down<unsigned long, unsigned int, 8",
+    "sort_up": r"k_up<unsigned int, unsigned int, 8",
     "sort_scan": r"k_scan_fused",
     "sv_deps": r"k_sv_deps",
     "sv_tails": r"k_sv_tails",
