@@ -34,7 +34,7 @@ from collections import defaultdict
 PROBES = {
     # k_down<K, VT, DB, Src>: pass 0 of an IOTA sort reads ArraySrc<..., true>
     "sort_scatter": r"k_down<unsigned int, unsigned int, 8, fh::(anonymous namespace)::ArraySrc<unsigned int, unsigned int, false>",
-    "sort_scatter_iota": r"ArraySrc<unsigned int, unsigned int, true>",
+    "sort_scatter_iota": r"k_down<unsigned int, unsigned int, 8, fh::(anonymous namespace)::ArraySrc<unsigned int, unsigned int, true>",
     "sort_scatter_dots": r"k_down<unsigned int, unsigned long, 8",
     "graph_tile": r"k_graph_tile<",
     "prev_engine": r"k_prev_views",
