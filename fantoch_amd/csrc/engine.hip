@@ -522,12 +522,29 @@ __global__ void __launch_bounds__(256)
 __global__ void k_sv_unpermute(uint32_t M, const uint32_t *__restrict__ vs,
                                const uint64_t *__restrict__ dep_sorted,
                                const uint64_t *__restrict__ dot, const uint64_t *__restrict__ dlog,
-                               uint64_t *__restrict__ dep_dot) {
+                               uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ cnt) {
   GRID_STRIDE(j, M) {
     const uint64_t x = dep_sorted[j];
-    dep_dot[vs[j]] = is_log_ref(x) ? dlog[x - kLogFlag]  // an earlier batch
-                     : (x != 0 && (x >> 56) == 0) ? dot[x - 1]  // in-batch index + 1
-                     : x;
+    const uint32_t c = vs[j];
+    dep_dot[c] = is_log_ref(x) ? dlog[x - kLogFlag]  // an earlier batch
+                 : (x != 0 && (x >> 56) == 0) ? dot[x - 1]  // in-batch index + 1
+                 : x;
+    cnt[c] = x != 0;  // the CSR row length (one slot per command)
+  }
+}
+
+// one slot per command: CSR compaction, and for a trivially ordered batch
+// (singleton SCCs in arrival order) label = own dot, rank = position
+__global__ void k_sv_compact(uint32_t n, const uint64_t *__restrict__ dd,
+                             const uint32_t *__restrict__ off, uint64_t *__restrict__ out,
+                             const uint64_t *__restrict__ dot, uint64_t *__restrict__ lab,
+                             uint32_t *__restrict__ rank) {
+  GRID_STRIDE(i, n) {
+    if (off[i + 1] != off[i]) out[off[i]] = dd[i];
+    if (lab) {
+      lab[i] = dot[i];
+      rank[i] = i;
+    }
   }
 }
 
@@ -573,10 +590,6 @@ __global__ void k_run_scatter(uint32_t m, const uint32_t *__restrict__ keys,
     const uint32_t k = keys[j];
     out[off[k] + (j - hp[k])] = dot[vids[j]];
   }
-}
-
-__global__ void k_cnt_nonzero(uint32_t n, const uint64_t *__restrict__ d, uint32_t *__restrict__ c) {
-  GRID_STRIDE(i, n) c[i] = d[i] != 0;
 }
 
 __global__ void k_bcast_u32(uint32_t n, uint32_t *p, uint32_t v) { GRID_STRIDE(i, n) p[i] = v; }
@@ -666,6 +679,7 @@ struct EngineDevice {
   DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
   // outputs of the last run (materialised inside run(), copied by results())
   bool deps_direct = false;  // run_general wrote o_dep_off / o_dep (no compaction)
+  bool sv_labels_done = false;  // k_sv_compact wrote the trivial labels / ranks
   // replica views' KeyDeps pipeline (second stream, second buffer set)
   hipStream_t s_prev = nullptr;
   hipEvent_t ev_start = nullptr, ev_join = nullptr, ev_sorted[2] = {}, ev_freed[2] = {};
@@ -1294,18 +1308,28 @@ struct EngineDevice {
       // written by the union (k_cmd_count sized the rows)
     } else {
     if (sv_fused) {
-      // one dependency slot per command: decode, count = slot used
-      S = 1;
+      // one dependency slot per command: decode + row length in one scatter,
+      // then compaction fused with the trivial order's labels and ranks
       k_sv_unpermute<<<grid_for(n, B), B, 0, stream>>>(n, sv_vs, dep_ext.get(), bdot, dot.get(),
-                                                        dep_dot.ensure(n + 1));
-      k_cnt_nonzero<<<grid_for(n, B), B, 0, stream>>>(n, dep_dot.get(), dep_cnt.ensure(n + 1));
+                                                        dep_dot.ensure(n + 1),
+                                                        dep_cnt.ensure(n + 1));
+      exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
+      uint64_t *lb = gout.trivial ? lab.ensure(n + 1) : nullptr;
+      uint32_t *rk = gout.trivial ? rank_tmp.ensure(n + 1) : nullptr;
+      k_sv_compact<<<grid_for(n, B), B, 0, stream>>>(n, dep_dot.get(), off, o_dep.ensure(n + 1),
+                                                      bdot, lb, rk);
+      sv_labels_done = gout.trivial;
+    } else {
+      exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
+      k_compact_deps<<<grid_for(n, B), B, 0, stream>>>(n, S, dep_dot.get(), off,
+                                                        o_dep.ensure(size_t(n) * S + 1));
     }
-    exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
-    k_compact_deps<<<grid_for(n, B), B, 0, stream>>>(n, S, dep_dot.get(), off,
-                                                      o_dep.ensure(size_t(n) * S + 1));
     }
     mark("out_deps");
-    if (gout.trivial) {
+    if (gout.trivial && sv_fused && sv_labels_done) {
+      o_label = lab.get();
+      o_rank = rank_tmp.get();
+    } else if (gout.trivial) {
       // singleton SCCs in arrival order: label = own dot, rank = position
       uint64_t *lb = lab.ensure(n + 1);
       uint32_t *rk = rank_tmp.ensure(n + 1);
