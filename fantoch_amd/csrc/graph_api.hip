@@ -431,19 +431,6 @@ struct GraphDevice {
     batch_seq0 = next_seq;
     index_requests(n, dot, dep_off, dep_dot, dep_shards);
     batch_seq0 = ~uint64_t(0);
-    // the batch joins the host's pending metadata (executed ones leave below)
-    for (size_t i = 0; i < n; i++) {
-      PInfo pi;
-      pi.seq = next_seq++;
-      pi.cshard = cmd_shards ? cmd_shards[i] : 0;
-      pi.time = now_ms;
-      pi.deps.assign(dep_dot + dep_off[i], dep_dot + dep_off[i + 1]);
-      pi.dshards.resize(pi.deps.size(), 0);
-      if (dep_shards)
-        std::copy(dep_shards + dep_off[i], dep_shards + dep_off[i + 1], pi.dshards.begin());
-      porder.emplace(pi.seq, dot[i]);
-      pend.emplace(dot[i], std::move(pi));
-    }
     uint32_t *dst = d_dst.ensure(E + 1);
     k_resolve_fill<<<grid_for(V, B), B, 0, stream>>>(uint32_t(V), ddot_v, ddo, dd, sd, sv,
                                                       d_frontier.get(), dexc,
@@ -461,6 +448,20 @@ struct GraphDevice {
     gin.want_per_key = false;  // the executor's monitor is fed from the drain order
     GraphOutput out;
     core.run(gin, out);
+    // the batch joins the host's pending metadata (executed ones leave below;
+    // after the pass, so a failed pass leaves host and device sets equal)
+    for (size_t i = 0; i < n; i++) {
+      PInfo pi;
+      pi.seq = next_seq++;
+      pi.cshard = cmd_shards ? cmd_shards[i] : 0;
+      pi.time = now_ms;
+      pi.deps.assign(dep_dot + dep_off[i], dep_dot + dep_off[i + 1]);
+      pi.dshards.resize(pi.deps.size(), 0);
+      if (dep_shards)
+        std::copy(dep_shards + dep_off[i], dep_shards + dep_off[i + 1], pi.dshards.begin());
+      porder.emplace(pi.seq, dot[i]);
+      pend.emplace(dot[i], std::move(pi));
+    }
     // executed vertices to the host: dots and labels in execution order
     const uint32_t nexec = out.nexec;
     std::vector<uint64_t> xdot(nexec), xlab(nexec);
