@@ -61,6 +61,8 @@ def parse():
                     help="kernels whose launches are timed in the probe pass")
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase profile pass")
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary C2 line")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the other BASELINE configurations (C1, C3, C4 key shard, C5 shard)")
     return ap.parse_args()
 
 
@@ -157,6 +159,45 @@ def phases_of(eng, rewind=True):
             acc.setdefault(name, []).append(ms)
     eng.set_profiling(False)
     return {k: round(float(np.median(v[1:] if len(v) > 1 else v)), 4) for k, v in acc.items()}
+
+
+def other_configs(local, steps=3):
+    """The other BASELINE configurations on this GPU, each one engine pass over
+    its whole staged stream per step (inputs resident, every output
+    materialised): C1 (10k, plumbing), C3 (10M, one stream-wide SCC), C4's
+    per-GPU key-shard size (12.5M) and a C5 shard (12.5M commands of 4 keys).
+    Parity at these shapes: tests/test_fullsize_gpu.py."""
+    from fantoch_amd.engine import Engine
+    from fantoch_amd.workload import Workload
+    cfgs = {
+        "c1": (Workload.conflict_rate_(10, k=1, views=3, window=64, seed=0xFA170C4000000001, n=5),
+               10_000, "Atlas n=5 f=1, ConflictRate 10%, 1 key, replica views"),
+        "c3": (Workload.conflict_pool(100, 16, k=2, views=3, window=64, seed=0xFA170C4000000003,
+                                      n=5), 10_000_000,
+               "EPaxos n=5, ConflictPool 100% (key 0 + 16-key pool), 2 keys, replica views"),
+        "c4_shard": (Workload.zipf(0.99, 1 << 20, k=1, views=3, window=64, seed=C4_SEED, n=5),
+                     12_500_000, "C4 per-GPU size at 8 GPUs: Zipf 0.99 / 2^20 keys, 1 key"),
+        "c5_shard": (Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64,
+                                   seed=0xFA170C4000000005, n=5), 12_500_000,
+                     "C5 shard: Zipf 0.99 / 2^20 keys, 4 keys/cmd, replica views"),
+    }
+    out = {}
+    for name, (w, n, desc) in cfgs.items():
+        s = w.generate(n, logs=True, times=False)
+        eng = Engine(s.key_space, n=5, device=local)
+        eng.stage(s)
+        eng.run(sync=True)  # warmup (also picks the graph path's entry)
+        eng.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.rewind()
+            eng.run(sync=False)
+        eng.sync()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        eng.close()
+        out[name] = {"workload": desc, "commands": n, "ms_per_step": round(ms, 3),
+                     "commands_per_s": n / (ms * 1e-3)}
+    return out
 
 
 def secondary_c2(args, local):
@@ -283,6 +324,8 @@ def main():
                                             f"incremental GraphExecutor, 1 thread, {dt:.2f}s"}
     if rank == 0 and world == 1 and not args.no_secondary:
         result["secondary"] = secondary_c2(args, local)
+    if rank == 0 and world == 1 and not args.no_configs:
+        result["configs"] = other_configs(local)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
