@@ -229,12 +229,20 @@ __device__ __forceinline__ void cmd_union_regs(
       const int kind = decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
       if (kind == 1) {
         vv[t] = v;
-        r[t] = dot[v];
       } else if (kind == 2) {
         r[t] = x;
         if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
       }
     }
+  }
+  // in-batch deps: one dot gather per distinct vid (the fast-quorum
+  // members' reports often name the same previous command)
+#pragma unroll
+  for (uint32_t t = 0; t < kRegSlots; t++) {
+    bool dup = vv[t] == ~0u;
+#pragma unroll
+    for (uint32_t q = 0; q < t; q++) dup |= vv[q] == vv[t];
+    if (!dup) r[t] = dot[vv[t]];
   }
   // bitonic sort of the 16 register slots, ascending
 #pragma unroll
@@ -923,6 +931,10 @@ struct EngineDevice {
       FH_CHECK(h_key[e] < key_space, FH_EINVAL, "stage: key id >= key_space");
       k32[e] = uint32_t(h_key[e]);
     }
+    // the all-ones dot, (255, 2^56 - 1), is the union's empty-slot sentinel
+    for (size_t i = 0; i < n * nb; i++)
+      FH_CHECK(h_dot[i] != ~0ull && (h_dot[i] >> 56) != 0, FH_EINVAL,
+               "stage: dot (255, 2^56 - 1) is reserved and ProcessId 0 is not a process");
     std::vector<uint32_t> ent, lo;
     if (d.views) {
       const size_t np = d.nproc;

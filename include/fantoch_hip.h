@@ -426,7 +426,9 @@ fh_status fh_engine_destroy(fh_engine *h);
 /* Reset all persistent state (latest tables, executed clock). */
 fh_status fh_engine_reset(fh_engine *h);
 /* Stage a batch into device memory (host -> HBM, not part of the timed
- * path).  key_id[n*k]; for views>0, fq_proc[n*fq] (replica of each member,
+ * path).  Dots must have a ProcessId >= 1 and must not be the all-ones dot
+ * (255, 2^56 - 1), reserved by the union (FH_EINVAL).
+ * key_id[n*k]; for views>0, fq_proc[n*fq] (replica of each member,
  * member 0 = coordinator) and fq_time[n*fq] (arrival time of the command at
  * that member; members process commands in (time, index) order). */
 fh_status fh_engine_stage(fh_engine *h, const fh_stream_desc *desc,
