@@ -33,6 +33,11 @@ namespace {
 constexpr unsigned B = 256;
 #define GRID_STRIDE(i, n) \
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
+// wave-uniform trip count (lanes past n see i >= n): shuffles inside are safe
+#define WAVE_STRIDE(i, n)                                                      \
+  for (uint32_t i##_b = blockIdx.x * blockDim.x; i##_b < (n);                  \
+       i##_b += gridDim.x * blockDim.x)                                        \
+    for (uint32_t i = i##_b + threadIdx.x, i##_once = 1; i##_once; i##_once = 0)
 
 // Replica views as per-replica arrival logs: replica r's SequentialKeyDeps
 // sees the commands of log r in log order (its add_cmd calls, atlas.rs:236,
@@ -68,9 +73,27 @@ struct LogSrc {
   }
 };
 
+// Dependency-code placement (replica views).  k_prev_views writes each
+// element's code straight to its command-major position: a 4-byte write to a
+// random address of the chunk's ~50 MB window, ~32 B of fabric traffic each.
+// Instead, one bucketing pass groups (position - base, code) pairs by the
+// position's bits [15, 24) -- an LDS-staged scatter with contiguous runs per
+// tile and bucket, as in the sort -- and k_place assembles each bucket's 32K
+// positions in LDS and writes them out whole.  An element below the base or
+// past the 2^24-position span wraps into some bucket; k_place writes such
+// strays directly (correct, slower).
+constexpr int kPlaceShift = 15;
+constexpr int kPlaceDB = 9;  // 512 buckets
+constexpr uint32_t kPlaceBuckets = 1u << kPlaceDB;
+constexpr uint32_t kPlaceSpan = 1u << kPlaceShift;
+constexpr uint32_t kPlaceSlack = 1u << 16;  // arrivals ahead of earlier commands
+constexpr uint32_t kPlaceNone = ~0u;        // never a code (log references < 2^31 - 1)
+
+// emin (may be null): the placement base of the chunk
 __global__ void k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, LogChunk ch,
                            const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
-                           uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+                           uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                           uint32_t *__restrict__ emin) {
   GRID_STRIDE(x, M) {
     uint32_t r = 0;
     while (r + 1 < nlog && x >= ch.cum[r + 1]) r++;
@@ -79,6 +102,136 @@ __global__ void k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, L
     const uint32_t e = ent[q];
     keys[x] = (r + 1) * K + key32[(e / fq) * k + s];
     vals[x] = e * k + s;
+  }
+  // placement base: the smallest first entry of the replicas' slices, less a
+  // slack for entries that arrive before earlier commands.  Only a hint (see
+  // above).  An exact minimum by atomics serialised the kernel on one word:
+  // 1.37 ms instead of 0.04 per chunk.
+  if (emin && blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t m = ~0u;
+    for (uint32_t r = 0; r < nlog; r++)
+      if (ch.cum[r + 1] > ch.cum[r]) m = min(m, ent[ch.first[r]] * k);
+    *emin = m > kPlaceSlack ? m - kPlaceSlack : 0u;
+  }
+}
+
+// bucketing source: element j of the chunk's (key, arrival) order yields
+// (its position - base, its dependency code) -- the code as k_prev_views
+// computes it
+struct PrevSrc {
+  const uint32_t *ks, *vs, *ebase;
+  const uint64_t *latest;
+  uint32_t per_cmd;
+  __device__ __forceinline__ uint32_t key(uint32_t j) const { return vs[j] - *ebase; }
+  __device__ __forceinline__ uint32_t code(uint32_t j) const {
+    const uint32_t seg = ks[j];
+    if (j == 0 || ks[j - 1] != seg) {
+      const uint64_t x = latest[seg];
+      return x ? (0x80000000u | uint32_t(x - kLogFlag)) : 0u;
+    }
+    return vs[j - 1] / per_cmd + 1;
+  }
+  // as a sort source (k_up's tile counts read the key only)
+  __device__ __forceinline__ void get(uint32_t j, uint32_t &k, uint32_t &v) const {
+    k = key(j);
+    v = 0;
+  }
+};
+
+// The bucketing pass: k_down's tile staging, but the order within a bucket
+// is free, so ranks come from LDS atomics (no ballot matching).  The tile
+// counts k_up wrote fix every tile's run per bucket.
+__global__ void __launch_bounds__(kThreads)
+    k_bucket_codes(PrevSrc src, uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                   uint32_t n, const uint32_t *__restrict__ counts,
+                   const uint32_t *__restrict__ gsum, uint32_t gsize,
+                   const uint32_t *__restrict__ dbase) {
+  constexpr uint32_t R = kPlaceBuckets, Q = R / kThreads;
+  __shared__ uint32_t s_k[kTile], s_v[kTile];
+  __shared__ uint32_t s_cnt[R], s_dex[R], s_gb[R];
+  __shared__ uint32_t s_tmp[kWaves];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t tile = blockIdx.x, base = tile * kTile;
+  for (uint32_t d = tid; d < R; d += kThreads) {
+    s_cnt[d] = 0;
+    s_gb[d] = dbase[d] + gsum[size_t(tile / gsize) * R + d] + counts[size_t(tile) * R + d];
+  }
+  uint32_t key[kItems], val[kItems];
+#pragma unroll
+  for (int i = 0; i < kItems; i++) {
+    const uint32_t idx = elem_index(base, w, i, lane);
+    key[i] = 0;
+    val[i] = 0;
+    if (idx < n) {
+      key[i] = src.key(idx);
+      val[i] = src.code(idx);
+    }
+  }
+  __syncthreads();
+  uint32_t rank[kItems];
+#pragma unroll
+  for (int i = 0; i < kItems; i++) {
+    const uint32_t idx = elem_index(base, w, i, lane);
+    rank[i] = idx < n ? atomicAdd(&s_cnt[(key[i] >> kPlaceShift) & (R - 1)], 1u) : 0u;
+  }
+  __syncthreads();
+  uint32_t cnt[Q], mine = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < Q; q++) {
+    cnt[q] = s_cnt[tid * Q + q];
+    mine += cnt[q];
+  }
+  uint32_t pre = block_excl_scan(mine, s_tmp);
+#pragma unroll
+  for (uint32_t q = 0; q < Q; q++) {
+    s_dex[tid * Q + q] = pre;
+    pre += cnt[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kItems; i++) {
+    const uint32_t idx = elem_index(base, w, i, lane);
+    if (idx < n) {
+      const uint32_t p = s_dex[(key[i] >> kPlaceShift) & (R - 1)] + rank[i];
+      s_k[p] = key[i];
+      s_v[p] = val[i];
+    }
+  }
+  __syncthreads();
+  const uint32_t tile_n = min(uint32_t(kTile), n - base);
+#pragma unroll 4
+  for (uint32_t j = tid; j < tile_n; j += kThreads) {
+    const uint32_t kk = s_k[j];
+    const uint32_t d = (kk >> kPlaceShift) & (R - 1);
+    const uint32_t o = s_gb[d] + (j - s_dex[d]);
+    kout[o] = kk;
+    vout[o] = s_v[j];
+  }
+}
+
+// one workgroup per bucket d: positions base + [d·2^15, (d+1)·2^15)
+__global__ void __launch_bounds__(1024)
+    k_place(uint32_t Mc, const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ rel,
+            const uint32_t *__restrict__ code, const uint32_t *__restrict__ ebase,
+            uint32_t *__restrict__ out) {
+  __shared__ uint32_t s_c[kPlaceSpan];  // 128 KB
+  const uint32_t d = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < kPlaceSpan; i += 1024) s_c[i] = kPlaceNone;
+  __syncthreads();
+  const uint32_t s = dbase[d], t = d + 1 < kPlaceBuckets ? dbase[d + 1] : Mc;
+  const uint32_t eb = *ebase;
+  for (uint32_t j = s + threadIdx.x; j < t; j += 1024) {
+    const uint32_t r = rel[j], c = code[j];
+    if ((r >> kPlaceShift) == d)
+      s_c[r & (kPlaceSpan - 1)] = c;
+    else
+      out[eb + r] = c;  // a stray (below the base or past the span)
+  }
+  __syncthreads();
+  uint32_t *o = out + eb + (d << kPlaceShift);
+  for (uint32_t i = threadIdx.x; i < kPlaceSpan; i += 1024) {
+    const uint32_t c = s_c[i];
+    if (c != kPlaceNone) o[i] = c;
   }
 }
 
@@ -708,6 +861,7 @@ struct EngineDevice {
   DBuf<uint32_t> edge_cnt, edge_off, edge_csr;  // replica views: in-batch edges as CSR
   DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
+  DBuf<uint32_t> place_base;  // replica views: per-chunk smallest element position
   DBuf<unsigned long long> srcstats;
   SortWorkspace sort_ws;
   ScanWorkspace scan_ws;
@@ -1121,11 +1275,25 @@ struct EngineDevice {
       const uint32_t np = desc.nproc;
       FH_CHECK(np <= uint32_t(kMaxLogs), FH_ENOTIMPL, "replica views: nproc <= 16");
       const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
+      // codes placed through LDS buckets (k_place; FH_VIEW_PLACE=0: direct
+      // scatter).  A chunk of Mc elements spans ~Mc positions, so chunks of
+      // 15.7M keep the placement window within its 2^24 positions.
+      static const bool place = [] {
+        const char *e = getenv("FH_VIEW_PLACE");
+        return !(e && *e == '0');
+      }();
       static const size_t chunk_elems = [] {
         const char *e = getenv("FH_VIEW_CHUNK");
-        return e ? size_t(std::max(1L, atol(e))) : size_t(12) << 20;
+        return e ? size_t(std::max(1L, atol(e))) : place ? size_t(15) << 20 : size_t(12) << 20;
       }();
       const uint32_t nch = uint32_t(std::max<size_t>(1, (size_t(M) + chunk_elems - 1) / chunk_elems));
+      uint32_t *pbase = nullptr;
+      if (place) {
+        // the sentinel kPlaceNone is the code of log reference 2^31 - 1
+        FH_CHECK(bbase + n < 0x7FFFFFFFull, FH_ENOTIMPL, "replica views: command log >= 2^31 - 1");
+        pbase = place_base.ensure(nch);
+        FH_HIP(hipMemsetAsync(pbase, 0xFF, size_t(nch) * sizeof(uint32_t), stream));
+      }
       // the chunk's elements are replica-major, so a stable sort by the key
       // alone already leaves every (replica, key) segment contiguous and in
       // arrival order ((key, replica, arrival) order): with K a power of two
@@ -1176,7 +1344,7 @@ struct EngineDevice {
         if (!fused) {
           probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys,
                         dim3(grid_for(Mc, B)), dim3(B), stream, Mc, k, fq, np, lc, bent, bkey,
-                        uint32_t(key_space), lk, lv);
+                        uint32_t(key_space), lk, lv, place ? pbase + c : (uint32_t *)nullptr);
           sort_pairs<uint32_t, uint32_t>(lk, lv, lk, lv, bkb.ensure(Mc + 1), bvb.ensure(Mc + 1),
                                          Mc, bits, sort_ws, stream, &ks, &vs);
         } else {
@@ -1191,10 +1359,16 @@ struct EngineDevice {
         }
         // heads read the latest table, tails then make the chunk's last
         // commands the latest (command-log references)
-        probed_launch("prev_engine", double(Mc) * (4.0 + 4.0 + 4.0), k_prev_views,
-                      dim3(grid_for(Mc, B)), dim3(B), sp, Mc, (const uint32_t *)ks,
-                      (const uint32_t *)vs, S, (const uint64_t *)views_latest(),
-                      dep32.ensure(M + 1));
+        if (place && !fused) {
+          // the sort's other buffer pair takes the bucketed (position, code)
+          uint32_t *bk = ks == lk ? bkb.get() : lk, *bv = ks == lk ? bvb.get() : lv;
+          place_codes(Mc, ks, vs, S, pbase + c, bk, bv, dep32.ensure(M + 1), sp);
+        } else {
+          probed_launch("prev_engine", double(Mc) * (4.0 + 4.0 + 4.0), k_prev_views,
+                        dim3(grid_for(Mc, B)), dim3(B), sp, Mc, (const uint32_t *)ks,
+                        (const uint32_t *)vs, S, (const uint64_t *)views_latest(),
+                        dep32.ensure(M + 1));
+        }
         k_tail_engine<uint32_t><<<grid_for(Mc, B), B, 0, sp>>>(
             Mc, ks, vs, 0, S, views_latest(), 1ull, ~0ull, nullptr, bbase);
         if (pipe) FH_HIP(hipEventRecord(ev_freed[set], sp));
@@ -1213,6 +1387,34 @@ struct EngineDevice {
       FH_HIP(hipEventElapsedTime(ms, ev0, ev1));
     }
     if (profile) collect_times();
+  }
+
+  // The chunk's dependency codes -> dep32 through the placement pass: bucket
+  // (position - base, code) by the position's bits [15, 23) with the radix
+  // kernels (PrevSrc computes each code on the fly), then k_place per bucket.
+  void place_codes(uint32_t Mc, const uint32_t *ks, const uint32_t *vs, uint32_t per_cmd,
+                   const uint32_t *ebase, uint32_t *bk, uint32_t *bv, uint32_t *out,
+                   hipStream_t s) {
+    if (Mc == 0) return;
+    const PrevSrc src{ks, vs, ebase, (const uint64_t *)views_latest(), per_cmd};
+    const uint32_t tiles = (Mc + kTile - 1) / kTile;
+    const uint32_t groups = (tiles + kGroup - 1) / kGroup;
+    sort_ws.prepare(tiles, 1, s);
+    constexpr uint32_t R = kPlaceBuckets;
+    uint32_t *counts = sort_ws.meta.get();
+    uint32_t *gsum = counts + size_t(tiles) * R;
+    uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
+    k_up<uint32_t, uint32_t, kPlaceDB, PrevSrc><<<tiles, kThreads, 0, s>>>(src, Mc, kPlaceShift,
+                                                                            counts, 1);
+    k_scan_a<kPlaceDB><<<groups, 256, 0, s>>>(counts, tiles, gsum);
+    k_scan_b<kPlaceDB><<<1, 256, 0, s>>>(gsum, groups, dbase);
+    // reads (key, arrival) keys + positions, the previous element's, and the
+    // latest table at heads; writes 8 B per element
+    probed_launch("prev_bucket", double(Mc) * (4.0 + 4.0 + 8.0), k_bucket_codes, dim3(tiles),
+                  dim3(kThreads), s, src, bk, bv, Mc, (const uint32_t *)counts,
+                  (const uint32_t *)gsum, uint32_t(kGroup), (const uint32_t *)dbase);
+    probed_launch("place", double(Mc) * (8.0 + 4.0), k_place, dim3(R), dim3(1024), s, Mc,
+                  (const uint32_t *)dbase, (const uint32_t *)bk, (const uint32_t *)bv, ebase, out);
   }
 
   void run_general(uint32_t n, uint32_t k, uint32_t fq, uint32_t S, uint32_t M, bool views,
