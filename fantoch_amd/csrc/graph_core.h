@@ -98,6 +98,11 @@ struct GraphCore {
   DBuf<uint8_t> fb_pushed;    // coloring reach: vertices that pushed this round
   bool prefer_full = false;   // the last global-path run needed the full coloring
   bool kap_seed_ok = true;    // kap holds a bounded run's ready times (k_fb_seed)
+  DBuf<uint32_t> conv;        // device-side convergence flags (converge())
+  template <class L>
+  void converge(uint32_t words, uint32_t &launches, L launch);
+  DBuf<uint32_t> hseed;       // [V] exact ready time per vertex from the full coloring
+  bool hseed_ok = false;      // hseed holds this run's first full coloring round
   uint32_t tile_r0 = 1536;  // graph_tile: first reach bound to try (set from
                             // the last run's maximum excess)
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)

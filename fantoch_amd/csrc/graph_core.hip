@@ -89,6 +89,73 @@ __device__ __forceinline__ void agg_min(T *p, uint32_t idx, T val, bool active) 
   if (active && val < ld_rel(p + idx)) atomicMin(p + idx, val);
 }
 
+// Block-level aggregation for per-class reductions (class maximum, minimum
+// dot, kappa and H raises).  The lanes of one 256-thread block put their
+// (class, value) into an LDS hash table; after a barrier each distinct class
+// costs one global read (and one atomic when it improves).  A large SCC whose
+// members are spread over the stream (C5: a 1.19M-member class, ~10 % of the
+// vertices, mixed into every wave) otherwise issues one same-address read per
+// member, and those serialise on one L2 channel.  One item per thread: the
+// kernels using it launch ceil(n / 256) blocks.
+constexpr uint32_t kAggSlots = 512;  // >= 2 x the block's items
+constexpr uint32_t kAggEmpty = ~0u;
+template <class T>
+struct AggTable {
+  uint32_t key[kAggSlots];
+  T val[kAggSlots];
+};
+template <class T, bool MAX>
+__device__ __forceinline__ void agg_init(AggTable<T> &t) {
+  for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
+    t.key[i] = kAggEmpty;
+    t.val[i] = MAX ? T(0) : ~T(0);
+  }
+}
+// put (idx, v) into the table (linear probing: at most 256 distinct keys
+// over 512 slots, so a slot is always found)
+template <class T, bool MAX>
+__device__ __forceinline__ void agg_put(AggTable<T> &t, uint32_t idx, T v) {
+  uint32_t h = (idx * 0x9E3779B1u) >> 23;  // 9 bits
+  for (uint32_t q = 0; q < kAggSlots; q++) {
+    const uint32_t k = atomicCAS(&t.key[h], kAggEmpty, idx);
+    if (k == kAggEmpty || k == idx) {
+      if (MAX)
+        atomicMax(&t.val[h], v);
+      else
+        atomicMin(&t.val[h], v);
+      return;
+    }
+    h = (h + 1) & (kAggSlots - 1);
+  }
+}
+// wave-uniform class (every active lane on one idx: C3's stream-wide SCC):
+// one put of the wave's reduction; else one put per active lane
+template <class T, bool MAX>
+__device__ __forceinline__ void agg_lane(AggTable<T> &t, uint32_t idx, T v, bool act) {
+  const int lead = wave_uniform_lead(idx, act);
+  if (lead == -1) return;
+  if (lead >= 0) {
+    const T m = MAX ? wave_max_all(act ? v : T(0)) : wave_min_all(act ? v : ~T(0));
+    if ((int)(threadIdx.x & 63) == lead) agg_put<T, MAX>(t, idx, m);
+    return;
+  }
+  if (act) agg_put<T, MAX>(t, idx, v);
+}
+// after a barrier: apply every slot; raised(idx) for each global improvement
+template <class T, bool MAX, class F>
+__device__ __forceinline__ void agg_flush(AggTable<T> &t, T *g, F raised) {
+  for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
+    const uint32_t k = t.key[i];
+    if (k == kAggEmpty) continue;
+    const T v = t.val[i];
+    if (MAX ? v > ld_rel(g + k) : v < ld_rel(g + k)) {
+      const T old = MAX ? atomicMax(g + k, v) : atomicMin(g + k, v);
+      if (MAX ? old < v : old > v) raised(k);
+    }
+  }
+}
+inline unsigned agg_blocks(uint32_t n) { return n ? (n + B - 1) / B : 1u; }
+
 // ---------------------------------------------------------------- pending
 __global__ void k_blocked_init(uint32_t V, const uint8_t *__restrict__ b0,
                                uint8_t *__restrict__ blocked) {
@@ -246,17 +313,21 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------- kappa
-__global__ void k_kap_init(uint32_t V, const uint8_t *__restrict__ blocked,
-                           const uint32_t *__restrict__ rep, uint64_t *kap) {
-  // highest vertex first: a class's maximum lands early and the later
-  // (smaller) members' waves see it and skip the atomic (one large SCC would
-  // otherwise serialise every wave on its representative's word)
-  WAVE_STRIDE(i, V) {
-    const uint32_t v = i < V ? V - 1 - i : 0u;
-    const bool act = i < V && !blocked[v];
-    agg_max<unsigned long long>((unsigned long long *)kap, act ? rep[v] : 0u,
-                                (unsigned long long)v << 32, act);
-  }
+__global__ void __launch_bounds__(256)
+    k_kap_init(uint32_t V, const uint8_t *__restrict__ blocked, const uint32_t *__restrict__ rep,
+               const uint32_t *__restrict__ hseed, uint64_t *kap) {
+  // class maximum, block-aggregated (one item per thread).  hseed: the exact
+  // ready time of every vertex's SCC (the full coloring's first round), so
+  // the relaxation below only has the depths left to find
+  __shared__ AggTable<unsigned long long> t;
+  agg_init<unsigned long long, true>(t);
+  __syncthreads();
+  const uint32_t v = blockIdx.x * B + threadIdx.x;
+  const bool act = v < V && !blocked[v];
+  const uint32_t h = act ? (hseed ? max(hseed[v], v) : v) : 0u;
+  agg_lane<unsigned long long, true>(t, act ? rep[v] : 0u, (unsigned long long)h << 32, act);
+  __syncthreads();
+  agg_flush<unsigned long long, true>(t, (unsigned long long *)kap, [](uint32_t) {});
 }
 
 // erep[e] = rep[dst[e]]: the representative of every edge's target, refreshed
@@ -269,42 +340,58 @@ __global__ void k_edge_rep(uint64_t E, const uint32_t *__restrict__ dst,
     erep[e] = rep[dst[e]];
 }
 
-__global__ void k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
-                            const uint32_t *__restrict__ erep, const uint8_t *__restrict__ blocked,
-                            const uint32_t *__restrict__ rep, uint64_t *kap, uint32_t *changed,
-                            uint32_t *kraise, uint32_t iter) {
-  WAVE_STRIDE(v, V) {
-    const bool act = v < V && !blocked[v];
-    const uint32_t r = act ? rep[v] : 0u;
-    uint64_t best = 0;
-    if (act) {
-      // four edges per trip, every gather issued before the first is used
-      const uint32_t eb = EB(v), ee = EE(v);
-      for (uint32_t e = eb; e < ee; e += 4) {
-        uint32_t ru[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
-        uint64_t c[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          // +1 on the depth half, saturated below 2^32 - 1: an unconverged
-          // run (a cycle the windows missed) must not carry into the ready
-          // time half that k_fb_seed reads
-          const uint64_t k = ru[j] != r ? ld_u64(&kap[ru[j]]) : 0;
-          c[j] = ru[j] == r ? 0 : (uint32_t(k) >= 0xFFFFFFFEu ? k : k + 1);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) best = c[j] > best ? c[j] : best;
-      }
-    }
-    const bool raised =
-        agg_max<unsigned long long>((unsigned long long *)kap, r, best, act && best != 0);
-    if (raised) __hip_atomic_store(&kraise[r], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // raises per iteration, over 8 counters (one per XCD under round-robin
-    // placement): the give-up rule watches whether they shrink
-    const uint64_t m = __ballot(raised);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&changed[blockIdx.x & 7], uint32_t(__popcll(m)));
+__global__ void __launch_bounds__(256)
+    k_kap_relax(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+                const uint32_t *__restrict__ erep, const uint8_t *__restrict__ blocked,
+                const uint32_t *__restrict__ rep, uint64_t *kap, uint32_t *changed,
+                uint32_t *kraise, uint32_t iter, uint32_t cmask,
+                const uint32_t *__restrict__ prev) {
+  // counters: changed[0..cmask]; the previous launch of a converge() group
+  // raised nothing (prev[0..cmask] all zero): converged, return
+  if (prev) {
+    uint32_t c = 0;
+    for (uint32_t i = 0; i <= cmask; i++) c |= ld_u32(prev + i);
+    if (c == 0) return;
   }
+  __shared__ AggTable<unsigned long long> t;
+  __shared__ uint32_t s_raised;
+  agg_init<unsigned long long, true>(t);
+  if (threadIdx.x == 0) s_raised = 0;
+  __syncthreads();
+  const uint32_t v = blockIdx.x * B + threadIdx.x;
+  const bool act = v < V && !blocked[v];
+  const uint32_t r = act ? rep[v] : 0u;
+  uint64_t best = 0;
+  if (act) {
+    // four edges per trip, every gather issued before the first is used
+    const uint32_t eb = EB(v), ee = EE(v);
+    for (uint32_t e = eb; e < ee; e += 4) {
+      uint32_t ru[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
+      uint64_t c[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        // +1 on the depth half, saturated below 2^32 - 1: an unconverged
+        // run (a cycle the windows missed) must not carry into the ready
+        // time half that k_fb_seed reads
+        const uint64_t k = ru[j] != r ? ld_u64(&kap[ru[j]]) : 0;
+        c[j] = ru[j] == r ? 0 : (uint32_t(k) >= 0xFFFFFFFEu ? k : k + 1);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) best = c[j] > best ? c[j] : best;
+    }
+  }
+  agg_lane<unsigned long long, true>(t, r, best, act && best != 0);
+  __syncthreads();
+  // raised classes per iteration, over 8 counters (one per XCD under
+  // round-robin placement): the give-up rule watches whether they shrink
+  agg_flush<unsigned long long, true>(t, (unsigned long long *)kap, [&](uint32_t k) {
+    __hip_atomic_store(&kraise[k], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    atomicAdd(&s_raised, 1u);
+  });
+  __syncthreads();
+  if (threadIdx.x == 0 && s_raised) atomicAdd(&changed[blockIdx.x & cmask], s_raised);
 }
 
 // Candidates of the restricted fallback: a cycle the windows missed keeps
@@ -337,25 +424,37 @@ __global__ void k_fb_hreset(uint32_t n, const uint32_t *__restrict__ list,
   GRID_STRIDE(j, n) H[rep[FB_VID(j)]] = 0;
 }
 
-__global__ void k_fb_init(uint32_t n, const uint32_t *__restrict__ list,
-                          const uint8_t *__restrict__ blocked,
-                          const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
-                          uint32_t *H, uint8_t *reached) {
-  // highest vertex first (lists are ascending), as in k_kap_init
-  WAVE_STRIDE(i, n) {
-    const uint32_t j = i < n ? n - 1 - i : 0u;
-    const uint32_t v = i < n ? FB_VID(j) : 0u;
-    const uint32_t r = i < n ? rep[v] : 0u;
-    if (i < n && r == v) reached[v] = 0;
-    const bool act = i < n && !blocked[v] && !done[v];
-    agg_max<uint32_t>(H, r, v, act);
-  }
+__global__ void __launch_bounds__(256)
+    k_fb_init(uint32_t n, const uint32_t *__restrict__ list, const uint8_t *__restrict__ blocked,
+              const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep, uint32_t *H,
+              uint8_t *reached) {
+  // class maximum, block-aggregated (one item per thread)
+  __shared__ AggTable<uint32_t> t;
+  agg_init<uint32_t, true>(t);
+  __syncthreads();
+  const uint32_t j = blockIdx.x * B + threadIdx.x;
+  const uint32_t v = j < n ? FB_VID(j) : 0u;
+  const uint32_t r = j < n ? rep[v] : 0u;
+  if (j < n && r == v) reached[v] = 0;
+  const bool act = j < n && !blocked[v] && !done[v];
+  agg_lane<uint32_t, true>(t, r, v, act);
+  __syncthreads();
+  agg_flush<uint32_t, true>(t, H, [](uint32_t) {});
 }
 
 // first full round: the high half of kappa (ready time) is the maximum
 // arrival position its bounded run reached from the class, a lower bound of
 // the propagation's fixpoint H, so starting from it converges to the same H
 // in fewer iterations
+// after the first round of the full coloring: every class is active, so H of
+// a vertex's class is the maximum arrival position its SCC reaches -- the
+// ready time kappa would otherwise propagate edge by edge
+__global__ void k_fb_save_h(uint32_t V, const uint8_t *__restrict__ blocked,
+                            const uint32_t *__restrict__ rep, const uint32_t *__restrict__ H,
+                            uint32_t *__restrict__ hseed) {
+  GRID_STRIDE(v, V) hseed[v] = blocked[v] ? 0u : H[rep[v]];
+}
+
 __global__ void k_fb_seed(uint32_t V, const uint8_t *__restrict__ blocked,
                           const uint32_t *__restrict__ rep, const uint64_t *__restrict__ kap,
                           uint32_t *H) {
@@ -366,13 +465,19 @@ __global__ void k_fb_seed(uint32_t V, const uint8_t *__restrict__ blocked,
   }
 }
 
-__global__ void k_fb_hprop(uint32_t V, uint32_t n, const uint32_t *__restrict__ list,
+__global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const uint32_t *__restrict__ list,
                            const uint32_t *__restrict__ off, uint32_t stride,
                            const uint32_t *__restrict__ dst, const uint32_t *__restrict__ erep,
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
-                           uint32_t *H, uint32_t *changed) {
-  WAVE_STRIDE(j, n) {
+                           uint32_t *H, uint32_t *changed, const uint32_t *__restrict__ prev) {
+  // the previous launch of the group changed nothing: converged, return
+  if (prev && ld_u32(prev) == 0) return;
+  __shared__ AggTable<uint32_t> tb;
+  agg_init<uint32_t, true>(tb);
+  __syncthreads();
+  {
+    const uint32_t j = blockIdx.x * B + threadIdx.x;
     const uint32_t v = j < n ? FB_VID(j) : 0u;
     const bool act = j < n && !blocked[v] && !done[v];
     const uint32_t r = act ? rep[v] : 0u;
@@ -418,8 +523,10 @@ __global__ void k_fb_hprop(uint32_t V, uint32_t n, const uint32_t *__restrict__ 
         best = hj > best ? hj : best;
       }
     }
-    if (agg_max<uint32_t>(H, r, best, act && best != 0)) *changed = 1;
+    agg_lane<uint32_t, true>(tb, r, best, act && best != 0);
   }
+  __syncthreads();
+  agg_flush<uint32_t, true>(tb, H, [&](uint32_t) { *changed = 1; });
 }
 
 __global__ void k_fb_roots(uint32_t n, const uint32_t *__restrict__ list,
@@ -439,7 +546,8 @@ __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            const uint32_t *__restrict__ H, uint8_t *reached, uint32_t *changed,
-                           uint8_t *__restrict__ pushed) {
+                           uint8_t *__restrict__ pushed, const uint32_t *__restrict__ prev) {
+  if (prev && ld_u32(prev) == 0) return;  // converged (see converge())
   GRID_STRIDE(j, n) {
     const uint32_t v = FB_VID(j);
     // a vertex pushes its edges once, in the launch after its class is
@@ -528,13 +636,19 @@ __global__ void k_compact(uint32_t V, const uint32_t *__restrict__ fl,
 // ---------------------------------------------------------------- orders
 __global__ void k_label_init(uint32_t V, uint64_t *label) { GRID_STRIDE(v, V) label[v] = ~0ull; }
 
-__global__ void k_label_min(uint32_t V, const uint32_t *__restrict__ rep,
-                            const uint64_t *__restrict__ dot, uint64_t *label) {
-  WAVE_STRIDE(v, V) {
-    const bool act = v < V;
-    agg_min<unsigned long long>((unsigned long long *)label, act ? rep[v] : 0u,
-                                act ? (unsigned long long)dot[v] : 0ull, act);
-  }
+__global__ void __launch_bounds__(256)
+    k_label_min(uint32_t V, const uint32_t *__restrict__ rep, const uint64_t *__restrict__ dot,
+                uint64_t *label) {
+  // class minimum dot, block-aggregated (one item per thread)
+  __shared__ AggTable<unsigned long long> t;
+  agg_init<unsigned long long, false>(t);
+  __syncthreads();
+  const uint32_t v = blockIdx.x * B + threadIdx.x;
+  const bool act = v < V;
+  agg_lane<unsigned long long, false>(t, act ? rep[v] : 0u, act ? (unsigned long long)dot[v] : 0ull,
+                                      act);
+  __syncthreads();
+  agg_flush<unsigned long long, false>(t, (unsigned long long *)label, [](uint32_t) {});
 }
 
 __global__ void k_label_bcast(uint32_t V, const uint32_t *__restrict__ rep,
@@ -660,6 +774,39 @@ uint32_t GraphCore::read_scalar(int i) {
   return fetch_u32(scalars.get() + i, stream);
 }
 
+// Device-side convergence of an iterated kernel: launches go out in groups of
+// kConvGroup, each with its own flag words (`words` per launch) and the
+// previous launch's; a launch whose predecessor changed nothing returns at
+// once.  The host reads one group's flags per round trip instead of one flag
+// per launch.  launch(changed, prev) enqueues one launch (prev null for the
+// group's first); `launches` counts the launches that can have done work.
+constexpr uint32_t kConvGroup = 4;
+template <class L>
+void GraphCore::converge(uint32_t words, uint32_t &launches, L launch) {
+  FH_CHECK(kConvGroup * words <= 12, FH_EINVAL, "converge: too many flag words");
+  uint32_t *cf = conv.ensure(16);
+  uint32_t h[16];
+  for (;;) {
+    FH_HIP(hipMemsetAsync(cf, 0, size_t(kConvGroup) * words * sizeof(uint32_t), stream));
+    for (uint32_t g = 0; g < kConvGroup; g++) {
+      launches++;
+      launch(cf + g * words, g ? cf + (g - 1) * words : nullptr);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    fetch_u32(cf, h, int(kConvGroup * words), stream);
+    dbg_sync_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    dbg_sync_n++;
+    for (uint32_t g = 0; g < kConvGroup; g++) {
+      uint32_t c = 0;
+      for (uint32_t w = 0; w < words; w++) c |= h[g * words + w];
+      if (c == 0) {
+        launches -= kConvGroup - 1 - g;  // the skipped ones
+        return;
+      }
+    }
+  }
+}
+
 void GraphCore::pending_closure(const GraphInput &in, GraphOutput &out) {
   const uint32_t V = in.V;
   k_blocked_init<<<grid_for(V, B), B, 0, stream>>>(V, in.blocked0, blocked.get());
@@ -707,15 +854,32 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
   const uint32_t V = in.V;
   FH_HIP(hipMemsetAsync(kap.get(), 0, size_t(V) * sizeof(uint64_t), stream));
   FH_HIP(hipMemsetAsync(kraise.ensure(V + 1), 0, size_t(V) * sizeof(uint32_t), stream));
-  k_kap_init<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get());
+  static const bool no_hseed = getenv("FH_NO_HSEED") != nullptr;
+  k_kap_init<<<agg_blocks(V), B, 0, stream>>>(V, blocked.get(), rep.get(),
+                                              hseed_ok && !no_hseed ? hseed.get() : nullptr,
+                                              kap.get());
   refresh_edge_rep(in);
+  if (!give_up_early) {
+    // to the fixpoint: device-side convergence, no per-iteration read-back
+    uint32_t launched = 0;
+    converge(1, launched, [&](uint32_t *changed, const uint32_t *prev) {
+      k_kap_relax<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(),
+                                                   rep.get(), kap.get(), changed, kraise.get(),
+                                                   launched, 0u, prev);
+      FH_CHECK(launched < max_iters, FH_EINVARIANT, "kappa: no fixpoint");
+    });
+    iters = launched;
+    mark("kappa");
+    return true;
+  }
   // raises of the last iterations; a cycle the windows missed keeps raising
   // its members forever, a converging run raises fewer and fewer vertices
   uint64_t r1 = 0, r2 = 0;
   for (uint32_t it = 0; it < max_iters; it++) {
     FH_HIP(hipMemsetAsync(scalars.get() + 16, 0, 8 * sizeof(uint32_t), stream));
-    k_kap_relax<<<grid_for(V, B), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(), rep.get(),
-                                                   kap.get(), scalars.get() + 16, kraise.get(), it + 1);
+    k_kap_relax<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(), rep.get(),
+                                                   kap.get(), scalars.get() + 16, kraise.get(), it + 1,
+                                                   7u, nullptr);
     iters = it + 1;
     uint32_t c[8];
     fetch_u32(scalars.get() + 16, c, 8, stream);
@@ -727,7 +891,7 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
     }
     // give up early (bounded runs only) when the raises stopped shrinking:
     // fewer than 10 % less than two iterations ago
-    if (give_up_early && iters >= 3 && raised * 10 > r2 * 9) break;
+    if (iters >= 3 && raised * 10 > r2 * 9) break;
     r2 = r1;
     r1 = raised;
   }
@@ -786,24 +950,24 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
       k_fb_hreset<<<G, B, 0, stream>>>(n, list, rep.get(), H);
     else
       FH_HIP(hipMemsetAsync(H, 0, size_t(V) * sizeof(uint32_t), stream));
-    k_fb_init<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
+    k_fb_init<<<agg_blocks(n), B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
     if (full && !list && kap_seed_ok)
       k_fb_seed<<<G, B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get(), H);
     dbg_rounds++;
-    do {
-      dbg_hprop++;
-      FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
-      k_fb_hprop<<<G, B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
-                                       rep.get(), H, scalars.get());
-    } while (read_scalar(0));
+    converge(1, dbg_hprop, [&](uint32_t *changed, const uint32_t *prev) {
+      k_fb_hprop<<<agg_blocks(n), B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er,
+                                                  blocked.get(), done, rep.get(), H, changed, prev);
+    });
+    if (!list && !recent_iter) {
+      k_fb_save_h<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), H, hseed.ensure(V));
+      hseed_ok = true;
+    }
     k_fb_roots<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
     FH_HIP(hipMemsetAsync(pushed, 0, V, stream));
-    do {
-      dbg_reach++;
-      FH_HIP(hipMemsetAsync(scalars.get(), 0, sizeof(uint32_t), stream));
+    converge(1, dbg_reach, [&](uint32_t *changed, const uint32_t *prev) {
       k_fb_reach<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
-                                       rep.get(), H, reached, scalars.get(), pushed);
-    } while (read_scalar(0));
+                                       rep.get(), H, reached, changed, pushed, prev);
+    });
     FH_HIP(hipMemsetAsync(scalars.get() + 1, 0, sizeof(uint32_t), stream));
     // unions go to a separate parent array so rep[] stays stable while read
     // (only the processed vertices' entries are read or written)
@@ -847,7 +1011,7 @@ void GraphCore::build_labels(const GraphInput &in, GraphOutput &out) {
   uint64_t *lab = label.ensure(V);
   uint64_t *lab_out = tmp64c.ensure(V);
   k_label_init<<<grid_for(V, B), B, 0, stream>>>(V, lab);
-  k_label_min<<<grid_for(V, B), B, 0, stream>>>(V, rep.get(), in.dot, lab);
+  k_label_min<<<agg_blocks(V), B, 0, stream>>>(V, rep.get(), in.dot, lab);
   k_label_bcast<<<grid_for(V, B), B, 0, stream>>>(V, rep.get(), lab, lab_out);
   out.scc_label = lab_out;
   mark("scc_label");
@@ -1012,6 +1176,7 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
   }
   uint32_t iters = 0, iters1 = 0;
+  hseed_ok = false;
   dbg_rounds = dbg_hprop = dbg_reach = dbg_sync_n = dbg_left = 0;
   dbg_sync_us = 0;
   // a cycle the windows missed makes kappa grow forever: give up early and let
