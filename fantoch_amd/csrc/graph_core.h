@@ -102,7 +102,8 @@ struct GraphCore {
   template <class L>
   void converge(uint32_t words, uint32_t &launches, L launch);
   DBuf<uint32_t> hseed;       // [V] exact ready time per vertex from the full coloring
-  bool hseed_ok = false;      // hseed holds this run's first full coloring round
+  bool hseed_ok = false;
+  uint32_t dbg_kap_list = 0;  // vertices the seeded kappa run relaxed after its first launch      // hseed holds this run's first full coloring round
   uint32_t tile_r0 = 1536;  // graph_tile: first reach bound to try (set from
                             // the last run's maximum excess)
   DBuf<uint32_t> scalars;  // device scalars (changed flags, counters)

@@ -345,7 +345,13 @@ __global__ void __launch_bounds__(256)
                 const uint32_t *__restrict__ erep, const uint8_t *__restrict__ blocked,
                 const uint32_t *__restrict__ rep, uint64_t *kap, uint32_t *changed,
                 uint32_t *kraise, uint32_t iter, uint32_t cmask,
-                const uint32_t *__restrict__ prev) {
+                const uint32_t *__restrict__ prev, const uint32_t *__restrict__ list,
+                uint32_t n, uint32_t *__restrict__ actf) {
+  // list (may be null): relax only the listed vertices (n of them; V when
+  // null).  actf (may be null): actf[v] = 1 iff v has an edge into another
+  // class with the same ready time -- with exact ready times seeded (hseed)
+  // no other vertex can ever raise its class, so later launches relax only
+  // the flagged ones.
   // counters: changed[0..cmask]; the previous launch of a converge() group
   // raised nothing (prev[0..cmask] all zero): converged, return
   if (prev) {
@@ -358,11 +364,14 @@ __global__ void __launch_bounds__(256)
   agg_init<unsigned long long, true>(t);
   if (threadIdx.x == 0) s_raised = 0;
   __syncthreads();
-  const uint32_t v = blockIdx.x * B + threadIdx.x;
-  const bool act = v < V && !blocked[v];
+  const uint32_t i = blockIdx.x * B + threadIdx.x;
+  const uint32_t v = i < n ? (list ? list[i] : i) : 0u;
+  const bool act = i < n && !blocked[v];
   const uint32_t r = act ? rep[v] : 0u;
   uint64_t best = 0;
+  bool same_h = false;
   if (act) {
+    const uint32_t hr = actf ? uint32_t(ld_u64(&kap[r]) >> 32) : 0u;
     // four edges per trip, every gather issued before the first is used
     const uint32_t eb = EB(v), ee = EE(v);
     for (uint32_t e = eb; e < ee; e += 4) {
@@ -377,11 +386,13 @@ __global__ void __launch_bounds__(256)
         // time half that k_fb_seed reads
         const uint64_t k = ru[j] != r ? ld_u64(&kap[ru[j]]) : 0;
         c[j] = ru[j] == r ? 0 : (uint32_t(k) >= 0xFFFFFFFEu ? k : k + 1);
+        same_h |= ru[j] != r && uint32_t(k >> 32) == hr;
       }
 #pragma unroll
       for (int j = 0; j < 4; j++) best = c[j] > best ? c[j] : best;
     }
   }
+  if (actf && i < n) actf[v] = same_h ? 1u : 0u;
   agg_lane<unsigned long long, true>(t, r, best, act && best != 0);
   __syncthreads();
   // raised classes per iteration, over 8 counters (one per XCD under
@@ -470,7 +481,10 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
                            const uint32_t *__restrict__ dst, const uint32_t *__restrict__ erep,
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
-                           uint32_t *H, uint32_t *changed, const uint32_t *__restrict__ prev) {
+                           uint32_t *H, uint32_t *changed, const uint32_t *__restrict__ prev,
+                           int nodone) {
+  // nodone: the first round of the full coloring (nothing done yet): the
+  // done[] gathers per edge are skipped
   // the previous launch of the group changed nothing: converged, return
   if (prev && ld_u32(prev) == 0) return;
   __shared__ AggTable<uint32_t> tb;
@@ -496,7 +510,7 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
           uint32_t h[4];
 #pragma unroll
           for (int j = 0; j < 4; j++) {
-            dn[j] = ru[j] != r ? done[ru[j]] : 1;
+            dn[j] = ru[j] != r ? (nodone ? uint8_t(0) : done[ru[j]]) : uint8_t(1);
             h[j] = ru[j] != r ? ld_u32(&H[ru[j]]) : 0;
           }
 #pragma unroll
@@ -518,7 +532,7 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
       // bound of the fixpoint, which stays the same); long forward chains
       // collapse in logarithmically many launches
       const uint32_t t = max(best, ld_u32(&H[r]));
-      if (t < V && !done[t] && !blocked[t]) {
+      if (t < V && (nodone || !done[t]) && !blocked[t]) {
         const uint32_t hj = ld_u32(&H[rep[t]]);
         best = hj > best ? hj : best;
       }
@@ -546,7 +560,8 @@ __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            const uint32_t *__restrict__ H, uint8_t *reached, uint32_t *changed,
-                           uint8_t *__restrict__ pushed, const uint32_t *__restrict__ prev) {
+                           uint8_t *__restrict__ pushed, const uint32_t *__restrict__ prev,
+                           int nodone) {
   if (prev && ld_u32(prev) == 0) return;  // converged (see converge())
   GRID_STRIDE(j, n) {
     const uint32_t v = FB_VID(j);
@@ -567,7 +582,7 @@ __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
         for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
         bool cand[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) cand[j] = ru[j] != r && !done[ru[j]] && H[ru[j]] == hr;
+        for (int j = 0; j < 4; j++) cand[j] = ru[j] != r && (nodone || !done[ru[j]]) && H[ru[j]] == hr;
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (cand[j] && !__hip_atomic_load(&reached[ru[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -693,6 +708,54 @@ __global__ void k_vertex_keys(uint32_t V, const uint32_t *__restrict__ flags,
     if (!flags[v]) continue;
     keys[pos[v]] = (uint64_t(scc_rank[rep[v]]) << bits) | dot_rank[v];
     vals[pos[v]] = v;
+  }
+}
+
+// dot range of the batch: the maximum source and sequence, so the dot sort
+// runs on (src, seq) packed into as few bits as the batch needs
+__global__ void k_dot_range(uint32_t V, const uint64_t *__restrict__ dot,
+                            unsigned long long *__restrict__ mx) {
+  unsigned long long ms = 0, mq = 0;
+  GRID_STRIDE(v, V) {
+    const uint64_t d = dot[v];
+    ms = max(ms, (unsigned long long)(d >> 56));
+    mq = max(mq, (unsigned long long)(d & 0x00FFFFFFFFFFFFFFull));
+  }
+  ms = wave_max_all(ms);
+  mq = wave_max_all(mq);
+  if ((threadIdx.x & 63) == 0) {
+    if (ms > ld_rel(mx)) atomicMax(mx, ms);
+    if (mq > ld_rel(mx + 1)) atomicMax(mx + 1, mq);
+  }
+}
+
+template <class K>
+__global__ void k_dot_keys(uint32_t V, const uint64_t *__restrict__ dot, int sb,
+                           K *__restrict__ keys) {
+  GRID_STRIDE(v, V) {
+    const uint64_t d = dot[v];
+    keys[v] = K(((d >> 56) << sb) | (d & 0x00FFFFFFFFFFFFFFull));
+  }
+}
+
+// vertices in dot order, executable ones compacted, keyed by their SCC's rank:
+// a stable sort by that key gives the execution order (SCC rank, then dot)
+__global__ void k_exec_flags_dord(uint32_t V, const uint32_t *__restrict__ dord,
+                                  const uint8_t *__restrict__ blocked,
+                                  uint32_t *__restrict__ flags) {
+  GRID_STRIDE(j, V) flags[j] = blocked[dord[j]] ? 0u : 1u;
+}
+__global__ void k_exec_keys_dord(uint32_t V, const uint32_t *__restrict__ dord,
+                                 const uint32_t *__restrict__ flags,
+                                 const uint32_t *__restrict__ pos,
+                                 const uint32_t *__restrict__ rep,
+                                 const uint32_t *__restrict__ scc_rank,
+                                 uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  GRID_STRIDE(j, V) {
+    if (!flags[j]) continue;
+    const uint32_t v = dord[j];
+    keys[pos[j]] = scc_rank[rep[v]];
+    vals[pos[j]] = v;
   }
 }
 
@@ -855,17 +918,44 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
   FH_HIP(hipMemsetAsync(kap.get(), 0, size_t(V) * sizeof(uint64_t), stream));
   FH_HIP(hipMemsetAsync(kraise.ensure(V + 1), 0, size_t(V) * sizeof(uint32_t), stream));
   static const bool no_hseed = getenv("FH_NO_HSEED") != nullptr;
+  const bool seeded = hseed_ok && !no_hseed;
   k_kap_init<<<agg_blocks(V), B, 0, stream>>>(V, blocked.get(), rep.get(),
-                                              hseed_ok && !no_hseed ? hseed.get() : nullptr,
+                                              seeded ? hseed.get() : nullptr,
                                               kap.get());
   refresh_edge_rep(in);
   if (!give_up_early) {
     // to the fixpoint: device-side convergence, no per-iteration read-back
     uint32_t launched = 0;
-    converge(1, launched, [&](uint32_t *changed, const uint32_t *prev) {
+    const uint32_t *lst = nullptr;
+    uint32_t nl = V;
+    if (seeded) {
+      // exact ready times: the first launch flags the vertices that can
+      // still raise their class; the rest of the run relaxes only those
+      uint32_t *fl = cnt.ensure(V), *ps = pos.ensure(V + 1), *lo = order.ensure(V + 1);
+      uint32_t *cf = conv.ensure(16);
+      FH_HIP(hipMemsetAsync(cf, 0, sizeof(uint32_t), stream));
       k_kap_relax<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(),
-                                                   rep.get(), kap.get(), changed, kraise.get(),
-                                                   launched, 0u, prev);
+                                                   rep.get(), kap.get(), cf, kraise.get(), 1u, 0u,
+                                                   nullptr, nullptr, V, fl);
+      launched = 1;
+      exclusive_scan_u32(fl, ps, V, scan_ws, stream);
+      k_compact<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, lo);
+      uint32_t h[2];
+      fetch_u32(cf, h, 1, stream);
+      fetch_u32(ps + V, h + 1, 1, stream);
+      dbg_kap_list = h[1];
+      if (h[0] == 0) {
+        iters = launched;
+        mark("kappa");
+        return true;
+      }
+      lst = lo;
+      nl = h[1];
+    }
+    converge(1, launched, [&](uint32_t *changed, const uint32_t *prev) {
+      k_kap_relax<<<agg_blocks(nl), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(),
+                                                    rep.get(), kap.get(), changed, kraise.get(),
+                                                    launched, 0u, prev, lst, nl, nullptr);
       FH_CHECK(launched < max_iters, FH_EINVARIANT, "kappa: no fixpoint");
     });
     iters = launched;
@@ -879,7 +969,7 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
     FH_HIP(hipMemsetAsync(scalars.get() + 16, 0, 8 * sizeof(uint32_t), stream));
     k_kap_relax<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(), rep.get(),
                                                    kap.get(), scalars.get() + 16, kraise.get(), it + 1,
-                                                   7u, nullptr);
+                                                   7u, nullptr, nullptr, V, nullptr);
     iters = it + 1;
     uint32_t c[8];
     fetch_u32(scalars.get() + 16, c, 8, stream);
@@ -945,6 +1035,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     refresh_edge_rep(in);
     er = erep.get();
   }
+  bool first_full = full;  // round 1 over every vertex: done[] is all zero
   for (;;) {
     if (list)
       k_fb_hreset<<<G, B, 0, stream>>>(n, list, rep.get(), H);
@@ -956,7 +1047,8 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     dbg_rounds++;
     converge(1, dbg_hprop, [&](uint32_t *changed, const uint32_t *prev) {
       k_fb_hprop<<<agg_blocks(n), B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er,
-                                                  blocked.get(), done, rep.get(), H, changed, prev);
+                                                  blocked.get(), done, rep.get(), H, changed, prev,
+                                                  int(first_full));
     });
     if (!list && !recent_iter) {
       k_fb_save_h<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), H, hseed.ensure(V));
@@ -966,7 +1058,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     FH_HIP(hipMemsetAsync(pushed, 0, V, stream));
     converge(1, dbg_reach, [&](uint32_t *changed, const uint32_t *prev) {
       k_fb_reach<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
-                                       rep.get(), H, reached, changed, pushed, prev);
+                                       rep.get(), H, reached, changed, pushed, prev, int(first_full));
     });
     FH_HIP(hipMemsetAsync(scalars.get() + 1, 0, sizeof(uint32_t), stream));
     // unions go to a separate parent array so rep[] stays stable while read
@@ -985,6 +1077,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
       FH_HIP(hipMemcpyAsync(rep.get(), parent, size_t(V) * sizeof(uint32_t),
                             hipMemcpyDeviceToDevice, stream));
     if (!read_scalar(1)) break;
+    first_full = false;
     if (full) {
       // vertices left for the next round -> list (the restricted pass's path)
       uint32_t *fl = cnt.ensure(V);
@@ -1021,14 +1114,35 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   const uint32_t V = in.V;
   const int bv = bits_for(uint64_t(V) + 1);
   build_labels(in, out);
-  // dot rank (intra-SCC order is dot order)
+  // vertices in dot order (intra-SCC order is dot order).  The dots are
+  // packed to (src, seq) over the bits the batch needs: 4 passes of u32 keys
+  // on the measured streams instead of 8 over the whole u64.
   uint64_t *ka = tmp64a.ensure(V), *kb = tmp64b.ensure(V);
   uint32_t *va = tmp32a.ensure(V), *vb = tmp32b.ensure(V);
   uint64_t *ks = nullptr;
   uint32_t *vs = nullptr;
-  uint32_t *dot_rank = rank.ensure(V);
-  sort_pairs<uint64_t, uint32_t>(in.dot, nullptr, ka, va, kb, vb, V, 64, sort_ws, stream, &ks, &vs);
-  k_rank_from_sorted<<<grid_for(V, B), B, 0, stream>>>(V, vs, dot_rank);
+  unsigned long long *mx = reinterpret_cast<unsigned long long *>(scalars.get() + 24);
+  FH_HIP(hipMemsetAsync(mx, 0, 2 * sizeof(unsigned long long), stream));
+  k_dot_range<<<grid_for(V, B, 2048), B, 0, stream>>>(V, in.dot, mx);
+  unsigned long long hmx[2] = {0, 0};
+  FH_HIP(hipMemcpyAsync(hmx, mx, sizeof(hmx), hipMemcpyDeviceToHost, stream));
+  FH_HIP(hipStreamSynchronize(stream));
+  const int sb = bits_for(hmx[1] + 1), dbits = bits_for(hmx[0] + 1) + sb;
+  uint32_t *dord = rank.ensure(V);
+  if (dbits <= 32) {
+    uint32_t *k32a = reinterpret_cast<uint32_t *>(ka), *k32b = reinterpret_cast<uint32_t *>(kb);
+    uint32_t *k32s = nullptr;
+    k_dot_keys<uint32_t><<<grid_for(V, B), B, 0, stream>>>(V, in.dot, sb, k32a);
+    sort_pairs<uint32_t, uint32_t>(k32a, nullptr, k32a, va, k32b, vb, V, dbits, sort_ws, stream,
+                                   &k32s, &vs);
+  } else if (dbits < 64) {
+    k_dot_keys<uint64_t><<<grid_for(V, B), B, 0, stream>>>(V, in.dot, sb, ka);
+    sort_pairs<uint64_t, uint32_t>(ka, nullptr, ka, va, kb, vb, V, dbits, sort_ws, stream, &ks, &vs);
+  } else {
+    sort_pairs<uint64_t, uint32_t>(in.dot, nullptr, ka, va, kb, vb, V, 64, sort_ws, stream, &ks,
+                                   &vs);
+  }
+  FH_HIP(hipMemcpyAsync(dord, vs, size_t(V) * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
   mark("dot_rank");
   // SCC order by kappa
   uint32_t *fl = cnt.ensure(V);
@@ -1043,15 +1157,18 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   sort_pairs<uint64_t, uint32_t>(ka, va, ka, va, kb, vb, nrep, 2 * bv, sort_ws, stream, &ks, &vs);
   k_rank_from_sorted<<<grid_for(nrep, B), B, 0, stream>>>(nrep, vs, scc_rank);
   mark("scc_order");
-  // vertex order: (scc rank, dot rank)
-  k_exec_flags<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), fl);
+  // execution order: the executable vertices in dot order, stable-sorted by
+  // their SCC's rank (bits for nrep instead of a (rank, dot rank) pair)
+  k_exec_flags_dord<<<grid_for(V, B), B, 0, stream>>>(V, dord, blocked.get(), fl);
   exclusive_scan_u32(fl, ps, V, scan_ws, stream);
   uint32_t nexec = 0;
   FH_HIP(hipMemcpyAsync(&nexec, ps + V, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-  k_vertex_keys<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, rep.get(), scc_rank, dot_rank, bv,
-                                                   ka, va);
+  uint32_t *k32a = reinterpret_cast<uint32_t *>(ka), *k32b = reinterpret_cast<uint32_t *>(kb);
+  k_exec_keys_dord<<<grid_for(V, B), B, 0, stream>>>(V, dord, fl, ps, rep.get(), scc_rank, k32a, va);
   FH_HIP(hipStreamSynchronize(stream));
-  sort_pairs<uint64_t, uint32_t>(ka, va, ka, va, kb, vb, nexec, 2 * bv, sort_ws, stream, &ks, &vs);
+  uint32_t *k32s = nullptr;
+  sort_pairs<uint32_t, uint32_t>(k32a, va, k32a, va, k32b, vb, nexec, bits_for(uint64_t(nrep) + 1),
+                                 sort_ws, stream, &k32s, &vs);
   uint32_t *ord = order.ensure(nexec + 1);
   FH_HIP(hipMemcpyAsync(ord, vs, size_t(nexec) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
                         stream));
@@ -1222,9 +1339,10 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   if (debug)
     fprintf(stderr,
             "fh graph: V=%u forward=%llu kappa=%u fallback=%d (candidates %u, restricted %u, "
-            "rounds %u, hprop %u, reach %u, left %u) kappa2=%u syncs %u %.0f us\n",
+            "rounds %u, hprop %u, reach %u, left %u) kappa2=%u (list %u) syncs %u %.0f us\n",
             V, (unsigned long long)nfwd, iters1, int(out.fallback_used), dbg_cand,
             dbg_restricted, dbg_rounds, dbg_hprop, dbg_reach, dbg_left, out.fallback_used ? iters : 0u,
+            dbg_kap_list,
             dbg_sync_n, dbg_sync_us);
   build_orders(in, out);
 }
