@@ -862,6 +862,8 @@ struct EngineDevice {
   DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
   DBuf<uint32_t> place_base;  // replica views: per-chunk smallest element position
+  bool deps_only = false;     // fh_engine_set_deps_only: stop after the committed deps
+  bool last_deps_only = false;
   DBuf<unsigned long long> srcstats;
   SortWorkspace sort_ws;
   ScanWorkspace scan_ws;
@@ -1173,6 +1175,7 @@ struct EngineDevice {
     const bool views = desc.views != 0;
     const size_t b = cursor++;
     last = b;
+    last_deps_only = deps_only;
     const uint64_t bbase = stage_base + b * n;  // log position of this batch
     const uint64_t *bdot = dot.get() + bbase;
     const uint32_t *bkey = key32.get() + b * size_t(n) * k;
@@ -1458,6 +1461,7 @@ struct EngineDevice {
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
                     scal.get(), ecnt, bbase, doff, scal.get() + 1);
     mark("keydeps_union");
+    if (deps_only) return;  // the committed deps are the output (partial replication)
     const uint32_t *gdst = dd, *goff = nullptr;
     if (views && S >= 8) {  // measured: a win at S = 12 (C5), flat or worse at 3 and 6
       uint32_t *eo = edge_off.ensure(n + 1);
@@ -1540,6 +1544,7 @@ struct EngineDevice {
     }
     }
     mark("out_deps");
+    if (deps_only) return;
     if (gout.trivial && sv_fused && sv_labels_done) {
       o_label = lab.get();
       o_rank = rank_tmp.get();
@@ -1592,6 +1597,8 @@ struct EngineDevice {
                uint64_t *scc_label, uint32_t *exec_rank, uint32_t *key_off, uint64_t *key_seq) {
     FH_HIP(hipSetDevice(device));
     FH_CHECK(staged && cursor > 0, FH_EINVAL, "no run to read results from");
+    FH_CHECK(!last_deps_only || (!scc_label && !exec_rank && !key_off && !key_seq), FH_EINVAL,
+             "deps-only run: only the committed deps are materialised");
     FH_HIP(hipStreamSynchronize(stream));
     const uint32_t n = uint32_t(desc.n);
     if (!sv_fused && deps_direct) {
@@ -1767,6 +1774,13 @@ fh_status fh_engine_set_profiling(fh_engine *h, int on) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
   h->dev.profile = on != 0;
+  FH_API_END
+}
+
+fh_status fh_engine_set_deps_only(fh_engine *h, int on) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  h->dev.deps_only = on != 0;
   FH_API_END
 }
 

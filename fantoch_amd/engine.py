@@ -46,6 +46,22 @@ class Engine:
     def set_profiling(self, on: bool):
         L.check(self._lib.fh_engine_set_profiling(self._h, 1 if on else 0))
 
+    def set_deps_only(self, on: bool):
+        """run() stops after the committed deps (fh_engine_set_deps_only)."""
+        L.check(self._lib.fh_engine_set_deps_only(self._h, 1 if on else 0))
+
+    def deps(self):
+        """The last run's committed deps only: (dep_off u32[n+1], deps u64)."""
+        n = self.n
+        dep_off = np.zeros(n + 1, dtype=np.uint32)
+        ln = C.c_size_t(0)
+        L.check(self._lib.fh_engine_results(self._h, L.ptr(dep_off), None, 0, C.byref(ln), None,
+                                            None, None, None))
+        deps = np.zeros(max(1, ln.value), dtype=np.uint64)
+        L.check(self._lib.fh_engine_results(self._h, L.ptr(dep_off), L.ptr(deps), len(deps),
+                                            C.byref(ln), None, None, None, None))
+        return dep_off, deps[:ln.value]
+
     def stage(self, stream, nproc: int = 5):
         """stream: fantoch_amd.workload.Stream (views taken from it; its
         per-replica logs if generated, else fq_proc / fq_time)."""

@@ -496,6 +496,12 @@ fh_status fh_engine_probe_stats_for(fh_engine *h, const char *kernel, float *avg
                                     size_t *launches, double *bytes_per_launch);
 /* Enable/disable per-kernel event timing (adds events between kernels). */
 fh_status fh_engine_set_profiling(fh_engine *h, int on);
+/* Deps-only runs (on != 0): run() stops after the committed deps (KeyDeps
+ * per replica view + the QuorumDeps union, quorum.rs:28-98) -- the
+ * per-shard stage of partial replication, whose graph runs after the
+ * cross-shard union (MShardCommit, atlas.rs:559-639).  results() then
+ * returns the deps only (FH_EINVAL for labels, ranks or per-key output). */
+fh_status fh_engine_set_deps_only(fh_engine *h, int on);
 
 /* ======================================================================
  * Multi-GPU fused engine from one process: one engine
