@@ -79,6 +79,28 @@ impl Engine {
         check(unsafe { ffi::fh_engine_run(self.h, null_mut()) });
     }
 
+    /// Deps-only runs: the per-shard stage of partial replication (the
+    /// committed deps feed the cross-shard union before any graph work).
+    pub fn set_deps_only(&mut self, on: bool) {
+        check(unsafe { ffi::fh_engine_set_deps_only(self.h, on as i32) });
+    }
+
+    /// The last run's committed deps (dep_off[n + 1], deps).
+    pub fn deps(&self) -> (Vec<u32>, Vec<u64>) {
+        let mut off = vec![0u32; self.n + 1];
+        let mut len = 0usize;
+        check(unsafe {
+            ffi::fh_engine_results(self.h, off.as_mut_ptr(), null_mut(), 0, &mut len,
+                null_mut(), null_mut(), null_mut(), null_mut())
+        });
+        let mut deps = vec![0u64; len];
+        check(unsafe {
+            ffi::fh_engine_results(self.h, off.as_mut_ptr(), deps.as_mut_ptr(), len, &mut len,
+                null_mut(), null_mut(), null_mut(), null_mut())
+        });
+        (off, deps)
+    }
+
     pub fn results(&self) -> EngineResults {
         let mut r = EngineResults {
             dep_off: vec![0; self.n + 1],
