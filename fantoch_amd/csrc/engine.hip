@@ -139,58 +139,78 @@ struct PrevSrc {
 };
 
 // The bucketing pass: k_down's tile staging, but the order within a bucket
-// is free, so ranks come from LDS atomics (no ballot matching).  The tile
-// counts k_up wrote fix every tile's run per bucket.
-__global__ void __launch_bounds__(kThreads)
+// is free, so ranks come from LDS atomics (no ballot matching).  One
+// 512-thread workgroup takes two count tiles (8192 elements): the runs of
+// consecutive tiles in one bucket are adjacent in the output, so a bucket's
+// run per workgroup averages 16 elements (64 B per array) instead of 8 --
+// 4096-element workgroups wrote 32 B runs, half-line writes.
+constexpr int kBucketThreads = 512;
+constexpr int kBucketWaves = kBucketThreads / 64;
+constexpr int kBucketTile = 2 * kTile;  // 8192
+__global__ void __launch_bounds__(kBucketThreads)
     k_bucket_codes(PrevSrc src, uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                    uint32_t n, const uint32_t *__restrict__ counts,
                    const uint32_t *__restrict__ gsum, uint32_t gsize,
                    const uint32_t *__restrict__ dbase) {
-  constexpr uint32_t R = kPlaceBuckets, Q = R / kThreads;
-  __shared__ uint32_t s_k[kTile], s_v[kTile];
+  constexpr uint32_t R = kPlaceBuckets;
+  static_assert(R == kBucketThreads, "one bucket per thread in the scan");
+  __shared__ uint32_t s_k[kBucketTile], s_v[kBucketTile];
   __shared__ uint32_t s_cnt[R], s_dex[R], s_gb[R];
-  __shared__ uint32_t s_tmp[kWaves];
+  __shared__ uint32_t s_tmp[kBucketWaves];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t tile = blockIdx.x, base = tile * kTile;
-  for (uint32_t d = tid; d < R; d += kThreads) {
-    s_cnt[d] = 0;
-    s_gb[d] = dbase[d] + gsum[size_t(tile / gsize) * R + d] + counts[size_t(tile) * R + d];
-  }
-  uint32_t key[kItems], val[kItems];
+  const uint32_t tile0 = blockIdx.x * 2, base = blockIdx.x * kBucketTile;
+  // this workgroup's run of bucket d starts where count tile tile0's does
+  s_cnt[tid] = 0;
+  s_gb[tid] = dbase[tid] + gsum[size_t(tile0 / gsize) * R + tid] + counts[size_t(tile0) * R + tid];
+  // all loads first: the element's key and position, its predecessor's,
+  // then the latest entries of the segment heads
+  const uint32_t eb = *src.ebase;
+  uint32_t key[kItems], val[kItems], seg[kItems], pseg[kItems], pv[kItems];
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = elem_index(base, w, i, lane);
-    key[i] = 0;
-    val[i] = 0;
-    if (idx < n) {
-      key[i] = src.key(idx);
-      val[i] = src.code(idx);
-    }
+    const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
+    const bool ok = idx < n;
+    key[i] = ok ? src.vs[idx] - eb : 0u;
+    seg[i] = ok ? src.ks[idx] : 0u;
+    pseg[i] = ok && idx > 0 ? src.ks[idx - 1] : ~0u;
+    pv[i] = ok && idx > 0 ? src.vs[idx - 1] : 0u;
   }
+  uint64_t lat[kItems];
+#pragma unroll
+  for (int i = 0; i < kItems; i++) lat[i] = pseg[i] != seg[i] ? src.latest[seg[i]] : 0ull;
+#pragma unroll
+  for (int i = 0; i < kItems; i++)
+    val[i] = pseg[i] != seg[i] ? (lat[i] ? (0x80000000u | uint32_t(lat[i] - kLogFlag)) : 0u)
+                               : pv[i] / src.per_cmd + 1;
   __syncthreads();
   uint32_t rank[kItems];
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = elem_index(base, w, i, lane);
+    const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
     rank[i] = idx < n ? atomicAdd(&s_cnt[(key[i] >> kPlaceShift) & (R - 1)], 1u) : 0u;
   }
   __syncthreads();
-  uint32_t cnt[Q], mine = 0;
+  {
+    // exclusive scan of the bucket counts, one bucket per thread
+    const uint32_t c = s_cnt[tid];
+    uint32_t x = c;
 #pragma unroll
-  for (uint32_t q = 0; q < Q; q++) {
-    cnt[q] = s_cnt[tid * Q + q];
-    mine += cnt[q];
-  }
-  uint32_t pre = block_excl_scan(mine, s_tmp);
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(x, o, 64);
+      if (lane >= o) x += t;
+    }
+    if (lane == 63) s_tmp[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
 #pragma unroll
-  for (uint32_t q = 0; q < Q; q++) {
-    s_dex[tid * Q + q] = pre;
-    pre += cnt[q];
+    for (int i = 0; i < kBucketWaves; i++)
+      if (i < w) pre += s_tmp[i];
+    s_dex[tid] = pre + x - c;
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
-    const uint32_t idx = elem_index(base, w, i, lane);
+    const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
     if (idx < n) {
       const uint32_t p = s_dex[(key[i] >> kPlaceShift) & (R - 1)] + rank[i];
       s_k[p] = key[i];
@@ -198,9 +218,9 @@ __global__ void __launch_bounds__(kThreads)
     }
   }
   __syncthreads();
-  const uint32_t tile_n = min(uint32_t(kTile), n - base);
+  const uint32_t tile_n = min(uint32_t(kBucketTile), n - base);
 #pragma unroll 4
-  for (uint32_t j = tid; j < tile_n; j += kThreads) {
+  for (uint32_t j = tid; j < tile_n; j += kBucketThreads) {
     const uint32_t kk = s_k[j];
     const uint32_t d = (kk >> kPlaceShift) & (R - 1);
     const uint32_t o = s_gb[d] + (j - s_dex[d]);
@@ -1413,8 +1433,8 @@ struct EngineDevice {
     k_scan_b<kPlaceDB><<<1, 256, 0, s>>>(gsum, groups, dbase);
     // reads (key, arrival) keys + positions, the previous element's, and the
     // latest table at heads; writes 8 B per element
-    probed_launch("prev_bucket", double(Mc) * (4.0 + 4.0 + 8.0), k_bucket_codes, dim3(tiles),
-                  dim3(kThreads), s, src, bk, bv, Mc, (const uint32_t *)counts,
+    probed_launch("prev_bucket", double(Mc) * (4.0 + 4.0 + 8.0), k_bucket_codes,
+                  dim3((tiles + 1) / 2), dim3(kBucketThreads), s, src, bk, bv, Mc, (const uint32_t *)counts,
                   (const uint32_t *)gsum, uint32_t(kGroup), (const uint32_t *)dbase);
     probed_launch("place", double(Mc) * (8.0 + 4.0), k_place, dim3(R), dim3(1024), s, Mc,
                   (const uint32_t *)dbase, (const uint32_t *)bk, (const uint32_t *)bv, ebase, out);
