@@ -38,6 +38,8 @@ PROBES = {
     "sort_scatter_dots": r"k_down<unsigned int, unsigned long, 8",
     "graph_tile": r"k_graph_tile<",
     "prev_engine": r"k_prev_views",
+    "prev_bucket": r"k_bucket_codes",
+    "place": r"k_place",
     "cmd_union": r"k_cmd_engine<unsigned int>",
     "cmd_count": r"k_cmd_count<unsigned int>",
     "log_keys": r"k_log_keys",
