@@ -86,14 +86,14 @@ constexpr int kPlaceShift = 15;
 constexpr int kPlaceDB = 9;  // 512 buckets
 constexpr uint32_t kPlaceBuckets = 1u << kPlaceDB;
 constexpr uint32_t kPlaceSpan = 1u << kPlaceShift;
-constexpr uint32_t kPlaceSlack = 1u << 16;  // arrivals ahead of earlier commands
+constexpr uint32_t kPlaceSlack = 1u << 16;  // default (FH_PLACE_SLACK): arrivals ahead of earlier commands
 constexpr uint32_t kPlaceNone = ~0u;        // never a code (log references < 2^31 - 1)
 
 // emin (may be null): the placement base of the chunk
 __global__ void k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, LogChunk ch,
                            const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
                            uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
-                           uint32_t *__restrict__ emin) {
+                           uint32_t *__restrict__ emin, uint32_t slack) {
   GRID_STRIDE(x, M) {
     uint32_t r = 0;
     while (r + 1 < nlog && x >= ch.cum[r + 1]) r++;
@@ -111,7 +111,7 @@ __global__ void k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, L
     uint32_t m = ~0u;
     for (uint32_t r = 0; r < nlog; r++)
       if (ch.cum[r + 1] > ch.cum[r]) m = min(m, ent[ch.first[r]] * k);
-    *emin = m > kPlaceSlack ? m - kPlaceSlack : 0u;
+    *emin = m > slack ? m - slack : 0u;
   }
 }
 
@@ -1305,6 +1305,10 @@ struct EngineDevice {
         const char *e = getenv("FH_VIEW_PLACE");
         return !(e && *e == '0');
       }();
+      static const uint32_t place_slack = [] {
+        const char *e = getenv("FH_PLACE_SLACK");  // tests: 0 makes reordered arrivals strays
+        return e ? uint32_t(atol(e)) : kPlaceSlack;
+      }();
       static const size_t chunk_elems = [] {
         const char *e = getenv("FH_VIEW_CHUNK");
         return e ? size_t(std::max(1L, atol(e))) : place ? size_t(15) << 20 : size_t(12) << 20;
@@ -1367,7 +1371,8 @@ struct EngineDevice {
         if (!fused) {
           probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys,
                         dim3(grid_for(Mc, B)), dim3(B), stream, Mc, k, fq, np, lc, bent, bkey,
-                        uint32_t(key_space), lk, lv, place ? pbase + c : (uint32_t *)nullptr);
+                        uint32_t(key_space), lk, lv, place ? pbase + c : (uint32_t *)nullptr,
+                        place_slack);
           sort_pairs<uint32_t, uint32_t>(lk, lv, lk, lv, bkb.ensure(Mc + 1), bvb.ensure(Mc + 1),
                                          Mc, bits, sort_ws, stream, &ks, &vs);
         } else {

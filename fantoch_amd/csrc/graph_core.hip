@@ -346,7 +346,10 @@ __global__ void __launch_bounds__(256)
                 const uint32_t *__restrict__ rep, uint64_t *kap, uint32_t *changed,
                 uint32_t *kraise, uint32_t iter, uint32_t cmask,
                 const uint32_t *__restrict__ prev, const uint32_t *__restrict__ list,
-                uint32_t n, uint32_t *__restrict__ actf) {
+                uint32_t n, uint32_t *__restrict__ actf, const uint32_t *__restrict__ dst) {
+  // erep null: the edge targets' representatives are gathered as rep[dst[e]]
+  // (the seeded run: one full launch, then a short vertex list -- cheaper
+  // than refreshing erep over every edge first).
   // list (may be null): relax only the listed vertices (n of them; V when
   // null).  actf (may be null): actf[v] = 1 iff v has an edge into another
   // class with the same ready time -- with exact ready times seeded (hseed)
@@ -377,7 +380,8 @@ __global__ void __launch_bounds__(256)
     for (uint32_t e = eb; e < ee; e += 4) {
       uint32_t ru[4];
 #pragma unroll
-      for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
+      for (int j = 0; j < 4; j++)
+        ru[j] = e + j < ee ? (erep ? erep[e + j] : rep[dst[e + j]]) : r;
       uint64_t c[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
@@ -922,7 +926,8 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
   k_kap_init<<<agg_blocks(V), B, 0, stream>>>(V, blocked.get(), rep.get(),
                                               seeded ? hseed.get() : nullptr,
                                               kap.get());
-  refresh_edge_rep(in);
+  if (!seeded) refresh_edge_rep(in);
+  const uint32_t *er = seeded ? nullptr : erep.get();
   if (!give_up_early) {
     // to the fixpoint: device-side convergence, no per-iteration read-back
     uint32_t launched = 0;
@@ -934,9 +939,9 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
       uint32_t *fl = cnt.ensure(V), *ps = pos.ensure(V + 1), *lo = order.ensure(V + 1);
       uint32_t *cf = conv.ensure(16);
       FH_HIP(hipMemsetAsync(cf, 0, sizeof(uint32_t), stream));
-      k_kap_relax<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(),
+      k_kap_relax<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, er, blocked.get(),
                                                    rep.get(), kap.get(), cf, kraise.get(), 1u, 0u,
-                                                   nullptr, nullptr, V, fl);
+                                                   nullptr, nullptr, V, fl, in.dst);
       launched = 1;
       exclusive_scan_u32(fl, ps, V, scan_ws, stream);
       k_compact<<<grid_for(V, B), B, 0, stream>>>(V, fl, ps, lo);
@@ -953,9 +958,9 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
       nl = h[1];
     }
     converge(1, launched, [&](uint32_t *changed, const uint32_t *prev) {
-      k_kap_relax<<<agg_blocks(nl), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(),
+      k_kap_relax<<<agg_blocks(nl), B, 0, stream>>>(V, in.off, in.stride, er, blocked.get(),
                                                     rep.get(), kap.get(), changed, kraise.get(),
-                                                    launched, 0u, prev, lst, nl, nullptr);
+                                                    launched, 0u, prev, lst, nl, nullptr, in.dst);
       FH_CHECK(launched < max_iters, FH_EINVARIANT, "kappa: no fixpoint");
     });
     iters = launched;
@@ -967,9 +972,9 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
   uint64_t r1 = 0, r2 = 0;
   for (uint32_t it = 0; it < max_iters; it++) {
     FH_HIP(hipMemsetAsync(scalars.get() + 16, 0, 8 * sizeof(uint32_t), stream));
-    k_kap_relax<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, erep.get(), blocked.get(), rep.get(),
+    k_kap_relax<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, er, blocked.get(), rep.get(),
                                                    kap.get(), scalars.get() + 16, kraise.get(), it + 1,
-                                                   7u, nullptr, nullptr, V, nullptr);
+                                                   7u, nullptr, nullptr, V, nullptr, in.dst);
     iters = it + 1;
     uint32_t c[8];
     fetch_u32(scalars.get() + 16, c, 8, stream);

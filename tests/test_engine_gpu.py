@@ -262,3 +262,42 @@ print("ok")
 """
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=200)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("delay", [False, True])
+def test_views_placement_strays_match_oracle(delay):
+    """Dependency-code placement (engine.hip place_codes) when the base hint
+    is wrong, so elements are placed directly as strays: a zero slack
+    (FH_PLACE_SLACK=0) makes every arrival ahead of the replicas' first
+    entries a stray, and with `delay` replica 1 receives its member events
+    after all of its coordinator events (its slices then span the whole
+    stream).  Small chunks (FH_VIEW_CHUNK); both are read once per process,
+    so the run is a child process.  Deps-only against the oracle's KeyDeps +
+    union."""
+    import subprocess, sys, os
+    code = f"""
+import numpy as np, sys
+sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+from fantoch_amd.engine import Engine
+from fantoch_amd.workload import Workload
+from oracle import oracle as O
+s = Workload.zipf(0.99, 4096, k=1, views=3, window=64, seed=5).generate(60_000)
+if {delay}:
+    t = s.fq_time.copy()
+    m = s.fq_proc == 1
+    m[:, 0] = False  # member events only: the coordinator's stay first
+    t[m] += np.uint64(1 << 39)
+    s.fq_time = t
+eng = Engine(s.key_space, n=5)
+eng.set_deps_only(True)
+eng.stage(s)
+eng.run()
+off, deps = eng.deps()
+o_off, o_deps = O.views_run(0, 5, s.dots, s.key_off(), s.keys.reshape(-1), s.fq_proc, s.fq_time)
+assert np.array_equal(off, o_off) and np.array_equal(deps, o_deps)
+print("ok")
+"""
+    env = dict(os.environ, FH_VIEW_CHUNK="20000", FH_PLACE_SLACK="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=200,
+                       env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
