@@ -255,6 +255,220 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Command-level KeyDeps over replica views (one key per command).
+//
+// The chunked path sorts every replica's elements: fq elements per command.
+// Here the commands are sorted once by key (stable, so each key's commands
+// stay in stream order) and every element finds its replica-local
+// predecessor among its key's neighbours in that order.  The search is
+// bounded by the logs' inversion span W: for each replica log,
+// W_r = max over positions of (largest command index seen so far - this
+// command), computed at staging, W = max_r W_r.  Then for two commands c, c'
+// that replica r both processes:
+//   c' <  c - W  =>  c' arrives at r before c;
+//   c' arrives at r before c  =>  c' <= c + W.
+// So the predecessor of (c, r) -- the latest arrival at r before c among the
+// key's commands (SequentialKeyDeps::add_cmd, sequential.rs:72-104) -- is
+// found scanning back until past (first r-command below c - W) - W, and
+// forward up to c + W; (c, r) is the key's last arrival at r (its tail:
+// latest_deps becomes c, :88-95) iff no r-command of the key arrives later,
+// which the same scans decide (any r-command beyond c + W arrives later).
+// Batches whose logs exceed kCmdMaxW take the chunked path.
+constexpr uint32_t kCmdMaxW = 4096;
+constexpr int kSrchThreads = 1024;
+constexpr uint32_t kRecT = 27;  // rec = replica << 27 | arrival position
+constexpr uint32_t kNoCmd = ~0u;
+
+struct LogOffs {
+  uint32_t off[kMaxLogs + 1];
+};
+
+// rec[e] for every element e = c·fq + j: which replica (log) holds it and at
+// which position of that log.  Element e sits at e / fq of the stream, so a
+// direct scatter from each log writes every line in fq pieces, far apart in
+// time (3.4 ms at C4).  Workgroup w instead takes the w-th slice of every
+// log -- commands ~[w·n/G, (w+1)·n/G) -- assembles their records in an LDS
+// window of kRecWin positions and writes the window out whole; an element
+// outside its window (a late arrival) is written directly.
+constexpr uint32_t kRecWin = 32768;   // 128 KB of LDS
+constexpr uint32_t kRecSlack = 2048;  // window positions below the slice's first command
+constexpr uint32_t kRecNone = ~0u;    // never a record (replica < 16)
+__global__ void __launch_bounds__(1024)
+    k_view_records(uint32_t n, uint32_t fq, uint32_t np, uint32_t G, LogOffs lo,
+                   const uint32_t *__restrict__ ent, uint32_t *__restrict__ rec) {
+  __shared__ uint32_t s_v[kRecWin];
+  const uint32_t w = blockIdx.x;
+  for (uint32_t p = threadIdx.x; p < kRecWin; p += 1024) s_v[p] = kRecNone;
+  const uint64_t c0 = uint64_t(n) * w / G;
+  const uint64_t e0 = c0 * fq > kRecSlack ? c0 * fq - kRecSlack : 0;
+  __syncthreads();
+  for (uint32_t r = 0; r < np; r++) {
+    const uint64_t len = lo.off[r + 1] - lo.off[r];
+    const uint32_t q0 = lo.off[r] + uint32_t(len * w / G), q1 = lo.off[r] + uint32_t(len * (w + 1) / G);
+    for (uint32_t q = q0 + threadIdx.x; q < q1; q += 1024) {
+      const uint32_t e = ent[q], v = (r << kRecT) | (q - lo.off[r]);
+      const uint64_t rel = uint64_t(e) - e0;
+      if (e >= e0 && rel < kRecWin)
+        s_v[rel] = v;
+      else
+        rec[e] = v;
+    }
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < kRecWin; p += 1024) {
+    const uint32_t v = s_v[p];
+    if (v != kRecNone) rec[e0 + p] = v;
+  }
+}
+
+// One thread per command in (key, command) order; a 1024-command tile of
+// keys, commands and view records staged in LDS with kSrchHalo neighbours on
+// either side (a scan that leaves them reads global memory: a chain of
+// dependent loads, so the halo keeps hot keys' tile-edge lanes in LDS).
+// Writes each element's dependency code (the chunked path's encoding) and a
+// per-command mask of the views it is the tail of.
+constexpr int kSrchHalo = 256;
+constexpr int kSrchSpan = kSrchThreads + 2 * kSrchHalo;
+__global__ void __launch_bounds__(kSrchThreads)
+    k_view_search(uint32_t n, uint32_t fq, uint32_t W, uint32_t K,
+                  const uint32_t *__restrict__ ks, const uint32_t *__restrict__ cs,
+                  const uint32_t *__restrict__ rec, const uint64_t *__restrict__ latest,
+                  uint32_t *__restrict__ code, uint8_t *__restrict__ tailm) {
+  __shared__ uint32_t s_k[kSrchSpan], s_c[kSrchSpan], s_r[kSrchSpan * 4];
+  const uint32_t tid = threadIdx.x, core = blockIdx.x * kSrchThreads, i = core + tid;
+  // staged span [lo, hi): the core and its halos, clipped to [0, n)
+  const uint32_t lo = core > uint32_t(kSrchHalo) ? core - kSrchHalo : 0u;
+  const uint32_t hi = min(n, core + kSrchThreads + kSrchHalo);
+  for (uint32_t x = lo + tid; x < hi; x += kSrchThreads) {
+    const uint32_t c = cs[x];
+    s_k[x - lo] = ks[x];
+    s_c[x - lo] = c;
+    for (uint32_t j = 0; j < fq; j++) s_r[(x - lo) * 4 + j] = rec[size_t(c) * fq + j];
+  }
+  __syncthreads();
+  if (i >= n) return;
+  const uint32_t base = lo, tile = hi - lo;
+  const uint32_t me = i - lo;
+  const uint32_t key = s_k[me], c = s_c[me];
+  constexpr uint32_t TM = (1u << kRecT) - 1;
+  uint32_t rj[4], tj[4], bt[4], bc[4], farc[4];
+  bool tail[4], doneB[4], doneF[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const bool v = uint32_t(j) < fq;
+    const uint32_t x = v ? s_r[me * 4 + j] : 0u;
+    rj[j] = v ? x >> kRecT : ~0u;
+    tj[j] = x & TM;
+    bt[j] = 0;
+    bc[j] = kNoCmd;
+    farc[j] = kNoCmd;
+    tail[j] = v;
+    doneB[j] = !v;
+    doneF[j] = !v;
+  }
+  // neighbour ip: key, command, view record j (LDS inside the tile)
+  auto nb = [&](uint32_t ip, uint32_t &kk, uint32_t &cc) {
+    if (ip - base < tile) {
+      kk = s_k[ip - base];
+      cc = s_c[ip - base];
+    } else {
+      kk = ks[ip];
+      cc = cs[ip];
+    }
+  };
+  auto nrec = [&](uint32_t ip, uint32_t cc, uint32_t j) {
+    return ip - base < tile ? s_r[(ip - base) * 4 + j] : rec[size_t(cc) * fq + j];
+  };
+  // backward: predecessors (and earlier commands arriving later: not tails)
+  for (uint32_t ip = i; ip-- > 0;) {
+    uint32_t kk, cc;
+    nb(ip, kk, cc);
+    if (kk != key) break;
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (!doneB[j] && farc[j] != kNoCmd && uint64_t(cc) + W < farc[j]) doneB[j] = true;
+      any |= !doneB[j];
+    }
+    if (!any) break;
+    for (uint32_t jj = 0; jj < fq; jj++) {
+      const uint32_t x = nrec(ip, cc, jj), r = x >> kRecT, t = x & TM;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (doneB[j] || r != rj[j]) continue;
+        if (t < tj[j]) {
+          if (bc[j] == kNoCmd || t > bt[j]) {
+            bt[j] = t;
+            bc[j] = cc;
+          }
+          if (farc[j] == kNoCmd && uint64_t(cc) + W < c) farc[j] = cc;
+        } else {
+          tail[j] = false;
+        }
+      }
+    }
+  }
+  // forward: earlier arrivals up to c + W, and later arrivals (not tails)
+  for (uint32_t ip = i + 1; ip < n; ip++) {
+    uint32_t kk, cc;
+    nb(ip, kk, cc);
+    if (kk != key) break;
+    const bool past = uint64_t(cc) > uint64_t(c) + W;
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (!doneF[j] && past && !tail[j]) doneF[j] = true;
+      any |= !doneF[j];
+    }
+    if (!any) break;
+    for (uint32_t jj = 0; jj < fq; jj++) {
+      const uint32_t x = nrec(ip, cc, jj), r = x >> kRecT, t = x & TM;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (doneF[j] || r != rj[j]) continue;
+        if (t < tj[j]) {
+          if (bc[j] == kNoCmd || t > bt[j]) {
+            bt[j] = t;
+            bc[j] = cc;
+          }
+        } else {
+          tail[j] = false;
+          if (past) doneF[j] = true;
+        }
+      }
+    }
+  }
+  uint32_t m = 0;
+  for (uint32_t j = 0; j < fq; j++) {
+    uint32_t cd;
+    if (bc[j] != kNoCmd) {
+      cd = bc[j] + 1;
+    } else {
+      const uint64_t x = latest[uint64_t(rj[j] + 1) * K + key];
+      cd = x ? (0x80000000u | uint32_t(x - kLogFlag)) : 0u;
+    }
+    code[size_t(c) * fq + j] = cd;
+    m |= tail[j] ? 1u << j : 0u;
+  }
+  tailm[i] = uint8_t(m);
+}
+
+// the tails become the replicas' latest entries (after every head's read)
+__global__ void k_view_tails(uint32_t n, uint32_t fq, uint32_t K, const uint32_t *__restrict__ ks,
+                             const uint32_t *__restrict__ cs, const uint32_t *__restrict__ rec,
+                             const uint8_t *__restrict__ tailm, uint64_t *__restrict__ latest,
+                             uint64_t log_base) {
+  GRID_STRIDE(i, n) {
+    const uint32_t m = tailm[i];
+    if (!m) continue;
+    const uint32_t c = cs[i], key = ks[i];
+    for (uint32_t j = 0; j < fq; j++)
+      if (m & (1u << j))
+        latest[uint64_t((rec[size_t(c) * fq + j] >> kRecT) + 1) * K + key] = kLogFlag | (log_base + c);
+  }
+}
+
 // Element dependency code (one u64 per element, command-major position e):
 // 0 = none, in-batch vid + 1 (< 2^48) for the previous element of its
 // segment, else the persistent latest entry of the segment at the head (a
@@ -882,6 +1096,9 @@ struct EngineDevice {
   DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
   DBuf<uint32_t> place_base;  // replica views: per-chunk smallest element position
+  DBuf<uint32_t> vrec;        // command-level views path: replica | arrival per element
+  DBuf<uint8_t> tailm;        // command-level views path: tail views per sorted command
+  std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
   bool deps_only = false;     // fh_engine_set_deps_only: stop after the committed deps
   bool last_deps_only = false;
   DBuf<unsigned long long> srcstats;
@@ -1120,6 +1337,7 @@ struct EngineDevice {
       lo.resize(nb * (np + 1));
       std::vector<uint8_t> seen(n);
       std::vector<int16_t> last_r(n);
+      h_win.assign(nb, 0);
       for (size_t b = 0; b < nb; b++) {
         std::fill(seen.begin(), seen.end(), 0);
         std::fill(last_r.begin(), last_r.end(), -1);
@@ -1129,8 +1347,11 @@ struct EngineDevice {
         for (size_t r = 0; r < np; r++) {
           lo[b * (np + 1) + r] = uint32_t(h_off[b * np + r] - base);
           FH_CHECK(h_off[b * np + r + 1] >= h_off[b * np + r], FH_EINVAL, "logs: offsets");
+          uint32_t pmax = 0;  // inversion span of this log (command-level path)
           for (uint64_t q = h_off[b * np + r]; q < h_off[b * np + r + 1]; q++) {
             const uint32_t c = h_cmd[q];
+            pmax = std::max(pmax, c);
+            h_win[b] = std::max(h_win[b], pmax - c);
             FH_CHECK(c < n, FH_EINVAL, "logs: command index >= n");
             FH_CHECK(last_r[c] != int16_t(r), FH_EINVAL,
                      "logs: a replica processes a command once");
@@ -1287,6 +1508,10 @@ struct EngineDevice {
       k_tail_engine<uint32_t><<<grid_for(M, B), B, 0, stream>>>(
           M, ks, vs, 0, S, latest.get(), uint64_t(lmul), uint64_t(lmask), nullptr, bbase);
       sorted_keys32 = ks;
+    } else if (cmd_views_ok(b, k, fq, n)) {
+      sv_fused = false;
+      cmd_views(b, n, fq, M, bkey, bbase);
+      mark("keydeps_views");
     } else {
       sv_fused = false;
       // every replica's KeyDeps over its arrival log, in chunks: chunk c
@@ -1415,6 +1640,51 @@ struct EngineDevice {
       FH_HIP(hipEventElapsedTime(ms, ev0, ev1));
     }
     if (profile) collect_times();
+  }
+
+  // The command-level views path (see k_view_search) applies to one key per
+  // command, fast quorums of <= 4, logs with an inversion span <= kCmdMaxW.
+  // Opt-in (FH_VIEW_CMD=1): bit-exact, but measured slower on C4 -- KeyDeps
+  // 13.8 ms against 12.8 chunked (records 1.1, command sort 1.6, search 10.4
+  // ms): the search touches ~3-4 random lines per command (its records in key
+  // order, the heads' latest entries, the scattered codes), more bytes than
+  // the chunked path's LDS-staged passes move.
+  bool cmd_views_ok(size_t b, uint32_t k, uint32_t fq, uint32_t n) const {
+    static const bool on = [] {
+      const char *e = getenv("FH_VIEW_CMD");
+      return e && *e == '1';
+    }();
+    return on && k == 1 && fq <= 4 && desc.nproc <= uint32_t(kMaxLogs) && b < h_win.size() &&
+           h_win[b] <= kCmdMaxW && n < (1u << kRecT);
+  }
+
+  void cmd_views(size_t b, uint32_t n, uint32_t fq, uint32_t M, const uint32_t *bkey,
+                 uint64_t bbase) {
+    const uint32_t np = desc.nproc;
+    LogOffs lo{};
+    const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
+    for (uint32_t r = 0; r <= np; r++) lo.off[r] = bl[r];
+    const uint32_t *bent = lent.get() + b * size_t(n) * fq;
+    uint32_t *rec = vrec.ensure(M + 1);
+    // ~9000 commands per workgroup: fq·9000 + slack positions fit the window
+    const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * kRecSlack) / fq);
+    const uint32_t G = std::max<uint32_t>(1, (n + per - 1) / per);
+    probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records, dim3(G), dim3(1024),
+                  stream, n, fq, np, G, lo, bent, rec);
+    uint32_t *ks = nullptr, *cs = nullptr;
+    sort_pairs<uint32_t, uint32_t>(bkey, nullptr, sk32a.ensure(n + 1), sva.ensure(n + 1),
+                                   sk32b.ensure(n + 1), svb.ensure(n + 1), n, key_bits, sort_ws,
+                                   stream, &ks, &cs);
+    uint8_t *tm = tailm.ensure(n + 1);
+    // reads the sorted keys and commands and the view records (one gather per
+    // command; neighbours from LDS), writes fq codes per command
+    probed_launch("view_search", double(n) * (4.0 + 4.0 + fq * 4.0 + fq * 4.0 + 1.0),
+                  k_view_search, dim3((n + kSrchThreads - 1) / kSrchThreads), dim3(kSrchThreads),
+                  stream, n, fq, h_win[b], uint32_t(key_space), (const uint32_t *)ks,
+                  (const uint32_t *)cs, (const uint32_t *)rec, (const uint64_t *)views_latest(),
+                  dep32.ensure(M + 1), tm);
+    k_view_tails<<<grid_for(n, B), B, 0, stream>>>(n, fq, uint32_t(key_space), ks, cs, rec, tm,
+                                                   views_latest(), bbase);
   }
 
   // The chunk's dependency codes -> dep32 through the placement pass: bucket

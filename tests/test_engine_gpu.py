@@ -301,3 +301,45 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=200,
                        env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_views_command_level_path_matches_oracle():
+    """The opt-in command-level KeyDeps path (FH_VIEW_CMD=1, engine.hip
+    k_view_search; read once per process: a child process): a C4-shaped
+    stream and a streamed multi-batch one, against the oracle."""
+    import subprocess, sys, os
+    code = f"""
+import numpy as np, sys
+sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+from fantoch_amd.engine import Engine
+from fantoch_amd.workload import Workload, Stream
+from oracle import oracle as O
+s = Workload.zipf(0.99, 1 << 16, k=1, views=3, window=64, seed=12).generate(120_000, logs=True)
+eng = Engine(s.key_space, n=5)
+eng.stage_logs([s])
+eng.run()
+r = eng.results()
+off, deps = O.views_run(0, 5, s.dots, s.key_off(), s.keys.reshape(-1), s.fq_proc, s.fq_time)
+ex, lab, kso, ks = O.graph_run(s.dots, s.key_off(), s.keys.reshape(-1), off, deps, s.key_space)
+assert np.array_equal(r["dep_off"], off) and np.array_equal(r["deps"], deps)
+assert np.array_equal(r["key_off"], kso) and np.array_equal(r["key_seq"], ks)
+w = Workload.zipf(0.99, 1 << 10, k=1, views=3, window=200, seed=13)
+parts = [w.generate(8000, first=i * 8000, logs=True) for i in range(3)]
+eng = Engine(w.key_space(), n=5)
+eng.stage_logs(parts)
+dots = np.concatenate([p.dots for p in parts]); keys = np.concatenate([p.keys for p in parts])
+proc = np.concatenate([p.fq_proc for p in parts])
+tim = np.concatenate([p.fq_time + np.uint64(i) * np.uint64(1 << 40) for i, p in enumerate(parts)])
+st = Stream(dots, keys, proc, tim, w.key_space())
+off, deps = O.views_run(0, 5, st.dots, st.key_off(), st.keys.reshape(-1), st.fq_proc, st.fq_time)
+got = []
+for i in range(3):
+    eng.run()
+    got.append(eng.results()["deps"])
+assert np.array_equal(np.concatenate(got), deps)
+print("ok")
+"""
+    env = dict(os.environ, FH_VIEW_CMD="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=200,
+                       env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
