@@ -334,12 +334,13 @@ __global__ void __launch_bounds__(kSrchThreads)
     k_view_search(uint32_t n, uint32_t fq, uint32_t W, uint32_t K,
                   const uint32_t *__restrict__ ks, const uint32_t *__restrict__ cs,
                   const uint32_t *__restrict__ rec, const uint64_t *__restrict__ latest,
-                  uint32_t *__restrict__ code, uint8_t *__restrict__ tailm) {
+                  uint32_t *__restrict__ code, uint8_t *__restrict__ tailm, uint32_t halo,
+                  uint32_t diag) {
   __shared__ uint32_t s_k[kSrchSpan], s_c[kSrchSpan], s_r[kSrchSpan * 4];
   const uint32_t tid = threadIdx.x, core = blockIdx.x * kSrchThreads, i = core + tid;
   // staged span [lo, hi): the core and its halos, clipped to [0, n)
-  const uint32_t lo = core > uint32_t(kSrchHalo) ? core - kSrchHalo : 0u;
-  const uint32_t hi = min(n, core + kSrchThreads + kSrchHalo);
+  const uint32_t lo = core > halo ? core - halo : 0u;
+  const uint32_t hi = min(n, core + kSrchThreads + halo);
   for (uint32_t x = lo + tid; x < hi; x += kSrchThreads) {
     const uint32_t c = cs[x];
     s_k[x - lo] = ks[x];
@@ -445,10 +446,10 @@ __global__ void __launch_bounds__(kSrchThreads)
     if (bc[j] != kNoCmd) {
       cd = bc[j] + 1;
     } else {
-      const uint64_t x = latest[uint64_t(rj[j] + 1) * K + key];
+      const uint64_t x = (diag & 1) ? 0ull : latest[uint64_t(rj[j] + 1) * K + key];
       cd = x ? (0x80000000u | uint32_t(x - kLogFlag)) : 0u;
     }
-    code[size_t(c) * fq + j] = cd;
+    if (!(diag & 2)) code[size_t(c) * fq + j] = cd;
     m |= tail[j] ? 1u << j : 0u;
   }
   tailm[i] = uint8_t(m);
@@ -1676,13 +1677,23 @@ struct EngineDevice {
                                    sk32b.ensure(n + 1), svb.ensure(n + 1), n, key_bits, sort_ws,
                                    stream, &ks, &cs);
     uint8_t *tm = tailm.ensure(n + 1);
+    // measurement knobs: FH_SRCH_HALO (<= kSrchHalo), FH_SRCH_DIAG (1: skip the
+    // latest reads, 2: skip the code writes -- diagnosis only, not bit-exact)
+    static const uint32_t srch_halo = [] {
+      const char *e = getenv("FH_SRCH_HALO");
+      return e ? std::min<uint32_t>(uint32_t(atol(e)), kSrchHalo) : uint32_t(kSrchHalo);
+    }();
+    static const uint32_t srch_diag = [] {
+      const char *e = getenv("FH_SRCH_DIAG");
+      return e ? uint32_t(atol(e)) : 0u;
+    }();
     // reads the sorted keys and commands and the view records (one gather per
     // command; neighbours from LDS), writes fq codes per command
     probed_launch("view_search", double(n) * (4.0 + 4.0 + fq * 4.0 + fq * 4.0 + 1.0),
                   k_view_search, dim3((n + kSrchThreads - 1) / kSrchThreads), dim3(kSrchThreads),
                   stream, n, fq, h_win[b], uint32_t(key_space), (const uint32_t *)ks,
                   (const uint32_t *)cs, (const uint32_t *)rec, (const uint64_t *)views_latest(),
-                  dep32.ensure(M + 1), tm);
+                  dep32.ensure(M + 1), tm, srch_halo, srch_diag);
     k_view_tails<<<grid_for(n, B), B, 0, stream>>>(n, fq, uint32_t(key_space), ks, cs, rec, tm,
                                                    views_latest(), bbase);
   }
