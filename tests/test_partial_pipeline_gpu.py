@@ -104,3 +104,39 @@ def test_deps_only_run_matches_full_run_deps():
     with pytest.raises(FhError):
         eng.results()  # labels / per-key output are not materialised
     eng.close()
+
+
+@pytest.mark.gpu
+def test_pipeline_over_rccl_world_one():
+    """PartialPipeline's collectives through a real RCCL group (world size 1 on
+    the one-GPU box: the all-to-all and all-gather are identities over RCCL),
+    HIP stages, against the oracle."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from fantoch_amd.partial import PartialPipeline
+    from oracle import oracle as O
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        s = stream()
+        out = PartialPipeline(0, 1, device=0).run(s)
+        dep_off, deps = O.views_run(0, 5, s.dots, s.key_off(), s.keys.reshape(-1), s.fq_proc,
+                                    s.fq_time)
+        ex, lab, kso, ks = O.graph_run(s.dots, s.key_off(), s.keys.reshape(-1), dep_off, deps,
+                                       s.key_space)
+        assert np.array_equal(out["dep_off"], dep_off) and np.array_equal(out["deps"], deps)
+        assert dict(zip(s.dots.tolist(), out["scc_label"].tolist())) == dict(
+            zip(ex.tolist(), lab.tolist()))
+        for key, seq in out["key_seq"].items():
+            assert seq == ks[kso[key]:kso[key + 1]].tolist(), key
+        assert len(out["key_seq"]) == len(np.unique(s.keys))
+    finally:
+        dist.destroy_process_group()
