@@ -630,9 +630,10 @@ static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint
                to.core + 4 * to.r0 <= kTileC && to.r0 >= 64,
            FH_EINVARIANT, "graph_tile: bad tile geometry");
   const uint32_t tiles = (V + to.core - 1) / to.core;
-  // algorithmic bytes: read the vertex's S edge slots and write rep, H, rank
-  // and group count (the context halo re-reads are overhead, not algorithmic)
-  const double bytes = double(V) * (4.0 * S + 16.0);
+  // algorithmic bytes: read the vertex's S edge slots and its dot (labels and
+  // dot tie-breaks), write rep, H, rank, group count and the label (the
+  // context halo re-reads are overhead, not algorithmic)
+  const double bytes = double(V) * (4.0 * S + 8.0 + 16.0 + 8.0);
   switch (S) {
     case 2:
       probed_launch("graph_tile", bytes, k_graph_tile<2>, dim3(tiles), dim3(kTileThreads),
