@@ -146,6 +146,30 @@ def device_route(keys, rec_cmd, rec_dep, world: int):
     return rec_cmd[order], rec_dep[order], counts, owner
 
 
+def exchange_records(group, world: int, dest: np.ndarray, cmd: np.ndarray, dep: np.ndarray):
+    """All-to-all of (command, dep) records by destination shard (RCCL on
+    GPUs, gloo on CPU): counts first, then the records."""
+    import torch
+    import torch.distributed as dist
+
+    order = np.argsort(dest, kind="stable")
+    cmd, dep = cmd[order], dep[order]
+    send = np.bincount(dest, minlength=world).astype(np.int64)
+    on_gpu = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    sc = torch.from_numpy(send).to(dev)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv = rc.cpu().numpy()
+    payload = torch.from_numpy(np.stack([cmd.astype(np.int64),
+                                         dep.astype(np.uint64).view(np.int64)], 1)).to(dev)
+    out = torch.empty((int(recv.sum()), 2), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(out, payload, output_split_sizes=recv.tolist(),
+                           input_split_sizes=send.tolist(), group=group)
+    out = out.cpu().numpy()
+    return out[:, 0], out[:, 1].view(np.uint64)
+
+
 class PartialShard:
     """One shard (one process, one GPU) of the partial-replication engine.
 
@@ -168,26 +192,7 @@ class PartialShard:
         self.device = device
 
     def _exchange(self, dest: np.ndarray, cmd: np.ndarray, dep: np.ndarray):
-        """All-to-all of (command, dep) records by destination shard."""
-        import torch
-        import torch.distributed as dist
-
-        order = np.argsort(dest, kind="stable")
-        cmd, dep = cmd[order], dep[order]
-        send = np.bincount(dest, minlength=self.world).astype(np.int64)
-        on_gpu = dist.get_backend(self.group) == "nccl"
-        dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
-        sc = torch.from_numpy(send).to(dev)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=self.group)
-        recv = rc.cpu().numpy()
-        payload = torch.from_numpy(np.stack([cmd.astype(np.int64),
-                                             dep.astype(np.uint64).view(np.int64)], 1)).to(dev)
-        out = torch.empty((int(recv.sum()), 2), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(out, payload, output_split_sizes=recv.tolist(),
-                               input_split_sizes=send.tolist(), group=self.group)
-        out = out.cpu().numpy()
-        return out[:, 0], out[:, 1].view(np.uint64)
+        return exchange_records(self.group, self.world, dest, cmd, dep)
 
     def step_device(self, dots, keys):
         """step() with the batch and every stage in HBM (dots[n], keys[n, k]:
@@ -264,6 +269,8 @@ def pseudo_stream(s, rank: int, world: int):
     command's pseudo commands where it lists the command."""
     from .workload import Stream
 
+    if s.log_cmd is None or s.log_off is None:
+        raise ValueError("pseudo_stream: the stream needs its replica logs (generate(logs=True))")
     fq = s.views
     mine = s.keys % np.uint64(world) == np.uint64(rank)
     c, t = np.nonzero(mine)  # command order, then key slot order
@@ -406,8 +413,6 @@ class PartialPipeline:
         self.keydeps = keydeps if keydeps is not None else hip_views_keydeps(device, nproc)
         self.union = union if union is not None else hip_union(device)
         self.order = order if order is not None else hip_order(device)
-        self._ex = PartialShard.__new__(PartialShard)
-        self._ex.rank, self._ex.world, self._ex.group = rank, world, group
 
     def run(self, s):
         """One stream with replica logs (every rank holds the same stream).
@@ -418,7 +423,7 @@ class PartialPipeline:
         pofs, pdeps = self.keydeps(ps)
         rec_cmd, rec_dep = pseudo_records(p2c, s.dots, pofs, pdeps)
         owner = command_owner(s.keys, self.world)
-        g_cmd, g_dep = self._ex._exchange(owner[rec_cmd], rec_cmd, rec_dep)
+        g_cmd, g_dep = exchange_records(self.group, self.world, owner[rec_cmd], rec_cmd, rec_dep)
         owned = np.nonzero(owner == self.rank)[0]
         pos = np.searchsorted(owned, g_cmd)
         odo, odeps = self.union(len(owned), pos, g_dep)
