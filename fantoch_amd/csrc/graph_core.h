@@ -82,6 +82,8 @@ struct GraphOutput {
   bool src_stats_done = false;    // src_mx / src_cnt accumulated
 };
 
+struct TileOut;  // graph_tile.hip
+
 struct GraphCore {
   hipStream_t stream = nullptr;
   SortWorkspace sort_ws;
@@ -93,6 +95,9 @@ struct GraphCore {
   DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c, pk_da, pk_db;
   DBuf<uint8_t> blocked;
   DBuf<uint32_t> t_h, t_rank, t_cnt, t_start;
+  DBuf<uint8_t> t_fail;     // graph_tile mixed bounds: pass-1 failed tiles
+  DBuf<uint32_t> t_cores;   // graph_tile mixed bounds: pass-2 cores (start, length)
+  uint32_t dbg_mixed_redo = 0;
   DBuf<uint64_t> t_prof;  // tile path: ready time, group rank/count/start
   uint32_t dbg_tile_fail = 0, dbg_tile_ok = 0;
   DBuf<uint8_t> fb_pushed;    // coloring reach: vertices that pushed this round
@@ -133,6 +138,7 @@ struct GraphCore {
   // tile-local path (graph_tile.hip): false = certificate failed, nothing set
   bool tiles_eligible(const GraphInput &in) const;
   bool run_tiles(const GraphInput &in, GraphOutput &out);
+  bool tiles_mixed(const GraphInput &in, TileOut &to, uint32_t r2, uint32_t *st);
 };
 
 }  // namespace fh

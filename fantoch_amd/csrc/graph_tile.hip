@@ -52,6 +52,7 @@ constexpr int kTileThreads = 1024;
 constexpr int kTileC = 10240;  // max context vertices (LDS: 15 B per vertex)
 constexpr uint16_t kNone = 0xFFFF;
 constexpr int kMaxCore = 8;     // core vertices per thread (T <= 8192)
+constexpr uint32_t kMixR1 = 512;  // pass-1 reach bound of the mixed tiling
 
 // R0 rounded up to a multiple of 64 (at least 256)
 static uint32_t round_r0(uint32_t x) { return std::max<uint32_t>(256, (x + 63) & ~63u); }
@@ -125,6 +126,10 @@ __device__ __forceinline__ uint16_t lds_xchg_u16(uint16_t *p, uint16_t v) {
   }
 }
 
+}  // namespace
+
+// graph_tile's outputs and launch parameters (named: GraphCore::tiles_mixed
+// takes it)
 struct TileOut {
   uint32_t *rep;     // [V] global vid of the SCC's min member
   uint64_t *label;   // [V] min dot of the SCC
@@ -135,6 +140,8 @@ struct TileOut {
                      // [2] core vertices over R0, [3] long forward edges,
                      // [4] max H sweeps, [5] max SCC rounds, [6] max group
   const uint8_t *redo;  // [tiles] or null: only tiles with redo[t] run
+  const uint32_t *cores;  // [2·tiles] or null: tile t's core is [cores[2t], + cores[2t+1])
+  uint8_t *failf;         // [tiles] or null: 1 for each tile whose certificate fails
   unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
   int r0;      // certified reach bound R0 (L = 2·R0)
   int core;    // core vertices per tile T (T + 2L <= kTileC, T <= kMaxCore·1024)
@@ -143,6 +150,9 @@ struct TileOut {
                // its later ones in the same sweep), 2 = the same in batches of
                // 5 vertices per lane (loads first), 0 = block-strided
 };
+
+namespace {
+
 
 // One tile: core [a, a + T), context [a - L, a + T + L) with L = 2·R0 and
 // T + 2L <= kTileC.
@@ -173,8 +183,8 @@ __global__ void __launch_bounds__(kTileThreads)
       t_last = now;
     }
   };
-  const uint32_t a = blockIdx.x * uint32_t(T);
-  const uint32_t b = min(V, a + uint32_t(T));
+  const uint32_t a = out.cores ? out.cores[2 * blockIdx.x] : blockIdx.x * uint32_t(T);
+  const uint32_t b = min(V, a + (out.cores ? out.cores[2 * blockIdx.x + 1] : uint32_t(T)));
   const uint32_t lo = a > uint32_t(L) ? a - L : 0u;
   const uint32_t hi = min(V, b + uint32_t(L));
   const int C = int(hi - lo);
@@ -324,6 +334,7 @@ __global__ void __launch_bounds__(kTileThreads)
     if (s_long) atomicAdd(&out.stat[3], s_long);
     atomicMax(&out.stat[4], uint32_t(hs));
     if (s_over || s_long) atomicAdd(&out.stat[0], 1u);
+    if ((s_over || s_long) && out.failf) out.failf[blockIdx.x] = 1;
   }
   if (s_over || s_long) return;
 
@@ -407,7 +418,10 @@ __global__ void __launch_bounds__(kTileThreads)
   int round = 0;
   for (; left; round++) {
     if (round >= 64) {  // adversarial nesting: leave it to the global path
-      if (tid == 0) atomicAdd(&out.stat[0], 1u);
+      if (tid == 0) {
+        atomicAdd(&out.stat[0], 1u);
+        if (out.failf) out.failf[blockIdx.x] = 1;
+      }
       return;
     }
     for (uint32_t i = tid; i < nraised; i += kTileThreads) {
@@ -625,15 +639,18 @@ __global__ void k_exec_from_groups(uint32_t V, const uint32_t *__restrict__ hgrp
 }  // namespace
 
 static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint64_t *dot,
-                         const TileOut &to, hipStream_t stream) {
+                         const TileOut &to, hipStream_t stream, uint32_t ncores = 0,
+                         bool count_bytes = true) {
   FH_CHECK(to.core >= 1024 && to.core <= kMaxCore * kTileThreads &&
                to.core + 4 * to.r0 <= kTileC && to.r0 >= 64,
            FH_EINVARIANT, "graph_tile: bad tile geometry");
-  const uint32_t tiles = (V + to.core - 1) / to.core;
+  const uint32_t tiles = to.cores ? ncores : (V + to.core - 1) / to.core;
+  if (tiles == 0) return;
   // algorithmic bytes: read the vertex's S edge slots and its dot (labels and
   // dot tie-breaks), write rep, H, rank, group count and the label (the
-  // context halo re-reads are overhead, not algorithmic)
-  const double bytes = double(V) * (4.0 * S + 8.0 + 16.0 + 8.0);
+  // context halo re-reads are overhead, not algorithmic; so is a redo pass
+  // over cores already ordered once: count_bytes = false)
+  const double bytes = count_bytes ? double(V) * (4.0 * S + 8.0 + 16.0 + 8.0) : 0.0;
   switch (S) {
     case 2:
       probed_launch("graph_tile", bytes, k_graph_tile<2>, dim3(tiles), dim3(kTileThreads),
@@ -644,6 +661,85 @@ static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint
                     stream, V, dst, dot, to);
       break;
   }
+}
+
+// Mixed reach bounds.  Pass 1 runs every tile at R1 = kMixR1 (T1 = 8192);
+// pass 2 reruns, at R2 (T2 = kTileC - 4·R2), the cores of every failed tile
+// and of its two neighbours.  Why the kept tiles are right: with global
+// excess < R2 (pass 2's certificate, below), a vertex whose excess is >= R1
+// climbs through the lowest vertex y of its climbing path, whose own tile
+// (or the tile of a long forward edge within R1 above y) sees the climb in
+// its context and fails; so such vertices lie less than R1 + R2 above a
+// failed core.  A kept tile's proof (file header, at R1) needs excess < R1
+// on [a - R1, b + R1), no climb back from below a - L1 (a vertex there with
+// excess > L1 - R1 = R1 would lie within R1 + R2 above a failed core, i.e.
+// within 2·R1 + 2·R2 <= 5120 below a), and its ready groups' members within
+// R1 below their roots (members of excess >= R1 again lie near a failed
+// core); a neighbour on each side keeps every failed core >= T1 = 8192 away.
+// Pass 2's proof at R2 needs excess < R2 everywhere: the lowest vertex with
+// excess >= R2 would be seen by its own tile -- a pass-2 tile (fails the
+// pass, and the run falls back to uniform bounds) or a kept tile, which sees
+// its climb past R1 inside its context and would have failed in pass 1.
+// Forward spans: kept tiles certify < L1 - R1 = R1 < R2.  Each pass writes
+// only certified cores; pass 2 overwrites its cores.
+bool GraphCore::tiles_mixed(const GraphInput &in, TileOut &to, uint32_t r2, uint32_t *st) {
+  const uint32_t V = in.V;
+  const uint32_t r1 = kMixR1;
+  uint32_t *stat = to.stat;
+  to.r0 = int(r1);
+  to.core = std::min(kTileC - 4 * int(r1), kMaxCore * kTileThreads);
+  const uint32_t t1 = uint32_t(to.core), tiles1 = (V + t1 - 1) / t1;
+  uint8_t *ff = t_fail.ensure(tiles1 + 1);
+  FH_HIP(hipMemsetAsync(ff, 0, tiles1, stream));
+  FH_HIP(hipMemsetAsync(stat, 0, 7 * sizeof(uint32_t), stream));
+  if (to.prof) FH_HIP(hipMemsetAsync(to.prof, 0, 8 * sizeof(unsigned long long), stream));
+  to.failf = ff;
+  to.cores = nullptr;
+  launch_tiles(V, in.stride, in.dst, in.dot, to, stream);
+  fetch_u32(stat, st, 7, stream);
+  to.failf = nullptr;
+  if (st[0] == 0) return true;
+  // the pass-2 bound: the requested one, at least what pass 1 saw
+  r2 = std::max(r2, round_r0(st[1] + st[1] / 32 + 16));
+  if (r2 > 2048) return false;
+  std::vector<uint8_t> hf(tiles1);
+  FH_HIP(hipMemcpyAsync(hf.data(), ff, tiles1, hipMemcpyDeviceToHost, stream));
+  FH_HIP(hipStreamSynchronize(stream));
+  std::vector<uint8_t> redo(tiles1, 0);
+  for (uint32_t t = 0; t < tiles1; t++)
+    if (hf[t])
+      for (int d = -1; d <= 1; d++)
+        if (int64_t(t) + d >= 0 && int64_t(t) + d < int64_t(tiles1)) redo[t + d] = 1;
+  const uint32_t t2 = uint32_t(std::min(kTileC - 4 * int(r2), kMaxCore * kTileThreads));
+  std::vector<uint32_t> cores;
+  for (uint32_t t = 0; t < tiles1;) {
+    if (!redo[t]) {
+      t++;
+      continue;
+    }
+    uint32_t e = t;
+    while (e < tiles1 && redo[e]) e++;
+    const uint32_t lo = t * t1, hi = std::min(V, e * t1);
+    for (uint32_t x = lo; x < hi; x += t2) {
+      cores.push_back(x);
+      cores.push_back(std::min(t2, hi - x));
+    }
+    t = e;
+  }
+  uint32_t *dc = t_cores.ensure(cores.size() + 1);
+  FH_HIP(hipMemcpyAsync(dc, cores.data(), cores.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                        stream));
+  const uint32_t pass1_max = st[1];
+  FH_HIP(hipMemsetAsync(stat, 0, 7 * sizeof(uint32_t), stream));
+  to.r0 = int(r2);
+  to.core = int(t2);
+  to.cores = dc;
+  launch_tiles(V, in.stride, in.dst, in.dot, to, stream, uint32_t(cores.size() / 2), false);
+  fetch_u32(stat, st, 7, stream);
+  to.cores = nullptr;
+  dbg_mixed_redo = uint32_t(cores.size() / 2);
+  st[1] = std::max(st[1], pass1_max);
+  return st[0] == 0;
 }
 
 bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
@@ -657,6 +753,8 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.gcount = t_cnt.ensure(V + 1);
   to.stat = stat;
   to.redo = nullptr;
+  to.cores = nullptr;
+  to.failf = nullptr;
   static const int hblock = getenv("FH_TILE_HBLOCK") ? atoi(getenv("FH_TILE_HBLOCK")) : 1;
   to.hblock = hblock;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
@@ -674,6 +772,20 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   uint32_t st[7] = {0, 0, 0, 0, 0, 0, 0};
   static const uint32_t r0_env = getenv("FH_TILE_R0") ? uint32_t(atoi(getenv("FH_TILE_R0"))) : 0;
   uint32_t r0 = r0_env ? round_r0(r0_env) : tile_r0;  // (env: first bound, measurement)
+  // mixed bounds (FH_TILE_MIXED=0: off): when the last run needed a bound
+  // above kMixR1, every tile first runs at kMixR1 (longer cores) and only the
+  // failed tiles and their neighbours run again at the larger bound
+  static const bool mixed_on = [] {
+    const char *e = getenv("FH_TILE_MIXED");
+    return !(e && *e == '0');
+  }();
+  if (mixed_on && !r0_env && tile_r0 > kMixR1) {
+    dbg_mixed_redo = 0;
+    ok = tiles_mixed(in, to, tile_r0, st);
+    if (debug)
+      fprintf(stderr, "fh graph_tile mixed: V=%u R1=%u R2=%u redo_cores=%u ok=%d max_excess=%u\n", V,
+              kMixR1, uint32_t(to.r0), dbg_mixed_redo, int(ok), st[1]);
+  }
   for (int attempt = 0; attempt < 4 && !ok; attempt++) {
     to.r0 = int(r0);
     to.core = std::min(kTileC - 4 * int(r0), kMaxCore * kTileThreads);
