@@ -89,20 +89,32 @@ constexpr uint32_t kPlaceSpan = 1u << kPlaceShift;
 constexpr uint32_t kPlaceSlack = 1u << 16;  // default (FH_PLACE_SLACK): arrivals ahead of earlier commands
 constexpr uint32_t kPlaceNone = ~0u;        // never a code (log references < 2^31 - 1)
 
-// emin (may be null): the placement base of the chunk
-__global__ void k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, LogChunk ch,
-                           const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
-                           uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
-                           uint32_t *__restrict__ emin, uint32_t slack) {
-  GRID_STRIDE(x, M) {
+// emin (may be null): the placement base of the chunk.  One workgroup per
+// sort tile (kTile consecutive elements): it also writes the tile's 8-bit
+// digit counts at shift 0 for the sort's first pass (sort_pairs_counted: no
+// separate counting pass over the keys it just wrote).
+__global__ void __launch_bounds__(kThreads)
+    k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, LogChunk ch,
+               const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
+               uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+               uint32_t *__restrict__ emin, uint32_t slack, uint32_t *__restrict__ counts) {
+  __shared__ uint32_t s_h[256];
+  s_h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(M, base + uint32_t(kTile));
+  for (uint32_t x = base + threadIdx.x; x < end; x += kThreads) {
     uint32_t r = 0;
     while (r + 1 < nlog && x >= ch.cum[r + 1]) r++;
     const uint32_t y = x - ch.cum[r];
     const uint32_t q = ch.first[r] + y / k, s = y % k;
     const uint32_t e = ent[q];
-    keys[x] = (r + 1) * K + key32[(e / fq) * k + s];
+    const uint32_t key = (r + 1) * K + key32[(e / fq) * k + s];
+    keys[x] = key;
     vals[x] = e * k + s;
+    atomicAdd(&s_h[key & 255], 1u);
   }
+  __syncthreads();
+  counts[size_t(blockIdx.x) * 256 + threadIdx.x] = s_h[threadIdx.x];
   // placement base: the smallest first entry of the replicas' slices, less a
   // slack for entries that arrive before earlier commands.  Only a hint (see
   // above).  An exact minimum by atomics serialised the kernel on one word:
@@ -1599,12 +1611,14 @@ struct EngineDevice {
         // gather move into both pass-0 kernels, which are compute bound
         static const bool fused = getenv("FH_LOG_FUSED") != nullptr;
         if (!fused) {
-          probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys,
-                        dim3(grid_for(Mc, B)), dim3(B), stream, Mc, k, fq, np, lc, bent, bkey,
+          const uint32_t tiles = (Mc + kTile - 1) / kTile;
+          sort_ws.prepare(tiles, 1, stream);
+          probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys, dim3(tiles),
+                        dim3(kThreads), stream, Mc, k, fq, np, lc, bent, bkey,
                         uint32_t(key_space), lk, lv, place ? pbase + c : (uint32_t *)nullptr,
-                        place_slack);
-          sort_pairs<uint32_t, uint32_t>(lk, lv, lk, lv, bkb.ensure(Mc + 1), bvb.ensure(Mc + 1),
-                                         Mc, bits, sort_ws, stream, &ks, &vs);
+                        place_slack, sort_ws.meta.get());
+          sort_pairs_counted<uint32_t, uint32_t>(lk, lv, bkb.ensure(Mc + 1), bvb.ensure(Mc + 1),
+                                                 Mc, bits, sort_ws, stream, &ks, &vs);
         } else {
           const LogSrc src{k, fq, np, uint32_t(key_space), lc, bent, bkey};
           sort_pairs_src<uint32_t, uint32_t, LogSrc>(src, lk, lv, bkb.ensure(Mc + 1),

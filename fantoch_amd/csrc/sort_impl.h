@@ -320,7 +320,7 @@ struct ArraySrc {
 template <class K, class VT, int DB, class Src>
 void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tiles,
                uint32_t groups, uint32_t *counts, uint32_t *gsum, uint32_t *dbase, hipStream_t s,
-               bool probe) {
+               bool probe, bool have_counts = false) {
   // tile counts by LDS atomics (FH_SORT_UP_ATOMIC=0: wave64 ballot matching).
   // Measured on C4 (Zipf 0.99, 20-bit keys): KeyDeps 15.44 -> 14.98 ms,
   // per-key 3.40 -> 3.32 -- the 8 ballots per item cost more than the
@@ -331,7 +331,8 @@ void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tile
     const char *e = getenv("FH_SORT_UP_ATOMIC");
     return e && *e == '0' ? 0 : 1;
   }();
-  k_up<K, VT, DB, Src><<<tiles, kThreads, 0, s>>>(src, uint32_t(n), shift, counts, atomic_up);
+  if (!have_counts)  // (else the producer of the input wrote the tile counts)
+    k_up<K, VT, DB, Src><<<tiles, kThreads, 0, s>>>(src, uint32_t(n), shift, counts, atomic_up);
   uint32_t gsize = kGroup;
   if (DB == 8 && tiles <= kFusedMaxTiles) {
     gsize = (tiles + 3) / 4;
@@ -359,7 +360,7 @@ void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tile
 template <class K, class VT, int DB, class Src0>
 void sort_passes(const Src0 &src0, bool probe0, K *ka, VT *va, K *kb, VT *vb, bool alias_a,
                  size_t n, int passes, int db, SortWorkspace &ws, hipStream_t s, K **kout,
-                 VT **vout) {
+                 VT **vout, bool counts0 = false) {
   const uint32_t tiles = uint32_t((n + kTile - 1) / kTile);
   const uint32_t groups = (tiles + kGroup - 1) / kGroup;
   ws.prepare(tiles, passes, s);
@@ -369,7 +370,8 @@ void sort_passes(const Src0 &src0, bool probe0, K *ka, VT *va, K *kb, VT *vb, bo
   uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
   K *ko = alias_a ? kb : ka;
   VT *vo = alias_a ? vb : va;
-  sort_pass<K, VT, DB, Src0>(src0, ko, vo, n, 0, tiles, groups, counts, gsum, dbase, s, probe0);
+  sort_pass<K, VT, DB, Src0>(src0, ko, vo, n, 0, tiles, groups, counts, gsum, dbase, s, probe0,
+                            counts0);
   const K *ki = ko;
   const VT *vi = vo;
   for (int p = 1; p < passes; p++) {
@@ -402,6 +404,25 @@ void sort_pairs_src(const Src &src, K *ka, VT *va, K *kb, VT *vb, size_t n, int 
     return;
   }
   sort_passes<K, VT, 8, Src>(src, true, ka, va, kb, vb, false, n, passes, db, ws, s, kout, vout);
+}
+
+// sort_pairs of (ka, va) whose pass-0 tile digit counts (8-bit digits at
+// shift 0, tiles of kTile consecutive elements, counts[tile][256] in
+// ws.meta after ws.prepare(tiles)) were written by the kernel that produced
+// the input; result in (ka, va) or (kb, vb).
+template <class K, class VT>
+void sort_pairs_counted(K *ka, VT *va, K *kb, VT *vb, size_t n, int key_bits, SortWorkspace &ws,
+                        hipStream_t s, K **kout, VT **vout) {
+  FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "sort: too many elements (>= 2^30)");
+  int passes = std::max(1, (key_bits + 7) / 8);
+  if (passes > int(sizeof(K))) passes = int(sizeof(K));
+  if (n == 0) {
+    *kout = ka;
+    *vout = va;
+    return;
+  }
+  sort_passes<K, VT, 8, ArraySrc<K, VT, false>>(ArraySrc<K, VT, false>{ka, va}, true, ka, va, kb,
+                                                 vb, true, n, passes, 8, ws, s, kout, vout, true);
 }
 
 }  // namespace
