@@ -343,3 +343,24 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=200,
                        env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("window,seed", [(64, 21), (80, 22)])
+def test_views_mixed_tile_bounds_match_oracle(window, seed):
+    """The tile kernel's mixed reach bounds (graph_tile.hip tiles_mixed):
+    wider reorder windows raise the maximum excess, so more pass-1 tiles fail
+    at R0 = 512 and pass 2 reruns them (and their neighbours) at a larger
+    bound.  Twice on one engine: the first run starts from the default bound,
+    the second from the one the first run measured."""
+    s = Workload.zipf(0.99, 1 << 16, k=1, views=3, window=window, seed=seed).generate(200_000)
+    dep_off, deps, ex, lab, kso, ks = oracle_pipeline(s)
+    eng = Engine(s.key_space, n=5)
+    eng.stage(s)
+    want_label = dict(zip(ex.tolist(), lab.tolist()))
+    for _ in range(2):
+        eng.rewind()
+        eng.run()
+        r = eng.results()
+        assert np.array_equal(r["dep_off"], dep_off) and np.array_equal(r["deps"], deps)
+        assert dict(zip(s.dots.tolist(), r["scc_label"].tolist())) == want_label
+        assert np.array_equal(r["key_off"], kso) and np.array_equal(r["key_seq"], ks)
