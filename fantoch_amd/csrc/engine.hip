@@ -156,6 +156,12 @@ struct PrevSrc {
 // consecutive tiles in one bucket are adjacent in the output, so a bucket's
 // run per workgroup averages 16 elements (64 B per array) instead of 8 --
 // 4096-element workgroups wrote 32 B runs, half-line writes.
+// With `defer` set the pass also makes the segment tails the latest entries
+// (k_tail_engine's job): every head of the workgroup has read its latest
+// entry before the barrier, so the tail of a segment that starts in the
+// workgroup is written in place; the tail of the first segment, if it began
+// in an earlier workgroup (whose head may not have read yet), goes to
+// defer[2·b] = (segment, command) for k_tail_defer.
 constexpr int kBucketThreads = 512;
 constexpr int kBucketWaves = kBucketThreads / 64;
 constexpr int kBucketTile = 2 * kTile;  // 8192
@@ -163,8 +169,10 @@ __global__ void __launch_bounds__(kBucketThreads)
     k_bucket_codes(PrevSrc src, uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                    uint32_t n, const uint32_t *__restrict__ counts,
                    const uint32_t *__restrict__ gsum, uint32_t gsize,
-                   const uint32_t *__restrict__ dbase) {
+                   const uint32_t *__restrict__ dbase, uint64_t *latest_w,  // aliases src.latest
+                   uint64_t log_base, uint32_t *__restrict__ defer) {
   constexpr uint32_t R = kPlaceBuckets;
+  __shared__ uint32_t s_def[2];
   static_assert(R == kBucketThreads, "one bucket per thread in the scan");
   __shared__ uint32_t s_k[kBucketTile], s_v[kBucketTile];
   __shared__ uint32_t s_cnt[R], s_dex[R], s_gb[R];
@@ -177,7 +185,7 @@ __global__ void __launch_bounds__(kBucketThreads)
   // all loads first: the element's key and position, its predecessor's,
   // then the latest entries of the segment heads
   const uint32_t eb = *src.ebase;
-  uint32_t key[kItems], val[kItems], seg[kItems], pseg[kItems], pv[kItems];
+  uint32_t key[kItems], val[kItems], seg[kItems], pseg[kItems], pv[kItems], nseg[kItems];
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
@@ -187,6 +195,21 @@ __global__ void __launch_bounds__(kBucketThreads)
     pseg[i] = ok && idx > 0 ? src.ks[idx - 1] : ~0u;
     pv[i] = ok && idx > 0 ? src.vs[idx - 1] : 0u;
   }
+  if (defer) {
+    // the next element's segment: lane + 1 of the same item, lane 0 of the
+    // next item for lane 63, a load for the wave's last element only
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+      const uint32_t up = __shfl_down(seg[i], 1, 64);
+      const uint32_t nx = i + 1 < kItems ? __shfl(seg[i + 1 < kItems ? i + 1 : i], 0, 64) : 0u;
+      const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
+      nseg[i] = lane < 63 ? up : nx;
+      if (idx + 1 >= n) nseg[i] = ~0u;
+      else if (lane == 63 && i + 1 == kItems) nseg[i] = src.ks[idx + 1];
+    }
+  }
+  const uint32_t first_seg = defer && base > 0 ? src.ks[base - 1] : ~0u;
+  if (defer && tid == 0) s_def[0] = ~0u;
   uint64_t lat[kItems];
 #pragma unroll
   for (int i = 0; i < kItems; i++) lat[i] = pseg[i] != seg[i] ? src.latest[seg[i]] : 0ull;
@@ -195,6 +218,21 @@ __global__ void __launch_bounds__(kBucketThreads)
     val[i] = pseg[i] != seg[i] ? (lat[i] ? (0x80000000u | uint32_t(lat[i] - kLogFlag)) : 0u)
                                : pv[i] / src.per_cmd + 1;
   __syncthreads();
+  if (defer) {
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+      const uint32_t idx = base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
+      if (idx < n && nseg[i] != seg[i]) {
+        const uint32_t cmd = (key[i] + eb) / src.per_cmd;
+        if (seg[i] == first_seg) {
+          s_def[0] = seg[i];
+          s_def[1] = cmd;
+        } else {
+          latest_w[seg[i]] = kLogFlag | (log_base + cmd);
+        }
+      }
+    }
+  }
   uint32_t rank[kItems];
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
@@ -230,6 +268,10 @@ __global__ void __launch_bounds__(kBucketThreads)
     }
   }
   __syncthreads();
+  if (defer && tid == 0) {
+    defer[2 * blockIdx.x] = s_def[0];
+    defer[2 * blockIdx.x + 1] = s_def[1];
+  }
   const uint32_t tile_n = min(uint32_t(kBucketTile), n - base);
 #pragma unroll 4
   for (uint32_t j = tid; j < tile_n; j += kBucketThreads) {
@@ -238,6 +280,15 @@ __global__ void __launch_bounds__(kBucketThreads)
     const uint32_t o = s_gb[d] + (j - s_dex[d]);
     kout[o] = kk;
     vout[o] = s_v[j];
+  }
+}
+
+// the deferred tails of k_bucket_codes (after every head has read)
+__global__ void k_tail_defer(uint32_t nb, const uint32_t *__restrict__ defer,
+                             uint64_t *__restrict__ latest, uint64_t log_base) {
+  GRID_STRIDE(b, nb) {
+    const uint32_t seg = defer[2 * b];
+    if (seg != ~0u) latest[seg] = kLogFlag | (log_base + defer[2 * b + 1]);
   }
 }
 
@@ -1113,6 +1164,7 @@ struct EngineDevice {
   DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
   DBuf<uint32_t> place_base;  // replica views: per-chunk smallest element position
+  DBuf<uint32_t> tail_defer;  // k_bucket_codes: deferred (segment, command) per workgroup
   DBuf<uint32_t> vrec;        // command-level views path: replica | arrival per element
   DBuf<uint8_t> tailm;        // command-level views path: tail views per sorted command
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
@@ -1566,8 +1618,9 @@ struct EngineDevice {
       // the chunk's elements are replica-major, so a stable sort by the key
       // alone already leaves every (replica, key) segment contiguous and in
       // arrival order ((key, replica, arrival) order): with K a power of two
-      // the key is the composite's low bits (2 passes of 10-bit digits at
-      // 2^20 keys instead of 3 of 8 over the 23-bit composite)
+      // the key is the composite's low bits (3 passes of 8-bit digits at
+      // 2^20 keys, the last of 4 bits, instead of 3 full ones over the
+      // 23-bit composite)
       const bool pow2 = (key_space & (key_space - 1)) == 0;
       const int bits = pow2 ? bits_for(key_space) : bits_for(uint64_t(np + 1) * key_space);
       const uint32_t *bent = lent.get() + b * size_t(n) * fq;
@@ -1582,6 +1635,11 @@ struct EngineDevice {
       static const bool pipe = [] {
         const char *e = getenv("FH_VIEW_PIPE");
         return e && *e == '1';
+      }();
+      // FH_TAIL_FUSED=0: the tails in a launch of their own (k_tail_engine)
+      static const bool tail_fused = [] {
+        const char *e = getenv("FH_TAIL_FUSED");
+        return !(e && *e == '0');
       }();
       hipStream_t sp = stream;
       if (pipe) {
@@ -1634,15 +1692,16 @@ struct EngineDevice {
         if (place && !fused) {
           // the sort's other buffer pair takes the bucketed (position, code)
           uint32_t *bk = ks == lk ? bkb.get() : lk, *bv = ks == lk ? bvb.get() : lv;
-          place_codes(Mc, ks, vs, S, pbase + c, bk, bv, dep32.ensure(M + 1), sp);
+          place_codes(Mc, ks, vs, S, pbase + c, bk, bv, dep32.ensure(M + 1), sp, tail_fused, bbase);
         } else {
           probed_launch("prev_engine", double(Mc) * (4.0 + 4.0 + 4.0), k_prev_views,
                         dim3(grid_for(Mc, B)), dim3(B), sp, Mc, (const uint32_t *)ks,
                         (const uint32_t *)vs, S, (const uint64_t *)views_latest(),
                         dep32.ensure(M + 1));
         }
-        k_tail_engine<uint32_t><<<grid_for(Mc, B), B, 0, sp>>>(
-            Mc, ks, vs, 0, S, views_latest(), 1ull, ~0ull, nullptr, bbase);
+        if (!(place && !fused && tail_fused))
+          k_tail_engine<uint32_t><<<grid_for(Mc, B), B, 0, sp>>>(
+              Mc, ks, vs, 0, S, views_latest(), 1ull, ~0ull, nullptr, bbase);
         if (pipe) FH_HIP(hipEventRecord(ev_freed[set], sp));
       }
       if (pipe) {
@@ -1721,9 +1780,11 @@ struct EngineDevice {
   // The chunk's dependency codes -> dep32 through the placement pass: bucket
   // (position - base, code) by the position's bits [15, 23) with the radix
   // kernels (PrevSrc computes each code on the fly), then k_place per bucket.
+  // tails != 0: also make the segment tails the latest entries (log
+  // references log_base + command), replacing k_tail_engine
   void place_codes(uint32_t Mc, const uint32_t *ks, const uint32_t *vs, uint32_t per_cmd,
                    const uint32_t *ebase, uint32_t *bk, uint32_t *bv, uint32_t *out,
-                   hipStream_t s) {
+                   hipStream_t s, bool tails, uint64_t log_base) {
     if (Mc == 0) return;
     const PrevSrc src{ks, vs, ebase, (const uint64_t *)views_latest(), per_cmd};
     const uint32_t tiles = (Mc + kTile - 1) / kTile;
@@ -1739,9 +1800,14 @@ struct EngineDevice {
     k_scan_b<kPlaceDB><<<1, 256, 0, s>>>(gsum, groups, dbase);
     // reads (key, arrival) keys + positions, the previous element's, and the
     // latest table at heads; writes 8 B per element
+    const uint32_t nb = (tiles + 1) / 2;
+    uint32_t *defer = tails ? tail_defer.ensure(2 * size_t(nb)) : nullptr;
     probed_launch("prev_bucket", double(Mc) * (4.0 + 4.0 + 8.0), k_bucket_codes,
-                  dim3((tiles + 1) / 2), dim3(kBucketThreads), s, src, bk, bv, Mc, (const uint32_t *)counts,
-                  (const uint32_t *)gsum, uint32_t(kGroup), (const uint32_t *)dbase);
+                  dim3(nb), dim3(kBucketThreads), s, src, bk, bv, Mc, (const uint32_t *)counts,
+                  (const uint32_t *)gsum, uint32_t(kGroup), (const uint32_t *)dbase,
+                  views_latest(), log_base, defer);
+    if (tails)
+      k_tail_defer<<<grid_for(nb, 256), 256, 0, s>>>(nb, defer, views_latest(), log_base);
     probed_launch("place", double(Mc) * (8.0 + 4.0), k_place, dim3(R), dim3(1024), s, Mc,
                   (const uint32_t *)dbase, (const uint32_t *)bk, (const uint32_t *)bv, ebase, out);
   }
