@@ -161,7 +161,7 @@ struct PrevSrc {
 // entry before the barrier, so the tail of a segment that starts in the
 // workgroup is written in place; the tail of the first segment, if it began
 // in an earlier workgroup (whose head may not have read yet), goes to
-// defer[2·b] = (segment, command) for k_tail_defer.
+// defer[2·b] = (segment, command) for k_place to apply.
 constexpr int kBucketThreads = 512;
 constexpr int kBucketWaves = kBucketThreads / 64;
 constexpr int kBucketTile = 2 * kTile;  // 8192
@@ -283,22 +283,19 @@ __global__ void __launch_bounds__(kBucketThreads)
   }
 }
 
-// the deferred tails of k_bucket_codes (after every head has read)
-__global__ void k_tail_defer(uint32_t nb, const uint32_t *__restrict__ defer,
-                             uint64_t *__restrict__ latest, uint64_t log_base) {
-  GRID_STRIDE(b, nb) {
-    const uint32_t seg = defer[2 * b];
-    if (seg != ~0u) latest[seg] = kLogFlag | (log_base + defer[2 * b + 1]);
-  }
-}
-
 // one workgroup per bucket d: positions base + [d·2^15, (d+1)·2^15)
+// It also applies k_bucket_codes' deferred tails (defer: nb slots).
 __global__ void __launch_bounds__(1024)
     k_place(uint32_t Mc, const uint32_t *__restrict__ dbase, const uint32_t *__restrict__ rel,
             const uint32_t *__restrict__ code, const uint32_t *__restrict__ ebase,
-            uint32_t *__restrict__ out) {
+            uint32_t *__restrict__ out, const uint32_t *__restrict__ defer, uint32_t nb,
+            uint64_t *__restrict__ latest, uint64_t log_base) {
   __shared__ uint32_t s_c[kPlaceSpan];  // 128 KB
   const uint32_t d = blockIdx.x;
+  if (defer) {
+    const uint32_t b = d * 1024 + threadIdx.x;
+    if (b < nb && defer[2 * b] != ~0u) latest[defer[2 * b]] = kLogFlag | (log_base + defer[2 * b + 1]);
+  }
   for (uint32_t i = threadIdx.x; i < kPlaceSpan; i += 1024) s_c[i] = kPlaceNone;
   __syncthreads();
   const uint32_t s = dbase[d], t = d + 1 < kPlaceBuckets ? dbase[d + 1] : Mc;
@@ -1796,8 +1793,8 @@ struct EngineDevice {
     uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
     k_up<uint32_t, uint32_t, kPlaceDB, PrevSrc><<<tiles, kThreads, 0, s>>>(src, Mc, kPlaceShift,
                                                                             counts, 1);
-    k_scan_a<kPlaceDB><<<groups, 256, 0, s>>>(counts, tiles, gsum);
-    k_scan_b<kPlaceDB><<<1, 256, 0, s>>>(gsum, groups, dbase);
+    k_scan_a<kPlaceDB><<<dim3(groups, R / 256), 256, 0, s>>>(counts, tiles, gsum);
+    scan_b<kPlaceDB>(gsum, groups, dbase, s);
     // reads (key, arrival) keys + positions, the previous element's, and the
     // latest table at heads; writes 8 B per element
     const uint32_t nb = (tiles + 1) / 2;
@@ -1806,10 +1803,10 @@ struct EngineDevice {
                   dim3(nb), dim3(kBucketThreads), s, src, bk, bv, Mc, (const uint32_t *)counts,
                   (const uint32_t *)gsum, uint32_t(kGroup), (const uint32_t *)dbase,
                   views_latest(), log_base, defer);
-    if (tails)
-      k_tail_defer<<<grid_for(nb, 256), 256, 0, s>>>(nb, defer, views_latest(), log_base);
+    FH_CHECK(nb <= size_t(R) * 1024, FH_EINVAL, "placement: too many bucketing workgroups");
     probed_launch("place", double(Mc) * (8.0 + 4.0), k_place, dim3(R), dim3(1024), s, Mc,
-                  (const uint32_t *)dbase, (const uint32_t *)bk, (const uint32_t *)bv, ebase, out);
+                  (const uint32_t *)dbase, (const uint32_t *)bk, (const uint32_t *)bv, ebase, out,
+                  (const uint32_t *)defer, nb, views_latest(), log_base);
   }
 
   void run_general(uint32_t n, uint32_t k, uint32_t fq, uint32_t S, uint32_t M, bool views,

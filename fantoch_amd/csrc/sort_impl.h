@@ -110,7 +110,8 @@ __global__ void __launch_bounds__(256)
   constexpr int R = 1 << DB;
   const uint32_t g = blockIdx.x;
   const uint32_t t0 = g * kGroup, t1 = min(tiles, t0 + kGroup);
-  for (uint32_t d = threadIdx.x; d < uint32_t(R); d += 256) {
+  // blockIdx.y: a 256-digit slice (grid y = R / 256), else the block loops
+  for (uint32_t d = blockIdx.y * 256 + threadIdx.x; d < uint32_t(R); d += 256 * gridDim.y) {
     uint32_t v[kGroup];
 #pragma unroll
     for (int i = 0; i < kGroup; i++) v[i] = (t0 + i < t1) ? counts[size_t(t0 + i) * R + d] : 0u;
@@ -158,6 +159,79 @@ __global__ void __launch_bounds__(256)
     dbase[threadIdx.x * Q + q] = pre;
     pre += tot[q];
   }
+}
+
+// k_scan_b over 1024 threads: P = 1024 / R threads per digit, each over a
+// contiguous slice of the groups (a first pass sums the slice, a second
+// writes its exclusive prefixes from the slice's base): two dependent load
+// rounds instead of one per 16 groups.
+template <int DB>
+__global__ void __launch_bounds__(1024)
+    k_scan_b_wide(uint32_t *__restrict__ gsum, uint32_t groups, uint32_t *__restrict__ dbase) {
+  constexpr int R = 1 << DB, P = 1024 / R;
+  static_assert(P >= 1 && 1024 % R == 0, "k_scan_b_wide: at most 1024 digits");
+  __shared__ uint32_t s_part[P][R];
+  __shared__ uint32_t s_tmp[16];
+  const uint32_t d = threadIdx.x % R, q = threadIdx.x / R;
+  const uint32_t per = (groups + P - 1) / P;
+  const uint32_t g0 = min(groups, q * per), g1 = min(groups, g0 + per);
+  uint32_t sum = 0;
+  for (uint32_t g = g0; g < g1; g += 16) {
+    uint32_t v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = (g + i < g1) ? gsum[size_t(g + i) * R + d] : 0u;
+#pragma unroll
+    for (int i = 0; i < 16; i++) sum += v[i];
+  }
+  s_part[q][d] = sum;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < P; i++) {
+    if (uint32_t(i) < q) run += s_part[i][d];
+    tot += s_part[i][d];
+  }
+  for (uint32_t g = g0; g < g1; g += 16) {
+    uint32_t v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = (g + i < g1) ? gsum[size_t(g + i) * R + d] : 0u;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      if (g + i < g1) gsum[size_t(g + i) * R + d] = run;
+      run += v[i];
+    }
+  }
+  // dbase: exclusive scan of the digit totals over threads q == 0 (tid = d)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = q == 0 ? tot : 0u;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  if (lane == 63) s_tmp[w] = x;
+  __syncthreads();
+  if (q == 0) {
+    uint32_t pre = 0;
+    for (int i = 0; i < w; i++) pre += s_tmp[i];
+    dbase[d] = pre + x - tot;
+  }
+}
+
+// k_scan_b, or its 1024-thread form (FH_SCAN_WIDE=0: the 256-thread one)
+template <int DB>
+inline void scan_b(uint32_t *gsum, uint32_t groups, uint32_t *dbase, hipStream_t s) {
+  static const bool wide = [] {
+    const char *e = getenv("FH_SCAN_WIDE");
+    return !(e && *e == '0');
+  }();
+  if constexpr (DB <= 10) {
+    if (wide) {
+      k_scan_b_wide<DB><<<1, 1024, 0, s>>>(gsum, groups, dbase);
+      return;
+    }
+  }
+  k_scan_b<DB><<<1, 256, 0, s>>>(gsum, groups, dbase);
 }
 
 // Small sorts (tiles <= kFusedMaxTiles): one 1024-thread workgroup does both
@@ -339,7 +413,7 @@ void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tile
     k_scan_fused<<<1, 1024, 0, s>>>(counts, tiles, gsize, gsum, dbase);
   } else {
     k_scan_a<DB><<<groups, 256, 0, s>>>(counts, tiles, gsum);
-    k_scan_b<DB><<<1, 256, 0, s>>>(gsum, groups, dbase);
+    scan_b<DB>(gsum, groups, dbase, s);
   }
   if (!probe) {
     k_down<K, VT, DB, Src><<<tiles, kThreads, 0, s>>>(src, ko, vo, uint32_t(n), shift, counts,
