@@ -1791,8 +1791,10 @@ struct EngineDevice {
     uint32_t *counts = sort_ws.meta.get();
     uint32_t *gsum = counts + size_t(tiles) * R;
     uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
+    // runs of a key's consecutive elements mostly share a bucket: one atomic
+    // per run (k_up mode 2)
     k_up<uint32_t, uint32_t, kPlaceDB, PrevSrc><<<tiles, kThreads, 0, s>>>(src, Mc, kPlaceShift,
-                                                                            counts, 1);
+                                                                            counts, 2);
     k_scan_a<kPlaceDB><<<dim3(groups, R / 256), 256, 0, s>>>(counts, tiles, gsum);
     scan_b<kPlaceDB>(gsum, groups, dbase, s);
     // reads (key, arrival) keys + positions, the previous element's, and the

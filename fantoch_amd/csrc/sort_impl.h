@@ -75,7 +75,24 @@ __global__ void __launch_bounds__(kThreads)
   }
   __syncthreads();
   const uint64_t lt = (uint64_t(1) << lane) - 1;
-  if (atomic_up) {
+  if (atomic_up == 2) {
+    // runs of equal digits in adjacent lanes (passes after the first see
+    // each key's elements contiguous: a hot key fills whole waves) add their
+    // length with one atomic from the run's first lane
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+      const uint32_t idx = elem_index(base, w, i, lane);
+      const uint32_t d = idx < n ? uint32_t((key[i] >> shift) & (R - 1)) : ~0u;
+      const uint32_t dp = __shfl_up(d, 1, 64);
+      const bool head = lane == 0 || d != dp;
+      const uint64_t heads = __ballot(head);
+      if (head && d != ~0u) {
+        const uint64_t after = lane == 63 ? 0ull : heads >> (lane + 1);
+        const uint32_t len = after ? uint32_t(__builtin_ctzll(after)) + 1u : uint32_t(64 - lane);
+        atomicAdd(&s_h[w][d], len);
+      }
+    }
+  } else if (atomic_up) {
     // one LDS atomic per item into the wave's histogram (same-digit lanes of
     // one instruction serialise on their bin)
 #pragma unroll
@@ -401,9 +418,11 @@ void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tile
   // same-bin serialisation of hot digits.  Counts only: k_down's ranks stay
   // ballot-matched (stable without relying on the order in which one
   // instruction's same-address atomics return).
+  // FH_SORT_UP_ATOMIC=1: an atomic per item; default 2: per run of equal
+  // digits in adjacent lanes
   static const int atomic_up = [] {
     const char *e = getenv("FH_SORT_UP_ATOMIC");
-    return e && *e == '0' ? 0 : 1;
+    return e && *e == '0' ? 0 : e && *e == '1' ? 1 : 2;
   }();
   if (!have_counts)  // (else the producer of the input wrote the tile counts)
     k_up<K, VT, DB, Src><<<tiles, kThreads, 0, s>>>(src, uint32_t(n), shift, counts, atomic_up);
