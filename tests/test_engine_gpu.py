@@ -345,6 +345,48 @@ print("ok")
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("env", [
+    {},
+    {"FH_TAIL_FUSED": "0", "FH_SORT_UP_ATOMIC": "1", "FH_SCAN_WIDE": "0"},
+    {"FH_SORT_UP_ATOMIC": "0"},
+])
+def test_views_kernel_variants_match_oracle(env):
+    """The replica-view path's kernel variants (read once per process: a
+    child process), each against the oracle on a hot-key stream cut into
+    chunks of 20,000 elements, so that segments cross the bucketing
+    workgroups and chunks: the segment tails written by k_bucket_codes (the
+    first segment's deferred to k_place) or by k_tail_engine
+    (FH_TAIL_FUSED=0); the radix tile counts by runs of equal digits
+    (default), one atomic per item (FH_SORT_UP_ATOMIC=1) or ballot matching
+    (=0); the 1024- or 256-thread second scan level (FH_SCAN_WIDE)."""
+    import subprocess, sys, os
+    code = f"""
+import numpy as np, sys
+sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+from fantoch_amd.engine import Engine
+from fantoch_amd.workload import Workload
+from oracle import oracle as O
+s = Workload.zipf(1.2, 1 << 12, k=1, views=3, window=64, seed=31).generate(90_000, logs=True)
+eng = Engine(s.key_space, n=5)
+eng.stage_logs([s])
+for _ in range(2):
+    eng.rewind()
+    eng.run()
+    r = eng.results()
+off, deps = O.views_run(0, 5, s.dots, s.key_off(), s.keys.reshape(-1), s.fq_proc, s.fq_time)
+ex, lab, kso, ks = O.graph_run(s.dots, s.key_off(), s.keys.reshape(-1), off, deps, s.key_space)
+assert np.array_equal(r["dep_off"], off) and np.array_equal(r["deps"], deps)
+assert np.array_equal(r["key_off"], kso) and np.array_equal(r["key_seq"], ks)
+m = dict(zip(ex.tolist(), lab.tolist()))
+assert np.array_equal(r["scc_label"], np.asarray([m[int(d)] for d in s.dots], np.uint64))
+print("ok")
+"""
+    e = dict(os.environ, FH_VIEW_CHUNK="20000", **env)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=200,
+                       env=e)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("window,seed", [(64, 21), (80, 22)])
 def test_views_mixed_tile_bounds_match_oracle(window, seed):
     """The tile kernel's mixed reach bounds (graph_tile.hip tiles_mixed):
