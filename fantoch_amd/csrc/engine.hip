@@ -766,10 +766,15 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint32_t *__restrict__ err) {
   // uniform: the register path, with a sorting network sized to the row
   if (S <= 4) {
-    GRID_STRIDE(i, n) {
-      cmd_union_regs<4>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n, out_off, err);
-    }
+    // XCD-contiguous blocks (grid a multiple of 8): workgroup b runs on XCD
+    // b mod 8, which takes the b/8-th block of its own eighth of the
+    // commands, so the recent dependencies' dot lines are gathered into the
+    // L2 of the XCD that gathers them again
+    const uint32_t nb = gridDim.x;
+    const uint32_t lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
+    for (size_t i = size_t(lb) * blockDim.x + threadIdx.x; i < n; i += size_t(nb) * blockDim.x)
+      cmd_union_regs<4>(uint32_t(i), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
+                        blocked0, nblocked, nv_out, bbase, n, out_off, err);
     return;
   }
   if (S <= 8) {
@@ -1839,9 +1844,17 @@ struct EngineDevice {
     } else {
       ddot = dep_dot.ensure(M + 1);
     }
+    // FH_UNION_XCD=0: the capped grid-stride launch
+    static const bool xcd_union = [] {
+      const char *e = getenv("FH_UNION_XCD");
+      return !(e && *e == '0');
+    }();
     if (views)
       probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
-                    k_cmd_engine<uint32_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
+                    k_cmd_engine<uint32_t>,
+                    dim3(S <= 4 && xcd_union ? (grid_for(n, B, 1u << 22) + 7) / 8 * 8
+                                             : grid_for(n, B)),
+                    dim3(B), stream, n, S, bdot,
                     (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
                     scal.get(), ecnt, bbase, doff, scal.get() + 1);
