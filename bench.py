@@ -27,6 +27,23 @@ the engine stream around its launches in a probe pass), the CPU baseline (the
 oracle restatement of the reference's per-replica SequentialKeyDeps +
 QuorumDeps + incremental GraphExecutor on a bounded prefix, rank 0 at N=1)
 and, as `secondary`, the C2 line (single-view KeyDeps, 1M-command batches).
+
+`c5` (N=1, rank 0): BASELINE.json configs[4] at its stated size -- Atlas
+partial replication over 8 key shards (shard = key mod 8), Zipf 0.99 over 2^20
+keys, 4 keys per command, 100M commands -- with all 8 shards on the one GPU.
+The shards' key sets are disjoint, so their SequentialKeyDeps tables are
+disjoint slices of one latest table: one fused KeyDeps pass computes every
+shard's reports, and the per-command union over the 4 keys x 3 views is the
+cross-shard MShardCommit union (atlas.rs:580-583).  Parity: the committed
+deps digest of this stream equals the oracle's shard-by-shard union
+(tests/golden/make_digests.py, tests/test_fullsize_gpu.py).
+
+Roofline bytes are SURVEY.md §8(d)'s algorithmic bytes per command: the
+dominant kernel's `achieved` = (its §8(d) term x commands per step) / (its
+device time per step); the builder's own per-kernel byte counts ride along
+as `*_builder` fields.  `cold_ms` = one run after fh_engine_forget_tuning
+(the graph stage's learned reach bound / global-path entry dropped), and
+`first_ms` = the first run of a fresh engine (buffer allocation included).
 """
 from __future__ import annotations
 
@@ -62,7 +79,11 @@ def parse():
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase profile pass")
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary C2 line")
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the other BASELINE configurations (C1, C3, C4 key shard, C5 shard)")
+                    help="skip the other BASELINE configurations (C1, C3, C4 key shard, C5 12.5M)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 100M line")
+    ap.add_argument("--c5-commands", type=int, default=100_000_000)
+    ap.add_argument("--no-cpu-sharded", action="store_true",
+                    help="skip the key-sharded multi-process CPU baseline")
     return ap.parse_args()
 
 
@@ -134,18 +155,53 @@ def probe_pass(eng, names, steps, rewind=True):
     return probes
 
 
-def roofline(probes, fallback):
+def sec8d_bytes(k, views, d, d_view=None):
+    """SURVEY.md §8(d) algorithmic bytes per command, by term.  d_view: deps
+    per command per view (<= k: the previous element of each key)."""
+    dv = k if d_view is None else d_view
+    b = {"deps": views * (8 * (1 + k) + 4 + 8 * dv),
+         "union": (views * (4 + 8 * dv) + 4 + 8 * d) if views > 1 else 0.0,
+         "exec": 4 + 4 * d + 8 + 4 + 4,
+         "order": 8 + 8 * k}
+    b["total"] = b["deps"] + b["union"] + b["exec"] + b["order"]
+    return b
+
+
+# the §8(d) term each probed kernel implements alone (the KeyDeps sort passes,
+# the bucketing and the placement share B_deps between them: no single term)
+SEC8D_TERM = {"graph_tile": "exec", "cmd_union": "union"}
+
+
+def roofline(probes, fallback, commands, b8d, steps):
     if not probes:
         return {"bound": "hbm", "kernel": fallback, "achieved": 0.0, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": 0.0, "traffic": None}
-    # dominant kernel: the most device time over the pass
+    # dominant kernel: the most device time over the probe pass
     dom = max(probes, key=lambda k: probes[k]["avg_launch_us"] * probes[k]["launches"])
     p = probes[dom]
-    ach = p["achieved_GBs"]
-    return {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "traffic": p["traffic"], "launches": p["launches"],
-            "avg_launch_us": p["avg_launch_us"],
-            "algorithmic_bytes_per_launch": p["algorithmic_bytes_per_launch"]}
+    per_step_s = p["avg_launch_us"] * 1e-6 * p["launches"] / steps
+    term = SEC8D_TERM.get(dom)
+    if term:
+        alg = b8d[term] * commands  # bytes per step
+        ach = alg / per_step_s / 1e9
+        basis = f"SURVEY §8(d) B_{term} = {b8d[term]:.2f} B/cmd x {commands} commands per step"
+    else:
+        alg = p["algorithmic_bytes_per_launch"] * p["launches"] / steps
+        ach = p["achieved_GBs"]
+        basis = "kernel's own algorithmic bytes (no single §8(d) term)"
+    launches_per_step = p["launches"] / steps
+    r = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": ach / HBM_PEAK_GBS, "traffic": p["traffic"], "launches": p["launches"],
+         "launches_per_step": launches_per_step, "avg_launch_us": p["avg_launch_us"],
+         "kernel_ms_per_step": per_step_s * 1e3,
+         "algorithmic_bytes_per_step": alg,
+         "algorithmic_bytes_per_launch": alg / launches_per_step, "basis": basis,
+         "achieved_builder": p["achieved_GBs"],
+         "frac_builder": p["achieved_GBs"] / HBM_PEAK_GBS,
+         "algorithmic_bytes_per_launch_builder": p["algorithmic_bytes_per_launch"]}
+    if p["traffic"] is not None:
+        r["traffic_per_step"] = p["traffic"] * launches_per_step
+    return r
 
 
 def phases_of(eng, rewind=True):
@@ -161,12 +217,19 @@ def phases_of(eng, rewind=True):
     return {k: round(float(np.median(v[1:] if len(v) > 1 else v)), 4) for k, v in acc.items()}
 
 
+def path_roofline(value, k, views, d, world=1):
+    b = sec8d_bytes(k, views, d)
+    ach = value * b["total"] / 1e9 / world
+    return {"bytes_per_cmd": b["total"], "terms": {t: b[t] for t in ("deps", "union", "exec", "order")},
+            "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS}
+
+
 def other_configs(local, steps=3):
     """The other BASELINE configurations on this GPU, each one engine pass over
     its whole staged stream per step (inputs resident, every output
     materialised): C1 (10k, plumbing), C3 (10M, one stream-wide SCC), C4's
-    per-GPU key-shard size (12.5M) and a C5 shard (12.5M commands of 4 keys).
-    Parity at these shapes: tests/test_fullsize_gpu.py."""
+    per-GPU key-shard size (12.5M) and the first 12.5M commands of C5's 4-key
+    stream, unsharded.  Parity at these shapes: tests/test_fullsize_gpu.py."""
     from fantoch_amd.engine import Engine
     from fantoch_amd.workload import Workload
     cfgs = {
@@ -177,9 +240,10 @@ def other_configs(local, steps=3):
                "EPaxos n=5, ConflictPool 100% (key 0 + 16-key pool), 2 keys, replica views"),
         "c4_shard": (Workload.zipf(0.99, 1 << 20, k=1, views=3, window=64, seed=C4_SEED, n=5),
                      12_500_000, "C4 per-GPU size at 8 GPUs: Zipf 0.99 / 2^20 keys, 1 key"),
-        "c5_shard": (Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64,
-                                   seed=0xFA170C4000000005, n=5), 12_500_000,
-                     "C5 shard: Zipf 0.99 / 2^20 keys, 4 keys/cmd, replica views"),
+        "c5_12m": (Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64,
+                                 seed=0xFA170C4000000005, n=5), 12_500_000,
+                   "first 12.5M commands of C5's stream, unsharded: Zipf 0.99 / 2^20 keys, "
+                   "4 keys/cmd, replica views"),
     }
     out = {}
     for name, (w, n, desc) in cfgs.items():
@@ -194,10 +258,83 @@ def other_configs(local, steps=3):
             eng.run(sync=False)
         eng.sync()
         ms = (time.perf_counter() - t0) / steps * 1e3
+        d = eng.dep_total() / n
         eng.close()
+        v = n / (ms * 1e-3)
         out[name] = {"workload": desc, "commands": n, "ms_per_step": round(ms, 3),
-                     "commands_per_s": n / (ms * 1e-3)}
+                     "commands_per_s": v, "deps_per_cmd": d,
+                     "path_roofline": path_roofline(v, s.k, 3, d)}
     return out
+
+
+def c5_line(args, local):
+    """C5 at its stated size on one GPU (all 8 key shards): one engine pass
+    over the 100M-command 4-key stream per step, every output materialised."""
+    from fantoch_amd.engine import Engine
+    from fantoch_amd.workload import Workload
+    n = args.c5_commands
+    w = Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64, seed=0xFA170C4000000005, n=5)
+    s = w.generate(n, logs=True, times=False)
+    eng = Engine(s.key_space, n=5, device=local)
+    eng.stage(s)
+    first = eng.run(sync=True)
+    steps = 3
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.rewind()
+        eng.run(sync=False)
+    eng.sync()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    d = eng.dep_total() / n
+    eng.forget_tuning()
+    eng.rewind()
+    cold = eng.run(sync=True)
+    phases = None
+    if not args.no_phases:
+        eng.set_profiling(True)
+        eng.rewind()
+        eng.run(sync=True)
+        phases = {k: round(v, 3) for k, v in eng.kernel_times()}
+        eng.set_profiling(False)
+    eng.close()
+    v = n / (ms * 1e-3)
+    r = {"workload": "C5: Atlas partial replication, 8 key shards (key mod 8) all on this GPU, "
+                     "Zipf 0.99 over 2^20 keys, 4 keys/cmd, replica views (fast quorum 3), "
+                     "100M commands; one step orders the whole stream, every output materialised",
+         "commands": n, "shards": 8, "steps": steps, "warmup": 1, "ms_per_step": round(ms, 3),
+         "commands_per_s": v, "first_ms": round(first, 3), "cold_ms": round(cold, 3),
+         "deps_per_cmd": d, "path_roofline": path_roofline(v, 4, 3, d)}
+    if phases:
+        r["phases_ms"] = phases
+    return r
+
+
+def cpu_sharded_worker(arg):
+    keys, nsh, sh, sample = arg
+    import numpy as np
+    from oracle import oracle as O
+    s = c4_workload(keys).generate(sample)
+    mine = np.nonzero(s.keys[:, 0] % np.uint64(nsh) == np.uint64(sh))[0]
+    dots, kk = s.dots[mine], s.keys[mine].reshape(-1)
+    ko = (np.arange(len(mine) + 1, dtype=np.uint64)).astype(np.uint32)
+    fp, ft = s.fq_proc[mine], s.fq_time[mine]
+    t0 = time.perf_counter()
+    off, deps = O.views_run(0, 5, dots, ko, kk, fp, ft)
+    O.graph_run(dots, ko, kk, off, deps, s.key_space)
+    return len(mine), time.perf_counter() - t0
+
+
+def cpu_baseline_sharded(keys, sample, procs):
+    """The oracle on `procs` key shards of the same prefix in parallel
+    processes (one key per command: every shard's graph is closed, as on the
+    GPUs): whole-prefix commands / the slowest shard's time."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(cpu_sharded_worker, [(keys, procs, i, sample) for i in range(procs)])
+    slow = max(t for _, t in res)
+    return sum(n for n, _ in res) / slow, slow
 
 
 def secondary_c2(args, local):
@@ -255,7 +392,12 @@ def main():
     t_gen = time.perf_counter() - t_gen
     eng = Engine(s.key_space, n=5, device=local)
     eng.stage(s)
-    for _ in range(args.warmup):
+    first_ms = None
+    for i in range(args.warmup):
+        if i == 0:
+            eng.rewind()
+            first_ms = eng.run(sync=True)
+            continue
         eng.rewind()
         eng.run(sync=False)
     eng.sync()
@@ -271,21 +413,18 @@ def main():
     n_local = s.n
     deps_total = int(r["dep_off"][-1])
     _, scc_sizes = np.unique(r["scc_label"], return_counts=True)
-    probes = probe_pass(eng, args.probe, min(args.steps, 10))
+    probe_steps = min(args.steps, 10)
+    probes = probe_pass(eng, args.probe, probe_steps)
     phases = None if (args.no_phases or rank != 0) else phases_of(eng)
+    # cold run: the graph stage's learned tuning dropped (fresh-engine guesses)
+    eng.forget_tuning()
+    eng.rewind()
+    cold_ms = eng.run(sync=True)
     eng.close()
 
     d = deps_total / max(1, n_local)
     k, views = 1, 3
-    # SURVEY §8d algorithmic bytes per command with replica views: KeyDeps per
-    # view (read dot + key ids, write offset + deps; d_v <= k), the union of
-    # the views' reports into d committed deps, the executor (CSR as vertex
-    # ids, dot for the tie-break, SCC id + exec rank) and the per-key order.
-    b_deps = views * (8 * (1 + k) + 4 + 8 * k)
-    b_union = views * (4 + 8 * k) + 4 + 8 * d
-    b_exec = 4 + 4 * d + 8 + 4 + 4
-    b_order = 8 + 8 * k
-    bpc = b_deps + b_union + b_exec + b_order
+    b8d = sec8d_bytes(k, views, d)
     result = {
         "metric": METRIC,
         "value": value,
@@ -304,11 +443,11 @@ def main():
                                "orders the whole stream, every output materialised on the device",
                    "commands": args.commands, "keys": args.keys, "zipf_s": 0.99, "views": views,
                    "parallelism": f"key-shard x{world}"},
-        "roofline": roofline(probes, "sort_scatter"),
+        "roofline": roofline(probes, "sort_scatter", n_local, b8d, probe_steps),
         "kernels": probes,
-        "path_roofline": {"bytes_per_cmd": bpc,
-                          "achieved_GBs": value * bpc / 1e9 / world,
-                          "frac": value * bpc / 1e9 / world / HBM_PEAK_GBS},
+        "path_roofline": path_roofline(value, k, views, d, world),
+        "cold_ms": round(cold_ms, 3),
+        "first_ms": round(first_ms, 3) if first_ms is not None else None,
         "stream": {"commands_this_rank": n_local, "deps_per_cmd": d, "sccs": int(len(scc_sizes)),
                    "largest_scc": int(scc_sizes.max()) if len(scc_sizes) else 0,
                    "generate_s": round(t_gen, 2)},
@@ -318,10 +457,25 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sample = min(args.cpu_sample, args.commands)
         v, dt = cpu_baseline_c4(w, sample)
+        try:
+            host = len(os.sched_getaffinity(0))
+        except AttributeError:
+            host = os.cpu_count()
         result["cpu_baseline"] = {"value": v, "unit": "commands/s", "cores": 1, "kind": "port",
+                                  "host_nproc": os.cpu_count(), "host_cpus_usable": host,
                                   "sample": f"first {sample} commands of the same C4 stream: oracle "
                                             f"per-replica SequentialKeyDeps + QuorumDeps union + "
                                             f"incremental GraphExecutor, 1 thread, {dt:.2f}s"}
+        if not args.no_cpu_sharded:
+            procs = 16  # the GPU box's CPU share for one GPU
+            vs, ts = cpu_baseline_sharded(args.keys, sample, procs)
+            result["cpu_baseline_sharded"] = {
+                "value": vs, "unit": "commands/s", "cores": procs, "kind": "port",
+                "sample": f"the same {sample}-command prefix split into {procs} key shards "
+                          f"(key mod {procs}), one oracle process per shard; slowest shard "
+                          f"{ts:.2f}s"}
+    if rank == 0 and world == 1 and not args.no_c5:
+        result["c5"] = c5_line(args, local)
     if rank == 0 and world == 1 and not args.no_secondary:
         result["secondary"] = secondary_c2(args, local)
     if rank == 0 and world == 1 and not args.no_configs:

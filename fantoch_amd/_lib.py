@@ -105,6 +105,7 @@ SIGNATURES = {
     "fh_engine_kernel_times": (C.c_int, [V, P(C.c_char_p), P(C.c_float), S, P(S)]),
     "fh_engine_set_profiling": (C.c_int, [V, C.c_int]),
     "fh_engine_set_deps_only": (C.c_int, [V, C.c_int]),
+    "fh_engine_forget_tuning": (C.c_int, [V]),
     "fh_engine_set_probe": (C.c_int, [V, C.c_char_p]),
     "fh_engine_probe_stats": (C.c_int, [V, P(C.c_float), P(S), P(C.c_double)]),
     "fh_engine_probe_stats_for": (C.c_int, [V, C.c_char_p, P(C.c_float), P(S), P(C.c_double)]),

@@ -1381,8 +1381,10 @@ struct EngineDevice {
     FH_CHECK(d.keys_per_cmd >= 1 && d.keys_per_cmd <= 8, FH_EINVAL, "keys_per_cmd in [1, 8]");
     const uint32_t fq = d.views ? d.views : 1;
     FH_CHECK(fq <= 16, FH_EINVAL, "views <= 16");
-    FH_CHECK(size_t(d.n) * fq * d.keys_per_cmd < (size_t(1) << 30), FH_EINVAL,
-             "batch too large (elements >= 2^30)");
+    // element positions (c·fq + j)·k + s and in-batch codes vid + 1 are u32
+    // with the top bit free (C5: 100M commands x 4 keys x 3 views = 1.2G)
+    FH_CHECK(size_t(d.n) * fq * d.keys_per_cmd < (size_t(1) << 31), FH_EINVAL,
+             "batch too large (elements >= 2^31)");
     FH_CHECK(!d.views || (h_off && h_cmd && d.nproc >= 1 && d.nproc <= 255), FH_EINVAL,
              "replica views need per-replica logs and nproc");
     FH_CHECK(!d.views || uint64_t(d.nproc + 1) * key_space <= 0xFFFFFFFFull, FH_ENOTIMPL,
@@ -2178,6 +2180,14 @@ fh_status fh_engine_set_profiling(fh_engine *h, int on) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
   h->dev.profile = on != 0;
+  FH_API_END
+}
+
+fh_status fh_engine_forget_tuning(fh_engine *h) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_HIP(hipStreamSynchronize(h->dev.stream));
+  h->dev.graph.forget_tuning();
   FH_API_END
 }
 

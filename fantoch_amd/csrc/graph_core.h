@@ -121,8 +121,14 @@ struct GraphCore {
 
   void run(const GraphInput &in, GraphOutput &out);
 
+  // back to a fresh engine's first guesses (fh_engine_forget_tuning)
+  void forget_tuning() {
+    prefer_full = false;
+    tile_r0 = 1536;
+  }
  private:
   void mark(const char *name);
+  void take_sorted(const uint32_t *vs, DBuf<uint32_t> &out);
   uint32_t read_scalar(int i);
   void pending_closure(const GraphInput &in, GraphOutput &out);
   uint64_t count_forward(const GraphInput &in);

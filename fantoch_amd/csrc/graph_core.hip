@@ -547,12 +547,17 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
   agg_flush<uint32_t, true>(tb, H, [&](uint32_t) { *changed = 1; });
 }
 
+// parent (the merge's union-find forest) starts as a copy of rep for every
+// processed vertex: written here, in a pass the round makes anyway, instead
+// of a V-sized device copy before the merge
 __global__ void k_fb_roots(uint32_t n, const uint32_t *__restrict__ list,
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
-                           const uint32_t *__restrict__ H, uint8_t *reached) {
+                           const uint32_t *__restrict__ H, uint8_t *reached,
+                           uint32_t *__restrict__ parent) {
   GRID_STRIDE(j, n) {
     const uint32_t v = FB_VID(j);
+    parent[v] = rep[v];
     if (blocked[v] || done[v]) continue;
     if (H[rep[v]] == v) reached[rep[v]] = 1;  // v is the class maximum: its SCC is the root
   }
@@ -625,18 +630,15 @@ __global__ void k_fb_merge(uint32_t n, const uint32_t *__restrict__ list,
   }
 }
 
-__global__ void k_fb_compress(uint32_t n, const uint32_t *__restrict__ list, uint32_t *parent) {
+// the merged forest, compressed, becomes rep (nothing reads rep during the
+// compression: the merge that read it has finished)
+__global__ void k_fb_compress(uint32_t n, const uint32_t *__restrict__ list, uint32_t *parent,
+                              uint32_t *__restrict__ rep) {
   GRID_STRIDE(j, n) {
     const uint32_t v = FB_VID(j);
-    parent[v] = uf_find(parent, v);
-  }
-}
-
-__global__ void k_fb_copy(uint32_t n, const uint32_t *__restrict__ list,
-                          const uint32_t *__restrict__ src, uint32_t *__restrict__ dst) {
-  GRID_STRIDE(j, n) {
-    const uint32_t v = FB_VID(j);
-    dst[v] = src[v];
+    const uint32_t r = uf_find(parent, v);
+    parent[v] = r;
+    rep[v] = r;
   }
 }
 
@@ -819,6 +821,20 @@ __global__ void k_copy_dot(uint32_t V, const uint64_t *__restrict__ dot, uint64_
 }
 
 }  // namespace
+
+// `out` takes over the scratch buffer (tmp32a or tmp32b) that holds a sort's
+// output values: the two swap, so no copy is made (both hold >= V words)
+void GraphCore::take_sorted(const uint32_t *vs, DBuf<uint32_t> &out) {
+  if (vs == tmp32a.get()) {
+    if (tmp32a.cap > out.cap) out.ensure(tmp32a.cap);
+    out.swap(tmp32a);
+  } else if (vs == tmp32b.get()) {
+    if (tmp32b.cap > out.cap) out.ensure(tmp32b.cap);
+    out.swap(tmp32b);
+  } else {
+    FH_CHECK(false, FH_EINVARIANT, "take_sorted: not a scratch buffer");
+  }
+}
 
 void GraphCore::mark(const char *name) {
   if (!profile || !marks) return;
@@ -1059,28 +1075,19 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
       k_fb_save_h<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), H, hseed.ensure(V));
       hseed_ok = true;
     }
-    k_fb_roots<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
+    k_fb_roots<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached, parent);
     FH_HIP(hipMemsetAsync(pushed, 0, V, stream));
     converge(1, dbg_reach, [&](uint32_t *changed, const uint32_t *prev) {
       k_fb_reach<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
                                        rep.get(), H, reached, changed, pushed, prev, int(first_full));
     });
     FH_HIP(hipMemsetAsync(scalars.get() + 1, 0, sizeof(uint32_t), stream));
-    // unions go to a separate parent array so rep[] stays stable while read
-    // (only the processed vertices' entries are read or written)
-    if (list)
-      k_fb_copy<<<G, B, 0, stream>>>(n, list, rep.get(), parent);
-    else
-      FH_HIP(hipMemcpyAsync(parent, rep.get(), size_t(V) * sizeof(uint32_t),
-                            hipMemcpyDeviceToDevice, stream));
+    // unions go to a separate parent array (seeded from rep by k_fb_roots)
+    // so rep[] stays stable while read; only the processed vertices' entries
+    // are read or written, and the compression writes the result back to rep
     k_fb_merge<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached, parent,
                                      scalars.get() + 1);
-    k_fb_compress<<<G, B, 0, stream>>>(n, list, parent);
-    if (list)
-      k_fb_copy<<<G, B, 0, stream>>>(n, list, parent, rep.get());
-    else
-      FH_HIP(hipMemcpyAsync(rep.get(), parent, size_t(V) * sizeof(uint32_t),
-                            hipMemcpyDeviceToDevice, stream));
+    k_fb_compress<<<G, B, 0, stream>>>(n, list, parent, rep.get());
     if (!read_scalar(1)) break;
     first_full = false;
     if (full) {
@@ -1133,7 +1140,8 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   FH_HIP(hipMemcpyAsync(hmx, mx, sizeof(hmx), hipMemcpyDeviceToHost, stream));
   FH_HIP(hipStreamSynchronize(stream));
   const int sb = bits_for(hmx[1] + 1), dbits = bits_for(hmx[0] + 1) + sb;
-  uint32_t *dord = rank.ensure(V);
+  rank.ensure(V);
+  uint32_t *dord = nullptr;
   if (dbits <= 32) {
     uint32_t *k32a = reinterpret_cast<uint32_t *>(ka), *k32b = reinterpret_cast<uint32_t *>(kb);
     uint32_t *k32s = nullptr;
@@ -1147,7 +1155,12 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
     sort_pairs<uint64_t, uint32_t>(in.dot, nullptr, ka, va, kb, vb, V, 64, sort_ws, stream, &ks,
                                    &vs);
   }
-  FH_HIP(hipMemcpyAsync(dord, vs, size_t(V) * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+  // the dot order stays in the sort's output buffer: it becomes `rank`
+  // (a buffer swap, not a V-sized copy), and the scratch pair is refreshed
+  take_sorted(vs, rank);
+  dord = rank.get();
+  va = tmp32a.get();
+  vb = tmp32b.get();
   mark("dot_rank");
   // SCC order by kappa
   uint32_t *fl = cnt.ensure(V);
@@ -1174,9 +1187,9 @@ void GraphCore::build_orders(const GraphInput &in, GraphOutput &out) {
   uint32_t *k32s = nullptr;
   sort_pairs<uint32_t, uint32_t>(k32a, va, k32a, va, k32b, vb, nexec, bits_for(uint64_t(nrep) + 1),
                                  sort_ws, stream, &k32s, &vs);
-  uint32_t *ord = order.ensure(nexec + 1);
-  FH_HIP(hipMemcpyAsync(ord, vs, size_t(nexec) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                        stream));
+  order.ensure(nexec + 1);
+  take_sorted(vs, order);
+  uint32_t *ord = order.get();
   uint32_t *er = tmp32d.ensure(V);
   k_exec_rank<<<grid_for(V, B), B, 0, stream>>>(V, er);
   k_rank_from_sorted<<<grid_for(nexec, B), B, 0, stream>>>(nexec, ord, er);

@@ -105,24 +105,35 @@ fh_status fh_multi_stage_logs(fh_multi *h, const fh_stream_desc *desc, const uin
                               const uint64_t *key_id, const uint64_t *log_off,
                               const uint32_t *log_cmd) {
   FH_API_BEGIN
-  FH_CHECK(h && desc && dot && key_id && log_off && log_cmd, FH_EINVAL, "null argument");
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  // whatever happens below, the previous staging is gone: run() and
+  // results() refuse until a staging completes
+  h->staged = false;
+  h->ran = false;
+  FH_CHECK(desc && dot && key_id && log_off && log_cmd, FH_EINVAL, "null argument");
   FH_CHECK(desc->keys_per_cmd == 1, FH_ENOTIMPL,
            "fh_multi: key shards need one key per command (closed per-shard graphs)");
   FH_CHECK(desc->views >= 1 && desc->nproc >= 1, FH_EINVAL, "fh_multi: replica views only");
   const size_t G = h->eng.size(), n = desc->n, np = desc->nproc;
+  // validate and partition into locals; h->cmds / h->n change only after
+  // every shard staged
+  FH_CHECK(log_off[0] == 0 && log_off[np] == n * desc->views, FH_EINVAL,
+           "logs: every command must appear in exactly `views` replica logs");
+  for (size_t r = 0; r < np; r++)
+    FH_CHECK(log_off[r + 1] >= log_off[r], FH_EINVAL, "logs: offsets");
+  for (uint64_t q = 0; q < log_off[np]; q++)
+    FH_CHECK(log_cmd[q] < n, FH_EINVAL, "logs: command index >= n");
   std::vector<uint32_t> shard_of(n), local(n);
-  h->cmds.assign(G, {});
+  std::vector<std::vector<uint32_t>> cmds(G);
   for (size_t i = 0; i < n; i++) {
     FH_CHECK(key_id[i] < h->cfg.key_space, FH_EINVAL, "key id >= key_space");
     const uint32_t g = uint32_t(key_id[i] % G);
     shard_of[i] = g;
-    local[i] = uint32_t(h->cmds[g].size());
-    h->cmds[g].push_back(uint32_t(i));
+    local[i] = uint32_t(cmds[g].size());
+    cmds[g].push_back(uint32_t(i));
   }
-  FH_CHECK(log_off[np] == n * desc->views, FH_EINVAL,
-           "logs: every command must appear in exactly `views` replica logs");
   per_shard(h, [&](size_t g) {
-    const auto &c = h->cmds[g];
+    const auto &c = cmds[g];
     std::vector<uint64_t> d(c.size()), k(c.size()), off(np + 1, 0);
     for (size_t j = 0; j < c.size(); j++) {
       d[j] = dot[c[j]];
@@ -131,10 +142,8 @@ fh_status fh_multi_stage_logs(fh_multi *h, const fh_stream_desc *desc, const uin
     std::vector<uint32_t> lc;
     lc.reserve(c.size() * desc->views);
     for (size_t r = 0; r < np; r++) {
-      for (uint64_t q = log_off[r]; q < log_off[r + 1]; q++) {
-        FH_CHECK(log_cmd[q] < n, FH_EINVAL, "logs: command index >= n");
+      for (uint64_t q = log_off[r]; q < log_off[r + 1]; q++)
         if (shard_of[log_cmd[q]] == g) lc.push_back(local[log_cmd[q]]);
-      }
       off[r + 1] = lc.size();
     }
     fh_stream_desc sd = *desc;
@@ -142,10 +151,10 @@ fh_status fh_multi_stage_logs(fh_multi *h, const fh_stream_desc *desc, const uin
     check_status(fh_engine_stage_logs(h->eng[g], &sd, 1, d.data(), k.data(), off.data(),
                                       lc.data()));
   });
+  h->cmds.swap(cmds);
   h->desc = *desc;
   h->n = n;
   h->staged = true;
-  h->ran = false;
   FH_API_END
 }
 

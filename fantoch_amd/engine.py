@@ -50,6 +50,18 @@ class Engine:
         """run() stops after the committed deps (fh_engine_set_deps_only)."""
         L.check(self._lib.fh_engine_set_deps_only(self._h, 1 if on else 0))
 
+    def forget_tuning(self):
+        """The next run starts from a fresh engine's tuning guesses
+        (fh_engine_forget_tuning): the cold-run cost of the graph stage."""
+        L.check(self._lib.fh_engine_forget_tuning(self._h))
+
+    def dep_total(self) -> int:
+        """Committed deps of the last run (the CSR's length), no copy."""
+        ln = C.c_size_t(0)
+        L.check(self._lib.fh_engine_results(self._h, None, None, 0, C.byref(ln), None, None,
+                                            None, None))
+        return int(ln.value)
+
     def deps(self):
         """The last run's committed deps only: (dep_off u32[n+1], deps u64)."""
         n = self.n

@@ -85,6 +85,11 @@ impl Engine {
         check(unsafe { ffi::fh_engine_set_deps_only(self.h, on as i32) });
     }
 
+    /// The next run starts from a fresh engine's tuning guesses (cold run).
+    pub fn forget_tuning(&mut self) {
+        check(unsafe { ffi::fh_engine_forget_tuning(self.h) });
+    }
+
     /// The last run's committed deps (dep_off[n + 1], deps).
     pub fn deps(&self) -> (Vec<u32>, Vec<u64>) {
         let mut off = vec![0u32; self.n + 1];

@@ -9,6 +9,22 @@
 //! clock the secondary role answers requests with is the main role's
 //! (`handle_executed`, graph/mod.rs:199-212, becomes a no-op).
 //!
+//! Every FFI sequence on the shared handle runs under one `Mutex` guard (the
+//! runner drives the clones from separate tokio tasks, and `fh_graph` is
+//! single-threaded).  Roles follow the reference's message routing
+//! (executor.rs:242-262): only the main role (executor index 0) adds
+//! vertices, drains ready commands and executes them on its `KVStore`; the
+//! secondary role (index 1) answers other shards' requests and sends the
+//! replies.  A drained dot therefore always reaches the store, monitor and
+//! client channel of the task that added it.
+//!
+//! `Executor::handle` is synchronous per `ExecutionInfo` (the runners drain
+//! `to_clients` after every call: run/task/executor.rs:150-175,
+//! sim/runner.rs:407-413), so an `Add` is one device pass over a batch of
+//! one.  `handle_batch` takes a run of infos at once (replay, benchmarks):
+//! consecutive `Add`s become one `fh_graph_add_batch`, with the same
+//! execution order as one at a time.
+//!
 //! `RequestReply` lives in a private module of fantoch_ps; the binding needs
 //! it re-exported next to `GraphExecutionInfo`
 //! (`pub use graph::{GraphExecutionInfo, GraphExecutor, RequestReply};` in
@@ -27,7 +43,7 @@ use fantoch_ps::executor::{GraphExecutionInfo, RequestReply};
 use fantoch_ps::protocol::common::graph::Dependency;
 use std::collections::VecDeque;
 use std::ptr::null_mut;
-use std::sync::{Arc, Mutex};
+use std::sync::{Arc, Mutex, MutexGuard};
 
 /// MONITOR_PENDING_THRESHOLD (graph/mod.rs:31)
 const MONITOR_PENDING_THRESHOLD_MS: u64 = 1000;
@@ -101,15 +117,23 @@ impl Batch {
 }
 
 impl HipGraphExecutor {
-    fn handle_ptr(&self) -> *mut ffi::FhGraph {
-        self.shared.lock().unwrap().h.0
+    /// The shared state, locked for a whole FFI sequence.  The guard borrows
+    /// the `Arc` passed in (a clone), not `self`, so the caller can still
+    /// update its own queues and metrics while holding it.
+    fn lock(shared: &Arc<Mutex<Shared>>) -> MutexGuard<'_, Shared> {
+        shared.lock().unwrap()
+    }
+
+    fn is_main(&self) -> bool {
+        self.executor_index == 0
     }
 
     /// DependencyGraph::handle_add for a run of adds (graph/mod.rs:215-277):
     /// the device finds every SCC whose reachable set is complete, in the
-    /// order the incremental Tarjan would have executed them.
-    fn add_batch(&mut self, adds: Vec<(Dot, Command, Vec<Dependency>)>, time: &dyn SysTime) {
-        let mut sh = self.shared.lock().unwrap();
+    /// order the incremental Tarjan would have executed them.  Main role only.
+    fn add_batch(&mut self, sh: &mut Shared, adds: Vec<(Dot, Command, Vec<Dependency>)>,
+                 time: &dyn SysTime) {
+        assert!(self.is_main(), "only executor 0 adds vertices (executor.rs:242-262)");
         let mut b = Batch::new();
         for (dot, cmd, deps) in adds {
             b.push(self.shard_id, &mut sh.keys, dot, &cmd, deps);
@@ -130,21 +154,25 @@ impl HipGraphExecutor {
         });
     }
 
-    /// fetch_actions (executor.rs:114-122)
-    fn fetch_actions(&mut self, time: &dyn SysTime) {
-        self.fetch_commands_to_execute();
-        self.fetch_metrics();
-        if self.config.shard_count() > 1 {
-            self.fetch_requests();
-            self.fetch_request_replies();
+    /// fetch_actions (executor.rs:114-122), under the caller's guard
+    fn fetch_actions(&mut self, sh: &mut Shared) {
+        if self.is_main() {
+            self.fetch_commands_to_execute(sh);
+            self.fetch_metrics(sh);
         }
-        let _ = time;
+        if self.config.shard_count() > 1 {
+            if self.is_main() {
+                self.fetch_requests(sh);
+            } else {
+                self.fetch_request_replies(sh);
+            }
+        }
     }
 
     /// fetch_commands_to_execute (executor.rs:124-145): drained dots in
     /// execution order, executed on the KVStore + monitor.
-    fn fetch_commands_to_execute(&mut self) {
-        let h = self.handle_ptr();
+    fn fetch_commands_to_execute(&mut self, sh: &mut Shared) {
+        let h = sh.h.0;
         let len = crate::sized(|cap, len| unsafe {
             ffi::fh_graph_drain(h, null_mut(), null_mut(), cap, len)
         });
@@ -154,22 +182,16 @@ impl HipGraphExecutor {
         let mut dots = vec![0u64; len];
         let mut got = 0usize;
         check(unsafe { ffi::fh_graph_drain(h, dots.as_mut_ptr(), null_mut(), len, &mut got) });
-        let cmds: Vec<Command> = {
-            let mut sh = self.shared.lock().unwrap();
-            dots[..got]
-                .iter()
-                .map(|d| sh.cmds.remove(&unpack(*d)).expect("drained dot has a command"))
-                .collect()
-        };
-        for cmd in cmds {
+        for d in &dots[..got] {
+            let cmd = sh.cmds.remove(&unpack(*d)).expect("drained dot has a command");
             self.execute(cmd);
         }
     }
 
     /// ChainSize / ExecutionDelay collected on the device side (save_scc,
     /// graph/mod.rs:490-525)
-    fn fetch_metrics(&mut self) {
-        let h = self.handle_ptr();
+    fn fetch_metrics(&mut self, sh: &mut Shared) {
+        let h = sh.h.0;
         let (mut nc, mut nd) = (0usize, 0usize);
         let st = unsafe {
             ffi::fh_graph_take_metrics(h, null_mut(), 0, null_mut(), 0, &mut nc, &mut nd)
@@ -191,8 +213,8 @@ impl HipGraphExecutor {
     }
 
     /// fetch_requests (executor.rs:161-174; graph/mod.rs:147-150)
-    fn fetch_requests(&mut self) {
-        let h = self.handle_ptr();
+    fn fetch_requests(&mut self, sh: &mut Shared) {
+        let h = sh.h.0;
         let len = crate::sized(|cap, len| unsafe {
             ffi::fh_graph_requests(h, null_mut(), null_mut(), cap, len)
         });
@@ -216,8 +238,8 @@ impl HipGraphExecutor {
     }
 
     /// fetch_request_replies (executor.rs:176-189; graph/mod.rs:152-157)
-    fn fetch_request_replies(&mut self) {
-        let h = self.handle_ptr();
+    fn fetch_request_replies(&mut self, sh: &mut Shared) {
+        let h = sh.h.0;
         let (mut nr, mut nd) = (0usize, 0usize);
         let st = unsafe {
             ffi::fh_graph_request_replies(h, 0, null_mut(), null_mut(), null_mut(), null_mut(),
@@ -235,7 +257,6 @@ impl HipGraphExecutor {
                 dot.as_mut_ptr(), cshard.as_mut_ptr(), off.as_mut_ptr(), nd, ddot.as_mut_ptr(),
                 dshard.as_mut_ptr(), &mut nr, &mut nd)
         });
-        let sh = self.shared.lock().unwrap();
         let mut by_shard: HashMap<ShardId, Vec<RequestReply>> = HashMap::new();
         for i in 0..nr {
             let d = unpack(dot[i]);
@@ -251,7 +272,6 @@ impl HipGraphExecutor {
             };
             by_shard.entry(to[i]).or_default().push(reply);
         }
-        drop(sh);
         for (to, infos) in by_shard {
             self.to_executors.push((to, GraphExecutionInfo::RequestReply { infos }));
         }
@@ -261,6 +281,35 @@ impl HipGraphExecutor {
     fn execute(&mut self, cmd: Command) {
         let results = cmd.execute(self.shard_id, &mut self.store, &mut self.monitor);
         self.to_clients.extend(results);
+    }
+
+    /// A run of infos at once: consecutive `Add`s go to the device as one
+    /// batch (one `fh_graph_add_batch`, the same execution order as one add
+    /// at a time); anything else is handled in place, in order.
+    pub fn handle_batch(&mut self, infos: Vec<GraphExecutionInfo>, time: &dyn SysTime) {
+        let mut run = Vec::new();
+        for info in infos {
+            match info {
+                GraphExecutionInfo::Add { dot, cmd, deps } if !self.config.execute_at_commit() => {
+                    run.push((dot, cmd, deps.into_iter().collect()));
+                }
+                other => {
+                    self.flush_adds(&mut run, time);
+                    self.handle(other, time);
+                }
+            }
+        }
+        self.flush_adds(&mut run, time);
+    }
+
+    fn flush_adds(&mut self, run: &mut Vec<(Dot, Command, Vec<Dependency>)>, time: &dyn SysTime) {
+        if run.is_empty() {
+            return;
+        }
+        let shared = Arc::clone(&self.shared);
+        let mut sh = Self::lock(&shared);
+        self.add_batch(&mut sh, std::mem::take(run), time);
+        self.fetch_actions(&mut sh);
     }
 }
 
@@ -299,11 +348,17 @@ impl Executor for HipGraphExecutor {
         self.executor_index = index;
     }
 
-    /// cleanup (executor.rs:65-70) -> check_pending_requests (mod.rs:168-179)
+    /// cleanup (executor.rs:65-70) -> check_pending_requests (mod.rs:168-179):
+    /// buffered requests are retried by the role that answers them
     fn cleanup(&mut self, time: &dyn SysTime) {
+        let _ = time;
         if self.config.shard_count() > 1 {
-            check(unsafe { ffi::fh_graph_cleanup(self.handle_ptr()) });
-            self.fetch_actions(time);
+            let shared = Arc::clone(&self.shared);
+            let mut sh = Self::lock(&shared);
+            if !self.is_main() {
+                check(unsafe { ffi::fh_graph_cleanup(sh.h.0) });
+            }
+            self.fetch_actions(&mut sh);
         }
     }
 
@@ -311,10 +366,12 @@ impl Executor for HipGraphExecutor {
     /// 53-103): pending commands older than 1 s are reported, and one without
     /// missing dependencies panics (FH_EINVARIANT -> check).
     fn monitor_pending(&mut self, time: &dyn SysTime) {
-        if self.executor_index != 0 {
+        if !self.is_main() {
             return;
         }
-        let h = self.handle_ptr();
+        let shared = Arc::clone(&self.shared);
+        let sh = Self::lock(&shared);
+        let h = sh.h.0;
         check(unsafe { ffi::fh_graph_set_time(h, time.millis()) });
         let len = crate::sized(|cap, len| unsafe {
             ffi::fh_graph_monitor_pending(h, MONITOR_PENDING_THRESHOLD_MS, null_mut(),
@@ -326,6 +383,7 @@ impl Executor for HipGraphExecutor {
             ffi::fh_graph_monitor_pending(h, MONITOR_PENDING_THRESHOLD_MS, dots.as_mut_ptr(),
                 ms.as_mut_ptr(), missing.as_mut_ptr(), len, &mut got)
         });
+        drop(sh);
         for i in 0..got {
             tracing::info!(
                 "p{}: {:?} is pending for {:?}ms | missing {} dependencies",
@@ -337,48 +395,50 @@ impl Executor for HipGraphExecutor {
         }
     }
 
-    /// handle (executor.rs:76-100)
+    /// handle (executor.rs:76-100).  Add and RequestReply come to executor 0,
+    /// Request and Executed to executor 1 (executor.rs:242-262).
     fn handle(&mut self, info: GraphExecutionInfo, time: &dyn SysTime) {
+        let shared = Arc::clone(&self.shared);
         match info {
             GraphExecutionInfo::Add { dot, cmd, deps } => {
                 if self.config.execute_at_commit() {
                     self.execute(cmd);
                 } else {
-                    self.add_batch(vec![(dot, cmd, deps.into_iter().collect())], time);
-                    self.fetch_actions(time);
+                    let mut sh = Self::lock(&shared);
+                    self.add_batch(&mut sh, vec![(dot, cmd, deps.into_iter().collect())], time);
+                    self.fetch_actions(&mut sh);
                 }
             }
             GraphExecutionInfo::Request { from, dots } => {
                 self.metrics.aggregate(ExecutorMetricsKind::InRequests, 1);
                 let d: Vec<u64> = dots.into_iter().map(pack).collect();
-                check(unsafe {
-                    ffi::fh_graph_handle_requests(self.handle_ptr(), from, d.len(), d.as_ptr())
-                });
-                self.fetch_actions(time);
+                let mut sh = Self::lock(&shared);
+                check(unsafe { ffi::fh_graph_handle_requests(sh.h.0, from, d.len(), d.as_ptr()) });
+                self.fetch_actions(&mut sh);
             }
             GraphExecutionInfo::RequestReply { infos } => {
                 // in reply order (graph/mod.rs:377-408): runs of Info replies
                 // are add batches, Executed updates the clock + retries
                 self.metrics.aggregate(ExecutorMetricsKind::InRequestReplies, 1);
+                let mut sh = Self::lock(&shared);
                 let mut run = Vec::new();
                 for info in infos {
                     match info {
                         RequestReply::Info { dot, cmd, deps } => run.push((dot, cmd, deps)),
                         RequestReply::Executed { dot } => {
                             if !run.is_empty() {
-                                self.add_batch(std::mem::take(&mut run), time);
+                                self.add_batch(&mut sh, std::mem::take(&mut run), time);
                             }
-                            let h = self.handle_ptr();
                             let d = [pack(dot)];
-                            check(unsafe { ffi::fh_graph_mark_executed(h, 1, d.as_ptr()) });
-                            self.add_batch(Vec::new(), time); // check_pending
+                            check(unsafe { ffi::fh_graph_mark_executed(sh.h.0, 1, d.as_ptr()) });
+                            self.add_batch(&mut sh, Vec::new(), time); // check_pending
                         }
                     }
                 }
                 if !run.is_empty() {
-                    self.add_batch(run, time);
+                    self.add_batch(&mut sh, run, time);
                 }
-                self.fetch_actions(time);
+                self.fetch_actions(&mut sh);
             }
             GraphExecutionInfo::Executed { .. } => {
                 // handle_executed: the shared handle already holds the clock
@@ -404,5 +464,65 @@ impl Executor for HipGraphExecutor {
 
     fn monitor(&self) -> Option<&ExecutionOrderMonitor> {
         self.monitor.as_ref()
+    }
+}
+
+#[cfg(test)]
+mod tests {
+    //! Needs a GPU (the handle is a real `fh_graph`): the two roles of one
+    //! shard driven from two threads, as the runner's tokio tasks drive the
+    //! clones (run/task/executor.rs:33-48).
+    use super::*;
+    use fantoch::id::Rifl;
+    use fantoch::kvs::KVOp;
+    use fantoch::time::RunTime;
+    use std::thread;
+
+    #[test]
+    fn two_roles_from_two_threads() {
+        let mut config = Config::new(3, 1);
+        config.set_shard_count(2);
+        let mut main = HipGraphExecutor::new(1, 0, config);
+        let mut secondary = main.clone();
+        secondary.set_executor_index(1);
+        let n = 2000u64;
+        let adder = thread::spawn(move || {
+            let time = RunTime;
+            for seq in 1..=n {
+                let dot = Dot::new(1, seq);
+                let key = format!("k{}", seq % 7);
+                let cmd = Command::from(Rifl::new(1, seq), vec![(key, KVOp::Put(String::new()))]);
+                // each command depends on the previous one: a chain
+                let deps = if seq > 1 {
+                    let mut s = HashSet::new();
+                    s.insert(Dependency { dot: Dot::new(1, seq - 1), shards: Some(
+                        std::iter::once(0u64).collect()) });
+                    s
+                } else {
+                    HashSet::new()
+                };
+                main.handle(GraphExecutionInfo::Add { dot, cmd, deps }, &time);
+            }
+            let mut results = 0usize;
+            while main.to_clients().is_some() {
+                results += 1;
+            }
+            results
+        });
+        let answerer = thread::spawn(move || {
+            let time = RunTime;
+            for i in 0..n {
+                // requests from the other shard for dots this shard holds or
+                // will hold; answered (Info / Executed) or buffered
+                let dots = std::iter::once(Dot::new(1, 1 + i % n)).collect();
+                secondary.handle(GraphExecutionInfo::Request { from: 1, dots }, &time);
+                secondary.cleanup(&time);
+                // the secondary role never executes commands
+                assert!(secondary.to_clients().is_none());
+            }
+        });
+        // every command executed exactly once, all by the main role
+        assert_eq!(adder.join().unwrap(), n as usize);
+        answerer.join().unwrap();
     }
 }

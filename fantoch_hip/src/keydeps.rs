@@ -184,18 +184,28 @@ impl KeyDeps for HipKeyDeps {
         self.noop(dot)
     }
 
-    #[cfg(test)]
-    fn cmd_deps(&self, cmd: &Command) -> HashSet<Dot> {
-        self.query_cmd_deps(cmd)
-    }
-
-    #[cfg(test)]
-    fn noop_deps(&self) -> HashSet<Dot> {
-        self.query_noop_deps()
-    }
+    // cmd_deps / noop_deps are #[cfg(test)] items of the trait
+    // (keys/mod.rs:54-60): they exist only while fantoch_ps compiles its own
+    // unit tests, and those never see this crate (it depends on fantoch_ps,
+    // not the other way round).  Implementing them here under this crate's
+    // cfg(test) would name trait items that do not exist (E0407) in
+    // `cargo test -p fantoch_hip`, so the queries are the inherent
+    // `query_cmd_deps` / `query_noop_deps` instead.
 
     fn parallel() -> bool {
         false // SequentialKeyDeps::parallel (sequential.rs:60-62)
+    }
+}
+
+impl HipLockedKeyDeps {
+    /// KeyDeps::cmd_deps (keys/mod.rs:54-56) as an inherent method.
+    pub fn query_cmd_deps(&self, cmd: &Command) -> HashSet<Dot> {
+        self.0.query_cmd_deps(cmd)
+    }
+
+    /// KeyDeps::noop_deps (keys/mod.rs:58-60) as an inherent method.
+    pub fn query_noop_deps(&self) -> HashSet<Dot> {
+        self.0.query_noop_deps()
     }
 }
 
@@ -218,15 +228,7 @@ impl KeyDeps for HipLockedKeyDeps {
         self.0.noop(dot)
     }
 
-    #[cfg(test)]
-    fn cmd_deps(&self, cmd: &Command) -> HashSet<Dot> {
-        self.0.query_cmd_deps(cmd)
-    }
-
-    #[cfg(test)]
-    fn noop_deps(&self) -> HashSet<Dot> {
-        self.0.query_noop_deps()
-    }
+    // (cmd_deps / noop_deps: see HipKeyDeps)
 
     // LockedKeyDeps::parallel() is true (locked.rs:70-72); the handle is
     // behind the Arc<Mutex>, so concurrent protocol workers serialise on it

@@ -502,6 +502,13 @@ fh_status fh_engine_set_profiling(fh_engine *h, int on);
  * cross-shard union (MShardCommit, atlas.rs:559-639).  results() then
  * returns the deps only (FH_EINVAL for labels, ranks or per-key output). */
 fh_status fh_engine_set_deps_only(fh_engine *h, int on);
+/* Forget what earlier runs taught the graph stage: the tile kernel's first
+ * reach bound (the last run's maximum excess, plus a margin) and the global
+ * path's entry (straight to the full coloring when the last run needed it).
+ * The next run starts from the defaults, as on a fresh engine; results are
+ * the same either way (every run re-checks its certificate).  For cold-run
+ * measurements. */
+fh_status fh_engine_forget_tuning(fh_engine *h);
 
 /* ======================================================================
  * Multi-GPU fused engine from one process: one engine

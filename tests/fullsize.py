@@ -25,10 +25,35 @@ CONFIGS = {
     "c3": dict(desc="C3 EPaxos ConflictPool 100% (key 0 + 16-key pool), 2 keys: deps at 10M, "
                     "everything on the first 50k", n=10_000_000, prefix=50_000,
                workload=lambda: Workload.conflict_pool(100, 16, k=2, seed=SEED + 3, **KW)),
-    "c5": dict(desc="C5 Zipf 0.99 over 2^20 keys, 4 keys: deps at 12.5M, everything on the "
-                    "first 30k", n=12_500_000, prefix=30_000,
+    # the 4-key stream's first 12.5M commands, unsharded (one KeyDeps per
+    # replica over all keys): deps at 12.5M, everything on the first 30k
+    "c5_12m": dict(desc="Zipf 0.99 over 2^20 keys, 4 keys, unsharded: deps at 12.5M, everything "
+                        "on the first 30k", n=12_500_000, prefix=30_000,
+                   workload=lambda: Workload.zipf(0.99, 1 << 20, k=4, seed=SEED + 5, **KW)),
+    # C5 as BASELINE.json states it: the same 4-key stream at 100M commands,
+    # partially replicated over 8 key shards (shard = key mod 8).  Each shard's
+    # replicas run KeyDeps over the command's keys on that shard only
+    # (Command::keys(shard), command.rs:95-100) and the committed deps are the
+    # union over the shards' reports (MShardCommit, atlas.rs:580-583).
+    "c5": dict(desc="C5 Atlas partial replication, 8 key shards (key mod 8), Zipf 0.99 over 2^20 "
+                    "keys, 4 keys/cmd, 100M commands: committed deps = union over shards",
+               n=100_000_000, shards=8,
                workload=lambda: Workload.zipf(0.99, 1 << 20, k=4, seed=SEED + 5, **KW)),
 }
+
+
+def shard_stream(s, nshards: int, shard: int):
+    """Shard `shard`'s part of a stream with replica views (key = global id):
+    (global command indices with a key on the shard, key_off CSR, the keys on
+    the shard in the command's key order).  The shard's replicas see these
+    commands in the stream's per-replica arrival order (fq_proc / fq_time of
+    the command)."""
+    mine = s.keys % np.uint64(nshards) == np.uint64(shard)
+    cnt = mine.sum(axis=1)
+    cmds = np.nonzero(cnt)[0]
+    key_off = np.zeros(len(cmds) + 1, dtype=np.uint32)
+    np.cumsum(cnt[cmds], out=key_off[1:])
+    return cmds, key_off, s.keys[cmds][mine[cmds]]
 
 
 def _sha(*arrays):
@@ -59,53 +84,84 @@ def cmd_index(dots, n, first=0):
     return (q - 1) * n + (p - 1) - first
 
 
-def check_properties(s, r):
+def check_properties(s, r, chunk=1 << 24, log=None):
     """Full-size properties of an engine result on stream s (no oracle):
     * execution order respects every dependency edge across SCCs;
-    * inside an SCC the execution order is dot order;
-    * per-key sequences hold exactly each key's commands;
-    * the SCC partition equals an independent SCC computation (scipy) over
-      the committed deps, and every SCC's label is its minimum dot."""
+    * inside an SCC the execution order is dot order, SCC members are
+      contiguous in it, and every SCC's label is its minimum dot;
+    * per-key sequences hold exactly each key's commands, in execution order;
+    * the SCC partition equals an independent SCC computation (scipy's
+      strongly connected components, Pearce's algorithm) over the committed
+      deps.
+    Linear-time and chunked (C5 at 100M: 856M deps, 400M per-key elements)."""
+    log = log or (lambda m: None)
     n = s.n
     dep_off = r["dep_off"].astype(np.int64)
     deps = r["deps"]
     lab = r["scc_label"]
     rank = r["exec_rank"].astype(np.int64)
-    assert np.array_equal(np.sort(rank), np.arange(n)), "exec ranks are a permutation"
-    first = 0
-    idx = cmd_index(deps, 5, first)
-    src = np.repeat(np.arange(n), np.diff(dep_off))
-    inb = (idx >= 0) & (idx < n)
-    src_i, dst_i = src[inb], idx[inb]
-    assert np.array_equal(s.dots[dst_i], deps[inb]), "dep dots resolve to stream commands"
-    cross = lab[src_i] != lab[dst_i]
-    assert np.all(rank[dst_i[cross]] < rank[src_i[cross]]), "deps across SCCs execute first"
-    # dot order inside SCCs along the execution order
-    order = np.argsort(rank)
+    assert rank.min() >= 0 and rank.max() < n, "exec ranks in range"
+    assert np.all(np.bincount(rank, minlength=n) == 1), "exec ranks are a permutation"
+    order = np.empty(n, dtype=np.int64)
+    order[rank] = np.arange(n)
+    # every dependency: a stream command, in the same SCC or executed earlier
+    idx = np.empty(len(deps), dtype=np.int32)
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        e0, e1 = int(dep_off[c0]), int(dep_off[c1])
+        d = cmd_index(deps[e0:e1], 5)
+        assert d.min(initial=0) >= 0 and d.max(initial=-1) < n, "deps are stream commands"
+        assert np.array_equal(s.dots[d], deps[e0:e1]), "dep dots resolve to stream commands"
+        src = np.repeat(np.arange(c0, c1), np.diff(dep_off[c0:c1 + 1]))
+        cross = lab[src] != lab[d]
+        assert np.all(rank[d[cross]] < rank[src[cross]]), "deps across SCCs execute first"
+        idx[e0:e1] = d
+    log("properties: dependency edges ok")
+    # SCCs along the execution order: contiguous, dot order inside, label =
+    # the first (= minimum) member's dot
     lo, do = lab[order], s.dots[order]
-    same = lo[1:] == lo[:-1]
-    assert np.all(do[1:][same] > do[:-1][same]), "SCC members run in dot order"
-    # SCC members contiguous in execution order
-    starts = np.concatenate([[True], lo[1:] != lo[:-1]])
-    assert len(np.unique(lo)) == int(starts.sum()), "SCC members contiguous"
-    # labels are the min dot
-    u, inv = np.unique(lab, return_inverse=True)
-    mn = np.full(len(u), np.iinfo(np.uint64).max, dtype=np.uint64)
-    np.minimum.at(mn, inv, s.dots)
-    assert np.array_equal(mn, u), "label = min dot of the SCC"
-    # per-key sequences: each key's commands, in execution order
-    keys = s.keys.reshape(-1)
-    cnt = np.bincount(keys.astype(np.int64), minlength=s.key_space)
-    assert np.array_equal(np.diff(r["key_off"].astype(np.int64)), cnt), "per-key lengths"
-    kcmd = np.repeat(np.arange(n), s.k)
-    want = np.lexsort((rank[kcmd], keys))
-    assert np.array_equal(r["key_seq"], s.dots[kcmd[want]]), "per-key sequence = exec order"
-    # the SCC partition itself, recomputed independently over the committed
-    # deps (scipy's strongly connected components, Pearce's algorithm)
+    head = np.ones(n, dtype=bool)
+    head[1:] = lo[1:] != lo[:-1]
+    inner = ~head[1:]
+    assert np.all(do[1:][inner] > do[:-1][inner]), "SCC members run in dot order"
+    assert np.array_equal(lo[head], do[head]), "label = min dot of the SCC"
+    heads = lo[head]
+    nscc = len(heads)
+    assert len(np.unique(heads)) == nscc, "SCC members contiguous in the execution order"
+    del lo, do, head, inner, heads
+    log("properties: SCC order and labels ok")
+    # per-key sequences: each key's commands in execution order
+    keys = s.keys
+    cnt = np.bincount(keys.reshape(-1).astype(np.int64), minlength=s.key_space)
+    key_off = r["key_off"].astype(np.int64)
+    assert np.array_equal(np.diff(key_off), cnt), "per-key lengths"
+    seq = r["key_seq"]
+    nel = len(seq)
+    for j0 in range(0, nel, chunk):
+        j1 = min(nel, j0 + chunk)
+        c = cmd_index(seq[j0:j1], 5)
+        assert c.min(initial=0) >= 0 and c.max(initial=-1) < n, "per-key dots are commands"
+        kk = np.searchsorted(key_off, np.arange(j0, j1), side="right") - 1
+        assert np.all((keys[c] == kk[:, None].astype(np.uint64)).any(axis=1)), \
+            "per-key element of a command holding the key"
+        rk = rank[c]
+        same = kk[1:] == kk[:-1]
+        assert np.all(rk[1:][same] > rk[:-1][same]), "per-key sequence in execution order"
+        if j1 < nel:  # the seam between chunks
+            c2 = cmd_index(seq[j1:j1 + 1], 5)
+            k2 = np.searchsorted(key_off, j1, side="right") - 1
+            assert k2 != kk[-1] or rank[c2[0]] > rk[-1], "per-key sequence in execution order"
+    # (every element belongs to a command holding its key, each key's ranks
+    # strictly increase and the per-key counts match: exactly the pairs)
+    log("properties: per-key sequences ok")
+    # the SCC partition itself, recomputed independently (scipy)
     from scipy.sparse import csr_matrix
     from scipy.sparse.csgraph import connected_components
-    g = csr_matrix((np.ones(len(src_i), dtype=np.int8), (src_i, dst_i)), shape=(n, n))
+    g = csr_matrix((np.ones(len(idx), dtype=np.int8), idx, dep_off), shape=(n, n))
     ncomp, comp = connected_components(g, directed=True, connection="strong")
-    assert ncomp == len(u), "number of SCCs"
-    pairs = np.unique(comp.astype(np.int64) * len(u) + inv)
-    assert len(pairs) == ncomp, "SCC partition equals an independent SCC computation"
+    del g, idx
+    log(f"properties: scipy SCC done ({ncomp} SCCs)")
+    assert ncomp == nscc, "number of SCCs"
+    lab_of = np.empty(ncomp, dtype=np.uint64)
+    lab_of[comp] = lab
+    assert np.array_equal(lab_of[comp], lab), "SCC partition equals an independent SCC computation"

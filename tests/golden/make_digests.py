@@ -41,7 +41,8 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(HERE))
 
-from fullsize import CONFIGS, cmd_index, digest_deps, digest_labels, digest_perkey  # noqa: E402
+from fullsize import (CONFIGS, cmd_index, digest_deps, digest_labels, digest_perkey,  # noqa: E402
+                      shard_stream)
 
 OUT = os.path.join(HERE, "digests.json")
 
@@ -54,6 +55,48 @@ def oracle_all(s):
     ex, lab, kso, ks = O.graph_run(s.dots, ko, kk, off, deps, s.key_space)
     assert len(ex) == s.n
     return off, deps, ex, lab, kso, ks
+
+
+def sharded_union(s, nshards):
+    """Partial replication (C5): every shard's replicas run the oracle's
+    per-replica SequentialKeyDeps + fast-quorum union over the commands' keys
+    on that shard (fo_views_run on the shard's part, tests/fullsize.py
+    shard_stream); a command's committed deps are the union over the shards
+    that replicate it (MShardCommit, atlas.rs:559-639, union :580-583).
+    Records are packed as command << 32 | source << 28 | sequence (the
+    generator's dots: source <= 5, sequence < 2^28), so one u64 sort + unique
+    is the union and leaves each row in ascending dot order."""
+    from oracle import oracle as O
+    n = s.n
+    assert n < (1 << 31) and int((s.dots & np.uint64((1 << 56) - 1)).max()) < (1 << 28)
+    assert int((s.dots >> np.uint64(56)).max()) < 8
+    recs = []
+    for sh in range(nshards):
+        t0 = time.time()
+        cmds, ko, kk = shard_stream(s, nshards, sh)
+        off, deps = O.views_run(0, 5, s.dots[cmds], ko, kk, s.fq_proc[cmds], s.fq_time[cmds])
+        per = np.diff(off.astype(np.int64))
+        r = np.repeat(cmds.astype(np.uint64), per) << np.uint64(32)
+        r |= (deps >> np.uint64(56)) << np.uint64(28)
+        r |= deps & np.uint64((1 << 28) - 1)
+        recs.append(r)
+        del off, deps, per, cmds, ko, kk
+        print(f"  shard {sh}: {len(r)} records, {time.time() - t0:.0f}s", flush=True)
+    rec = np.concatenate(recs)
+    del recs
+    rec.sort()
+    keep = np.ones(len(rec), dtype=bool)
+    keep[1:] = rec[1:] != rec[:-1]
+    rec = rec[keep]
+    del keep
+    cmd = (rec >> np.uint64(32)).astype(np.int64)
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(cmd, minlength=n), out=off[1:])
+    del cmd
+    lo = rec & np.uint64(0xFFFFFFFF)
+    del rec
+    deps = ((lo >> np.uint64(28)) << np.uint64(56)) | (lo & np.uint64((1 << 28) - 1))
+    return off.astype(np.uint32), deps
 
 
 def labels_in_command_order(s, ex, lab, first=0):
@@ -89,6 +132,10 @@ def main():
             labels[np.array([pos[int(d)] for d in ex.tolist()])] = lab
             entry.update(n=int(s.n), deps=digest_deps(off, deps), labels=digest_labels(labels),
                          perkey=digest_perkey(kso, ks))
+        elif "shards" in c:
+            off, deps = sharded_union(w.generate(c["n"]), c["shards"])
+            entry.update(n=int(c["n"]), shards=c["shards"], deps=digest_deps(off, deps),
+                         ndeps=int(off[-1]))
         elif "prefix" in c:
             s = w.generate(c["n"])
             ko = s.key_off()

@@ -45,3 +45,28 @@ def test_multi_rejects_multi_key_streams():
     m = MultiEngine(s.key_space, [0, 0])
     with pytest.raises(L.FhError):
         m.stage(s)
+
+
+def test_multi_failed_staging_leaves_nothing_to_run():
+    """A staging that fails validation (a key id >= key_space) drops the
+    previous staging: run() and results() refuse instead of combining the new
+    partition with the old engines."""
+    from fantoch_amd import _lib as L
+    w = Workload.zipf(0.99, 1 << 10, k=1, views=3, window=64, seed=5)
+    s = w.generate(5000, logs=True)
+    m = MultiEngine(s.key_space, [0, 0])
+    m.stage(s)
+    m.run()
+    assert len(m.results()["deps"]) > 0
+    bad = w.generate(7000, logs=True)
+    bad.keys[123, 0] = np.uint64(s.key_space)  # out of the key space
+    with pytest.raises(L.FhError):
+        m.stage(bad)
+    with pytest.raises(L.FhError):
+        m.results()
+    with pytest.raises(L.FhError):
+        m.run()
+    # a good staging afterwards works again
+    m.stage(s)
+    m.run()
+    assert len(m.results()["deps"]) > 0
