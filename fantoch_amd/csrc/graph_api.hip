@@ -448,20 +448,11 @@ struct GraphDevice {
     gin.want_per_key = false;  // the executor's monitor is fed from the drain order
     GraphOutput out;
     core.run(gin, out);
-    // the batch joins the host's pending metadata (executed ones leave below;
-    // after the pass, so a failed pass leaves host and device sets equal)
-    for (size_t i = 0; i < n; i++) {
-      PInfo pi;
-      pi.seq = next_seq++;
-      pi.cshard = cmd_shards ? cmd_shards[i] : 0;
-      pi.time = now_ms;
-      pi.deps.assign(dep_dot + dep_off[i], dep_dot + dep_off[i + 1]);
-      pi.dshards.resize(pi.deps.size(), 0);
-      if (dep_shards)
-        std::copy(dep_shards + dep_off[i], dep_shards + dep_off[i + 1], pi.dshards.begin());
-      porder.emplace(pi.seq, dot[i]);
-      pend.emplace(dot[i], std::move(pi));
-    }
+    // which batch vertices stay pending: only those get host metadata (a
+    // batch vertex executed in this pass needs none: its execution delay is 0)
+    std::vector<uint8_t> bflag(n);
+    if (n && out.blocked)
+      FH_HIP(hipMemcpyAsync(bflag.data(), out.blocked + P, n, hipMemcpyDeviceToHost, stream));
     // executed vertices to the host: dots and labels in execution order
     const uint32_t nexec = out.nexec;
     std::vector<uint64_t> xdot(nexec), xlab(nexec);
@@ -538,11 +529,30 @@ struct GraphDevice {
       if (j == 0 || xlab[j - 1] != xlab[j]) m_chain.push_back(0);
       m_chain.back()++;
       auto it = pend.find(d);
-      FH_CHECK(it != pend.end(), FH_EINVARIANT, "graph: executed dot was not a vertex");
-      m_delay.push_back(now_ms >= it->second.time ? now_ms - it->second.time : 0);
-      porder.erase(it->second.seq);
-      pend.erase(it);
+      if (it != pend.end()) {  // a carried vertex
+        m_delay.push_back(now_ms >= it->second.time ? now_ms - it->second.time : 0);
+        porder.erase(it->second.seq);
+        pend.erase(it);
+      } else {  // a vertex of this batch (stamped now)
+        m_delay.push_back(0);
+      }
     }
+    // the batch's survivors join the host's pending metadata, in arrival
+    // order (after the pass: a failed pass leaves host and device sets equal)
+    for (size_t i = 0; i < n; i++) {
+      if (!bflag[i]) continue;
+      PInfo pi;
+      pi.seq = next_seq++;
+      pi.cshard = cmd_shards ? cmd_shards[i] : 0;
+      pi.time = now_ms;
+      pi.deps.assign(dep_dot + dep_off[i], dep_dot + dep_off[i + 1]);
+      pi.dshards.resize(pi.deps.size(), 0);
+      if (dep_shards)
+        std::copy(dep_shards + dep_off[i], dep_shards + dep_off[i + 1], pi.dshards.begin());
+      porder.emplace(pi.seq, dot[i]);
+      pend.emplace(dot[i], std::move(pi));
+    }
+    FH_CHECK(pend.size() == P2, FH_EINVARIANT, "graph: host pending set disagrees with the pass");
     std::sort(mlist.begin(), mlist.end());
     mlist.erase(std::unique(mlist.begin(), mlist.end()), mlist.end());
     missing_now.swap(mlist);

@@ -6,7 +6,7 @@ fantoch_ps/src/executor/graph/executor.rs:19-197:
 
     Executor::new(process_id, shard_id, config)   -> HipGraphExecutor(process_id, shard_id, n, f)
     handle(GraphExecutionInfo::Add{dot,cmd,deps})  -> handle(GraphExecutionInfo.add(dot, cmd, deps))
-    to_clients() -> Option<ExecutorResult>         -> to_clients() -> (rifl, key) | None
+    to_clients() -> Option<ExecutorResult>         -> to_clients() -> ExecutorResult(rifl, key, op_result) | None
     monitor() -> Option<&ExecutionOrderMonitor>    -> monitor() -> {key: [rifl, ...]}
     parallel() -> bool                             -> parallel() (True, like GraphExecutor)
 
@@ -34,6 +34,7 @@ import numpy as np
 
 from . import _lib as L
 from .keydeps import Dependency, KeyInterner, make_config
+from .kvs import ExecutorResult, KVStore
 
 
 @dataclass
@@ -101,6 +102,11 @@ class HipGraphExecutor:
         self._cmds = {}          # dot -> command, until executed
         self._to_clients = deque()
         self._monitor = {} if monitor else None
+        self.store = KVStore()  # GraphExecutor's KVStore (executor.rs:29, 191-196)
+        # request replies taken from the handle as soon as they are made, with
+        # the command attached then (process_requests clones vertex.cmd when
+        # it answers, graph/mod.rs:323-330: a later execution must not lose it)
+        self._replies = {}
 
     def close(self):
         if getattr(self, "_h", None):
@@ -176,6 +182,7 @@ class HipGraphExecutor:
         a = np.asarray(list(dots), dtype=np.uint64)
         L.check(self._lib.fh_graph_handle_requests(self._h, from_shard, len(a),
                                                    L.ptr(a) if len(a) else None))
+        self._take_replies()
 
     def handle_request_reply(self, replies):
         """In reply order (mod.rs:377-408): each run of consecutive Info
@@ -236,6 +243,7 @@ class HipGraphExecutor:
     def cleanup(self):
         """Executor::cleanup -> check_pending_requests (mod.rs:168-179)."""
         L.check(self._lib.fh_graph_cleanup(self._h))
+        self._take_replies()
 
     def requests(self):
         """fetch_requests: {target shard: set(dots)} (mod.rs:147-150)."""
@@ -254,12 +262,18 @@ class HipGraphExecutor:
         return out
 
     def request_replies(self):
-        """fetch_request_replies: {to shard: [RequestReply]} (mod.rs:152-157)."""
+        """fetch_request_replies: {to shard: [RequestReply]} (mod.rs:152-157),
+        taken."""
+        self._take_replies()
+        out, self._replies = self._replies, {}
+        return out
+
+    def _take_replies(self):
         nr, nd = C.c_size_t(0), C.c_size_t(0)
         st = self._lib.fh_graph_request_replies(self._h, 0, None, None, None, None, None, 0,
                                                 None, None, C.byref(nr), C.byref(nd))
         if nr.value == 0:
-            return {}
+            return
         if st != L.FH_ECAP:
             L.check(st)
         r, d = nr.value, max(1, nd.value)
@@ -273,17 +287,17 @@ class HipGraphExecutor:
         L.check(self._lib.fh_graph_request_replies(
             self._h, r, L.ptr(to), L.ptr(kind), L.ptr(dot), L.ptr(csh), L.ptr(off), d,
             L.ptr(ddot), L.ptr(dsh), C.byref(nr), C.byref(nd)))
-        out = {}
         for i in range(r):
             dt = int(dot[i])
             if kind[i] == L.FH_REPLY_INFO:
                 deps = [Dependency(int(ddot[e]), _unmask(int(dsh[e])) if dsh[e] else None)
                         for e in range(off[i], off[i + 1])]
-                rep = RequestReply("info", dt, self._cmds.get(dt, (None,))[0], deps)
+                # the handle answered Info: the vertex is pending, so its
+                # command is still held here
+                rep = RequestReply("info", dt, self._cmds[dt][0], deps)
             else:
                 rep = RequestReply("executed", dt)
-            out.setdefault(int(to[i]), []).append(rep)
-        return out
+            self._replies.setdefault(int(to[i]), []).append(rep)
 
     def _fetch(self):
         """fetch_commands_to_execute + execute (executor.rs:133-145, 191-196)."""
@@ -296,11 +310,15 @@ class HipGraphExecutor:
             for i in range(ln.value):
                 d = int(buf[i])
                 cmd, ks = self._cmds.pop(d)
-                rifl = getattr(cmd, "rifl", d)
-                for k in ks:
-                    self._to_clients.append((rifl, k))
-                    if self._monitor is not None:
-                        self._monitor.setdefault(k, []).append(rifl)
+                if hasattr(cmd, "execute"):
+                    # Command::execute on this executor's KVStore + monitor
+                    self._to_clients.extend(cmd.execute(self.shard_id, self.store, self._monitor))
+                else:  # a bare key list (tests): the order only
+                    rifl = getattr(cmd, "rifl", d)
+                    for k in ks:
+                        self._to_clients.append(ExecutorResult(rifl, k, None))
+                        if self._monitor is not None:
+                            self._monitor.setdefault(k, []).append(rifl)
                 self.last_labels = getattr(self, "last_labels", {})
                 self.last_labels[d] = int(lab[i])
             if ln.value < len(buf):

@@ -590,8 +590,9 @@ typedef struct {
   uint64_t dot;
   uint64_t keys_at; /* offset in key pool */
   uint32_t nkeys;
-  uint64_t deps_at; /* offset in dep pool */
+  uint64_t deps_at; /* offset in dep pool (dep masks at the same offsets) */
   uint32_t ndeps;
+  uint64_t cmask;   /* Command::shards() as a bitmask (command.rs:103-110) */
   uint64_t id, low; /* tarjan.rs:329-331 */
   uint8_t on_stack;
   uint8_t alive;
@@ -617,8 +618,17 @@ struct fo_graph {
   uint64_t *kpool;
   size_t nk, capk;
   uint64_t *dpool;
+  uint64_t *mpool;           /* Dependency::shards bitmask of each dpool entry
+                                (0 = None, a noop) */
   size_t nd, capd;
   u64map pindex;             /* PendingIndex: dot -> head node, index.rs:145 */
+  /* partial replication (graph/mod.rs:139-157, 168-179, 279-408) */
+  u64map depmask;            /* dep dot -> its Dependency::shards bitmask */
+  vec64 req_shard, req_dot;  /* out_requests, not yet taken (mod.rs:147-150) */
+  vec64 buf_from, buf_dot;   /* buffered_in_requests (mod.rs:363-371) */
+  vec64 rep_to, rep_kind, rep_dot, rep_cmask, rep_doff; /* out_request_replies */
+  vec64 rep_ddot, rep_dmask;
+  int violation;             /* an invariant the reference panics on */
   pend_node *pnodes;
   size_t npn, cappn;
   /* finder state tarjan.rs:26-34 */
@@ -650,6 +660,7 @@ fo_graph *fo_graph_new(uint32_t process_id, uint64_t shard_id, uint32_t n,
   ae_init(&g->executed);
   map_init(&g->vindex, 1024);
   map_init(&g->pindex, 256);
+  map_init(&g->depmask, 256);
   return g;
 }
 
@@ -658,9 +669,22 @@ void fo_graph_free(fo_graph *g) {
   map_free(&g->executed.exc);
   map_free(&g->vindex);
   map_free(&g->pindex);
+  map_free(&g->depmask);
   free(g->vs);
   free(g->kpool);
   free(g->dpool);
+  free(g->mpool);
+  free(g->req_shard.a);
+  free(g->req_dot.a);
+  free(g->buf_from.a);
+  free(g->buf_dot.a);
+  free(g->rep_to.a);
+  free(g->rep_kind.a);
+  free(g->rep_dot.a);
+  free(g->rep_cmask.a);
+  free(g->rep_doff.a);
+  free(g->rep_ddot.a);
+  free(g->rep_dmask.a);
   free(g->pnodes);
   free(g->stack.a);
   free(g->sccs_flat.a);
@@ -672,7 +696,8 @@ void fo_graph_free(fo_graph *g) {
 }
 
 static size_t new_vertex(fo_graph *g, uint64_t dot, const uint64_t *keys,
-                         size_t nkeys, const uint64_t *deps, size_t ndeps) {
+                         size_t nkeys, const uint64_t *deps, size_t ndeps,
+                         uint64_t cmask, const uint64_t *dmasks) {
   if (g->nvs == g->capvs) {
     g->capvs = g->capvs ? g->capvs * 2 : 1024;
     g->vs = (vertex *)xrealloc(g->vs, g->capvs * sizeof(vertex));
@@ -684,6 +709,7 @@ static size_t new_vertex(fo_graph *g, uint64_t dot, const uint64_t *keys,
   while (g->nd + ndeps > g->capd) {
     g->capd = g->capd ? g->capd * 2 : 4096;
     g->dpool = (uint64_t *)xrealloc(g->dpool, g->capd * sizeof(uint64_t));
+    g->mpool = (uint64_t *)xrealloc(g->mpool, g->capd * sizeof(uint64_t));
   }
   vertex *v = &g->vs[g->nvs];
   v->dot = dot;
@@ -694,7 +720,12 @@ static size_t new_vertex(fo_graph *g, uint64_t dot, const uint64_t *keys,
   v->deps_at = g->nd;
   v->ndeps = (uint32_t)ndeps;
   if (ndeps) memcpy(g->dpool + g->nd, deps, ndeps * sizeof(uint64_t));
+  for (size_t i = 0; i < ndeps; i++) {
+    g->mpool[g->nd + i] = dmasks ? dmasks[i] : 0;
+    if (dmasks) map_put(&g->depmask, deps[i], dmasks[i]);
+  }
   g->nd += ndeps;
+  v->cmask = cmask;
   v->id = v->low = 0;
   v->on_stack = 0;
   v->alive = 1;
@@ -703,14 +734,15 @@ static size_t new_vertex(fo_graph *g, uint64_t dot, const uint64_t *keys,
 
 /* VertexIndex::index  index.rs:33-37; panics on double index mod.rs:235 */
 static size_t index_vertex(fo_graph *g, uint64_t dot, const uint64_t *keys,
-                           size_t nkeys, const uint64_t *deps, size_t ndeps) {
+                           size_t nkeys, const uint64_t *deps, size_t ndeps,
+                           uint64_t cmask, const uint64_t *dmasks) {
   if (map_get(&g->vindex, dot)) {
     fprintf(stderr, "oracle: Graph::handle_add tried to index already indexed "
                     "dot (%u,%llu)\n",
             FO_SRC(dot), (unsigned long long)FO_SEQ(dot));
     abort();
   }
-  size_t slot = new_vertex(g, dot, keys, nkeys, deps, ndeps);
+  size_t slot = new_vertex(g, dot, keys, nkeys, deps, ndeps, cmask, dmasks);
   map_put(&g->vindex, dot, slot);
   return slot;
 }
@@ -952,8 +984,12 @@ static void find_scc(fo_graph *g, int first_find, uint64_t dot,
   }
 }
 
-/* PendingIndex::index  index.rs:171-205 (request bookkeeping omitted:
- * single-process oracle keeps every vertex local) */
+/* index_pending  mod.rs:527-556 -> PendingIndex::index  index.rs:171-205:
+ * `dot` becomes a child of each missing dependency; the first time a
+ * dependency is indexed (a vacant entry) and its shard set excludes this
+ * shard, it is requested from Dot::target_shard(n) = (source - 1) / n
+ * (id.rs:59-61).  "shards should be set if it's not a noop" (index.rs:
+ * 190-194): a noop dependency there is an invariant violation. */
 static void index_pending(fo_graph *g, uint64_t dot, const vec64 *missing) {
   for (size_t i = 0; i < missing->len; i++) {
     uint64_t parent = missing->a[i];
@@ -965,10 +1001,21 @@ static void index_pending(fo_graph *g, uint64_t dot, const vec64 *missing) {
     uint64_t *head = map_get(&g->pindex, parent);
     g->pnodes[g->npn].child = dot;
     g->pnodes[g->npn].next = head ? (int64_t)*head : -1;
-    if (head)
+    if (head) {
       *head = g->npn;
-    else
+    } else {
       map_put(&g->pindex, parent, g->npn);
+      if (g->shard_count > 1) { /* vacant: maybe ask another shard */
+        uint64_t *m = map_get(&g->depmask, parent);
+        uint64_t mask = m ? *m : 0;
+        if (mask == 0) {
+          g->violation = 1;
+        } else if (!((g->shard_id < 64) && ((mask >> g->shard_id) & 1))) {
+          vpush(&g->req_shard, (FO_SRC(parent) - 1) / (g->n ? g->n : 1));
+          vpush(&g->req_dot, parent);
+        }
+      }
+    }
     g->npn++;
   }
 }
@@ -1025,9 +1072,10 @@ static void try_pending(fo_graph *g, vec64 *pending, vec64 *dots,
 }
 
 /* handle_add  mod.rs:215-277 */
-size_t fo_graph_add(fo_graph *g, uint64_t dot, const uint64_t *keys,
-                    size_t nkeys, const uint64_t *deps, size_t ndeps) {
-  index_vertex(g, dot, keys, nkeys, deps, ndeps);
+static size_t graph_add(fo_graph *g, uint64_t dot, const uint64_t *keys, size_t nkeys,
+                        uint64_t cmask, const uint64_t *deps, const uint64_t *dmasks,
+                        size_t ndeps) {
+  index_vertex(g, dot, keys, nkeys, deps, ndeps, cmask, dmasks);
   size_t initial_ready = g->qtail - g->qhead;
   size_t total = 0;
   finder_info fi;
@@ -1050,9 +1098,164 @@ size_t fo_graph_add(fo_graph *g, uint64_t dot, const uint64_t *keys,
   return total;
 }
 
+size_t fo_graph_add(fo_graph *g, uint64_t dot, const uint64_t *keys,
+                    size_t nkeys, const uint64_t *deps, size_t ndeps) {
+  return graph_add(g, dot, keys, nkeys, 0, deps, NULL, ndeps);
+}
+
+size_t fo_graph_add_sharded(fo_graph *g, uint64_t dot, const uint64_t *keys, size_t nkeys,
+                            uint64_t cmask, const uint64_t *deps, const uint64_t *dmasks,
+                            size_t ndeps) {
+  return graph_add(g, dot, keys, nkeys, cmask, deps, dmasks, ndeps);
+}
+
+/* process_requests  mod.rs:297-375: Info{dot, cmd, deps} for an indexed
+ * vertex (panic if the requester replicates it, :313-322), Executed{dot} for
+ * an executed dot, otherwise buffered until the next cleanup.  Dots are
+ * processed in the order given. */
+static void process_requests(fo_graph *g, uint64_t from, const uint64_t *dots, size_t n) {
+  for (size_t i = 0; i < n; i++) {
+    uint64_t d = dots[i];
+    vertex *v = find_vertex(g, d);
+    if (v) {
+      if (from < 64 && ((v->cmask >> from) & 1)) {
+        g->violation = 1;
+        continue;
+      }
+      vpush(&g->rep_to, from);
+      vpush(&g->rep_kind, 0); /* FH_REPLY_INFO */
+      vpush(&g->rep_dot, d);
+      vpush(&g->rep_cmask, v->cmask);
+      for (uint32_t e = 0; e < v->ndeps; e++) {
+        vpush(&g->rep_ddot, g->dpool[v->deps_at + e]);
+        vpush(&g->rep_dmask, g->mpool[v->deps_at + e]);
+      }
+      vpush(&g->rep_doff, g->rep_ddot.len);
+    } else if (ae_contains(&g->executed, d)) {
+      vpush(&g->rep_to, from);
+      vpush(&g->rep_kind, 1); /* FH_REPLY_EXECUTED */
+      vpush(&g->rep_dot, d);
+      vpush(&g->rep_cmask, 0);
+      vpush(&g->rep_doff, g->rep_ddot.len);
+    } else {
+      int dup = 0; /* HashMap<ShardId, HashSet<Dot>> */
+      for (size_t b = 0; b < g->buf_dot.len && !dup; b++)
+        dup = g->buf_from.a[b] == from && g->buf_dot.a[b] == d;
+      if (!dup) {
+        vpush(&g->buf_from, from);
+        vpush(&g->buf_dot, d);
+      }
+    }
+  }
+}
+
+/* handle_request  mod.rs:279-295 */
+void fo_graph_handle_requests(fo_graph *g, uint64_t from, const uint64_t *dots, size_t n) {
+  process_requests(g, from, dots, n);
+}
+
+typedef struct {
+  uint64_t from, dot;
+} fo_pair;
+static int cmp_pair(const void *a, const void *b) {
+  const fo_pair *x = (const fo_pair *)a, *y = (const fo_pair *)b;
+  if (x->from != y->from) return x->from < y->from ? -1 : 1;
+  return x->dot < y->dot ? -1 : x->dot > y->dot;
+}
+
+/* cleanup -> check_pending_requests  mod.rs:168-179, 673-678: the buffered
+ * requests, taken, processed again (shard by shard, dots ascending: hash
+ * order in the reference) */
+void fo_graph_cleanup(fo_graph *g) {
+  size_t n = g->buf_dot.len;
+  if (!n) return;
+  fo_pair *p = (fo_pair *)xmalloc(n * sizeof(fo_pair));
+  for (size_t i = 0; i < n; i++) {
+    p[i].from = g->buf_from.a[i];
+    p[i].dot = g->buf_dot.a[i];
+  }
+  g->buf_from.len = g->buf_dot.len = 0;
+  qsort(p, n, sizeof(fo_pair), cmp_pair);
+  uint64_t *d = (uint64_t *)xmalloc(n * sizeof(uint64_t));
+  for (size_t i = 0; i < n;) {
+    size_t j = i;
+    while (j < n && p[j].from == p[i].from) {
+      d[j - i] = p[j].dot;
+      j++;
+    }
+    process_requests(g, p[i].from, d, j - i);
+    i = j;
+  }
+  free(d);
+  free(p);
+}
+
+/* requests()  mod.rs:147-150: taken, as (target shard, dot) sorted unique */
+size_t fo_graph_requests(fo_graph *g, uint64_t *shard, uint64_t *dot, size_t cap) {
+  size_t n = g->req_dot.len;
+  fo_pair *p = (fo_pair *)xmalloc((n ? n : 1) * sizeof(fo_pair));
+  for (size_t i = 0; i < n; i++) {
+    p[i].from = g->req_shard.a[i];
+    p[i].dot = g->req_dot.a[i];
+  }
+  qsort(p, n, sizeof(fo_pair), cmp_pair);
+  size_t m = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (m && p[i].from == p[m - 1].from && p[i].dot == p[m - 1].dot) continue;
+    p[m++] = p[i];
+  }
+  if (m <= cap) {
+    for (size_t i = 0; i < m; i++) {
+      shard[i] = p[i].from;
+      dot[i] = p[i].dot;
+    }
+    g->req_shard.len = g->req_dot.len = 0;
+  }
+  free(p);
+  return m;
+}
+
+/* request_replies()  mod.rs:152-157: sizes, then taken in list order:
+ * to[nr], kind[nr] (0 Info, 1 Executed), dot[nr], cmask[nr] (Info: the
+ * command's shards), doff[nr+1] into ddot / dmask (Info: the vertex's deps) */
+void fo_graph_replies_size(const fo_graph *g, size_t *nr, size_t *nd) {
+  *nr = g->rep_dot.len;
+  *nd = g->rep_ddot.len;
+}
+void fo_graph_replies_take(fo_graph *g, uint64_t *to, uint64_t *kind, uint64_t *dot,
+                           uint64_t *cmask, uint64_t *doff, uint64_t *ddot, uint64_t *dmask) {
+  size_t nr = g->rep_dot.len, nd = g->rep_ddot.len;
+  memcpy(to, g->rep_to.a, nr * sizeof(uint64_t));
+  memcpy(kind, g->rep_kind.a, nr * sizeof(uint64_t));
+  memcpy(dot, g->rep_dot.a, nr * sizeof(uint64_t));
+  memcpy(cmask, g->rep_cmask.a, nr * sizeof(uint64_t));
+  doff[0] = 0;
+  memcpy(doff + 1, g->rep_doff.a, nr * sizeof(uint64_t));
+  if (nd) {
+    memcpy(ddot, g->rep_ddot.a, nd * sizeof(uint64_t));
+    memcpy(dmask, g->rep_dmask.a, nd * sizeof(uint64_t));
+  }
+  g->rep_to.len = g->rep_kind.len = g->rep_dot.len = g->rep_cmask.len = g->rep_doff.len = 0;
+  g->rep_ddot.len = g->rep_dmask.len = 0;
+}
+
+/* handle_request_reply's Executed{dot}  mod.rs:393-405: the executed clock
+ * advances and the dot's pending children are retried */
+size_t fo_graph_mark_executed(fo_graph *g, uint64_t dot) {
+  ae_add(&g->executed, dot);
+  vec64 dots = {0};
+  vpush(&dots, dot);
+  size_t total = 0;
+  check_pending(g, &dots, &total);
+  free(dots.a);
+  return total;
+}
+
+int fo_graph_violation(const fo_graph *g) { return g->violation; }
+
 void fo_graph_index_only(fo_graph *g, uint64_t dot, const uint64_t *keys,
                          size_t nkeys, const uint64_t *deps, size_t ndeps) {
-  index_vertex(g, dot, keys, nkeys, deps, ndeps);
+  index_vertex(g, dot, keys, nkeys, deps, ndeps, 0, NULL);
 }
 
 void fo_graph_set_executed_frontier(fo_graph *g, uint32_t source,

@@ -156,6 +156,23 @@ size_t fo_graph_drain(fo_graph *g, uint64_t *dots, uint64_t *scc_label,
                       size_t cap);
 size_t fo_graph_pending_count(const fo_graph *g);
 
+/* Partial replication (executor/graph/mod.rs:139-157, 168-179, 279-408;
+ * index.rs:171-205).  One graph plays both executor roles of its shard, as
+ * the reference's executors 0 and 1 share the VertexIndex (index.rs:21); its
+ * executed clock is the main role's (Executed notifications delivered
+ * before the next request).  Masks: bit s = shard s; 0 = None (a noop). */
+size_t fo_graph_add_sharded(fo_graph *g, uint64_t dot, const uint64_t *keys, size_t nkeys,
+                            uint64_t cmask, const uint64_t *deps, const uint64_t *dmasks,
+                            size_t ndeps);
+void fo_graph_handle_requests(fo_graph *g, uint64_t from, const uint64_t *dots, size_t n);
+void fo_graph_cleanup(fo_graph *g);
+size_t fo_graph_requests(fo_graph *g, uint64_t *shard, uint64_t *dot, size_t cap);
+void fo_graph_replies_size(const fo_graph *g, size_t *nr, size_t *nd);
+void fo_graph_replies_take(fo_graph *g, uint64_t *to, uint64_t *kind, uint64_t *dot,
+                           uint64_t *cmask, uint64_t *doff, uint64_t *ddot, uint64_t *dmask);
+size_t fo_graph_mark_executed(fo_graph *g, uint64_t dot);
+int fo_graph_violation(const fo_graph *g);
+
 /* Whole-stream driver: GraphExecutor::handle(Add) for every command in
  * arrival order, followed by fetch_commands_to_execute + execute (executor.rs:
  * 76-100, 133-145, 191-196); per-key ExecutionOrderMonitor (monitor.rs:20-28).

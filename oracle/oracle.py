@@ -83,6 +83,18 @@ def _load():
     lib.fo_pred_drain.argtypes = [V, V, S]
     lib.fo_pred_pending_count.restype = S
     lib.fo_pred_pending_count.argtypes = [V]
+    lib.fo_graph_add_sharded.restype = S
+    lib.fo_graph_add_sharded.argtypes = [V, C.c_uint64, V, S, C.c_uint64, V, V, S]
+    lib.fo_graph_handle_requests.argtypes = [V, C.c_uint64, V, S]
+    lib.fo_graph_cleanup.argtypes = [V]
+    lib.fo_graph_requests.restype = S
+    lib.fo_graph_requests.argtypes = [V, V, V, S]
+    lib.fo_graph_replies_size.argtypes = [V, C.POINTER(S), C.POINTER(S)]
+    lib.fo_graph_replies_take.argtypes = [V, V, V, V, V, V, V, V]
+    lib.fo_graph_mark_executed.restype = S
+    lib.fo_graph_mark_executed.argtypes = [V, C.c_uint64]
+    lib.fo_graph_violation.restype = C.c_int
+    lib.fo_graph_violation.argtypes = [V]
     lib.fo_graph_run.restype = S
     lib.fo_graph_run.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, S, u64p, u32p, u64p,
                                  u32p, u64p, u64p, u64p, C.c_uint64, u32p, u64p]
@@ -304,6 +316,77 @@ class Graph:
 
     def pending(self):
         return lib().fo_graph_pending_count(self._h)
+
+    # -- partial replication (graph/mod.rs:139-157, 168-179, 279-408) -----
+    def add_sharded(self, dot_, keys, cmd_shards, deps):
+        """handle_add with shard sets: deps = [(dot, shards or None)]."""
+        k = _arr(keys)
+        d = _arr(x for x, _ in deps)
+        m = _arr(_mask(s) for _, s in deps)
+        return lib().fo_graph_add_sharded(self._h, dot_, _ptr(k), len(k), _mask(cmd_shards),
+                                          _ptr(d), _ptr(m), len(d))
+
+    def handle_requests(self, from_shard, dots):
+        d = _arr(dots)
+        lib().fo_graph_handle_requests(self._h, from_shard, _ptr(d), len(d))
+
+    def cleanup(self):
+        lib().fo_graph_cleanup(self._h)
+
+    def requests(self):
+        """requests(): {target shard: {dots}} (taken)."""
+        n = lib().fo_graph_requests(self._h, None, None, 0)
+        sh = np.zeros(max(1, n), dtype=np.uint64)
+        dt = np.zeros(max(1, n), dtype=np.uint64)
+        m = lib().fo_graph_requests(self._h, _ptr(sh), _ptr(dt), n)
+        assert m == n
+        out = {}
+        for s, d in zip(sh[:n].tolist(), dt[:n].tolist()):
+            out.setdefault(s, set()).add(d)
+        return out
+
+    def request_replies(self):
+        """request_replies(): {to: [("info", dot, cmd_shards, [(dep, shards)]) |
+        ("executed", dot)]} in list order (taken)."""
+        nr, nd = C.c_size_t(0), C.c_size_t(0)
+        lib().fo_graph_replies_size(self._h, C.byref(nr), C.byref(nd))
+        nr, nd = nr.value, nd.value
+        if nr == 0:
+            return {}
+        a = [np.zeros(max(1, x), dtype=np.uint64) for x in (nr, nr, nr, nr, nr + 1, nd, nd)]
+        lib().fo_graph_replies_take(self._h, *[_ptr(x) for x in a])
+        to, kind, dot_, cm, off, dd, dm = [x.tolist() for x in a]
+        out = {}
+        for i in range(nr):
+            if kind[i] == 0:
+                deps = [(dd[e], _unmask(dm[e])) for e in range(off[i], off[i + 1])]
+                r = ("info", dot_[i], _unmask(cm[i]), deps)
+            else:
+                r = ("executed", dot_[i])
+            out.setdefault(to[i], []).append(r)
+        return out
+
+    def mark_executed(self, dot_):
+        """RequestReply::Executed{dot} (mod.rs:393-405)."""
+        return lib().fo_graph_mark_executed(self._h, dot_)
+
+    def violation(self):
+        return bool(lib().fo_graph_violation(self._h))
+
+
+def _mask(shards):
+    if shards is None:
+        return 0
+    m = 0
+    for s in shards:
+        m |= 1 << int(s)
+    return m
+
+
+def _unmask(m):
+    if m == 0:
+        return None
+    return frozenset(i for i in range(64) if (m >> i) & 1)
 
 
 def graph_run(dots, key_off, keys, dep_off, deps, key_space, process_id=1, n=1, f=1):

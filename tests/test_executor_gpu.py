@@ -253,3 +253,38 @@ def test_device_resident_backlog_then_release_matches_oracle():
     assert ex.pending() == 0 and ex.missing() == []
     assert ex.monitor() == want
     assert ex.last_labels == dict(zip(ex_o.tolist(), lab_o.tolist()))
+
+
+def test_kv_results_follow_the_oracle_order():
+    """Command / KV execution: the HIP executor runs each
+    drained command on its KVStore (Command::execute, command.rs:114-127;
+    KVStore::do_execute, kvs.rs:52-68).  With every command a Put of its own
+    value, each ExecutorResult is the previous Put's value on that key in the
+    oracle's per-key execution order (None for the key's first command)."""
+    from fantoch_amd.kvs import KVOp
+    s = Workload.zipf(0.99, 256, k=2, views=3, window=64, seed=23).generate(3000)
+    key_off = s.key_off()
+    keys = s.keys.reshape(-1)
+    dep_off, deps = O.views_run(0, 5, s.dots, key_off, keys, s.fq_proc, s.fq_time)
+    _, _, kso, ks = O.graph_run(s.dots, key_off, keys, dep_off, deps, s.key_space)
+    want = {}
+    for k in np.nonzero(np.diff(kso))[0]:
+        seq = ks[kso[k]:kso[k + 1]].tolist()
+        for j, d in enumerate(seq):
+            want[(d, str(int(k)))] = str(seq[j - 1]) if j else None
+    ex = HipGraphExecutor(1, 0, 5, 1, key_space=s.key_space)
+    infos = []
+    for i in range(s.n):
+        d = int(s.dots[i])
+        c = Command.from_ops(d, [(str(int(k)), KVOp.put(str(d))) for k in s.keys[i]])
+        infos.append(GraphExecutionInfo.add(d, c, deps[dep_off[i]:dep_off[i + 1]].tolist()))
+    for b0 in range(0, s.n, 700):
+        ex.handle_batch(infos[b0:b0 + 700])
+    assert ex.pending() == 0
+    got = {}
+    while (r := ex.to_clients()) is not None:
+        got[(r.rifl, r.key)] = r.op_result
+    assert got == want
+    # the store holds each key's last Put
+    for k in np.nonzero(np.diff(kso))[0]:
+        assert ex.store.execute(str(int(k)), KVOp.get()) == str(int(ks[kso[k + 1] - 1]))

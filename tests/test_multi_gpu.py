@@ -66,7 +66,9 @@ def test_multi_failed_staging_leaves_nothing_to_run():
         m.results()
     with pytest.raises(L.FhError):
         m.run()
-    # a good staging afterwards works again
-    m.stage(s)
+    # a good staging afterwards works again (the next commands of the
+    # stream: the engines' command logs keep the first batch's dots)
+    s2 = w.generate(5000, first=5000, logs=True)
+    m.stage(s2)
     m.run()
     assert len(m.results()["deps"]) > 0

@@ -6,12 +6,15 @@ buffered requests and cleanup (executor/graph/mod.rs:139-157, 168-179,
 The reference has no unit test for these paths (parity via
 `check_monitors` only, protocol/mod.rs:924-1013), so the checks are
   * hand-derived cases of the rules themselves (which dots are requested, from
-    which shard, and how a request is answered), and
+    which shard, and how a request is answered);
   * the monitor property on multi-shard streams: every shard executes every
     command it replicates exactly once, and each key's execution sequence is
     the key's commands in commit order -- what the oracle's SequentialKeyDeps
     per shard + union gives for a single view (every dependency is an earlier
-    command, so the per-key order is the stream order).
+    command, so the per-key order is the stream order); and
+  * lock step with the oracle's restatement of the protocol (oracle.c,
+    tests/test_oracle_partial.py): identical requests and replies at every
+    exchange of a multi-shard run.
 """
 import random
 
@@ -190,3 +193,100 @@ def test_multi_shard_stream_monitors(seed, S, n, K):
                 if shard_of_key(k, S) == s:
                     want.setdefault(str(k), []).append(dot)
         assert mon == want, f"shard {s}: per-key execution order differs"
+
+
+def _oracle_reply(r):
+    """A HIP RequestReply in the oracle's form."""
+    if r.kind == "info":
+        return ("info", r.dot, frozenset(r.cmd.shards()),
+                [(d.dot, d.shards) for d in r.deps])
+    return ("executed", r.dot)
+
+
+@pytest.mark.parametrize("seed,S,n,K", [(3, 2, 1, 24), (4, 3, 3, 40), (5, 4, 2, 64)])
+def test_requests_and_replies_match_oracle(seed, S, n, K):
+    """The partial-replication protocol in lock step with the oracle's
+    restatement of it (oracle.c: PendingIndex::index requests, index.rs:
+    171-205; process_requests Info / Executed / buffered, graph/mod.rs:
+    297-375; cleanup, :168-179, 673-678; reply ingest in list order,
+    :377-408): every shard's HIP executor and oracle graph get the same
+    Adds, requests and replies, and each requests() / request_replies() must
+    be identical -- the requested dots per target shard, and every reply's
+    kind, dot, command shards and dependencies with their shard sets, in
+    list order.  At the end both have executed every command they replicate
+    with the same per-key sequences."""
+    cmds, shards_of = partial_stream(seed, 1200, S, n, K, kmax=3)
+    rng = random.Random(200 + seed)
+    exs = [HipGraphExecutor(process_id=n * s + 1, shard_id=s, n=n, f=0, shard_count=S,
+                            key_space=K) for s in range(S)]
+    ors = [O.Graph(process_id=n * s + 1, shard_id=s, n=n, f=0, shard_count=S) for s in range(S)]
+    keys_of = {c[0]: c[1] for c in cmds}
+    omon = [dict() for _ in range(S)]
+
+    def odrain(s):
+        ex, _ = ors[s].drain()
+        for d in ex:
+            for k in keys_of.get(d, []):
+                if shard_of_key(k, S) == s:
+                    omon[s].setdefault(str(k), []).append(d)
+
+    def oadd(s, dot, keys, shards, deps):
+        mine = [k for k in keys if shard_of_key(k, S) == s]
+        ors[s].add_sharded(dot, mine, shards, deps)
+
+    arrivals = []
+    for s in range(S):
+        mine = [(i + rng.randrange(48), i) for i, c in enumerate(cmds) if s in c[2]]
+        arrivals.append([i for _, i in sorted(mine)])
+    pos = [0] * S
+    nreq = nrep = ninfo = 0
+    while True:
+        progressed = False
+        for s in range(S):
+            if pos[s] < len(arrivals[s]):
+                b = rng.randint(1, 64)
+                infos = []
+                for i in arrivals[s][pos[s]:pos[s] + b]:
+                    dot, keys, shards, deps = cmds[i]
+                    c = Command(dot, [str(k) for k in keys], shard_of=lambda k: int(k) % S)
+                    dl = [(d, frozenset(shards_of[d])) for d in sorted(deps)]
+                    infos.append(GraphExecutionInfo.add(dot, c, [Dependency(d, sh) for d, sh in dl]))
+                    oadd(s, dot, keys, shards, dl)
+                pos[s] += b
+                exs[s].handle_batch(infos)
+                odrain(s)
+                progressed = True
+        for s in range(S):
+            hr, orq = exs[s].requests(), ors[s].requests()
+            assert hr == orq, f"shard {s}: requests differ"
+            for t in sorted(hr):
+                dots = sorted(hr[t])
+                exs[t].handle(GraphExecutionInfo.request(s, dots))
+                ors[t].handle_requests(s, dots)
+                nreq += len(dots)
+                progressed = True
+        for t in range(S):
+            exs[t].cleanup()
+            ors[t].cleanup()
+            hrep, orep = exs[t].request_replies(), ors[t].request_replies()
+            assert {s: [_oracle_reply(r) for r in v] for s, v in hrep.items()} == orep, \
+                f"shard {t}: request replies differ"
+            for s in sorted(hrep):
+                exs[s].handle(GraphExecutionInfo.request_reply(hrep[s]))
+                for r in orep[s]:
+                    if r[0] == "info":
+                        _, dot, csh, deps = r
+                        oadd(s, dot, keys_of[dot], csh, deps)
+                        ninfo += 1
+                    else:
+                        ors[s].mark_executed(r[1])
+                odrain(s)
+                nrep += len(hrep[s])
+                progressed = True
+        if not progressed:
+            break
+    assert nreq > 0 and nrep > 0 and ninfo > 0, "the stream must exercise Info replies"
+    for s in range(S):
+        assert not ors[s].violation()
+        assert exs[s].pending() == 0 and ors[s].pending() == 0
+        assert exs[s].monitor() == omon[s], f"shard {s}: per-key sequences differ from the oracle"
