@@ -90,14 +90,16 @@ constexpr uint32_t kPlaceSlack = 1u << 16;  // default (FH_PLACE_SLACK): arrival
 constexpr uint32_t kPlaceNone = ~0u;        // never a code (log references < 2^31 - 1)
 
 // emin (may be null): the placement base of the chunk.  One workgroup per
-// sort tile (kTile consecutive elements): it also writes the tile's 8-bit
-// digit counts at shift 0 for the sort's first pass (sort_pairs_counted: no
-// separate counting pass over the keys it just wrote).
+// sort tile (kTile consecutive elements): it also writes the tile's digit
+// counts at shift 0 (digits of dmask + 1 values, sort_digit_bits) for the
+// sort's first pass (sort_pairs_counted: no separate counting pass over the
+// keys it just wrote).
 __global__ void __launch_bounds__(kThreads)
     k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, LogChunk ch,
                const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
                uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
-               uint32_t *__restrict__ emin, uint32_t slack, uint32_t *__restrict__ counts) {
+               uint32_t *__restrict__ emin, uint32_t slack, uint32_t *__restrict__ counts,
+               uint32_t dmask) {
   __shared__ uint32_t s_h[256];
   s_h[threadIdx.x] = 0;
   __syncthreads();
@@ -111,10 +113,10 @@ __global__ void __launch_bounds__(kThreads)
     const uint32_t key = (r + 1) * K + key32[(e / fq) * k + s];
     keys[x] = key;
     vals[x] = e * k + s;
-    atomicAdd(&s_h[key & 255], 1u);
+    atomicAdd(&s_h[key & dmask], 1u);
   }
   __syncthreads();
-  counts[size_t(blockIdx.x) * 256 + threadIdx.x] = s_h[threadIdx.x];
+  if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
   // placement base: the smallest first entry of the replicas' slices, less a
   // slack for entries that arrive before earlier commands.  Only a hint (see
   // above).  An exact minimum by atomics serialised the kernel on one word:
@@ -653,6 +655,20 @@ __device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
   return w;
 }
 
+// streamed once: with nt set, loads and stores skip cache residency so the
+// Infinity Cache keeps the gathered dots (FH_UNION_NT)
+template <class T>
+__device__ __forceinline__ void st_maybe_nt(T *p, T v, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+template <class T>
+__device__ __forceinline__ T ld_maybe_nt(const T *p, bool nt) {
+  return nt ? __builtin_nontemporal_load(p) : *p;
+}
+
 // k_cmd_engine for rows of at most kRegSlots slots, in registers: every slot
 // is read into a fixed register position (absent = all ones), a bitonic
 // network sorts the 16 dots, and the unique ones stream out.  (The general
@@ -667,7 +683,7 @@ __device__ __forceinline__ void cmd_union_regs(
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n,
-    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err) {
+    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, bool nt) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
@@ -678,7 +694,8 @@ __device__ __forceinline__ void cmd_union_regs(
     if (t < S) {
       uint64_t x = 0;
       uint32_t v = 0;
-      const int kind = decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
+      const int kind =
+          decode_dep(ld_maybe_nt(dep_code + size_t(i) * S + t, nt), &v, &x, dlog, bbase, n);
       if (kind == 1) {
         vv[t] = v;
       } else if (kind == 2) {
@@ -722,7 +739,7 @@ __device__ __forceinline__ void cmd_union_regs(
 #pragma unroll
   for (uint32_t t = 0; t < kRegSlots; t++) {
     if (r[t] != ~0ull && r[t] != prev) {
-      if (m < cap) dd[m] = r[t];
+      if (m < cap) st_maybe_nt(dd + m, r[t], nt);
       m++;
       prev = r[t];
     }
@@ -730,7 +747,7 @@ __device__ __forceinline__ void cmd_union_regs(
   if (out_off) {
     if (m != cap) atomicOr(err, 1u);  // an in-batch dot repeated outside the batch
   } else {
-    for (uint32_t q = m; q < S; q++) dd[q] = 0;
+    for (uint32_t q = m; q < S; q++) st_maybe_nt(dd + q, uint64_t(0), nt);
   }
   uint32_t *ds = dst + size_t(i) * S;
   uint32_t nv = 0;
@@ -740,12 +757,12 @@ __device__ __forceinline__ void cmd_union_regs(
       bool dup = false;
 #pragma unroll
       for (uint32_t q = 0; q < t; q++) dup |= vv[q] == vv[t];
-      if (!dup) ds[nv++] = vv[t];
+      if (!dup) st_maybe_nt(ds + nv++, vv[t], nt);
     }
   }
-  for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
-  if (nv_out) nv_out[i] = nv;
-  dep_cnt[i] = m;
+  for (uint32_t q = nv; q < S; q++) st_maybe_nt(ds + q, i, nt);  // padding: self loops are ignored
+  if (nv_out) st_maybe_nt(nv_out + i, nv, nt);
+  st_maybe_nt(dep_cnt + i, m, nt);
   if (blocked0) blocked0[i] = missing;
   if (missing) atomicAdd(nblocked, 1u);
 }
@@ -763,8 +780,11 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
                              uint64_t bbase, const uint32_t *__restrict__ out_off,
-                             uint32_t *__restrict__ err) {
+                             uint32_t *__restrict__ err, uint32_t c0, uint32_t c1, int nt) {
+  // commands [c0, c1) of the batch (a launch per command range keeps the
+  // gathered dots of recent dependencies cache-resident: FH_UNION_CHUNK)
   // uniform: the register path, with a sorting network sized to the row
+  const uint32_t cn = c1 - c0;
   if (S <= 4) {
     // XCD-contiguous blocks (grid a multiple of 8): workgroup b runs on XCD
     // b mod 8, which takes the b/8-th block of its own eighth of the
@@ -772,26 +792,27 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     // L2 of the XCD that gathers them again
     const uint32_t nb = gridDim.x;
     const uint32_t lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
-    for (size_t i = size_t(lb) * blockDim.x + threadIdx.x; i < n; i += size_t(nb) * blockDim.x)
-      cmd_union_regs<4>(uint32_t(i), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                        blocked0, nblocked, nv_out, bbase, n, out_off, err);
+    for (size_t j = size_t(lb) * blockDim.x + threadIdx.x; j < cn; j += size_t(nb) * blockDim.x)
+      cmd_union_regs<4>(c0 + uint32_t(j), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
+                        blocked0, nblocked, nv_out, bbase, n, out_off, err, nt != 0);
     return;
   }
   if (S <= 8) {
-    GRID_STRIDE(i, n) {
-      cmd_union_regs<8>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n, out_off, err);
+    GRID_STRIDE(j, cn) {
+      cmd_union_regs<8>(c0 + j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
+                        nblocked, nv_out, bbase, n, out_off, err, nt != 0);
     }
     return;
   }
   if (S <= kRegSlots) {
-    GRID_STRIDE(i, n) {
-      cmd_union_regs<kRegSlots>(i, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                                blocked0, nblocked, nv_out, bbase, n, out_off, err);
+    GRID_STRIDE(j, cn) {
+      cmd_union_regs<kRegSlots>(c0 + j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
+                                blocked0, nblocked, nv_out, bbase, n, out_off, err, nt != 0);
     }
     return;
   }
-  GRID_STRIDE(i, n) {
+  GRID_STRIDE(jj, cn) {
+    const uint32_t i = c0 + jj;
     uint64_t *dd = dep_dot + size_t(i) * S;
     uint32_t *ds = dst + size_t(i) * S;
     uint32_t nv = 0, nd = 0;
@@ -1675,12 +1696,13 @@ struct EngineDevice {
         if (!fused) {
           const uint32_t tiles = (Mc + kTile - 1) / kTile;
           sort_ws.prepare(tiles, 1, stream);
+          const int db = sort_digit_bits(bits, 4);
           probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys, dim3(tiles),
                         dim3(kThreads), stream, Mc, k, fq, np, lc, bent, bkey,
                         uint32_t(key_space), lk, lv, place ? pbase + c : (uint32_t *)nullptr,
-                        place_slack, sort_ws.meta.get());
+                        place_slack, sort_ws.meta.get(), (1u << db) - 1);
           sort_pairs_counted<uint32_t, uint32_t>(lk, lv, bkb.ensure(Mc + 1), bvb.ensure(Mc + 1),
-                                                 Mc, bits, sort_ws, stream, &ks, &vs);
+                                                 Mc, bits, sort_ws, stream, &ks, &vs, db);
         } else {
           const LogSrc src{k, fq, np, uint32_t(key_space), lc, bent, bkey};
           sort_pairs_src<uint32_t, uint32_t, LogSrc>(src, lk, lv, bkb.ensure(Mc + 1),
@@ -1851,21 +1873,37 @@ struct EngineDevice {
       const char *e = getenv("FH_UNION_XCD");
       return !(e && *e == '0');
     }();
-    if (views)
-      probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
-                    k_cmd_engine<uint32_t>,
-                    dim3(S <= 4 && xcd_union ? (grid_for(n, B, 1u << 22) + 7) / 8 * 8
-                                             : grid_for(n, B)),
-                    dim3(B), stream, n, S, bdot,
-                    (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
-                    (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                    scal.get(), ecnt, bbase, doff, scal.get() + 1);
-    else
-      probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
-                    k_cmd_engine<uint64_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
-                    (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
-                    (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                    scal.get(), ecnt, bbase, doff, scal.get() + 1);
+    // FH_UNION_CHUNK (commands per launch, 0 = one launch): launches over
+    // consecutive command ranges keep the dots of recent dependencies within
+    // a window the Infinity Cache can hold; FH_UNION_NT=1: the streamed
+    // codes and outputs bypass cache residency
+    static const uint32_t union_chunk = [] {
+      const char *e = getenv("FH_UNION_CHUNK");
+      return e ? uint32_t(atol(e)) : 0u;
+    }();
+    static const int union_nt = [] {
+      const char *e = getenv("FH_UNION_NT");
+      return e && *e == '1' ? 1 : 0;
+    }();
+    const uint32_t uc = union_chunk ? union_chunk : n;
+    for (uint32_t c0 = 0; c0 < n; c0 += uc) {
+      const uint32_t c1 = std::min<uint32_t>(n, c0 + uc), cn = c1 - c0;
+      if (views)
+        probed_launch("cmd_union", double(cn) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
+                      k_cmd_engine<uint32_t>,
+                      dim3(S <= 4 && xcd_union ? (grid_for(cn, B, 1u << 22) + 7) / 8 * 8
+                                               : grid_for(cn, B)),
+                      dim3(B), stream, n, S, bdot,
+                      (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
+                      (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
+                      scal.get(), ecnt, bbase, doff, scal.get() + 1, c0, c1, union_nt);
+      else
+        probed_launch("cmd_union", double(cn) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
+                      k_cmd_engine<uint64_t>, dim3(grid_for(cn, B)), dim3(B), stream, n, S,
+                      bdot, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
+                      (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
+                      scal.get(), ecnt, bbase, doff, scal.get() + 1, c0, c1, union_nt);
+    }
     mark("keydeps_union");
     if (deps_only) return;  // the committed deps are the output (partial replication)
     const uint32_t *gdst = dd, *goff = nullptr;

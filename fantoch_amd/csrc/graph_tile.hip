@@ -294,7 +294,53 @@ __global__ void __launch_bounds__(kTileThreads)
     __syncthreads();
     return it + 1;
   };
-  const int hs = out.hblock == 2 ? h_sweeps_batched() : sweeps(
+  // hblock 1 (default) with each thread's vertices' context edges and own H
+  // in registers: the thread owning x is the only writer of sH[x], so its
+  // register copy stays exact, and a sweep's LDS traffic is the random
+  // sH[y] / sH[H] reads alone (the edge rows and own H were conflict-free
+  // re-reads of the same words every sweep)
+  auto h_sweeps_regs = [&]() {
+    constexpr int kHI = kTileC / kTileThreads;
+    const int w = tid >> 6, lane = tid & 63, nk = hP / 64;
+    uint16_t ey[kHI][S];
+    uint32_t hv[kHI];
+#pragma unroll
+    for (int j = 0; j < kHI; j++) {
+      const int x = w * hP + j * 64 + lane;
+      const bool ok = j < nk && x < C;
+      hv[j] = ok ? uint32_t(x) : 0xFFFFFFFFu;  // sH[x] starts at x; ~0: no vertex
+#pragma unroll
+      for (int q = 0; q < S; q++) ey[j][q] = ok ? eL[q][x] : kNone;
+    }
+    int it = 0;
+    for (;; it++) {
+      bool ch = false;
+#pragma unroll
+      for (int j = 0; j < kHI; j++) {
+        if (hv[j] == 0xFFFFFFFFu) continue;
+        uint32_t h = hv[j];
+        const uint32_t h0 = h;
+#pragma unroll
+        for (int q = 0; q < S; q++)
+          if (ey[j][q] != kNone) h = max(h, uint32_t(sH[ey[j][q]]));
+        h = max(h, uint32_t(sH[h]));
+        if (h > h0) {
+          sH[w * hP + j * 64 + lane] = uint16_t(h);
+          hv[j] = h;
+          ch = true;
+        }
+      }
+      if (ch) s_ch[it % 3] = 1;
+      if (tid == 0) s_ch[(it + 1) % 3] = 0;
+      __syncthreads();
+      if (!s_ch[it % 3]) break;
+    }
+    __syncthreads();
+    if (tid < 3) s_ch[tid] = 0;
+    __syncthreads();
+    return it + 1;
+  };
+  const int hs = out.hblock == 2 ? h_sweeps_batched() : out.hblock == 1 ? h_sweeps_regs() : sweeps(
       [&](int i) {
         const int x = out.hblock ? ((i & (kTileThreads - 1)) >> 6) * hP + (i >> 10) * 64 + (i & 63)
                                  : i;

@@ -33,7 +33,8 @@ void SortWorkspace::prepare(size_t tiles, int, hipStream_t) {
   meta.ensure((tiles + groups + 1) * (size_t(1) << kWideMax));
 }
 
-// Digit plan: 8-bit digits.  FH_SORT_WIDE=1 sorts keys of 17..22 bits in two
+// Digit plan: sort_digit_bits (sort_impl.h), balanced digits of <= 8 bits.
+// FH_SORT_WIDE=1 sorts keys of 17..22 bits in two
 // passes of 10 or 11 bits instead of three of 8 (the per-tile count matrix
 // grows 4-8x, one whole read + write of the pairs goes away).  Measured on
 // C4 (20-bit keys): no faster -- KeyDeps 15.75 vs 15.53 ms, per-key 3.40 vs
@@ -47,7 +48,7 @@ void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *v
     const char *e = getenv("FH_SORT_WIDE");
     return e && *e && *e != '0';
   }();
-  int db = 8;
+  int db = sort_digit_bits(key_bits, int(sizeof(K)));
   if (wide && key_bits > 16 && key_bits <= 2 * kWideMax) db = key_bits <= 20 ? 10 : 11;
   int passes = (key_bits + db - 1) / db;
   if (passes < 1) passes = 1;
@@ -74,6 +75,10 @@ void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *v
     FH_SORT_RUN(10)
   } else if (db == 11) {
     FH_SORT_RUN(11)
+  } else if (db == 6) {
+    FH_SORT_RUN(6)
+  } else if (db == 7) {
+    FH_SORT_RUN(7)
   } else {
     FH_SORT_RUN(8)
   }

@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(1024)
   }
   if (lane == 63) s_tmp[w] = x;
   __syncthreads();
-  if (q == 0) {
+  if (q == 0 && d < R) {
     uint32_t pre = 0;
     for (int i = 0; i < w; i++) pre += s_tmp[i];
     dbase[d] = pre + x - tot;
@@ -242,34 +242,40 @@ inline void scan_b(uint32_t *gsum, uint32_t groups, uint32_t *dbase, hipStream_t
     const char *e = getenv("FH_SCAN_WIDE");
     return !(e && *e == '0');
   }();
-  if constexpr (DB <= 10) {
-    if (wide) {
-      k_scan_b_wide<DB><<<1, 1024, 0, s>>>(gsum, groups, dbase);
-      return;
+  if constexpr (DB < 8) {  // (k_scan_b assumes at least 256 digits)
+    k_scan_b_wide<DB><<<1, 1024, 0, s>>>(gsum, groups, dbase);
+  } else {
+    if constexpr (DB <= 10) {
+      if (wide) {
+        k_scan_b_wide<DB><<<1, 1024, 0, s>>>(gsum, groups, dbase);
+        return;
+      }
     }
+    k_scan_b<DB><<<1, 256, 0, s>>>(gsum, groups, dbase);
   }
-  k_scan_b<DB><<<1, 256, 0, s>>>(gsum, groups, dbase);
 }
 
 // Small sorts (tiles <= kFusedMaxTiles): one 1024-thread workgroup does both
 // scan levels -- 4 threads per digit, each over a contiguous quarter of the
 // tiles (gsum[q][d] <- quarter prefix, dbase[d] <- digit base).
 constexpr int kFusedMaxTiles = 1024;
+template <int DB>
 __global__ void __launch_bounds__(1024)
     k_scan_fused(uint32_t *__restrict__ counts, uint32_t tiles, uint32_t per,
                  uint32_t *__restrict__ gsum, uint32_t *__restrict__ dbase) {
+  constexpr uint32_t R = 1u << DB;  // <= 256: threads d >= R only join the barriers
   __shared__ uint32_t s_part[4][256];
   __shared__ uint32_t s_tmp[4];
   const uint32_t d = threadIdx.x & 255, q = threadIdx.x >> 8;
-  const uint32_t t0 = q * per, t1 = min(tiles, t0 + per);
+  const uint32_t t0 = q * per, t1 = d < R ? min(tiles, t0 + per) : t0;
   uint32_t run = 0;
   for (uint32_t t = t0; t < t1; t += 16) {
     uint32_t v[16];
 #pragma unroll
-    for (int i = 0; i < 16; i++) v[i] = (t + i < t1) ? counts[size_t(t + i) * 256 + d] : 0u;
+    for (int i = 0; i < 16; i++) v[i] = (t + i < t1) ? counts[size_t(t + i) * R + d] : 0u;
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-      if (t + i < t1) counts[size_t(t + i) * 256 + d] = run;
+      if (t + i < t1) counts[size_t(t + i) * R + d] = run;
       run += v[i];
     }
   }
@@ -281,7 +287,7 @@ __global__ void __launch_bounds__(1024)
     if (uint32_t(i) < q) qpre += s_part[i][d];
     tot += s_part[i][d];
   }
-  gsum[q * 256 + d] = qpre;
+  if (d < R) gsum[q * R + d] = qpre;
   // exclusive scan of the digit totals (waves 0..3 hold digits 0..255; every
   // thread reaches the barrier)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -293,7 +299,7 @@ __global__ void __launch_bounds__(1024)
   }
   if (q == 0 && lane == 63) s_tmp[w] = x;
   __syncthreads();
-  if (q == 0) {
+  if (q == 0 && d < R) {
     uint32_t pre = 0;
     for (int i = 0; i < w; i++) pre += s_tmp[i];
     dbase[d] = pre + x - tot;
@@ -305,7 +311,9 @@ __global__ void __launch_bounds__(kThreads)
     k_down(Src src, K *__restrict__ kout, VT *__restrict__ vout, uint32_t n, int shift,
            const uint32_t *__restrict__ counts, const uint32_t *__restrict__ gsum,
            uint32_t gsize, const uint32_t *__restrict__ dbase) {
-  constexpr int R = 1 << DB, Q = R / 256;
+  // digits per thread in the tile-wide scan: Q = R / 256, or one digit for
+  // the first R threads when R < 256 (6- and 7-bit digits)
+  constexpr int R = 1 << DB, Q = R >= 256 ? R / 256 : 1;
   __shared__ K s_k[kTile];
   __shared__ VT s_v[kTile];
   __shared__ uint32_t s_wh[kWaves][R];
@@ -353,11 +361,13 @@ __global__ void __launch_bounds__(kThreads)
   for (int q = 0; q < Q; q++) {
     const int d = tid * Q + q;
     uint32_t c0 = 0;
+    if (d < R) {
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ww++) {
-      const uint32_t c = s_wh[ww][d];
-      s_wh[ww][d] = c0;
-      c0 += c;
+      for (int ww = 0; ww < kWaves; ww++) {
+        const uint32_t c = s_wh[ww][d];
+        s_wh[ww][d] = c0;
+        c0 += c;
+      }
     }
     cnt[q] = c0;
   }
@@ -367,7 +377,7 @@ __global__ void __launch_bounds__(kThreads)
   uint32_t lpre = block_excl_scan(mine, s_tmp);
 #pragma unroll
   for (int q = 0; q < Q; q++) {
-    s_dex[tid * Q + q] = lpre;
+    if (tid * Q + q < R) s_dex[tid * Q + q] = lpre;
     lpre += cnt[q];
   }
   __syncthreads();
@@ -427,9 +437,9 @@ void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tile
   if (!have_counts)  // (else the producer of the input wrote the tile counts)
     k_up<K, VT, DB, Src><<<tiles, kThreads, 0, s>>>(src, uint32_t(n), shift, counts, atomic_up);
   uint32_t gsize = kGroup;
-  if (DB == 8 && tiles <= kFusedMaxTiles) {
+  if (DB <= 8 && tiles <= kFusedMaxTiles) {
     gsize = (tiles + 3) / 4;
-    k_scan_fused<<<1, 1024, 0, s>>>(counts, tiles, gsize, gsum, dbase);
+    k_scan_fused<DB><<<1, 1024, 0, s>>>(counts, tiles, gsize, gsum, dbase);
   } else {
     k_scan_a<DB><<<groups, 256, 0, s>>>(counts, tiles, gsum);
     scan_b<DB>(gsum, groups, dbase, s);
@@ -503,19 +513,43 @@ void sort_pairs_src(const Src &src, K *ka, VT *va, K *kb, VT *vb, size_t n, int 
 // shift 0, tiles of kTile consecutive elements, counts[tile][256] in
 // ws.meta after ws.prepare(tiles)) were written by the kernel that produced
 // the input; result in (ka, va) or (kb, vb).
+// The digit plan: the fewest passes of at most 8 bits, the bits spread evenly
+// over them (20-bit keys: 7 + 7 + 6 instead of 8 + 8 + 4).  A narrower digit
+// means fewer ballots per item in k_down and longer same-digit runs per tile
+// (32 instead of 16 elements on average at 7 bits: 128-B writes instead of
+// 64-B ones).  FH_SORT_BALANCED=0: 8-bit digits throughout.
+inline int sort_digit_bits(int key_bits, int key_bytes) {
+  static const bool balanced = [] {
+    const char *e = getenv("FH_SORT_BALANCED");
+    return !(e && *e == '0');
+  }();
+  int passes = std::max(1, (key_bits + 7) / 8);
+  if (passes > key_bytes) passes = key_bytes;
+  if (!balanced) return 8;
+  const int db = (key_bits + passes - 1) / passes;
+  return db >= 8 ? 8 : db <= 6 ? 6 : 7;
+}
+
 template <class K, class VT>
 void sort_pairs_counted(K *ka, VT *va, K *kb, VT *vb, size_t n, int key_bits, SortWorkspace &ws,
-                        hipStream_t s, K **kout, VT **vout) {
+                        hipStream_t s, K **kout, VT **vout, int db) {
   FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "sort: too many elements (>= 2^30)");
-  int passes = std::max(1, (key_bits + 7) / 8);
-  if (passes > int(sizeof(K))) passes = int(sizeof(K));
+  const int passes = std::max(1, (key_bits + db - 1) / db);
   if (n == 0) {
     *kout = ka;
     *vout = va;
     return;
   }
-  sort_passes<K, VT, 8, ArraySrc<K, VT, false>>(ArraySrc<K, VT, false>{ka, va}, true, ka, va, kb,
-                                                 vb, true, n, passes, 8, ws, s, kout, vout, true);
+  using Src = ArraySrc<K, VT, false>;
+  if (db == 6)
+    sort_passes<K, VT, 6, Src>(Src{ka, va}, true, ka, va, kb, vb, true, n, passes, 6, ws, s, kout,
+                               vout, true);
+  else if (db == 7)
+    sort_passes<K, VT, 7, Src>(Src{ka, va}, true, ka, va, kb, vb, true, n, passes, 7, ws, s, kout,
+                               vout, true);
+  else
+    sort_passes<K, VT, 8, Src>(Src{ka, va}, true, ka, va, kb, vb, true, n, passes, 8, ws, s, kout,
+                               vout, true);
 }
 
 }  // namespace
