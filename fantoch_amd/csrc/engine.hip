@@ -384,155 +384,254 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
-// One thread per command in (key, command) order; a 1024-command tile of
-// keys, commands and view records staged in LDS with kSrchHalo neighbours on
-// either side (a scan that leaves them reads global memory: a chain of
-// dependent loads, so the halo keeps hot keys' tile-edge lanes in LDS).
-// Writes each element's dependency code (the chunked path's encoding) and a
-// per-command mask of the views it is the tail of.
+// The command-level sort input.  Each command travels through the key sort
+// with everything the search needs, so the search reads only the sorted
+// arrays (a gather of its view records in key order, as round 2's first
+// version did, cost a random line per command: 10.4 ms at C4).  The key word
+// holds the key in bits [0, kb) -- the sort's digits cover exactly those --
+// and meta bits above; the u64 value holds the command in bits [0, cb) and
+// the rest of the meta.  The meta is, per view j, the replica id (rb bits)
+// and its arrival position in that replica's log modulo 2^qb.
+//
+// Arrival order from the truncated positions.  For two commands c1 != c2
+// that replica r both processes, with the logs' inversion span W:
+//   c1 + W < c2  =>  c1 arrives first;   c2 + W < c1  =>  c2 arrives first;
+// otherwise every log entry between their arrivals is a command in
+// [min - W, max + W] (one arriving later than that range would have been
+// preceded by a larger command than W allows, and symmetrically), so their
+// positions differ by at most 3W + 1 < 2^(qb-1): the sign of the difference
+// modulo 2^qb decides.  The host checks 3W + 1 < 2^(qb-1) before taking
+// this path.
+struct CmdMeta {
+  uint32_t fq, rb, qb, vb;  // views; bits per view: replica, arrival, both
+  uint32_t kb, cb;          // key word: meta from bit kb; value: command in [0, cb)
+  uint32_t kmask, W;
+  uint64_t cmask, qmask;
+  __device__ __forceinline__ uint64_t meta(uint32_t kw, uint64_t v) const {
+    return (v >> cb) | ((uint64_t(kw) >> kb) << (64 - cb));
+  }
+  __device__ __forceinline__ uint32_t rep(uint64_t m, uint32_t j) const {
+    return uint32_t(m >> (j * vb + qb)) & ((1u << rb) - 1);
+  }
+  __device__ __forceinline__ uint32_t arr(uint64_t m, uint32_t j) const {
+    return uint32_t((m >> (j * vb)) & qmask);
+  }
+  // the arrival of the command whose meta is m at replica r, if it has one
+  __device__ __forceinline__ bool find(uint64_t m, uint32_t r, uint32_t *t) const {
+    bool f = false;
+    for (uint32_t j = 0; j < fq; j++) {
+      const bool h = rep(m, j) == r;
+      *t = h ? arr(m, j) : *t;
+      f |= h;
+    }
+    return f;
+  }
+  // (c1, arrival q1) reaches the replica before (c2, q2)
+  __device__ __forceinline__ bool before(uint32_t c1, uint32_t q1, uint32_t c2, uint32_t q2) const {
+    const bool lo = uint64_t(c1) + W < c2, hi = uint64_t(c2) + W < c1;
+    const uint32_t d = (q2 - q1) & uint32_t(qmask);
+    return lo || (!hi && d != 0 && d <= uint32_t(qmask >> 1));
+  }
+};
+
+// One workgroup per sort tile: packs each command's key, index and view
+// records (k_view_records) into the sort input, and writes the tile's digit
+// counts for the sort's first pass (sort_pairs_counted).
+__global__ void __launch_bounds__(kThreads)
+    k_cmd_pack(uint32_t n, CmdMeta cm, const uint32_t *__restrict__ key32,
+               const uint32_t *__restrict__ rec, uint32_t *__restrict__ kw,
+               uint64_t *__restrict__ val, uint32_t *__restrict__ counts, uint32_t dmask) {
+  __shared__ uint32_t s_h[256];
+  s_h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(n, base + uint32_t(kTile));
+  for (uint32_t x = base + threadIdx.x; x < end; x += kThreads) {
+    const uint32_t key = key32[x];
+    uint64_t m = 0;
+    for (uint32_t j = 0; j < cm.fq; j++) {
+      const uint32_t r = rec[size_t(x) * cm.fq + j];
+      m |= ((uint64_t(r >> kRecT) << cm.qb) | (r & cm.qmask)) << (j * cm.vb);
+    }
+    val[x] = uint64_t(x) | (m << cm.cb);
+    kw[x] = key | uint32_t((m >> (64 - cm.cb)) << cm.kb);
+    atomicAdd(&s_h[key & dmask], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
+}
+
+// One thread per command in (key, command) order, a 1024-command tile staged
+// in LDS with kSrchHalo neighbours on either side, unpacked: key, command and
+// the arrival position at each replica (kNoArr if the replica does not
+// process it).  A scan that leaves the staged span continues on the packed
+// global arrays.  Per view j the predecessor is the key's latest arrival at
+// replica r_j before the command (SequentialKeyDeps::add_cmd,
+// sequential.rs:72-104): scanning back, every r_j-command arriving earlier is
+// a candidate; a command c' with c' + W below the best candidate so far (or
+// below the first candidate under c - W) arrives before it and cannot win,
+// nor can anything further back.  Forward, commands up to c + W may still
+// arrive earlier.  The command is its view's tail (latest_deps becomes it,
+// :88-95) iff no r_j-command of the key arrives later; any beyond c + W does.
+// Writes the fq dependency codes of the command (the chunked path's encoding)
+// and a mask of the views it is the tail of.
 constexpr int kSrchHalo = 256;
 constexpr int kSrchSpan = kSrchThreads + 2 * kSrchHalo;
+constexpr int kSrchMaxRep = 8;  // replicas (logs) of the command-level path
+constexpr uint32_t kNoArr = ~0u;
+
+// Per-view scan state.  Each step takes one neighbour (command cc, arrival t
+// at the view's replica or kNoArr) and returns whether the scan goes on; the
+// body is branch-free (bitwise logic, 32-bit arithmetic: c + W < 2^32), since
+// the short-circuit form compiled to a chain of divergent exec-mask branches
+// per neighbour.
+struct ViewScan {
+  uint32_t c, tq, W, qm, half;
+  uint32_t bc = kNoCmd, bt = 0, farc = kNoCmd;
+  bool tail = true;
+  // (c1, q1) reaches the replica before (c2, q2) (CmdMeta::before)
+  __device__ __forceinline__ bool before(uint32_t c1, uint32_t q1, uint32_t c2, uint32_t q2) const {
+    const uint32_t d = (q2 - q1) & qm;
+    return (c1 + W < c2) | (!(c2 + W < c1) & (d != 0) & (d <= half));
+  }
+  __device__ __forceinline__ void take(uint32_t cc, uint32_t t, bool earlier, bool mine) {
+    const bool repl = earlier & ((bc == kNoCmd) | before(bc, bt, cc, t));
+    bt = repl ? t : bt;
+    bc = repl ? cc : bc;
+    tail = tail & !(mine & !earlier);
+  }
+  // backward: false once nothing further back can matter (a command c' with
+  // c' + W below the best candidate, or below the first candidate under
+  // c - W, arrives before it)
+  __device__ __forceinline__ bool back(bool same_key, uint32_t cc, uint32_t t) {
+    const uint32_t lim = max(bc == kNoCmd ? 0u : bc, farc == kNoCmd ? 0u : farc);
+    const bool go = same_key & !((lim != 0u) & (cc + W < lim));
+    const bool mine = go & (t != kNoArr);
+    const bool earlier = mine & before(cc, t, c, tq);
+    take(cc, t, earlier, mine);
+    farc = earlier & (farc == kNoCmd) & (cc + W < c) ? cc : farc;
+    return go;
+  }
+  // forward: false once past c + W with the tail decided
+  __device__ __forceinline__ bool fwd(bool same_key, uint32_t cc, uint32_t t) {
+    const bool go = same_key & !((cc > c + W) & !tail);
+    const bool mine = go & (t != kNoArr);
+    const bool earlier = mine & before(cc, t, c, tq);
+    take(cc, t, earlier, mine);
+    return go;
+  }
+};
+
 __global__ void __launch_bounds__(kSrchThreads)
-    k_view_search(uint32_t n, uint32_t fq, uint32_t W, uint32_t K,
-                  const uint32_t *__restrict__ ks, const uint32_t *__restrict__ cs,
-                  const uint32_t *__restrict__ rec, const uint64_t *__restrict__ latest,
-                  uint32_t *__restrict__ code, uint8_t *__restrict__ tailm, uint32_t halo,
-                  uint32_t diag) {
-  __shared__ uint32_t s_k[kSrchSpan], s_c[kSrchSpan], s_r[kSrchSpan * 4];
+    k_cmd_search(uint32_t n, CmdMeta cm, uint32_t K, uint32_t np, const uint32_t *__restrict__ kws,
+                 const uint64_t *__restrict__ vals, const uint64_t *__restrict__ latest,
+                 uint32_t *__restrict__ code, uint8_t *__restrict__ tailm, uint32_t diag) {
+  __shared__ uint32_t s_key[kSrchSpan], s_c[kSrchSpan];
+  __shared__ uint32_t s_q[kSrchSpan * kSrchMaxRep];
   const uint32_t tid = threadIdx.x, core = blockIdx.x * kSrchThreads, i = core + tid;
-  // staged span [lo, hi): the core and its halos, clipped to [0, n)
-  const uint32_t lo = core > halo ? core - halo : 0u;
-  const uint32_t hi = min(n, core + kSrchThreads + halo);
-  for (uint32_t x = lo + tid; x < hi; x += kSrchThreads) {
-    const uint32_t c = cs[x];
-    s_k[x - lo] = ks[x];
-    s_c[x - lo] = c;
-    for (uint32_t j = 0; j < fq; j++) s_r[(x - lo) * 4 + j] = rec[size_t(c) * fq + j];
+  const uint32_t lo = core > uint32_t(kSrchHalo) ? core - kSrchHalo : 0u;
+  const uint32_t hi = min(n, core + kSrchThreads + kSrchHalo);
+  const uint32_t span = hi - lo;
+  for (uint32_t x = tid; x < span * np; x += kSrchThreads) s_q[x] = kNoArr;
+  __syncthreads();
+  for (uint32_t x = tid; x < span; x += kSrchThreads) {
+    const uint32_t kw = kws[lo + x];
+    const uint64_t v = vals[lo + x];
+    const uint64_t m = cm.meta(kw, v);
+    s_key[x] = kw & cm.kmask;
+    s_c[x] = uint32_t(v & cm.cmask);
+    for (uint32_t j = 0; j < cm.fq; j++) s_q[x * np + cm.rep(m, j)] = cm.arr(m, j);
   }
   __syncthreads();
   if (i >= n) return;
-  const uint32_t base = lo, tile = hi - lo;
   const uint32_t me = i - lo;
-  const uint32_t key = s_k[me], c = s_c[me];
-  constexpr uint32_t TM = (1u << kRecT) - 1;
-  uint32_t rj[4], tj[4], bt[4], bc[4], farc[4];
-  bool tail[4], doneB[4], doneF[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const bool v = uint32_t(j) < fq;
-    const uint32_t x = v ? s_r[me * 4 + j] : 0u;
-    rj[j] = v ? x >> kRecT : ~0u;
-    tj[j] = x & TM;
-    bt[j] = 0;
-    bc[j] = kNoCmd;
-    farc[j] = kNoCmd;
-    tail[j] = v;
-    doneB[j] = !v;
-    doneF[j] = !v;
-  }
-  // neighbour ip: key, command, view record j (LDS inside the tile)
-  auto nb = [&](uint32_t ip, uint32_t &kk, uint32_t &cc) {
-    if (ip - base < tile) {
-      kk = s_k[ip - base];
-      cc = s_c[ip - base];
-    } else {
-      kk = ks[ip];
-      cc = cs[ip];
-    }
+  const uint32_t key = s_key[me], c = s_c[me];
+  const uint64_t m0 = cm.meta(kws[i], vals[i]);
+  const uint32_t fq = cm.fq;
+  // a neighbour outside the staged span: unpack from the global arrays
+  auto far = [&](uint32_t ip, uint32_t rr, uint32_t &kk, uint32_t &cc, uint32_t &t) {
+    const uint32_t kw = kws[ip];
+    const uint64_t v = vals[ip];
+    kk = kw & cm.kmask;
+    cc = uint32_t(v & cm.cmask);
+    t = kNoArr;
+    cm.find(cm.meta(kw, v), rr, &t);
   };
-  auto nrec = [&](uint32_t ip, uint32_t cc, uint32_t j) {
-    return ip - base < tile ? s_r[(ip - base) * 4 + j] : rec[size_t(cc) * fq + j];
-  };
-  // backward: predecessors (and earlier commands arriving later: not tails)
-  for (uint32_t ip = (diag & 4) ? 0u : i; ip-- > 0;) {
-    uint32_t kk, cc;
-    nb(ip, kk, cc);
-    if (kk != key) break;
-    bool any = false;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      if (!doneB[j] && farc[j] != kNoCmd && uint64_t(cc) + W < farc[j]) doneB[j] = true;
-      any |= !doneB[j];
-    }
-    if (!any) break;
-    for (uint32_t jj = 0; jj < fq; jj++) {
-      const uint32_t x = nrec(ip, cc, jj), r = x >> kRecT, t = x & TM;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (doneB[j] || r != rj[j]) continue;
-        if (t < tj[j]) {
-          if (bc[j] == kNoCmd || t > bt[j]) {
-            bt[j] = t;
-            bc[j] = cc;
-          }
-          if (farc[j] == kNoCmd && uint64_t(cc) + W < c) farc[j] = cc;
-        } else {
-          tail[j] = false;
-        }
-      }
-    }
-  }
-  // forward: earlier arrivals up to c + W, and later arrivals (not tails)
-  for (uint32_t ip = (diag & 4) ? n : i + 1; ip < n; ip++) {
-    uint32_t kk, cc;
-    nb(ip, kk, cc);
-    if (kk != key) break;
-    const bool past = uint64_t(cc) > uint64_t(c) + W;
-    bool any = false;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      if (!doneF[j] && past && !tail[j]) doneF[j] = true;
-      any |= !doneF[j];
-    }
-    if (!any) break;
-    for (uint32_t jj = 0; jj < fq; jj++) {
-      const uint32_t x = nrec(ip, cc, jj), r = x >> kRecT, t = x & TM;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (doneF[j] || r != rj[j]) continue;
-        if (t < tj[j]) {
-          if (bc[j] == kNoCmd || t > bt[j]) {
-            bt[j] = t;
-            bc[j] = cc;
-          }
-        } else {
-          tail[j] = false;
-          if (past) doneF[j] = true;
-        }
-      }
-    }
-  }
-  uint32_t m = 0;
-  // (unrolled with a guard: a runtime trip count here would index the view
-  // arrays dynamically and put them in scratch memory)
+  uint32_t msk = 0;
+  uint32_t cds[4] = {0, 0, 0, 0};
+  // one view at a time, scalar scan state; the views' codes leave in one
+  // store per command
 #pragma unroll
   for (uint32_t j = 0; j < 4; j++) {
     if (j >= fq) break;
-    uint32_t cd;
-    if (bc[j] != kNoCmd) {
-      cd = bc[j] + 1;
-    } else {
-      const uint64_t x = (diag & 1) ? 0ull : latest[uint64_t(rj[j] + 1) * K + key];
-      cd = x ? (0x80000000u | uint32_t(x - kLogFlag)) : 0u;
+    if (diag & 4) {
+      cds[j] = c;
+      continue;
     }
-    if (!(diag & 2)) code[size_t(c) * fq + j] = cd;
-    m |= tail[j] ? 1u << j : 0u;
+    const uint32_t rr = cm.rep(m0, j);
+    ViewScan vs;
+    vs.c = c;
+    vs.W = cm.W;
+    vs.qm = uint32_t(cm.qmask);
+    vs.half = uint32_t(cm.qmask >> 1);
+    vs.tq = cm.arr(m0, j);
+    const uint32_t *sq = s_q + rr;
+    // backward: the staged span (lim 0: a leftmost element, the command 0,
+    // bounds nothing), then global memory
+    bool go = true;
+    for (uint32_t x = me; go && x > 0;) {
+      x--;
+      go = vs.back(s_key[x] == key, s_c[x], sq[x * np]);
+    }
+    go = go && lo > 0;
+    for (uint32_t ip = lo; go && ip-- > 0;) {
+      uint32_t kk, cc, t;
+      far(ip, rr, kk, cc, t);
+      go = vs.back(kk == key, cc, t);
+    }
+    // forward
+    go = true;
+    for (uint32_t x = me + 1; go && x < span; x++) go = vs.fwd(s_key[x] == key, s_c[x], sq[x * np]);
+    go = go && hi < n;
+    for (uint32_t ip = hi; go && ip < n; ip++) {
+      uint32_t kk, cc, t;
+      far(ip, rr, kk, cc, t);
+      go = vs.fwd(kk == key, cc, t);
+    }
+    uint32_t cd;
+    if (vs.bc != kNoCmd) {
+      cd = vs.bc + 1;
+    } else {
+      const uint64_t xl = (diag & 1) ? 0ull : latest[uint64_t(rr + 1) * K + key];
+      cd = xl ? (0x80000000u | uint32_t(xl - kLogFlag)) : 0u;
+    }
+    cds[j] = cd;
+    msk |= vs.tail ? 1u << j : 0u;
   }
-  tailm[i] = uint8_t(m);
+  uint32_t *o = (diag & 2) ? code + size_t(n) * fq + size_t(i) * fq : code + size_t(c) * fq;
+  if (fq == 3) {
+    *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(o) = HIP_vector_type<uint32_t, 3>(cds[0], cds[1], cds[2]);
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++)
+      if (j < fq) o[j] = cds[j];
+  }
+  tailm[i] = uint8_t(msk);
 }
 
 // the tails become the replicas' latest entries (after every head's read)
-__global__ void k_view_tails(uint32_t n, uint32_t fq, uint32_t K, const uint32_t *__restrict__ ks,
-                             const uint32_t *__restrict__ cs, const uint32_t *__restrict__ rec,
-                             const uint8_t *__restrict__ tailm, uint64_t *__restrict__ latest,
-                             uint64_t log_base) {
+__global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *__restrict__ kws,
+                            const uint64_t *__restrict__ vals, const uint8_t *__restrict__ tailm,
+                            uint64_t *__restrict__ latest, uint64_t log_base) {
   GRID_STRIDE(i, n) {
-    const uint32_t m = tailm[i];
-    if (!m) continue;
-    const uint32_t c = cs[i], key = ks[i];
-    for (uint32_t j = 0; j < fq; j++)
-      if (m & (1u << j))
-        latest[uint64_t((rec[size_t(c) * fq + j] >> kRecT) + 1) * K + key] = kLogFlag | (log_base + c);
+    const uint32_t msk = tailm[i];
+    if (!msk) continue;
+    const uint32_t kw = kws[i];
+    const uint64_t v = vals[i];
+    const uint64_t m = cm.meta(kw, v);
+    const uint32_t key = kw & cm.kmask, c = uint32_t(v & cm.cmask);
+    for (uint32_t j = 0; j < cm.fq; j++)
+      if (msk & (1u << j))
+        latest[uint64_t(cm.rep(m, j) + 1) * K + key] = kLogFlag | (log_base + c);
   }
 }
 
@@ -1190,6 +1289,7 @@ struct EngineDevice {
   DBuf<uint32_t> tail_defer;  // k_bucket_codes: deferred (segment, command) per workgroup
   DBuf<uint32_t> vrec;        // command-level views path: replica | arrival per element
   DBuf<uint8_t> tailm;        // command-level views path: tail views per sorted command
+  DBuf<uint64_t> cv64a, cv64b;  // command-level views path: packed sort values
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
   bool deps_only = false;     // fh_engine_set_deps_only: stop after the committed deps
   bool last_deps_only = false;
@@ -1602,9 +1702,9 @@ struct EngineDevice {
       k_tail_engine<uint32_t><<<grid_for(M, B), B, 0, stream>>>(
           M, ks, vs, 0, S, latest.get(), uint64_t(lmul), uint64_t(lmask), nullptr, bbase);
       sorted_keys32 = ks;
-    } else if (cmd_views_ok(b, k, fq, n)) {
+    } else if (CmdMeta cm; cmd_meta(b, k, fq, n, &cm)) {
       sv_fused = false;
-      cmd_views(b, n, fq, M, bkey, bbase);
+      cmd_views(b, n, fq, M, bkey, bbase, cm);
       mark("keydeps_views");
     } else {
       sv_fused = false;
@@ -1746,24 +1846,43 @@ struct EngineDevice {
     if (profile) collect_times();
   }
 
-  // The command-level views path (see k_view_search) applies to one key per
-  // command, fast quorums of <= 4, logs with an inversion span <= kCmdMaxW.
-  // Opt-in (FH_VIEW_CMD=1): bit-exact, but measured slower on C4 -- KeyDeps
-  // 13.8 ms against 12.8 chunked (records 1.1, command sort 1.6, search 10.4
-  // ms): the search touches ~3-4 random lines per command (its records in key
-  // order, the heads' latest entries, the scattered codes), more bytes than
-  // the chunked path's LDS-staged passes move.
-  bool cmd_views_ok(size_t b, uint32_t k, uint32_t fq, uint32_t n) const {
+  // The command-level views path (k_cmd_search) applies to one key per
+  // command, fast quorums of <= 4, and logs whose inversion span W leaves the
+  // packed arrival positions enough bits (CmdMeta: 3W + 1 < 2^(qb-1)).
+  // FH_VIEW_CMD=0 keeps the chunked path.
+  bool cmd_meta(size_t b, uint32_t k, uint32_t fq, uint32_t n, CmdMeta *cm) const {
     static const bool on = [] {
       const char *e = getenv("FH_VIEW_CMD");
-      return e && *e == '1';
+      return !(e && *e == '0');
     }();
-    return on && k == 1 && fq <= 4 && desc.nproc <= uint32_t(kMaxLogs) && b < h_win.size() &&
-           h_win[b] <= kCmdMaxW && n < (1u << kRecT);
+    if (!on || k != 1 || fq > 4 || desc.nproc > uint32_t(kSrchMaxRep) || b >= h_win.size() ||
+        n >= (1u << kRecT) || n < 2)
+      return false;
+    CmdMeta m{};
+    m.fq = fq;
+    m.rb = uint32_t(bits_for(desc.nproc));
+    const int db = sort_digit_bits(key_bits, 4);
+    const int passes = std::max(1, (key_bits + db - 1) / db);
+    m.kb = uint32_t(passes * db);
+    m.cb = uint32_t(bits_for(n));
+    if (m.kb > 32) return false;
+    // the meta travels in the key word's and the value's free bits and is
+    // handled as one u64
+    const uint32_t spare = std::min<uint32_t>(64, (64 - m.cb) + (32 - m.kb));
+    if (spare / fq <= m.rb + 2) return false;
+    m.qb = std::min<uint32_t>(spare / fq - m.rb, uint32_t(kRecT));
+    m.vb = m.rb + m.qb;
+    m.kmask = key_bits >= 32 ? ~0u : (1u << key_bits) - 1;
+    m.W = h_win[b];
+    m.cmask = (uint64_t(1) << m.cb) - 1;
+    m.qmask = (uint64_t(1) << m.qb) - 1;
+    if (uint64_t(3) * m.W + 1 >= (uint64_t(1) << (m.qb - 1))) return false;
+    *cm = m;
+    return true;
   }
 
   void cmd_views(size_t b, uint32_t n, uint32_t fq, uint32_t M, const uint32_t *bkey,
-                 uint64_t bbase) {
+                 uint64_t bbase, const CmdMeta &cm) {
     const uint32_t np = desc.nproc;
     LogOffs lo{};
     const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
@@ -1775,32 +1894,40 @@ struct EngineDevice {
     const uint32_t G = std::max<uint32_t>(1, (n + per - 1) / per);
     probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records, dim3(G), dim3(1024),
                   stream, n, fq, np, G, lo, bent, rec);
-    uint32_t *ks = nullptr, *cs = nullptr;
-    sort_pairs<uint32_t, uint32_t>(bkey, nullptr, sk32a.ensure(n + 1), sva.ensure(n + 1),
-                                   sk32b.ensure(n + 1), svb.ensure(n + 1), n, key_bits, sort_ws,
-                                   stream, &ks, &cs);
-    uint8_t *tm = tailm.ensure(n + 1);
-    // measurement knobs: FH_SRCH_HALO (<= kSrchHalo), FH_SRCH_DIAG (1: skip the
-    // latest reads, 2: skip the code writes, 4: skip the scans -- diagnosis
-    // only, not bit-exact).  Measured at C4 (us): full 10440; no scans 8270;
-    // no scans, latest reads or code writes 4200, and without the halo 2580.
-    static const uint32_t srch_halo = [] {
-      const char *e = getenv("FH_SRCH_HALO");
-      return e ? std::min<uint32_t>(uint32_t(atol(e)), kSrchHalo) : uint32_t(kSrchHalo);
-    }();
+    const uint32_t tiles = (n + kTile - 1) / kTile;
+    sort_ws.prepare(tiles, 1, stream);
+    const int db = sort_digit_bits(key_bits, 4);
+    uint32_t *kwa = sk32a.ensure(n + 1);
+    uint64_t *va = cv64a.ensure(n + 1);
+    // reads the key and fq records, writes the key word and the value
+    probed_launch("cmd_pack", double(n) * (4.0 + 4.0 * fq + 4.0 + 8.0), k_cmd_pack, dim3(tiles),
+                  dim3(kThreads), stream, n, cm, bkey, (const uint32_t *)rec, kwa, va,
+                  sort_ws.meta.get(), (1u << db) - 1);
+    uint32_t *ks = nullptr;
+    uint64_t *vs = nullptr;
+    sort_pairs_counted<uint32_t, uint64_t>(kwa, va, sk32b.ensure(n + 1), cv64b.ensure(n + 1), n,
+                                           key_bits, sort_ws, stream, &ks, &vs, db);
+    // measurement knob FH_SRCH_DIAG (after the first run; not bit-exact): 1
+    // skips the heads' latest reads, 2 writes the codes in sorted order to
+    // scratch, 4 skips the scans
     static const uint32_t srch_diag = [] {
       const char *e = getenv("FH_SRCH_DIAG");
       return e ? uint32_t(atol(e)) : 0u;
     }();
-    // reads the sorted keys and commands and the view records (one gather per
-    // command; neighbours from LDS), writes fq codes per command
-    probed_launch("view_search", double(n) * (4.0 + 4.0 + fq * 4.0 + fq * 4.0 + 1.0),
-                  k_view_search, dim3((n + kSrchThreads - 1) / kSrchThreads), dim3(kSrchThreads),
-                  stream, n, fq, h_win[b], uint32_t(key_space), (const uint32_t *)ks,
-                  (const uint32_t *)cs, (const uint32_t *)rec, (const uint64_t *)views_latest(),
-                  dep32.ensure(M + 1), tm, srch_halo, srch_diag);
-    k_view_tails<<<grid_for(n, B), B, 0, stream>>>(n, fq, uint32_t(key_space), ks, cs, rec, tm,
-                                                   views_latest(), bbase);
+    // (the first run writes the real codes: later runs of the same stream
+    // keep them, so the rest of the step stays exact)
+    static uint32_t srch_runs = 0;
+    const uint32_t diag_now = srch_runs++ ? srch_diag : 0u;
+    uint8_t *tm = tailm.ensure(n + 1);
+    // reads the sorted key words and values (12 B, neighbours from LDS) and
+    // the heads' latest entries, writes fq codes and the tail mask
+    probed_launch("cmd_search", double(n) * (12.0 + fq * 4.0 + 1.0), k_cmd_search,
+                  dim3((n + kSrchThreads - 1) / kSrchThreads), dim3(kSrchThreads), stream, n, cm,
+                  uint32_t(key_space), np, (const uint32_t *)ks, (const uint64_t *)vs,
+                  (const uint64_t *)views_latest(), dep32.ensure((srch_diag & 2 ? 2 * size_t(M) : size_t(M)) + 1), tm,
+                  diag_now);
+    k_cmd_tails<<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks, vs, tm,
+                                                  views_latest(), bbase);
   }
 
   // The chunk's dependency codes -> dep32 through the placement pass: bucket

@@ -304,9 +304,11 @@ print("ok")
 
 
 def test_views_command_level_path_matches_oracle():
-    """The opt-in command-level KeyDeps path (FH_VIEW_CMD=1, engine.hip
-    k_view_search; read once per process: a child process): a C4-shaped
-    stream and a streamed multi-batch one, against the oracle."""
+    """The command-level KeyDeps path (engine.hip k_cmd_pack / k_cmd_search,
+    the default for one key per command; a child process, as the knob is
+    read once): a C4-shaped stream, and a streamed multi-batch one whose
+    reorder window (200) leaves the packed arrival positions fewer spare
+    bits, against the oracle."""
     import subprocess, sys, os
     code = f"""
 import numpy as np, sys
@@ -347,12 +349,14 @@ print("ok")
 
 @pytest.mark.parametrize("env", [
     {},
-    {"FH_TAIL_FUSED": "0", "FH_SORT_UP_ATOMIC": "1", "FH_SCAN_WIDE": "0"},
-    {"FH_SORT_UP_ATOMIC": "0"},
+    {"FH_VIEW_CMD": "0"},
+    {"FH_VIEW_CMD": "0", "FH_TAIL_FUSED": "0", "FH_SORT_UP_ATOMIC": "1", "FH_SCAN_WIDE": "0"},
+    {"FH_VIEW_CMD": "0", "FH_SORT_UP_ATOMIC": "0"},
 ])
 def test_views_kernel_variants_match_oracle(env):
     """The replica-view path's kernel variants (read once per process: a
-    child process), each against the oracle on a hot-key stream cut into
+    child process): the command-level path (default) and the chunked one
+    (FH_VIEW_CMD=0), each against the oracle on a hot-key stream cut into
     chunks of 20,000 elements, so that segments cross the bucketing
     workgroups and chunks: the segment tails written by k_bucket_codes (the
     first segment's deferred to k_place) or by k_tail_engine
