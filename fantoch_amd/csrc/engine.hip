@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(kThreads)
 // :88-95) iff no r_j-command of the key arrives later; any beyond c + W does.
 // Writes the fq dependency codes of the command (the chunked path's encoding)
 // and a mask of the views it is the tail of.
-constexpr int kSrchHalo = 256;
+constexpr int kSrchHalo = 128;
 constexpr int kSrchSpan = kSrchThreads + 2 * kSrchHalo;
 constexpr int kSrchMaxRep = 8;  // replicas (logs) of the command-level path
 constexpr uint32_t kNoArr = ~0u;
@@ -521,6 +521,7 @@ struct ViewScan {
   }
 };
 
+template <uint32_t FQ>
 __global__ void __launch_bounds__(kSrchThreads)
     k_cmd_search(uint32_t n, CmdMeta cm, uint32_t K, uint32_t np, const uint32_t *__restrict__ kws,
                  const uint64_t *__restrict__ vals, const uint64_t *__restrict__ latest,
@@ -539,81 +540,111 @@ __global__ void __launch_bounds__(kSrchThreads)
     const uint64_t m = cm.meta(kw, v);
     s_key[x] = kw & cm.kmask;
     s_c[x] = uint32_t(v & cm.cmask);
-    for (uint32_t j = 0; j < cm.fq; j++) s_q[x * np + cm.rep(m, j)] = cm.arr(m, j);
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) s_q[x * np + cm.rep(m, j)] = cm.arr(m, j);
   }
   __syncthreads();
   if (i >= n) return;
   const uint32_t me = i - lo;
   const uint32_t key = s_key[me], c = s_c[me];
   const uint64_t m0 = cm.meta(kws[i], vals[i]);
-  const uint32_t fq = cm.fq;
-  // a neighbour outside the staged span: unpack from the global arrays
-  auto far = [&](uint32_t ip, uint32_t rr, uint32_t &kk, uint32_t &cc, uint32_t &t) {
+  // all views in one pass over the neighbours (shared key and command
+  // loads); each view's scan stops on its own
+  ViewScan vs[FQ];
+  uint32_t rr[FQ];
+  bool on[FQ];
+#pragma unroll
+  for (uint32_t j = 0; j < FQ; j++) {
+    rr[j] = cm.rep(m0, j);
+    vs[j].c = c;
+    vs[j].W = cm.W;
+    vs[j].qm = uint32_t(cm.qmask);
+    vs[j].half = uint32_t(cm.qmask >> 1);
+    vs[j].tq = cm.arr(m0, j);
+    on[j] = !(diag & 4);
+  }
+  // backward: the staged span, then global memory (a neighbour outside the
+  // span is unpacked from the packed arrays)
+  bool go = !(diag & 4);
+  for (uint32_t x = me; go && x > 0;) {
+    x--;
+    const bool sk = s_key[x] == key;
+    const uint32_t cc = s_c[x];
+    go = false;
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) {
+      on[j] = vs[j].back(sk & on[j], cc, s_q[x * np + rr[j]]);
+      go |= on[j];
+    }
+  }
+  for (uint32_t ip = lo; go && ip-- > 0;) {
     const uint32_t kw = kws[ip];
     const uint64_t v = vals[ip];
-    kk = kw & cm.kmask;
-    cc = uint32_t(v & cm.cmask);
-    t = kNoArr;
-    cm.find(cm.meta(kw, v), rr, &t);
-  };
-  uint32_t msk = 0;
-  uint32_t cds[4] = {0, 0, 0, 0};
-  // one view at a time, scalar scan state; the views' codes leave in one
-  // store per command
+    const uint64_t m = cm.meta(kw, v);
+    const bool sk = (kw & cm.kmask) == key;
+    const uint32_t cc = uint32_t(v & cm.cmask);
+    go = false;
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    if (j >= fq) break;
+    for (uint32_t j = 0; j < FQ; j++) {
+      uint32_t t = kNoArr;
+      cm.find(m, rr[j], &t);
+      on[j] = vs[j].back(sk & on[j], cc, t);
+      go |= on[j];
+    }
+  }
+  // forward
+  go = !(diag & 4);
+#pragma unroll
+  for (uint32_t j = 0; j < FQ; j++) on[j] = go;
+  for (uint32_t x = me + 1; go && x < span; x++) {
+    const bool sk = s_key[x] == key;
+    const uint32_t cc = s_c[x];
+    go = false;
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) {
+      on[j] = vs[j].fwd(sk & on[j], cc, s_q[x * np + rr[j]]);
+      go |= on[j];
+    }
+  }
+  for (uint32_t ip = hi; go && ip < n; ip++) {
+    const uint32_t kw = kws[ip];
+    const uint64_t v = vals[ip];
+    const uint64_t m = cm.meta(kw, v);
+    const bool sk = (kw & cm.kmask) == key;
+    const uint32_t cc = uint32_t(v & cm.cmask);
+    go = false;
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) {
+      uint32_t t = kNoArr;
+      cm.find(m, rr[j], &t);
+      on[j] = vs[j].fwd(sk & on[j], cc, t);
+      go |= on[j];
+    }
+  }
+  uint32_t cds[FQ];
+  uint32_t msk = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < FQ; j++) {
     if (diag & 4) {
       cds[j] = c;
-      continue;
-    }
-    const uint32_t rr = cm.rep(m0, j);
-    ViewScan vs;
-    vs.c = c;
-    vs.W = cm.W;
-    vs.qm = uint32_t(cm.qmask);
-    vs.half = uint32_t(cm.qmask >> 1);
-    vs.tq = cm.arr(m0, j);
-    const uint32_t *sq = s_q + rr;
-    // backward: the staged span (lim 0: a leftmost element, the command 0,
-    // bounds nothing), then global memory
-    bool go = true;
-    for (uint32_t x = me; go && x > 0;) {
-      x--;
-      go = vs.back(s_key[x] == key, s_c[x], sq[x * np]);
-    }
-    go = go && lo > 0;
-    for (uint32_t ip = lo; go && ip-- > 0;) {
-      uint32_t kk, cc, t;
-      far(ip, rr, kk, cc, t);
-      go = vs.back(kk == key, cc, t);
-    }
-    // forward
-    go = true;
-    for (uint32_t x = me + 1; go && x < span; x++) go = vs.fwd(s_key[x] == key, s_c[x], sq[x * np]);
-    go = go && hi < n;
-    for (uint32_t ip = hi; go && ip < n; ip++) {
-      uint32_t kk, cc, t;
-      far(ip, rr, kk, cc, t);
-      go = vs.fwd(kk == key, cc, t);
-    }
-    uint32_t cd;
-    if (vs.bc != kNoCmd) {
-      cd = vs.bc + 1;
+    } else if (vs[j].bc != kNoCmd) {
+      cds[j] = vs[j].bc + 1;
     } else {
-      const uint64_t xl = (diag & 1) ? 0ull : latest[uint64_t(rr + 1) * K + key];
-      cd = xl ? (0x80000000u | uint32_t(xl - kLogFlag)) : 0u;
+      const uint64_t xl = (diag & 1) ? 0ull : latest[uint64_t(rr[j] + 1) * K + key];
+      cds[j] = xl ? (0x80000000u | uint32_t(xl - kLogFlag)) : 0u;
     }
-    cds[j] = cd;
-    msk |= vs.tail ? 1u << j : 0u;
+    msk |= vs[j].tail ? 1u << j : 0u;
   }
-  uint32_t *o = (diag & 2) ? code + size_t(n) * fq + size_t(i) * fq : code + size_t(c) * fq;
-  if (fq == 3) {
-    *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(o) = HIP_vector_type<uint32_t, 3>(cds[0], cds[1], cds[2]);
+  // the views' codes leave in one store per command
+  uint32_t *o = (diag & 2) ? code + size_t(n) * FQ + size_t(i) * FQ : code + size_t(c) * FQ;
+  if constexpr (FQ == 3) {
+    *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(o) =
+        HIP_vector_type<uint32_t, 3>(cds[0], cds[1], cds[2]);
+  } else if constexpr (FQ == 4) {
+    *reinterpret_cast<uint4 *>(o) = make_uint4(cds[0], cds[1], cds[2], cds[3]);
   } else {
 #pragma unroll
-    for (uint32_t j = 0; j < 4; j++)
-      if (j < fq) o[j] = cds[j];
+    for (uint32_t j = 0; j < FQ; j++) o[j] = cds[j];
   }
   tailm[i] = uint8_t(msk);
 }
@@ -1921,11 +1952,29 @@ struct EngineDevice {
     uint8_t *tm = tailm.ensure(n + 1);
     // reads the sorted key words and values (12 B, neighbours from LDS) and
     // the heads' latest entries, writes fq codes and the tail mask
-    probed_launch("cmd_search", double(n) * (12.0 + fq * 4.0 + 1.0), k_cmd_search,
-                  dim3((n + kSrchThreads - 1) / kSrchThreads), dim3(kSrchThreads), stream, n, cm,
-                  uint32_t(key_space), np, (const uint32_t *)ks, (const uint64_t *)vs,
-                  (const uint64_t *)views_latest(), dep32.ensure((srch_diag & 2 ? 2 * size_t(M) : size_t(M)) + 1), tm,
-                  diag_now);
+    const dim3 sg((n + kSrchThreads - 1) / kSrchThreads);
+    uint32_t *codes = dep32.ensure((srch_diag & 2 ? 2 * size_t(M) : size_t(M)) + 1);
+    const double sb = double(n) * (12.0 + fq * 4.0 + 1.0);
+    const uint32_t K = uint32_t(key_space);
+    const uint64_t *lat = views_latest();
+    switch (fq) {
+      case 1:
+        probed_launch("cmd_search", sb, k_cmd_search<1>, sg, dim3(kSrchThreads), stream, n, cm, K, np,
+                      (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
+        break;
+      case 2:
+        probed_launch("cmd_search", sb, k_cmd_search<2>, sg, dim3(kSrchThreads), stream, n, cm, K, np,
+                      (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
+        break;
+      case 3:
+        probed_launch("cmd_search", sb, k_cmd_search<3>, sg, dim3(kSrchThreads), stream, n, cm, K, np,
+                      (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
+        break;
+      default:
+        probed_launch("cmd_search", sb, k_cmd_search<4>, sg, dim3(kSrchThreads), stream, n, cm, K, np,
+                      (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
+        break;
+    }
     k_cmd_tails<<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks, vs, tm,
                                                   views_latest(), bbase);
   }
