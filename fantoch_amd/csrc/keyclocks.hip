@@ -18,9 +18,13 @@
 //   predecessors per query, each key's segment is clock-sorted: the prefix
 //                below the query clock (predecessors) and the suffix above it
 //                (higher); one thread k-way merges the query's segments by
-//                clock, dropping repeats (timestamps are unique, so a repeat
-//                is the same dot on another key); two passes (count, scan,
-//                write).  Output order: ascending clock.
+//                (clock, dot), dropping repeats of a (clock, dot) pair (the
+//                same dot on another key of a multi-key command); two
+//                different dots with one clock on different keys are both
+//                reported, as the reference's HashSet<Dot> keeps them; two
+//                passes (count, scan, write).  Output order: ascending
+//                (clock, dot).  At most kMaxKeys keys per command
+//                (FH_ENOTIMPL beyond).
 #include <algorithm>
 #include <vector>
 
@@ -135,23 +139,25 @@ __global__ void k_kc_query(uint32_t n, const uint32_t *__restrict__ koff,
     }
     uint32_t c = 0;
     const uint32_t o = out_off ? out_off[i] : 0u;
-    uint64_t last = ~0ull;
+    uint64_t last = ~0ull, last_dot = 0;
     for (;;) {
       int best = -1;
-      uint64_t bc = ~0ull;
+      uint64_t bc = ~0ull, bd = ~0ull;
       for (uint32_t s = 0; s < kn; s++)
         if (cur[s] < end[s]) {
-          const uint64_t x = comp[cur[s]] & mask;
-          if (x < bc) {
+          const uint64_t x = comp[cur[s]] & mask, d = edot[cur[s]];
+          if (x < bc || (x == bc && d < bd)) {
             bc = x;
+            bd = d;
             best = int(s);
           }
         }
       if (best < 0) break;
-      if (bc != last) {
-        if (out) out[o + c] = edot[cur[best]];
+      if (bc != last || bd != last_dot) {  // (the reference's predecessors HashSet<Dot>)
+        if (out) out[o + c] = bd;
         c++;
         last = bc;
+        last_dot = bd;
       }
       cur[best]++;
     }
@@ -204,8 +210,9 @@ struct KeyClocksDevice {
     for (size_t i = 0; i < n; i++) mx = std::max(mx, clock[i]);
     std::vector<uint32_t> k32(m + 1);
     for (size_t i = 0; i < n; i++) {
-      FH_CHECK(key_off[i + 1] >= key_off[i] && key_off[i + 1] - key_off[i] <= uint32_t(kMaxKeys),
-               FH_EINVAL, "keyclocks: at most 8 keys per command");
+      FH_CHECK(key_off[i + 1] >= key_off[i], FH_EINVAL, "keyclocks: key offsets decrease");
+      FH_CHECK(key_off[i + 1] - key_off[i] <= uint32_t(kMaxKeys), FH_ENOTIMPL,
+               "keyclocks: more than 8 keys in a command (the device merge holds 8 segments)");
       for (uint32_t e = key_off[i]; e < key_off[i + 1]; e++) {
         FH_CHECK(key_id[e] < cfg.key_space, FH_EINVAL, "key id >= key_space");
         k32[e] = uint32_t(key_id[e]);

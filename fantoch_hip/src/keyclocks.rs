@@ -2,7 +2,9 @@
 //! mod.rs:13-45, SequentialKeyClocks sequential.rs:14-152) on
 //! `fh_keyclocks_*`.  Needs `Clock::{seq, process_id}` accessors (the
 //! reference keeps the fields private, clocks/mod.rs:27-30) -- one-line
-//! `pub fn`s.
+//! `pub fn`s.  Limit: commands of at most 8 keys (the device merge holds 8
+//! key segments); a larger command gets `FH_ENOTIMPL`, which `check` turns
+//! into a panic naming the limit.
 use crate::{check, ffi, pack, unpack, Interner};
 use fantoch::command::Command;
 use fantoch::id::{Dot, ProcessId, ShardId};

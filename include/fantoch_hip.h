@@ -375,9 +375,11 @@ fh_status fh_keyclocks_destroy(fh_keyclocks *h);
 fh_status fh_keyclocks_clock_next(fh_keyclocks *h, uint64_t *clock);
 fh_status fh_keyclocks_clock_join(fh_keyclocks *h, uint64_t clock);
 /* A batch of KeyClocks::add(dot, cmd, clock) (sequential.rs:43-56): each
- * command's keys (key_off[n+1], key_id[], <= 8 per command) get the entry
- * clock -> dot.  FH_EINVARIANT (no state change) for a timestamp added twice
- * on a key. */
+ * command's keys (key_off[n+1], key_id[]) get the entry clock -> dot.
+ * FH_EINVARIANT (no state change) for a timestamp added twice on a key.
+ * Commands of more than 8 keys: FH_ENOTIMPL (the reference takes any
+ * number; the device merge holds 8 key segments), here and in remove /
+ * predecessors. */
 fh_status fh_keyclocks_add(fh_keyclocks *h, size_t n, const uint64_t *dot,
                            const uint32_t *key_off, const uint64_t *key_id,
                            const uint64_t *clock);
@@ -388,7 +390,10 @@ fh_status fh_keyclocks_remove(fh_keyclocks *h, size_t n, const uint32_t *key_off
 /* A batch of KeyClocks::predecessors(dot, cmd, clock, higher)
  * (sequential.rs:77-119): pred_off[n+1] / pred_dot[] = the dots on the
  * command's keys with a lower clock; higher_off / higher_dot (all three
- * higher_* NULL = `higher: None`) = those with a higher clock.  Sizes are
+ * higher_* NULL = `higher: None`) = those with a higher clock, each row in
+ * ascending (clock, dot) order, one entry per distinct dot (the reference's
+ * HashSet<Dot>: two dots holding one clock on different keys are both
+ * reported; the same dot on several keys once).  Sizes are
  * always reported (*pred_len, *higher_len); FH_ECAP if a cap is short
  * (nothing written there).  FH_EINVARIANT if another command holds the same
  * timestamp on a key (:108-112). */

@@ -42,6 +42,34 @@ def test_invariants_leave_state_unchanged():
     assert kc.predecessors(D((1, 1)), ["A"], clock(5, 1)) == set()
 
 
+def test_two_dots_with_one_clock_on_different_keys():
+    """`add` only rejects a repeated timestamp on one key (sequential.rs:43-56),
+    so two dots may hold one clock on different keys; predecessors' HashSet<Dot>
+    (:77-119) then reports both, and the same dot on several keys once (ADVICE
+    r2: the merge used to drop repeats by clock alone).  The oracle agrees."""
+    kc, orc = HipKeyClocks(1, key_space=16), KeyClocks(1, 0)
+    for obj in (kc, orc):
+        obj.add(D((1, 1)), ["A"], clock(3, 1))
+        obj.add(D((2, 1)), ["B"], clock(3, 1))       # another dot, same clock, other key
+        obj.add(D((3, 1)), ["A", "B"], clock(2, 1))  # one dot on both keys
+    want = {D((1, 1)), D((2, 1)), D((3, 1))}
+    assert orc.predecessors(D((4, 1)), ["A", "B"], clock(9, 1)) == want
+    po, pd = kc.predecessors_batch([D((4, 1))], [["A", "B"]], [clock(9, 1)])
+    assert sorted(pd.tolist()) == sorted(want) and len(pd) == 3
+    assert pd.tolist()[0] == D((3, 1))  # ascending (clock, dot)
+
+
+def test_more_than_eight_keys_is_not_implemented():
+    kc = HipKeyClocks(1, key_space=64)
+    keys = [f"k{i}" for i in range(9)]
+    with pytest.raises(L.FhError) as e:
+        kc.add(D((1, 1)), keys, clock(1, 1))
+    assert e.value.status == L.FH_ENOTIMPL and len(kc) == 0
+    with pytest.raises(L.FhError) as e:
+        kc.predecessors(D((1, 1)), keys, clock(2, 1))
+    assert e.value.status == L.FH_ENOTIMPL
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_random_batches_match_oracle(seed):
     """Batches of adds, removes and predecessor queries (with `higher`) over
