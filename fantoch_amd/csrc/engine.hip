@@ -20,6 +20,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "graph_core.h"
@@ -353,17 +354,21 @@ struct LogOffs {
 // log -- commands ~[w·n/G, (w+1)·n/G) -- assembles their records in an LDS
 // window of kRecWin positions and writes the window out whole; an element
 // outside its window (a late arrival) is written directly.
-constexpr uint32_t kRecWin = 32768;   // 128 KB of LDS
-constexpr uint32_t kRecSlack = 2048;  // window positions below the slice's first command
+// 64 KB of LDS: two workgroups per CU (FH_REC_WIN=32768, one: 1072 against
+// 935 us per C4 launch; 8192: 1391)
+constexpr uint32_t kRecWin = 16384;
 constexpr uint32_t kRecNone = ~0u;    // never a record (replica < 16)
+// window positions below the slice's first command
+constexpr uint32_t rec_slack(uint32_t win) { return win / 16; }
+template <uint32_t WIN>
 __global__ void __launch_bounds__(1024)
     k_view_records(uint32_t n, uint32_t fq, uint32_t np, uint32_t G, LogOffs lo,
                    const uint32_t *__restrict__ ent, uint32_t *__restrict__ rec) {
-  __shared__ uint32_t s_v[kRecWin];
+  __shared__ uint32_t s_v[WIN];
   const uint32_t w = blockIdx.x;
-  for (uint32_t p = threadIdx.x; p < kRecWin; p += 1024) s_v[p] = kRecNone;
+  for (uint32_t p = threadIdx.x; p < WIN; p += 1024) s_v[p] = kRecNone;
   const uint64_t c0 = uint64_t(n) * w / G;
-  const uint64_t e0 = c0 * fq > kRecSlack ? c0 * fq - kRecSlack : 0;
+  const uint64_t e0 = c0 * fq > rec_slack(WIN) ? c0 * fq - rec_slack(WIN) : 0;
   __syncthreads();
   for (uint32_t r = 0; r < np; r++) {
     const uint64_t len = lo.off[r + 1] - lo.off[r];
@@ -371,14 +376,14 @@ __global__ void __launch_bounds__(1024)
     for (uint32_t q = q0 + threadIdx.x; q < q1; q += 1024) {
       const uint32_t e = ent[q], v = (r << kRecT) | (q - lo.off[r]);
       const uint64_t rel = uint64_t(e) - e0;
-      if (e >= e0 && rel < kRecWin)
+      if (e >= e0 && rel < WIN)
         s_v[rel] = v;
       else
         rec[e] = v;
     }
   }
   __syncthreads();
-  for (uint32_t p = threadIdx.x; p < kRecWin; p += 1024) {
+  for (uint32_t p = threadIdx.x; p < WIN; p += 1024) {
     const uint32_t v = s_v[p];
     if (v != kRecNone) rec[e0 + p] = v;
   }
@@ -475,7 +480,6 @@ __global__ void __launch_bounds__(kThreads)
 // Writes the fq dependency codes of the command (the chunked path's encoding)
 // and a mask of the views it is the tail of.
 constexpr int kSrchHalo = 128;
-constexpr int kSrchSpan = kSrchThreads + 2 * kSrchHalo;
 constexpr int kSrchMaxRep = 8;  // replicas (logs) of the command-level path
 constexpr uint32_t kNoArr = ~0u;
 
@@ -521,20 +525,21 @@ struct ViewScan {
   }
 };
 
-template <uint32_t FQ>
-__global__ void __launch_bounds__(kSrchThreads)
+template <uint32_t FQ, int TH>
+__global__ void __launch_bounds__(TH)
     k_cmd_search(uint32_t n, CmdMeta cm, uint32_t K, uint32_t np, const uint32_t *__restrict__ kws,
                  const uint64_t *__restrict__ vals, const uint64_t *__restrict__ latest,
                  uint32_t *__restrict__ code, uint8_t *__restrict__ tailm, uint32_t diag) {
-  __shared__ uint32_t s_key[kSrchSpan], s_c[kSrchSpan];
-  __shared__ uint32_t s_q[kSrchSpan * kSrchMaxRep];
-  const uint32_t tid = threadIdx.x, core = blockIdx.x * kSrchThreads, i = core + tid;
+  constexpr int kSpan = TH + 2 * kSrchHalo;
+  __shared__ uint32_t s_key[kSpan], s_c[kSpan];
+  __shared__ uint32_t s_q[kSpan * kSrchMaxRep];
+  const uint32_t tid = threadIdx.x, core = blockIdx.x * TH, i = core + tid;
   const uint32_t lo = core > uint32_t(kSrchHalo) ? core - kSrchHalo : 0u;
-  const uint32_t hi = min(n, core + kSrchThreads + kSrchHalo);
+  const uint32_t hi = min(n, core + TH + kSrchHalo);
   const uint32_t span = hi - lo;
-  for (uint32_t x = tid; x < span * np; x += kSrchThreads) s_q[x] = kNoArr;
+  for (uint32_t x = tid; x < span * np; x += TH) s_q[x] = kNoArr;
   __syncthreads();
-  for (uint32_t x = tid; x < span; x += kSrchThreads) {
+  for (uint32_t x = tid; x < span; x += TH) {
     const uint32_t kw = kws[lo + x];
     const uint64_t v = vals[lo + x];
     const uint64_t m = cm.meta(kw, v);
@@ -637,7 +642,11 @@ __global__ void __launch_bounds__(kSrchThreads)
   }
   // the views' codes leave in one store per command
   uint32_t *o = (diag & 2) ? code + size_t(n) * FQ + size_t(i) * FQ : code + size_t(c) * FQ;
-  if constexpr (FQ == 3) {
+  if (diag & 8) {  // measurement: one aligned 16-B store per command (scratch)
+    uint32_t *o4 = code + size_t(n) * FQ + size_t((diag & 2) ? i : c) * 4;
+    *reinterpret_cast<uint4 *>(o4) = make_uint4(cds[0], FQ > 1 ? cds[FQ > 1 ? 1 : 0] : 0u,
+                                                FQ > 2 ? cds[FQ > 2 ? 2 : 0] : 0u, msk);
+  } else if constexpr (FQ == 3) {
     *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(o) =
         HIP_vector_type<uint32_t, 3>(cds[0], cds[1], cds[2]);
   } else if constexpr (FQ == 4) {
@@ -813,7 +822,10 @@ __device__ __forceinline__ void cmd_union_regs(
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n,
-    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, bool nt) {
+    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, bool nt, int mode) {
+  // mode 0: committed dots and graph edges; 1: edges (and the missing flags)
+  // only; 2: committed dots only (FH_UNION_SIDE: the dots on a second stream,
+  // beside the graph stage, which needs only the edges)
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
@@ -834,6 +846,11 @@ __device__ __forceinline__ void cmd_union_regs(
       }
     }
   }
+  if (mode != 2) {
+    if (blocked0) blocked0[i] = missing;
+    if (missing) atomicAdd(nblocked, 1u);
+  }
+  if (mode != 1) {
   // in-batch deps: one dot gather per distinct vid (the fast-quorum
   // members' reports often name the same previous command)
 #pragma unroll
@@ -879,6 +896,9 @@ __device__ __forceinline__ void cmd_union_regs(
   } else {
     for (uint32_t q = m; q < S; q++) st_maybe_nt(dd + q, uint64_t(0), nt);
   }
+  st_maybe_nt(dep_cnt + i, m, nt);
+  }
+  if (mode == 2) return;
   uint32_t *ds = dst + size_t(i) * S;
   uint32_t nv = 0;
 #pragma unroll
@@ -892,9 +912,6 @@ __device__ __forceinline__ void cmd_union_regs(
   }
   for (uint32_t q = nv; q < S; q++) st_maybe_nt(ds + q, i, nt);  // padding: self loops are ignored
   if (nv_out) st_maybe_nt(nv_out + i, nv, nt);
-  st_maybe_nt(dep_cnt + i, m, nt);
-  if (blocked0) blocked0[i] = missing;
-  if (missing) atomicAdd(nblocked, 1u);
 }
 
 // Per command: union of its fast-quorum members' element deps (vids and
@@ -910,7 +927,8 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
                              uint64_t bbase, const uint32_t *__restrict__ out_off,
-                             uint32_t *__restrict__ err, uint32_t c0, uint32_t c1, int nt) {
+                             uint32_t *__restrict__ err, uint32_t c0, uint32_t c1, int nt,
+                             int mode) {
   // commands [c0, c1) of the batch (a launch per command range keeps the
   // gathered dots of recent dependencies cache-resident: FH_UNION_CHUNK)
   // uniform: the register path, with a sorting network sized to the row
@@ -924,20 +942,20 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     const uint32_t lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
     for (size_t j = size_t(lb) * blockDim.x + threadIdx.x; j < cn; j += size_t(nb) * blockDim.x)
       cmd_union_regs<4>(c0 + uint32_t(j), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                        blocked0, nblocked, nv_out, bbase, n, out_off, err, nt != 0);
+                        blocked0, nblocked, nv_out, bbase, n, out_off, err, nt != 0, mode);
     return;
   }
   if (S <= 8) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<8>(c0 + j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n, out_off, err, nt != 0);
+                        nblocked, nv_out, bbase, n, out_off, err, nt != 0, mode);
     }
     return;
   }
   if (S <= kRegSlots) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<kRegSlots>(c0 + j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                                blocked0, nblocked, nv_out, bbase, n, out_off, err, nt != 0);
+                                blocked0, nblocked, nv_out, bbase, n, out_off, err, nt != 0, mode);
     }
     return;
   }
@@ -1327,6 +1345,8 @@ struct EngineDevice {
   DBuf<unsigned long long> srcstats;
   SortWorkspace sort_ws;
   ScanWorkspace scan_ws;
+  ScanWorkspace scan_ws_side;  // the side stream's scans (FH_UNION_SIDE)
+  bool union_side = false;    // this run's committed dots are on s_prev
   GraphCore graph;
   GraphOutput gout;
   Probe probe;
@@ -1920,11 +1940,25 @@ struct EngineDevice {
     for (uint32_t r = 0; r <= np; r++) lo.off[r] = bl[r];
     const uint32_t *bent = lent.get() + b * size_t(n) * fq;
     uint32_t *rec = vrec.ensure(M + 1);
-    // ~9000 commands per workgroup: fq·9000 + slack positions fit the window
-    const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * kRecSlack) / fq);
+    // ~4800 commands per workgroup: fq·4800 + slack positions fit the window
+    // (FH_REC_WIN: a smaller window, more workgroups per CU)
+    static const uint32_t rec_win = [] {
+      const char *e = getenv("FH_REC_WIN");
+      const uint32_t v = e ? uint32_t(atol(e)) : kRecWin;
+      return v == 8192 || v == 32768 ? v : kRecWin;
+    }();
+    const uint32_t per = std::max<uint32_t>(1, (rec_win - 2 * rec_slack(rec_win)) / fq);
     const uint32_t G = std::max<uint32_t>(1, (n + per - 1) / per);
-    probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records, dim3(G), dim3(1024),
-                  stream, n, fq, np, G, lo, bent, rec);
+    auto recs = [&](auto kern) {
+      probed_launch("view_records", double(M) * (4.0 + 4.0), kern, dim3(G), dim3(1024), stream, n,
+                    fq, np, G, lo, bent, rec);
+    };
+    if (rec_win == 8192)
+      recs(k_view_records<8192>);
+    else if (rec_win == 32768)
+      recs(k_view_records<32768>);
+    else
+      recs(k_view_records<kRecWin>);
     const uint32_t tiles = (n + kTile - 1) / kTile;
     sort_ws.prepare(tiles, 1, stream);
     const int db = sort_digit_bits(key_bits, 4);
@@ -1940,7 +1974,7 @@ struct EngineDevice {
                                            key_bits, sort_ws, stream, &ks, &vs, db);
     // measurement knob FH_SRCH_DIAG (after the first run; not bit-exact): 1
     // skips the heads' latest reads, 2 writes the codes in sorted order to
-    // scratch, 4 skips the scans
+    // scratch, 4 skips the scans, 8 writes aligned 16-B records to scratch
     static const uint32_t srch_diag = [] {
       const char *e = getenv("FH_SRCH_DIAG");
       return e ? uint32_t(atol(e)) : 0u;
@@ -1952,28 +1986,37 @@ struct EngineDevice {
     uint8_t *tm = tailm.ensure(n + 1);
     // reads the sorted key words and values (12 B, neighbours from LDS) and
     // the heads' latest entries, writes fq codes and the tail mask
-    const dim3 sg((n + kSrchThreads - 1) / kSrchThreads);
-    uint32_t *codes = dep32.ensure((srch_diag & 2 ? 2 * size_t(M) : size_t(M)) + 1);
+    // workgroup size (FH_SRCH_THREADS: 256, 512 or 1024): a 1024-thread
+    // group holds 4 waves per SIMD, and the kernel's registers leave room for
+    // only one such group per CU
+    static const int srch_th = [] {
+      const char *e = getenv("FH_SRCH_THREADS");
+      const int v = e ? atoi(e) : kSrchThreads;
+      return v == 256 || v == 512 ? v : 1024;
+    }();
+    uint32_t *codes = dep32.ensure((srch_diag & 10 ? size_t(M) + 4 * size_t(n) : size_t(M)) + 1);
     const double sb = double(n) * (12.0 + fq * 4.0 + 1.0);
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
+    auto go = [&](auto kern, int th) {
+      probed_launch("cmd_search", sb, kern, dim3((n + th - 1) / th), dim3(th), stream, n, cm, K, np,
+                    (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
+    };
+    auto by_th = [&](auto fqc) {
+      constexpr uint32_t F = decltype(fqc)::value;
+      if (srch_th == 256) {
+        go(k_cmd_search<F, 256>, 256);
+      } else if (srch_th == 512) {
+        go(k_cmd_search<F, 512>, 512);
+      } else {
+        go(k_cmd_search<F, 1024>, 1024);
+      }
+    };
     switch (fq) {
-      case 1:
-        probed_launch("cmd_search", sb, k_cmd_search<1>, sg, dim3(kSrchThreads), stream, n, cm, K, np,
-                      (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
-        break;
-      case 2:
-        probed_launch("cmd_search", sb, k_cmd_search<2>, sg, dim3(kSrchThreads), stream, n, cm, K, np,
-                      (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
-        break;
-      case 3:
-        probed_launch("cmd_search", sb, k_cmd_search<3>, sg, dim3(kSrchThreads), stream, n, cm, K, np,
-                      (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
-        break;
-      default:
-        probed_launch("cmd_search", sb, k_cmd_search<4>, sg, dim3(kSrchThreads), stream, n, cm, K, np,
-                      (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
-        break;
+      case 1: by_th(std::integral_constant<uint32_t, 1>()); break;
+      case 2: by_th(std::integral_constant<uint32_t, 2>()); break;
+      case 3: by_th(std::integral_constant<uint32_t, 3>()); break;
+      default: by_th(std::integral_constant<uint32_t, 4>()); break;
     }
     k_cmd_tails<<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks, vs, tm,
                                                   views_latest(), bbase);
@@ -2027,20 +2070,45 @@ struct EngineDevice {
     // rows of <= kRegSlots slots: count, scan, and the union writes the
     // committed-deps CSR directly; wider rows go through fixed-stride rows
     deps_direct = S <= kRegSlots;
+    // The committed dots (count, scan, dot gathers, CSR rows) are an output
+    // nothing later in the step reads: with FH_UNION_SIDE=1 they
+    // run on a second stream beside the graph stage, which needs only the
+    // edges (decoded from the codes alone).  The graph kernels are latency
+    // bound with one workgroup per CU; the union's gathers fill the idle
+    // SIMDs.  The side stream joins before the executed clock moves.
+    // Measured on C4: the graph kernel slows down more than the union's 3.3
+    // ms it would hide (21.8 against 21.6 ms per step; with the side launch
+    // capped at 256 / 512 workgroups, 24.0 / 22.8), so it is opt-in
+    // (FH_UNION_SIDE=1).
+    static const bool side_on = [] {
+      const char *e = getenv("FH_UNION_SIDE");
+      return e && *e == '1';
+    }();
+    union_side = side_on && deps_direct && !deps_only;
+    hipStream_t us = stream;
+    if (union_side) {
+      ensure_prev_stream();
+      us = s_prev;
+    }
     uint64_t *ddot = nullptr;
     const uint32_t *doff = nullptr;
-    if (deps_direct) {
+    // the count + scan that size the CSR rows (on `us`)
+    auto count_rows = [&]() {
       if (views)
-        k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, stream>>>(
+        k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, us>>>(
             n, S, (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(), bbase, dcnt);
       else
-        k_cmd_count<uint64_t><<<grid_for(n, B), B, 0, stream>>>(
+        k_cmd_count<uint64_t><<<grid_for(n, B), B, 0, us>>>(
             n, S, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(), bbase, dcnt);
-      uint32_t *off = o_dep_off.ensure(n + 1);
-      exclusive_scan_u32(dcnt, off, n, scan_ws, stream);
-      doff = off;
+      exclusive_scan_u32(dcnt, o_dep_off.get(), n, union_side ? scan_ws_side : scan_ws, us);
+    };
+    if (deps_direct) {
+      doff = o_dep_off.ensure(n + 1);
       ddot = o_dep.ensure(M + 1);
-      mark("keydeps_count");
+      if (!union_side) {
+        count_rows();
+        mark("keydeps_count");
+      }
     } else {
       ddot = dep_dot.ensure(M + 1);
     }
@@ -2062,23 +2130,45 @@ struct EngineDevice {
       return e && *e == '1' ? 1 : 0;
     }();
     const uint32_t uc = union_chunk ? union_chunk : n;
-    for (uint32_t c0 = 0; c0 < n; c0 += uc) {
-      const uint32_t c1 = std::min<uint32_t>(n, c0 + uc), cn = c1 - c0;
-      if (views)
-        probed_launch("cmd_union", double(cn) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
-                      k_cmd_engine<uint32_t>,
-                      dim3(S <= 4 && xcd_union ? (grid_for(cn, B, 1u << 22) + 7) / 8 * 8
-                                               : grid_for(cn, B)),
-                      dim3(B), stream, n, S, bdot,
-                      (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
-                      (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                      scal.get(), ecnt, bbase, doff, scal.get() + 1, c0, c1, union_nt);
-      else
-        probed_launch("cmd_union", double(cn) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
-                      k_cmd_engine<uint64_t>, dim3(grid_for(cn, B)), dim3(B), stream, n, S,
-                      bdot, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
-                      (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                      scal.get(), ecnt, bbase, doff, scal.get() + 1, c0, c1, union_nt);
+    // one union launch per command range: mode 0 both outputs, 1 the edges,
+    // 2 the committed dots (on `hs`)
+    // FH_UNION_SIDE_WG: workgroups of the side stream's launch (0: the full
+    // grid); a small grid leaves the CUs' wave slots to the graph kernels
+    static const uint32_t side_wg = [] {
+      const char *e = getenv("FH_UNION_SIDE_WG");
+      return e ? uint32_t(atol(e)) / 8 * 8 : 0u;
+    }();
+    auto union_launch = [&](int mode, hipStream_t hs) {
+      for (uint32_t c0 = 0; c0 < n; c0 += uc) {
+        const uint32_t c1 = std::min<uint32_t>(n, c0 + uc), cn = c1 - c0;
+        const char *nm = mode == 1 ? "cmd_edges" : "cmd_union";
+        uint32_t g = S <= 4 && xcd_union ? (grid_for(cn, B, 1u << 22) + 7) / 8 * 8 : grid_for(cn, B);
+        if (mode == 2 && side_wg) g = std::min(g, side_wg);
+        if (views)
+          probed_launch(nm, double(cn) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
+                        k_cmd_engine<uint32_t>, dim3(g),
+                        dim3(B), hs, n, S, bdot,
+                        (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
+                        (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
+                        scal.get(), ecnt, bbase, doff, scal.get() + 1, c0, c1, union_nt, mode);
+        else
+          probed_launch(nm, double(cn) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
+                        k_cmd_engine<uint64_t>, dim3(mode == 2 && side_wg ? std::min(grid_for(cn, B), side_wg) : grid_for(cn, B)), dim3(B), hs, n, S,
+                        bdot, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
+                        (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
+                        scal.get(), ecnt, bbase, doff, scal.get() + 1, c0, c1, union_nt, mode);
+      }
+    };
+    if (union_side) {
+      // the edges first (the graph waits for them), then the side stream
+      union_launch(1, stream);
+      FH_HIP(hipEventRecord(ev_start, stream));
+      FH_HIP(hipStreamWaitEvent(us, ev_start, 0));
+      count_rows();
+      union_launch(2, us);
+      FH_HIP(hipEventRecord(ev_join, us));
+    } else {
+      union_launch(0, stream);
     }
     mark("keydeps_union");
     if (deps_only) return;  // the committed deps are the output (partial replication)
@@ -2124,6 +2214,11 @@ struct EngineDevice {
       k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, bdot, sq);
       o_seq = sq;
       mark("per_key_dots");
+    }
+    if (union_side) {  // the committed dots (side stream) before the clock moves
+      FH_HIP(hipStreamWaitEvent(stream, ev_join, 0));
+      union_side = false;
+      mark("union_join");
     }
     // executed clock: the whole batch executed
     unsigned long long *st = srcstats.get();

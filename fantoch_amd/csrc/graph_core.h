@@ -98,6 +98,9 @@ struct GraphCore {
   DBuf<uint8_t> t_fail;     // graph_tile mixed bounds: pass-1 failed tiles
   DBuf<uint32_t> t_cores;   // graph_tile mixed bounds: pass-2 cores (start, length)
   uint32_t dbg_mixed_redo = 0;
+  // run_tiles left the execution order as (ready time, rank in group, group
+  // starts): build_per_key's fill computes each rank itself (no order array)
+  bool fill_from_groups = false;
   DBuf<uint64_t> t_prof;  // tile path: ready time, group rank/count/start
   uint32_t dbg_tile_fail = 0, dbg_tile_ok = 0;
   DBuf<uint8_t> fb_pushed;    // coloring reach: vertices that pushed this round

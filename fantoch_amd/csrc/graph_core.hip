@@ -816,6 +816,34 @@ __global__ void __launch_bounds__(256)
   if (src_mx) acc.commit(src_mx, src_cnt);  // (src_mx is uniform)
 }
 
+// the same from the tile kernel's groups, one thread per vertex: its rank
+// r = start[H] + rank in group is written, and (key, dot) go to element r
+// (r stays within the reach bound of v, so the writes stay coalesced)
+__global__ void __launch_bounds__(256)
+    k_exec_fill_dots(uint32_t n, uint32_t k, const uint32_t *__restrict__ hgrp,
+                     const uint32_t *__restrict__ grank, const uint32_t *__restrict__ gstart,
+                     const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot,
+                     uint32_t *__restrict__ rank, uint32_t *__restrict__ ek,
+                     uint64_t *__restrict__ ed, unsigned long long *__restrict__ src_mx,
+                     unsigned int *__restrict__ src_cnt) {
+  __shared__ unsigned long long s_mx[256];
+  __shared__ unsigned int s_cnt[256];
+  SrcAcc acc;
+  acc.init(s_mx, s_cnt);
+  __syncthreads();
+  GRID_STRIDE(v, n) {
+    const uint32_t r = gstart[hgrp[v]] + grank[v];
+    rank[v] = r;
+    const uint64_t d = dot[v];
+    for (uint32_t s = 0; s < k; s++) {
+      ek[size_t(r) * k + s] = key32[size_t(v) * k + s];
+      ed[size_t(r) * k + s] = d;
+    }
+    if (src_mx) acc.add(d);
+  }
+  if (src_mx) acc.commit(src_mx, src_cnt);  // (src_mx is uniform)
+}
+
 __global__ void k_copy_dot(uint32_t V, const uint64_t *__restrict__ dot, uint64_t *__restrict__ out) {
   GRID_STRIDE(v, V) out[v] = dot[v];
 }
@@ -1213,8 +1241,15 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
     const uint32_t ne = nexec * in.k;
     uint32_t *ek = tmp32a.ensure(ne + 1), *k2 = flags.ensure(ne + 1);
     uint64_t *ed = pk_da.ensure(ne + 1), *d2 = pk_db.ensure(ne + 1);
-    k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, in.k, ord, in.key32, in.dot, ek,
-                                                           ed, in.src_mx, in.src_cnt);
+    if (fill_from_groups) {
+      fill_from_groups = false;
+      k_exec_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(
+          nexec, in.k, t_h.get(), t_rank.get(), t_start.get(), in.key32, in.dot, out.exec_rank,
+          ek, ed, in.src_mx, in.src_cnt);
+    } else {
+      k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, in.k, ord, in.key32, in.dot,
+                                                             ek, ed, in.src_mx, in.src_cnt);
+    }
     out.src_stats_done = in.src_mx != nullptr;
     uint32_t *ko = nullptr;
     uint64_t *dout = nullptr;
@@ -1250,6 +1285,7 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
 void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   const uint32_t V = in.V;
   out = GraphOutput();
+  fill_from_groups = false;
   scalars.ensure(32);
   blocked.ensure(V + 1);
   rep.ensure(V + 1);

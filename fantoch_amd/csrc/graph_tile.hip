@@ -131,7 +131,7 @@ __device__ __forceinline__ uint16_t lds_xchg_u16(uint16_t *p, uint16_t v) {
 // graph_tile's outputs and launch parameters (named: GraphCore::tiles_mixed
 // takes it)
 struct TileOut {
-  uint32_t *rep;     // [V] global vid of the SCC's min member
+  uint32_t *rep;     // [V] global vid of the SCC's min member, or null (not written)
   uint64_t *label;   // [V] min dot of the SCC
   uint32_t *hgrp;    // [V] ready time H (a vertex position)
   uint32_t *grank;   // [V] rank inside the ready group
@@ -661,7 +661,7 @@ __global__ void __launch_bounds__(kTileThreads)
       gmax = max(gmax, cnt + 1);
     }
     out.label[v] = (lab == 0 || dotx < lab) ? dotx : lab;
-    out.rep[v] = lo + sR[x];
+    if (out.rep) out.rep[v] = lo + sR[x];
     out.hgrp[v] = lo + t;
     out.grank[v] = rk;
     out.gcount[v] = t == uint32_t(x) ? cnt + 1 : 0u;
@@ -693,10 +693,11 @@ static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint
   const uint32_t tiles = to.cores ? ncores : (V + to.core - 1) / to.core;
   if (tiles == 0) return;
   // algorithmic bytes: read the vertex's S edge slots and its dot (labels and
-  // dot tie-breaks), write rep, H, rank, group count and the label (the
-  // context halo re-reads are overhead, not algorithmic; so is a redo pass
-  // over cores already ordered once: count_bytes = false)
-  const double bytes = count_bytes ? double(V) * (4.0 * S + 8.0 + 16.0 + 8.0) : 0.0;
+  // dot tie-breaks), write H, rank, group count and the label (rep too when
+  // asked for; the context halo re-reads are overhead, not algorithmic; so is
+  // a redo pass over cores already ordered once: count_bytes = false)
+  const double bytes =
+      count_bytes ? double(V) * (4.0 * S + 8.0 + (to.rep ? 16.0 : 12.0) + 8.0) : 0.0;
   switch (S) {
     case 2:
       probed_launch("graph_tile", bytes, k_graph_tile<2>, dim3(tiles), dim3(kTileThreads),
@@ -792,7 +793,7 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   const uint32_t V = in.V;
   uint32_t *stat = scalars.get() + 24;
   TileOut to;
-  to.rep = rep.ensure(V + 1);
+  to.rep = nullptr;  // (no consumer: the engine and the executor read labels and ranks)
   to.label = tmp64c.ensure(V + 1);
   to.hgrp = t_h.ensure(V + 1);
   to.grank = t_rank.ensure(V + 1);
@@ -829,8 +830,10 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
     dbg_mixed_redo = 0;
     ok = tiles_mixed(in, to, tile_r0, st);
     if (debug)
-      fprintf(stderr, "fh graph_tile mixed: V=%u R1=%u R2=%u redo_cores=%u ok=%d max_excess=%u\n", V,
-              kMixR1, uint32_t(to.r0), dbg_mixed_redo, int(ok), st[1]);
+      fprintf(stderr,
+              "fh graph_tile mixed: V=%u R1=%u R2=%u redo_cores=%u ok=%d max_excess=%u "
+              "max_sweeps=%u max_rounds=%u max_group=%u\n",
+              V, kMixR1, uint32_t(to.r0), dbg_mixed_redo, int(ok), st[1], st[4], st[5], st[6]);
   }
   for (int attempt = 0; attempt < 4 && !ok; attempt++) {
     to.r0 = int(r0);
@@ -873,13 +876,21 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   uint32_t *gs = t_start.ensure(V + 1);
   exclusive_scan_u32(t_cnt.get(), gs, V, scan_ws, stream);
   uint32_t *er = tmp32d.ensure(V + 1);
-  uint32_t *ord = order.ensure(V + 1);
-  k_exec_from_groups<<<grid_for(V, 256), 256, 0, stream>>>(V, t_h.get(), t_rank.get(), gs, er, ord);
-  out.exec_order = ord;
+  // the per-key pass of dots takes each vertex's rank from its group and
+  // writes (key, dot) at it directly (build_per_key): no order array
+  fill_from_groups = in.want_per_key && in.per_key_dots && !in.key_off && in.k >= 1 &&
+                     size_t(V) * in.k < (size_t(1) << 30);
+  if (fill_from_groups) {
+    out.exec_order = nullptr;
+  } else {
+    uint32_t *ord = order.ensure(V + 1);
+    k_exec_from_groups<<<grid_for(V, 256), 256, 0, stream>>>(V, t_h.get(), t_rank.get(), gs, er, ord);
+    out.exec_order = ord;
+  }
   out.exec_rank = er;
   out.nexec = V;
   out.npending = 0;
-  out.rep = rep.get();
+  out.rep = nullptr;
   out.scc_label = tmp64c.get();
   mark("exec_order");
   return true;
