@@ -646,6 +646,9 @@ __global__ void __launch_bounds__(TH)
     uint32_t *o4 = code + size_t(n) * FQ + size_t((diag & 2) ? i : c) * 4;
     *reinterpret_cast<uint4 *>(o4) = make_uint4(cds[0], FQ > 1 ? cds[FQ > 1 ? 1 : 0] : 0u,
                                                 FQ > 2 ? cds[FQ > 2 ? 2 : 0] : 0u, msk);
+  } else if (diag & 16) {  // measurement: non-temporal stores
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) __builtin_nontemporal_store(cds[j], o + j);
   } else if constexpr (FQ == 3) {
     *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(o) =
         HIP_vector_type<uint32_t, 3>(cds[0], cds[1], cds[2]);
@@ -1974,7 +1977,8 @@ struct EngineDevice {
                                            key_bits, sort_ws, stream, &ks, &vs, db);
     // measurement knob FH_SRCH_DIAG (after the first run; not bit-exact): 1
     // skips the heads' latest reads, 2 writes the codes in sorted order to
-    // scratch, 4 skips the scans, 8 writes aligned 16-B records to scratch
+    // scratch, 4 skips the scans, 8 writes aligned 16-B records to scratch,
+    // 16 stores the codes non-temporally (exact)
     static const uint32_t srch_diag = [] {
       const char *e = getenv("FH_SRCH_DIAG");
       return e ? uint32_t(atol(e)) : 0u;

@@ -145,6 +145,7 @@ struct TileOut {
   unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
   int r0;      // certified reach bound R0 (L = 2·R0)
   int core;    // core vertices per tile T (T + 2L <= kTileC, T <= kMaxCore·1024)
+  int batch_load;  // 1: the load phase issues all of a thread's edge loads first
   int hblock;  // H sweeps: 1 = each wave walks a contiguous block in ascending
                // steps of 64 (updates of a block's earlier vertices are seen by
                // its later ones in the same sweep), 2 = the same in batches of
@@ -200,19 +201,47 @@ __global__ void __launch_bounds__(kTileThreads)
     pdot[j] = x < cb ? dot[lo + x] : 0ull;
   }
 
-  // 1. context edges; certificate part 2: forward spans of core vertices
+  // 1. context edges; certificate part 2: forward spans of core vertices.
+  // Every edge load of the thread is issued before the first is used (one
+  // memory round trip instead of one per vertex).
   uint32_t nlong = 0;
-  for (int x = tid; x < C; x += kTileThreads) {
-    const uint32_t v = lo + x;
+  if (!out.batch_load) {
+    for (int x = tid; x < C; x += kTileThreads) {
+      const uint32_t v = lo + x;
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-      const uint32_t u = dst[size_t(v) * S + s];
-      uint16_t l = kNone;
-      if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
-      if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
-      eL[s][x] = l;
+      for (int s = 0; s < S; s++) {
+        const uint32_t u = dst[size_t(v) * S + s];
+        uint16_t l = kNone;
+        if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
+        if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
+        eL[s][x] = l;
+      }
+      sH[x] = uint16_t(x);
     }
-    sH[x] = uint16_t(x);
+  } else {
+    constexpr int kLd = kTileC / kTileThreads;
+    uint32_t uu[kLd][S];
+#pragma unroll
+    for (int i = 0; i < kLd; i++) {
+      const int x = tid + i * kTileThreads;
+#pragma unroll
+      for (int s = 0; s < S; s++) uu[i][s] = x < C ? dst[size_t(lo + x) * S + s] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kLd; i++) {
+      const int x = tid + i * kTileThreads;
+      if (x >= C) break;
+      const uint32_t v = lo + x;
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const uint32_t u = uu[i][s];
+        uint16_t l = kNone;
+        if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
+        if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
+        eL[s][x] = l;
+      }
+      sH[x] = uint16_t(x);
+    }
   }
   __syncthreads();
   phase(0);
@@ -804,6 +833,8 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.failf = nullptr;
   static const int hblock = getenv("FH_TILE_HBLOCK") ? atoi(getenv("FH_TILE_HBLOCK")) : 1;
   to.hblock = hblock;
+  static const int batch_load = getenv("FH_TILE_BATCH_LOAD") ? atoi(getenv("FH_TILE_BATCH_LOAD")) : 1;
+  to.batch_load = batch_load;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   to.prof = nullptr;
   if (debug) {
