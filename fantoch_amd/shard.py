@@ -15,11 +15,15 @@ from .workload import Stream, Workload
 
 def shard_batches(w: Workload, rank: int, world: int, batch: int, nbatches: int,
                   return_index: bool = False):
-    """The `rank`-th key shard of w's global stream, cut into `nbatches`
-    batches of `batch` commands.  Keys are renumbered to shard-local ids
-    (key // world).  With return_index, also returns the global stream index
-    of every shard command (for checking against the unsharded stream)."""
-    assert w.keys_per_cmd == 1 and w.views == 0, "key sharding here is for 1-key streams"
+    """The `rank`-th key shard of w's global single-view stream (the C2
+    shape), cut into `nbatches` batches of `batch` commands.  Keys are
+    renumbered to shard-local ids (key // world).  With return_index, also
+    returns the global stream index of every shard command (for checking
+    against the unsharded stream).  Replica-view streams (C4) are sharded on
+    the device instead, with their replica logs filtered to the shard:
+    `Workload.generate_shard` (fh_workload_generate_shard)."""
+    assert w.keys_per_cmd == 1 and w.views == 0, \
+        "single-view 1-key streams only (replica views: Workload.generate_shard)"
     out, index = [], []
     first, local_count = 0, 0
     carry_k = np.zeros(0, dtype=np.uint64)

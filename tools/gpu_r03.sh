@@ -29,6 +29,8 @@ if [ -z "$SKIP_PROF" ]; then
   step rocprof
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 $C4ONLY > $OUT/prof_$TAG.log 2>&1 || { tail -30 $OUT/prof_$TAG.log; exit 1; }
   tail -1 $OUT/prof_$TAG.log
+  python tools/attribute_copies.py "$(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1)" > $OUT/copybuffer_$TAG.json || exit 1
+  find $OUT/prof_$TAG -name '*kernel_trace.csv' -delete
   step pmc
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_$TAG/fetch -o run -- python3 $C4ONLY > $OUT/pmc_fetch_$TAG.log 2>&1 || { tail -30 $OUT/pmc_fetch_$TAG.log; exit 1; }
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_$TAG/write -o run -- python3 $C4ONLY > $OUT/pmc_write_$TAG.log 2>&1 || { tail -30 $OUT/pmc_write_$TAG.log; exit 1; }

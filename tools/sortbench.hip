@@ -53,10 +53,10 @@ int main(int argc, char **argv) {
     for (int c : cl) {
       setenv("FH_SORT_CFG", std::to_string(c).c_str(), 1);
       uint32_t *ko, *vo;
-      sort_pairs<uint32_t>(dk, nullptr, ka, va, kb, vb, n, bits, ws, st, &ko, &vo);
+      sort_pairs<uint32_t, uint32_t>(dk, nullptr, ka, va, kb, vb, n, bits, ws, st, &ko, &vo);
       hipEventRecord(e0, st);
       for (int i = 0; i < iters; i++)
-        sort_pairs<uint32_t>(dk, nullptr, ka, va, kb, vb, n, bits, ws, st, &ko, &vo);
+        sort_pairs<uint32_t, uint32_t>(dk, nullptr, ka, va, kb, vb, n, bits, ws, st, &ko, &vo);
       hipEventRecord(e1, st);
       hipEventSynchronize(e1);
       float ms;
