@@ -52,7 +52,15 @@ constexpr int kTileThreads = 1024;
 constexpr int kTileC = 10240;  // max context vertices (LDS: 15 B per vertex)
 constexpr uint16_t kNone = 0xFFFF;
 constexpr int kMaxCore = 8;     // core vertices per thread (T <= 8192)
-constexpr uint32_t kMixR1 = 512;  // pass-1 reach bound of the mixed tiling
+constexpr uint32_t kMixR1 = 512;  // pass-1 reach bound of the mixed tiling (FH_TILE_R1)
+static uint32_t mix_r1() {
+  static const uint32_t r = [] {
+    const char *e = getenv("FH_TILE_R1");
+    const uint32_t v = e ? uint32_t(atoi(e)) : kMixR1;
+    return v >= 256 && v <= 1024 && v % 64 == 0 ? v : kMixR1;
+  }();
+  return r;
+}
 
 // R0 rounded up to a multiple of 64 (at least 256)
 static uint32_t round_r0(uint32_t x) { return std::max<uint32_t>(256, (x + 63) & ~63u); }
@@ -760,7 +768,7 @@ static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint
 // only certified cores; pass 2 overwrites its cores.
 bool GraphCore::tiles_mixed(const GraphInput &in, TileOut &to, uint32_t r2, uint32_t *st) {
   const uint32_t V = in.V;
-  const uint32_t r1 = kMixR1;
+  const uint32_t r1 = mix_r1();
   uint32_t *stat = to.stat;
   to.r0 = int(r1);
   to.core = std::min(kTileC - 4 * int(r1), kMaxCore * kTileThreads);
@@ -778,6 +786,8 @@ bool GraphCore::tiles_mixed(const GraphInput &in, TileOut &to, uint32_t r2, uint
   // the pass-2 bound: the requested one, at least what pass 1 saw
   r2 = std::max(r2, round_r0(st[1] + st[1] / 32 + 16));
   if (r2 > 2048) return false;
+  // the proof below keeps failed cores >= T1 >= 2·R1 + 2·R2 from a kept tile
+  if (2 * r1 + 2 * r2 > t1) return false;
   std::vector<uint8_t> hf(tiles1);
   FH_HIP(hipMemcpyAsync(hf.data(), ff, tiles1, hipMemcpyDeviceToHost, stream));
   FH_HIP(hipStreamSynchronize(stream));
@@ -859,14 +869,14 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
     const char *e = getenv("FH_TILE_MIXED");
     return !(e && *e == '0');
   }();
-  if (mixed_on && !r0_env && tile_r0 > kMixR1) {
+  if (mixed_on && !r0_env && tile_r0 > mix_r1()) {
     dbg_mixed_redo = 0;
     ok = tiles_mixed(in, to, tile_r0, st);
     if (debug)
       fprintf(stderr,
               "fh graph_tile mixed: V=%u R1=%u R2=%u redo_cores=%u ok=%d max_excess=%u "
               "max_sweeps=%u max_rounds=%u max_group=%u\n",
-              V, kMixR1, uint32_t(to.r0), dbg_mixed_redo, int(ok), st[1], st[4], st[5], st[6]);
+              V, mix_r1(), uint32_t(to.r0), dbg_mixed_redo, int(ok), st[1], st[4], st[5], st[6]);
   }
   for (int attempt = 0; attempt < 4 && !ok; attempt++) {
     to.r0 = int(r0);
