@@ -31,12 +31,15 @@ and, as `secondary`, the C2 line (single-view KeyDeps, 1M-command batches).
 `c5` (N=1, rank 0): BASELINE.json configs[4] at its stated size -- Atlas
 partial replication over 8 key shards (shard = key mod 8), Zipf 0.99 over 2^20
 keys, 4 keys per command, 100M commands -- with all 8 shards on the one GPU.
-The shards' key sets are disjoint, so their SequentialKeyDeps tables are
-disjoint slices of one latest table: one fused KeyDeps pass computes every
-shard's reports, and the per-command union over the 4 keys x 3 views is the
-cross-shard MShardCommit union (atlas.rs:580-583).  Parity: the committed
-deps digest of this stream equals the oracle's shard-by-shard union
-(tests/golden/make_digests.py, tests/test_fullsize_gpu.py).
+Shard h holds processes 5h+1..5h+5 (fantoch/src/util.rs:115-122); a command's
+dot comes from its target shard (its first key's, id.rs:59-61) and every
+shard it touches collects it with its own fast quorum and arrival order
+(atlas.rs:214-328), so the 40 processes' KeyDeps each see only their shard's
+keys of a command (element logs, FH_STREAM_ELEMENT_LOGS) and the committed
+deps are the union over the shards (MShardCommit, atlas.rs:559-639).  Parity:
+the committed-deps digest at 100M and every output on a 20k prefix equal the
+oracle's shard-by-shard computation (tests/golden/make_digests.py,
+tests/test_fullsize_gpu.py).
 
 Roofline bytes are SURVEY.md §8(d)'s algorithmic bytes per command: the
 dominant kernel's `achieved` = (its §8(d) term x commands per step) / (its
@@ -268,14 +271,21 @@ def other_configs(local, steps=3):
     return out
 
 
-def c5_line(args, local):
-    """C5 at its stated size on one GPU (all 8 key shards): one engine pass
-    over the 100M-command 4-key stream per step, every output materialised."""
-    from fantoch_amd.engine import Engine
+def c5_workload():
     from fantoch_amd.workload import Workload
+    return Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64, seed=0xFA170C4000000005, n=5,
+                         shards=8)
+
+
+def c5_line(args, local):
+    """C5 at its stated size on one GPU (all 8 key shards, 40 processes): one
+    engine pass over the 100M-command partially replicated stream per step,
+    every output materialised."""
+    from fantoch_amd.engine import Engine
     n = args.c5_commands
-    w = Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64, seed=0xFA170C4000000005, n=5)
-    s = w.generate(n, logs=True, times=False)
+    t_gen = time.perf_counter()
+    s = c5_workload().generate(n, logs=True, times=False)
+    t_gen = time.perf_counter() - t_gen
     eng = Engine(s.key_space, n=5, device=local)
     eng.stage(s)
     first = eng.run(sync=True)
@@ -288,6 +298,9 @@ def c5_line(args, local):
     eng.sync()
     ms = (time.perf_counter() - t0) / steps * 1e3
     d = eng.dep_total() / n
+    r_out = eng.results()
+    _, scc_sizes = np.unique(r_out["scc_label"], return_counts=True)
+    del r_out
     eng.forget_tuning()
     eng.rewind()
     cold = eng.run(sync=True)
@@ -300,12 +313,16 @@ def c5_line(args, local):
         eng.set_profiling(False)
     eng.close()
     v = n / (ms * 1e-3)
-    r = {"workload": "C5: Atlas partial replication, 8 key shards (key mod 8) all on this GPU, "
-                     "Zipf 0.99 over 2^20 keys, 4 keys/cmd, replica views (fast quorum 3), "
-                     "100M commands; one step orders the whole stream, every output materialised",
-         "commands": n, "shards": 8, "steps": steps, "warmup": 1, "ms_per_step": round(ms, 3),
-         "commands_per_s": v, "first_ms": round(first, 3), "cold_ms": round(cold, 3),
-         "deps_per_cmd": d, "path_roofline": path_roofline(v, 4, 3, d)}
+    r = {"workload": "C5: Atlas partial replication, 8 key shards (key mod 8; shard h = processes "
+                     "5h+1..5h+5, dots from the target shard, every shard its own collect and "
+                     "arrival order), all on this GPU; Zipf 0.99 over 2^20 keys, 4 keys/cmd, fast "
+                     "quorum 3, 100M commands; one step orders the whole stream, every output "
+                     "materialised",
+         "commands": n, "shards": 8, "processes": 40, "steps": steps, "warmup": 1,
+         "ms_per_step": round(ms, 3), "commands_per_s": v, "first_ms": round(first, 3),
+         "cold_ms": round(cold, 3), "deps_per_cmd": d, "sccs": int(len(scc_sizes)),
+         "largest_scc": int(scc_sizes.max()), "generate_s": round(t_gen, 2),
+         "path_roofline": path_roofline(v, 4, 3, d)}
     if phases:
         r["phases_ms"] = phases
     return r

@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfantoch_hip.so")
 
 FH_OK, FH_EINVAL, FH_EHIP, FH_EOOM, FH_EINVARIANT, FH_ECAP, FH_ENOTIMPL = range(7)
+FH_STREAM_ELEMENT_LOGS = 1  # fh_stream_desc.flags (include/fantoch_hip.h)
 FH_REPLY_INFO, FH_REPLY_EXECUTED = 0, 1  # RequestReply kinds (include/fantoch_hip.h)
 # execution-log event kinds (include/fantoch_hip.h)
 FH_LOG_ADD, FH_LOG_REQUEST, FH_LOG_REPLY_INFO, FH_LOG_REPLY_EXECUTED, FH_LOG_EXECUTED = range(5)
@@ -33,14 +34,15 @@ class fh_config(C.Structure):
 
 class fh_stream_desc(C.Structure):
     _fields_ = [("n", C.c_size_t), ("keys_per_cmd", C.c_uint32), ("views", C.c_uint32),
-                ("nproc", C.c_uint32), ("pad", C.c_uint32)]
+                ("nproc", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class fh_workload(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("n", C.c_uint32), ("keys_per_cmd", C.c_uint32),
                 ("kind", C.c_uint32), ("conflict_rate", C.c_uint32), ("pool_size", C.c_uint32),
                 ("clients", C.c_uint32), ("zipf_s", C.c_double), ("key_count", C.c_uint64),
-                ("views", C.c_uint32), ("window", C.c_uint32)]
+                ("views", C.c_uint32), ("window", C.c_uint32),
+                ("shards", C.c_uint32), ("pad", C.c_uint32)]
 
 
 V, S, P = C.c_void_p, C.c_size_t, C.POINTER
@@ -120,6 +122,7 @@ SIGNATURES = {
     "fh_workload_key_space": (C.c_uint64, [P(fh_workload)]),
     "fh_workload_generate": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V, V, V]),
     "fh_workload_generate_logs": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V]),
+    "fh_workload_generate_element_logs": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V]),
     "fh_workload_generate_shard": (C.c_int, [P(fh_workload), C.c_uint64, S, C.c_uint32,
                                              C.c_uint32, P(S), V, V, V, V]),
     "fh_engine_rewind": (C.c_int, [V]),

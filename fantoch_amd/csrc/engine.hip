@@ -42,41 +42,39 @@ constexpr unsigned B = 256;
 
 // Replica views as per-replica arrival logs: replica r's SequentialKeyDeps
 // sees the commands of log r in log order (its add_cmd calls, atlas.rs:236,
-// :303-309).  Element x = q·k + s is key slot s of log entry q; entries are
-// concatenated replica by replica, so element order is (replica, arrival,
-// slot) and a stable sort by the segment id (r + 1)·K + key yields every
-// (replica, key) segment in arrival order.  The value is the element's
+// :303-309).  Command logs: element x = q·k + s is key slot s of log entry q
+// (entry e = c·fq + j: command c as fast-quorum member j).  Element logs
+// (partial replication, FH_STREAM_ELEMENT_LOGS): entry q is one element,
+// position (c·fq + j)·k + s, as each shard's replicas process only the
+// command's keys on their shard (Command::keys(shard), command.rs:95-100).
+// Entries are concatenated replica by replica, so element order is (replica,
+// arrival, slot) and a stable sort by the segment id (r + 1)·K + key yields
+// every (replica, key) segment in arrival order.  The value is the element's
 // command-major position (c·fq + j)·k + s, where the union reads it.
 // One chunk of the logs: replica r contributes its entries
 // [first[r], first[r] + count[r]) (chunk-local element order = replica, then
 // arrival, then slot); cum[r] = elements of the replicas before r.
-constexpr int kMaxLogs = 16;
+constexpr int kMaxLogs = 64;
 struct LogChunk {
   uint32_t first[kMaxLogs];
   uint32_t cum[kMaxLogs + 1];
-};
-
-// the same as a sort source: the first radix pass reads the logs directly
-// (no materialised key/value arrays: one write and one read of 8 B per
-// element saved, opt-in: measured slower, see the chunk loop)
-struct LogSrc {
-  uint32_t k, fq, nlog, K;
-  LogChunk ch;
-  const uint32_t *ent, *key32;
-  __device__ __forceinline__ void get(uint32_t x, uint32_t &key, uint32_t &val) const {
-    uint32_t r = 0;
-    while (r + 1 < nlog && x >= ch.cum[r + 1]) r++;
-    const uint32_t y = x - ch.cum[r];
-    const uint32_t q = ch.first[r] + y / k, s = y % k;
-    const uint32_t e = ent[q];
-    key = (r + 1) * K + key32[(e / fq) * k + s];
-    val = e * k + s;
+  // the replica holding chunk element x: the last r with cum[r] <= x
+  __device__ __forceinline__ uint32_t replica(uint32_t x, uint32_t nlog) const {
+    uint32_t lo = 0, hi = nlog - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (cum[mid] <= x)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    return lo;
   }
 };
 
-// Dependency-code placement (replica views).  k_prev_views writes each
-// element's code straight to its command-major position: a 4-byte write to a
-// random address of the chunk's ~50 MB window, ~32 B of fabric traffic each.
+// Dependency-code placement (replica views).  Writing each element's code
+// straight to its command-major position is a 4-byte write to a random
+// address of the chunk's ~50 MB window, ~32 B of fabric traffic each.
 // Instead, one bucketing pass groups (position - base, code) pairs by the
 // position's bits [15, 24) -- an LDS-staged scatter with contiguous runs per
 // tile and bucket, as in the sort -- and k_place assembles each bucket's 32K
@@ -95,8 +93,9 @@ constexpr uint32_t kPlaceNone = ~0u;        // never a code (log references < 2^
 // counts at shift 0 (digits of dmask + 1 values, sort_digit_bits) for the
 // sort's first pass (sort_pairs_counted: no separate counting pass over the
 // keys it just wrote).
+// elem != 0: element logs (each entry a position (c·fq + j)·k + s).
 __global__ void __launch_bounds__(kThreads)
-    k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, LogChunk ch,
+    k_log_keys(uint32_t M, uint32_t k, uint32_t fq, uint32_t nlog, uint32_t elem, LogChunk ch,
                const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
                uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
                uint32_t *__restrict__ emin, uint32_t slack, uint32_t *__restrict__ counts,
@@ -105,15 +104,22 @@ __global__ void __launch_bounds__(kThreads)
   s_h[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(M, base + uint32_t(kTile));
+  const uint32_t per = fq * k;
   for (uint32_t x = base + threadIdx.x; x < end; x += kThreads) {
-    uint32_t r = 0;
-    while (r + 1 < nlog && x >= ch.cum[r + 1]) r++;
+    const uint32_t r = ch.replica(x, nlog);
     const uint32_t y = x - ch.cum[r];
-    const uint32_t q = ch.first[r] + y / k, s = y % k;
-    const uint32_t e = ent[q];
-    const uint32_t key = (r + 1) * K + key32[(e / fq) * k + s];
+    uint32_t key, val;
+    if (elem) {
+      val = ent[ch.first[r] + y];
+      key = (r + 1) * K + key32[(val / per) * k + val % k];
+    } else {
+      const uint32_t q = ch.first[r] + y / k, s = y % k;
+      const uint32_t e = ent[q];
+      key = (r + 1) * K + key32[(e / fq) * k + s];
+      val = e * k + s;
+    }
     keys[x] = key;
-    vals[x] = e * k + s;
+    vals[x] = val;
     atomicAdd(&s_h[key & dmask], 1u);
   }
   __syncthreads();
@@ -125,14 +131,14 @@ __global__ void __launch_bounds__(kThreads)
   if (emin && blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t m = ~0u;
     for (uint32_t r = 0; r < nlog; r++)
-      if (ch.cum[r + 1] > ch.cum[r]) m = min(m, ent[ch.first[r]] * k);
+      if (ch.cum[r + 1] > ch.cum[r]) m = min(m, elem ? ent[ch.first[r]] : ent[ch.first[r]] * k);
     *emin = m > slack ? m - slack : 0u;
   }
 }
 
 // bucketing source: element j of the chunk's (key, arrival) order yields
-// (its position - base, its dependency code) -- the code as k_prev_views
-// computes it
+// (its position - base, its dependency code): the previous element's
+// command, or the latest entry at a segment head
 struct PrevSrc {
   const uint32_t *ks, *vs, *ebase;
   const uint64_t *latest;
@@ -529,7 +535,7 @@ template <uint32_t FQ, int TH>
 __global__ void __launch_bounds__(TH)
     k_cmd_search(uint32_t n, CmdMeta cm, uint32_t K, uint32_t np, const uint32_t *__restrict__ kws,
                  const uint64_t *__restrict__ vals, const uint64_t *__restrict__ latest,
-                 uint32_t *__restrict__ code, uint8_t *__restrict__ tailm, uint32_t diag) {
+                 uint32_t *__restrict__ code, uint8_t *__restrict__ tailm) {
   constexpr int kSpan = TH + 2 * kSrchHalo;
   __shared__ uint32_t s_key[kSpan], s_c[kSpan];
   __shared__ uint32_t s_q[kSpan * kSrchMaxRep];
@@ -566,11 +572,11 @@ __global__ void __launch_bounds__(TH)
     vs[j].qm = uint32_t(cm.qmask);
     vs[j].half = uint32_t(cm.qmask >> 1);
     vs[j].tq = cm.arr(m0, j);
-    on[j] = !(diag & 4);
+    on[j] = true;
   }
   // backward: the staged span, then global memory (a neighbour outside the
   // span is unpacked from the packed arrays)
-  bool go = !(diag & 4);
+  bool go = true;
   for (uint32_t x = me; go && x > 0;) {
     x--;
     const bool sk = s_key[x] == key;
@@ -598,9 +604,9 @@ __global__ void __launch_bounds__(TH)
     }
   }
   // forward
-  go = !(diag & 4);
+  go = true;
 #pragma unroll
-  for (uint32_t j = 0; j < FQ; j++) on[j] = go;
+  for (uint32_t j = 0; j < FQ; j++) on[j] = true;
   for (uint32_t x = me + 1; go && x < span; x++) {
     const bool sk = s_key[x] == key;
     const uint32_t cc = s_c[x];
@@ -630,26 +636,18 @@ __global__ void __launch_bounds__(TH)
   uint32_t msk = 0;
 #pragma unroll
   for (uint32_t j = 0; j < FQ; j++) {
-    if (diag & 4) {
-      cds[j] = c;
-    } else if (vs[j].bc != kNoCmd) {
+    if (vs[j].bc != kNoCmd) {
       cds[j] = vs[j].bc + 1;
     } else {
-      const uint64_t xl = (diag & 1) ? 0ull : latest[uint64_t(rr[j] + 1) * K + key];
+      const uint64_t xl = latest[uint64_t(rr[j] + 1) * K + key];
       cds[j] = xl ? (0x80000000u | uint32_t(xl - kLogFlag)) : 0u;
     }
     msk |= vs[j].tail ? 1u << j : 0u;
   }
-  // the views' codes leave in one store per command
-  uint32_t *o = (diag & 2) ? code + size_t(n) * FQ + size_t(i) * FQ : code + size_t(c) * FQ;
-  if (diag & 8) {  // measurement: one aligned 16-B store per command (scratch)
-    uint32_t *o4 = code + size_t(n) * FQ + size_t((diag & 2) ? i : c) * 4;
-    *reinterpret_cast<uint4 *>(o4) = make_uint4(cds[0], FQ > 1 ? cds[FQ > 1 ? 1 : 0] : 0u,
-                                                FQ > 2 ? cds[FQ > 2 ? 2 : 0] : 0u, msk);
-  } else if (diag & 16) {  // measurement: non-temporal stores
-#pragma unroll
-    for (uint32_t j = 0; j < FQ; j++) __builtin_nontemporal_store(cds[j], o + j);
-  } else if constexpr (FQ == 3) {
+  // the views' codes leave in one store per command (tried: 16-B aligned
+  // stores and non-temporal stores, both flat; round 3)
+  uint32_t *o = code + size_t(c) * FQ;
+  if constexpr (FQ == 3) {
     *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(o) =
         HIP_vector_type<uint32_t, 3>(cds[0], cds[1], cds[2]);
   } else if constexpr (FQ == 4) {
@@ -762,25 +760,6 @@ __device__ __forceinline__ int decode_dep(uint32_t c, uint32_t *v, uint64_t *x,
   return 2;
 }
 
-// replica views: segment heads take the latest entry as a 32-bit log code,
-// the rest the previous element's command
-__global__ void k_prev_views(uint32_t M, const uint32_t *__restrict__ ks,
-                             const uint32_t *__restrict__ vs, uint32_t per_cmd,
-                             const uint64_t *__restrict__ latest, uint32_t *__restrict__ code) {
-  GRID_STRIDE(j, M) {
-    const uint32_t e = vs[j];
-    const uint32_t seg = ks[j];
-    uint32_t c;
-    if (j == 0 || ks[j - 1] != seg) {
-      const uint64_t x = latest[seg];
-      c = x ? (0x80000000u | uint32_t(x - kLogFlag)) : 0u;
-    } else {
-      c = vs[j - 1] / per_cmd + 1;
-    }
-    code[e] = c;
-  }
-}
-
 __device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
   for (uint32_t i = 1; i < n; i++) {
     const uint64_t x = a[i];
@@ -797,20 +776,6 @@ __device__ __forceinline__ uint32_t sort_unique_u64(uint64_t *a, uint32_t n) {
   return w;
 }
 
-// streamed once: with nt set, loads and stores skip cache residency so the
-// Infinity Cache keeps the gathered dots (FH_UNION_NT)
-template <class T>
-__device__ __forceinline__ void st_maybe_nt(T *p, T v, bool nt) {
-  if (nt)
-    __builtin_nontemporal_store(v, p);
-  else
-    *p = v;
-}
-template <class T>
-__device__ __forceinline__ T ld_maybe_nt(const T *p, bool nt) {
-  return nt ? __builtin_nontemporal_load(p) : *p;
-}
-
 // k_cmd_engine for rows of at most kRegSlots slots, in registers: every slot
 // is read into a fixed register position (absent = all ones), a bitonic
 // network sorts the 16 dots, and the unique ones stream out.  (The general
@@ -825,10 +790,7 @@ __device__ __forceinline__ void cmd_union_regs(
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n,
-    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, bool nt, int mode) {
-  // mode 0: committed dots and graph edges; 1: edges (and the missing flags)
-  // only; 2: committed dots only (FH_UNION_SIDE: the dots on a second stream,
-  // beside the graph stage, which needs only the edges)
+    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
@@ -840,7 +802,7 @@ __device__ __forceinline__ void cmd_union_regs(
       uint64_t x = 0;
       uint32_t v = 0;
       const int kind =
-          decode_dep(ld_maybe_nt(dep_code + size_t(i) * S + t, nt), &v, &x, dlog, bbase, n);
+          decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
       if (kind == 1) {
         vv[t] = v;
       } else if (kind == 2) {
@@ -849,11 +811,9 @@ __device__ __forceinline__ void cmd_union_regs(
       }
     }
   }
-  if (mode != 2) {
-    if (blocked0) blocked0[i] = missing;
-    if (missing) atomicAdd(nblocked, 1u);
-  }
-  if (mode != 1) {
+  if (blocked0) blocked0[i] = missing;
+  if (missing) atomicAdd(nblocked, 1u);
+  {
   // in-batch deps: one dot gather per distinct vid (the fast-quorum
   // members' reports often name the same previous command)
 #pragma unroll
@@ -889,7 +849,7 @@ __device__ __forceinline__ void cmd_union_regs(
 #pragma unroll
   for (uint32_t t = 0; t < kRegSlots; t++) {
     if (r[t] != ~0ull && r[t] != prev) {
-      if (m < cap) st_maybe_nt(dd + m, r[t], nt);
+      if (m < cap) dd[m] = r[t];
       m++;
       prev = r[t];
     }
@@ -897,11 +857,10 @@ __device__ __forceinline__ void cmd_union_regs(
   if (out_off) {
     if (m != cap) atomicOr(err, 1u);  // an in-batch dot repeated outside the batch
   } else {
-    for (uint32_t q = m; q < S; q++) st_maybe_nt(dd + q, uint64_t(0), nt);
+    for (uint32_t q = m; q < S; q++) dd[q] = 0;
   }
-  st_maybe_nt(dep_cnt + i, m, nt);
+  dep_cnt[i] = m;
   }
-  if (mode == 2) return;
   uint32_t *ds = dst + size_t(i) * S;
   uint32_t nv = 0;
 #pragma unroll
@@ -910,11 +869,11 @@ __device__ __forceinline__ void cmd_union_regs(
       bool dup = false;
 #pragma unroll
       for (uint32_t q = 0; q < t; q++) dup |= vv[q] == vv[t];
-      if (!dup) st_maybe_nt(ds + nv++, vv[t], nt);
+      if (!dup) ds[nv++] = vv[t];
     }
   }
-  for (uint32_t q = nv; q < S; q++) st_maybe_nt(ds + q, i, nt);  // padding: self loops are ignored
-  if (nv_out) st_maybe_nt(nv_out + i, nv, nt);
+  for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
+  if (nv_out) nv_out[i] = nv;
 }
 
 // Per command: union of its fast-quorum members' element deps (vids and
@@ -930,12 +889,9 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
                              uint64_t bbase, const uint32_t *__restrict__ out_off,
-                             uint32_t *__restrict__ err, uint32_t c0, uint32_t c1, int nt,
-                             int mode) {
-  // commands [c0, c1) of the batch (a launch per command range keeps the
-  // gathered dots of recent dependencies cache-resident: FH_UNION_CHUNK)
+                             uint32_t *__restrict__ err) {
   // uniform: the register path, with a sorting network sized to the row
-  const uint32_t cn = c1 - c0;
+  const uint32_t cn = n;
   if (S <= 4) {
     // XCD-contiguous blocks (grid a multiple of 8): workgroup b runs on XCD
     // b mod 8, which takes the b/8-th block of its own eighth of the
@@ -944,26 +900,25 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     const uint32_t nb = gridDim.x;
     const uint32_t lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
     for (size_t j = size_t(lb) * blockDim.x + threadIdx.x; j < cn; j += size_t(nb) * blockDim.x)
-      cmd_union_regs<4>(c0 + uint32_t(j), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                        blocked0, nblocked, nv_out, bbase, n, out_off, err, nt != 0, mode);
+      cmd_union_regs<4>(uint32_t(j), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
+                        blocked0, nblocked, nv_out, bbase, n, out_off, err);
     return;
   }
   if (S <= 8) {
     GRID_STRIDE(j, cn) {
-      cmd_union_regs<8>(c0 + j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n, out_off, err, nt != 0, mode);
+      cmd_union_regs<8>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
+                        nblocked, nv_out, bbase, n, out_off, err);
     }
     return;
   }
   if (S <= kRegSlots) {
     GRID_STRIDE(j, cn) {
-      cmd_union_regs<kRegSlots>(c0 + j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                                blocked0, nblocked, nv_out, bbase, n, out_off, err, nt != 0, mode);
+      cmd_union_regs<kRegSlots>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
+                                blocked0, nblocked, nv_out, bbase, n, out_off, err);
     }
     return;
   }
-  GRID_STRIDE(jj, cn) {
-    const uint32_t i = c0 + jj;
+  GRID_STRIDE(i, cn) {
     uint64_t *dd = dep_dot + size_t(i) * S;
     uint32_t *ds = dst + size_t(i) * S;
     uint32_t nv = 0, nd = 0;
@@ -1562,6 +1517,10 @@ struct EngineDevice {
              "batch too large (elements >= 2^31)");
     FH_CHECK(!d.views || (h_off && h_cmd && d.nproc >= 1 && d.nproc <= 255), FH_EINVAL,
              "replica views need per-replica logs and nproc");
+    const bool elem = (d.flags & FH_STREAM_ELEMENT_LOGS) != 0;
+    FH_CHECK((d.flags & ~FH_STREAM_ELEMENT_LOGS) == 0, FH_EINVAL, "stream desc: unknown flags");
+    FH_CHECK(!elem || (d.views && d.nproc <= uint32_t(kMaxLogs)), FH_EINVAL,
+             "element logs need replica views and nproc <= 64");
     FH_CHECK(!d.views || uint64_t(d.nproc + 1) * key_space <= 0xFFFFFFFFull, FH_ENOTIMPL,
              "replica views: (nproc + 1) * key_space must fit 32 bits");
     FH_HIP(hipSetDevice(device));
@@ -1577,7 +1536,35 @@ struct EngineDevice {
       FH_CHECK(h_dot[i] != ~0ull && (h_dot[i] >> 56) != 0, FH_EINVAL,
                "stage: dot (255, 2^56 - 1) is reserved and ProcessId 0 is not a process");
     std::vector<uint32_t> ent, lo;
-    if (d.views) {
+    if (d.views && elem) {
+      // element logs: every position (c·fq + j)·k + s of a batch in exactly
+      // one log (a replica may hold several of a command's key slots)
+      const size_t np = d.nproc, per_b = n * fq * d.keys_per_cmd;
+      FH_CHECK(h_off[0] == 0 && h_off[nb * np] == per_b * nb, FH_EINVAL,
+               "element logs: every element position must appear in exactly one log");
+      ent.resize(per_b * nb);
+      lo.resize(nb * (np + 1));
+      std::vector<uint8_t> seen(per_b);
+      h_win.assign(nb, 0);
+      for (size_t b = 0; b < nb; b++) {
+        std::fill(seen.begin(), seen.end(), 0);
+        const uint64_t base = h_off[b * np];
+        FH_CHECK(h_off[(b + 1) * np] - base == per_b, FH_EINVAL,
+                 "element logs: a batch's logs must hold n * views * keys_per_cmd entries");
+        for (size_t r = 0; r < np; r++) {
+          lo[b * (np + 1) + r] = uint32_t(h_off[b * np + r] - base);
+          FH_CHECK(h_off[b * np + r + 1] >= h_off[b * np + r], FH_EINVAL, "logs: offsets");
+          for (uint64_t q = h_off[b * np + r]; q < h_off[b * np + r + 1]; q++) {
+            const uint32_t p = h_cmd[q];
+            FH_CHECK(p < per_b && !seen[p], FH_EINVAL,
+                     "element logs: every element position must appear in exactly one log");
+            seen[p] = 1;
+            ent[q] = p;
+          }
+        }
+        lo[b * (np + 1) + np] = uint32_t(per_b);
+      }
+    } else if (d.views) {
       const size_t np = d.nproc;
       FH_CHECK(h_off[0] == 0 && h_off[nb * np] == n * fq * nb, FH_EINVAL,
                "logs: every command must appear in exactly `views` replica logs");
@@ -1769,31 +1756,25 @@ struct EngineDevice {
       // window of the stream, so its dependency scatter stays in a cache-
       // sized slice of the dependency array.
       const uint32_t np = desc.nproc;
-      FH_CHECK(np <= uint32_t(kMaxLogs), FH_ENOTIMPL, "replica views: nproc <= 16");
+      const bool elem = (desc.flags & FH_STREAM_ELEMENT_LOGS) != 0;
+      FH_CHECK(np <= uint32_t(kMaxLogs), FH_ENOTIMPL, "replica views: nproc <= 64");
       const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
-      // codes placed through LDS buckets (k_place; FH_VIEW_PLACE=0: direct
-      // scatter).  A chunk of Mc elements spans ~Mc positions, so chunks of
-      // 15.7M keep the placement window within its 2^24 positions.
-      static const bool place = [] {
-        const char *e = getenv("FH_VIEW_PLACE");
-        return !(e && *e == '0');
-      }();
+      // codes placed through LDS buckets (k_place).  A chunk of Mc elements
+      // spans ~Mc positions, so chunks of 15.7M keep the placement window
+      // within its 2^24 positions.
       static const uint32_t place_slack = [] {
         const char *e = getenv("FH_PLACE_SLACK");  // tests: 0 makes reordered arrivals strays
         return e ? uint32_t(atol(e)) : kPlaceSlack;
       }();
       static const size_t chunk_elems = [] {
-        const char *e = getenv("FH_VIEW_CHUNK");
-        return e ? size_t(std::max(1L, atol(e))) : place ? size_t(15) << 20 : size_t(12) << 20;
+        const char *e = getenv("FH_VIEW_CHUNK");  // tests: small chunks
+        return e ? size_t(std::max(1L, atol(e))) : size_t(15) << 20;
       }();
       const uint32_t nch = uint32_t(std::max<size_t>(1, (size_t(M) + chunk_elems - 1) / chunk_elems));
-      uint32_t *pbase = nullptr;
-      if (place) {
-        // the sentinel kPlaceNone is the code of log reference 2^31 - 1
-        FH_CHECK(bbase + n < 0x7FFFFFFFull, FH_ENOTIMPL, "replica views: command log >= 2^31 - 1");
-        pbase = place_base.ensure(nch);
-        FH_HIP(hipMemsetAsync(pbase, 0xFF, size_t(nch) * sizeof(uint32_t), stream));
-      }
+      // the sentinel kPlaceNone is the code of log reference 2^31 - 1
+      FH_CHECK(bbase + n < 0x7FFFFFFFull, FH_ENOTIMPL, "replica views: command log >= 2^31 - 1");
+      uint32_t *pbase = place_base.ensure(nch);
+      FH_HIP(hipMemsetAsync(pbase, 0xFF, size_t(nch) * sizeof(uint32_t), stream));
       // the chunk's elements are replica-major, so a stable sort by the key
       // alone already leaves every (replica, key) segment contiguous and in
       // arrival order ((key, replica, arrival) order): with K a power of two
@@ -1802,31 +1783,8 @@ struct EngineDevice {
       // 23-bit composite)
       const bool pow2 = (key_space & (key_space - 1)) == 0;
       const int bits = pow2 ? bits_for(key_space) : bits_for(uint64_t(np + 1) * key_space);
-      const uint32_t *bent = lent.get() + b * size_t(n) * fq;
-      // Two streams (opt-in): chunk c's dependency scatter + tails (random
-      // writes, memory bound) on `s_prev` while chunk c+1's keys and sort
-      // (ballot-matching compute) run on `stream`; two buffer sets, an event
-      // pair per set.  prev(c+1) follows tail(c) on s_prev, so every head
-      // reads the latest table the previous chunk left.
-      // Measured on C4: 17.1 ms against 15.5 on one stream (the scatter and
-      // the sorts slow each other down more than they overlap), so the
-      // pipeline is opt-in (FH_VIEW_PIPE=1).
-      static const bool pipe = [] {
-        const char *e = getenv("FH_VIEW_PIPE");
-        return e && *e == '1';
-      }();
-      // FH_TAIL_FUSED=0: the tails in a launch of their own (k_tail_engine)
-      static const bool tail_fused = [] {
-        const char *e = getenv("FH_TAIL_FUSED");
-        return !(e && *e == '0');
-      }();
-      hipStream_t sp = stream;
-      if (pipe) {
-        ensure_prev_stream();
-        sp = s_prev;
-        FH_HIP(hipEventRecord(ev_start, stream));
-        FH_HIP(hipStreamWaitEvent(sp, ev_start, 0));
-      }
+      const uint32_t per_entry = elem ? 1u : k;  // elements per log entry
+      const uint32_t *bent = lent.get() + b * size_t(n) * fq * (elem ? k : 1);
       for (uint32_t c = 0; c < nch; c++) {
         LogChunk lc;
         lc.cum[0] = 0;
@@ -1834,59 +1792,25 @@ struct EngineDevice {
           const uint64_t len = bl[r + 1] - bl[r];
           const uint32_t q0 = uint32_t(len * c / nch), q1 = uint32_t(len * (c + 1) / nch);
           lc.first[r] = bl[r] + q0;
-          lc.cum[r + 1] = lc.cum[r] + (q1 - q0) * k;
+          lc.cum[r + 1] = lc.cum[r] + (q1 - q0) * per_entry;
         }
         const uint32_t Mc = lc.cum[np];
-        const int set = pipe ? int(c & 1) : 0;
-        DBuf<uint32_t> &bka = set ? sk32c : sk32a, &bva = set ? svc : sva;
-        DBuf<uint32_t> &bkb = set ? sk32d : sk32b, &bvb = set ? svd : svb;
-        if (pipe && c >= 2) FH_HIP(hipStreamWaitEvent(stream, ev_freed[set], 0));
-        uint32_t *lk = bka.ensure(Mc + 1), *lv = bva.ensure(Mc + 1);
+        uint32_t *lk = sk32a.ensure(Mc + 1), *lv = sva.ensure(Mc + 1);
         uint32_t *ks = nullptr;
-        // FH_LOG_FUSED=1: pass 0 reads the logs (LogSrc).  Measured on C4:
-        // 16.7 ms against 15.5 materialised -- the divisions and the key
-        // gather move into both pass-0 kernels, which are compute bound
-        static const bool fused = getenv("FH_LOG_FUSED") != nullptr;
-        if (!fused) {
-          const uint32_t tiles = (Mc + kTile - 1) / kTile;
-          sort_ws.prepare(tiles, 1, stream);
-          const int db = sort_digit_bits(bits, 4);
-          probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys, dim3(tiles),
-                        dim3(kThreads), stream, Mc, k, fq, np, lc, bent, bkey,
-                        uint32_t(key_space), lk, lv, place ? pbase + c : (uint32_t *)nullptr,
-                        place_slack, sort_ws.meta.get(), (1u << db) - 1);
-          sort_pairs_counted<uint32_t, uint32_t>(lk, lv, bkb.ensure(Mc + 1), bvb.ensure(Mc + 1),
-                                                 Mc, bits, sort_ws, stream, &ks, &vs, db);
-        } else {
-          const LogSrc src{k, fq, np, uint32_t(key_space), lc, bent, bkey};
-          sort_pairs_src<uint32_t, uint32_t, LogSrc>(src, lk, lv, bkb.ensure(Mc + 1),
-                                                     bvb.ensure(Mc + 1), Mc, bits, sort_ws, stream,
-                                                     &ks, &vs);
-        }
-        if (pipe) {
-          FH_HIP(hipEventRecord(ev_sorted[set], stream));
-          FH_HIP(hipStreamWaitEvent(sp, ev_sorted[set], 0));
-        }
+        const uint32_t tiles = (Mc + kTile - 1) / kTile;
+        sort_ws.prepare(tiles, 1, stream);
+        const int db = sort_digit_bits(bits, 4);
+        probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys, dim3(tiles),
+                      dim3(kThreads), stream, Mc, k, fq, np, uint32_t(elem), lc, bent, bkey,
+                      uint32_t(key_space), lk, lv, pbase + c, place_slack, sort_ws.meta.get(),
+                      (1u << db) - 1);
+        sort_pairs_counted<uint32_t, uint32_t>(lk, lv, sk32b.ensure(Mc + 1), svb.ensure(Mc + 1), Mc,
+                                               bits, sort_ws, stream, &ks, &vs, db);
         // heads read the latest table, tails then make the chunk's last
-        // commands the latest (command-log references)
-        if (place && !fused) {
-          // the sort's other buffer pair takes the bucketed (position, code)
-          uint32_t *bk = ks == lk ? bkb.get() : lk, *bv = ks == lk ? bvb.get() : lv;
-          place_codes(Mc, ks, vs, S, pbase + c, bk, bv, dep32.ensure(M + 1), sp, tail_fused, bbase);
-        } else {
-          probed_launch("prev_engine", double(Mc) * (4.0 + 4.0 + 4.0), k_prev_views,
-                        dim3(grid_for(Mc, B)), dim3(B), sp, Mc, (const uint32_t *)ks,
-                        (const uint32_t *)vs, S, (const uint64_t *)views_latest(),
-                        dep32.ensure(M + 1));
-        }
-        if (!(place && !fused && tail_fused))
-          k_tail_engine<uint32_t><<<grid_for(Mc, B), B, 0, sp>>>(
-              Mc, ks, vs, 0, S, views_latest(), 1ull, ~0ull, nullptr, bbase);
-        if (pipe) FH_HIP(hipEventRecord(ev_freed[set], sp));
-      }
-      if (pipe) {
-        FH_HIP(hipEventRecord(ev_join, sp));
-        FH_HIP(hipStreamWaitEvent(stream, ev_join, 0));
+        // commands the latest (command-log references); the sort's other
+        // buffer pair takes the bucketed (position, code)
+        uint32_t *bk = ks == lk ? sk32b.get() : lk, *bv = ks == lk ? svb.get() : lv;
+        place_codes(Mc, ks, vs, S, pbase + c, bk, bv, dep32.ensure(M + 1), stream, bbase);
       }
       mark("keydeps_views");
     }
@@ -1910,6 +1834,7 @@ struct EngineDevice {
       return !(e && *e == '0');
     }();
     if (!on || k != 1 || fq > 4 || desc.nproc > uint32_t(kSrchMaxRep) || b >= h_win.size() ||
+        (desc.flags & FH_STREAM_ELEMENT_LOGS) ||
         n >= (1u << kRecT) || n < 2)
       return false;
     CmdMeta m{};
@@ -1944,24 +1869,11 @@ struct EngineDevice {
     const uint32_t *bent = lent.get() + b * size_t(n) * fq;
     uint32_t *rec = vrec.ensure(M + 1);
     // ~4800 commands per workgroup: fq·4800 + slack positions fit the window
-    // (FH_REC_WIN: a smaller window, more workgroups per CU)
-    static const uint32_t rec_win = [] {
-      const char *e = getenv("FH_REC_WIN");
-      const uint32_t v = e ? uint32_t(atol(e)) : kRecWin;
-      return v == 8192 || v == 32768 ? v : kRecWin;
-    }();
-    const uint32_t per = std::max<uint32_t>(1, (rec_win - 2 * rec_slack(rec_win)) / fq);
+    // (tried: 8K windows 1391 us per C4 launch, 32K 1072, 16K 935)
+    const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * rec_slack(kRecWin)) / fq);
     const uint32_t G = std::max<uint32_t>(1, (n + per - 1) / per);
-    auto recs = [&](auto kern) {
-      probed_launch("view_records", double(M) * (4.0 + 4.0), kern, dim3(G), dim3(1024), stream, n,
-                    fq, np, G, lo, bent, rec);
-    };
-    if (rec_win == 8192)
-      recs(k_view_records<8192>);
-    else if (rec_win == 32768)
-      recs(k_view_records<32768>);
-    else
-      recs(k_view_records<kRecWin>);
+    probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records<kRecWin>, dim3(G),
+                  dim3(1024), stream, n, fq, np, G, lo, bent, rec);
     const uint32_t tiles = (n + kTile - 1) / kTile;
     sort_ws.prepare(tiles, 1, stream);
     const int db = sort_digit_bits(key_bits, 4);
@@ -1975,52 +1887,24 @@ struct EngineDevice {
     uint64_t *vs = nullptr;
     sort_pairs_counted<uint32_t, uint64_t>(kwa, va, sk32b.ensure(n + 1), cv64b.ensure(n + 1), n,
                                            key_bits, sort_ws, stream, &ks, &vs, db);
-    // measurement knob FH_SRCH_DIAG (after the first run; not bit-exact): 1
-    // skips the heads' latest reads, 2 writes the codes in sorted order to
-    // scratch, 4 skips the scans, 8 writes aligned 16-B records to scratch,
-    // 16 stores the codes non-temporally (exact)
-    static const uint32_t srch_diag = [] {
-      const char *e = getenv("FH_SRCH_DIAG");
-      return e ? uint32_t(atol(e)) : 0u;
-    }();
-    // (the first run writes the real codes: later runs of the same stream
-    // keep them, so the rest of the step stays exact)
-    static uint32_t srch_runs = 0;
-    const uint32_t diag_now = srch_runs++ ? srch_diag : 0u;
     uint8_t *tm = tailm.ensure(n + 1);
     // reads the sorted key words and values (12 B, neighbours from LDS) and
-    // the heads' latest entries, writes fq codes and the tail mask
-    // workgroup size (FH_SRCH_THREADS: 256, 512 or 1024): a 1024-thread
-    // group holds 4 waves per SIMD, and the kernel's registers leave room for
-    // only one such group per CU
-    static const int srch_th = [] {
-      const char *e = getenv("FH_SRCH_THREADS");
-      const int v = e ? atoi(e) : kSrchThreads;
-      return v == 256 || v == 512 ? v : 1024;
-    }();
-    uint32_t *codes = dep32.ensure((srch_diag & 10 ? size_t(M) + 4 * size_t(n) : size_t(M)) + 1);
+    // the heads' latest entries, writes fq codes and the tail mask.  1024
+    // threads (tried 256 / 512: flat)
+    uint32_t *codes = dep32.ensure(size_t(M) + 1);
     const double sb = double(n) * (12.0 + fq * 4.0 + 1.0);
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
-    auto go = [&](auto kern, int th) {
-      probed_launch("cmd_search", sb, kern, dim3((n + th - 1) / th), dim3(th), stream, n, cm, K, np,
-                    (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, tm, diag_now);
-    };
-    auto by_th = [&](auto fqc) {
-      constexpr uint32_t F = decltype(fqc)::value;
-      if (srch_th == 256) {
-        go(k_cmd_search<F, 256>, 256);
-      } else if (srch_th == 512) {
-        go(k_cmd_search<F, 512>, 512);
-      } else {
-        go(k_cmd_search<F, 1024>, 1024);
-      }
+    auto go = [&](auto kern) {
+      probed_launch("cmd_search", sb, kern, dim3((n + kSrchThreads - 1) / kSrchThreads),
+                    dim3(kSrchThreads), stream, n, cm, K, np, (const uint32_t *)ks,
+                    (const uint64_t *)vs, lat, codes, tm);
     };
     switch (fq) {
-      case 1: by_th(std::integral_constant<uint32_t, 1>()); break;
-      case 2: by_th(std::integral_constant<uint32_t, 2>()); break;
-      case 3: by_th(std::integral_constant<uint32_t, 3>()); break;
-      default: by_th(std::integral_constant<uint32_t, 4>()); break;
+      case 1: go(k_cmd_search<1, kSrchThreads>); break;
+      case 2: go(k_cmd_search<2, kSrchThreads>); break;
+      case 3: go(k_cmd_search<3, kSrchThreads>); break;
+      default: go(k_cmd_search<4, kSrchThreads>); break;
     }
     k_cmd_tails<<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks, vs, tm,
                                                   views_latest(), bbase);
@@ -2029,11 +1913,11 @@ struct EngineDevice {
   // The chunk's dependency codes -> dep32 through the placement pass: bucket
   // (position - base, code) by the position's bits [15, 23) with the radix
   // kernels (PrevSrc computes each code on the fly), then k_place per bucket.
-  // tails != 0: also make the segment tails the latest entries (log
-  // references log_base + command), replacing k_tail_engine
+  // The bucketing pass also makes the segment tails the latest entries (log
+  // references log_base + command).
   void place_codes(uint32_t Mc, const uint32_t *ks, const uint32_t *vs, uint32_t per_cmd,
                    const uint32_t *ebase, uint32_t *bk, uint32_t *bv, uint32_t *out,
-                   hipStream_t s, bool tails, uint64_t log_base) {
+                   hipStream_t s, uint64_t log_base) {
     if (Mc == 0) return;
     const PrevSrc src{ks, vs, ebase, (const uint64_t *)views_latest(), per_cmd};
     const uint32_t tiles = (Mc + kTile - 1) / kTile;
@@ -2044,15 +1928,15 @@ struct EngineDevice {
     uint32_t *gsum = counts + size_t(tiles) * R;
     uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
     // runs of a key's consecutive elements mostly share a bucket: one atomic
-    // per run (k_up mode 2)
+    // per run (k_up)
     k_up<uint32_t, uint32_t, kPlaceDB, PrevSrc><<<tiles, kThreads, 0, s>>>(src, Mc, kPlaceShift,
-                                                                            counts, 2);
+                                                                            counts);
     k_scan_a<kPlaceDB><<<dim3(groups, R / 256), 256, 0, s>>>(counts, tiles, gsum);
     scan_b<kPlaceDB>(gsum, groups, dbase, s);
     // reads (key, arrival) keys + positions, the previous element's, and the
     // latest table at heads; writes 8 B per element
     const uint32_t nb = (tiles + 1) / 2;
-    uint32_t *defer = tails ? tail_defer.ensure(2 * size_t(nb)) : nullptr;
+    uint32_t *defer = tail_defer.ensure(2 * size_t(nb));
     probed_launch("prev_bucket", double(Mc) * (4.0 + 4.0 + 8.0), k_bucket_codes,
                   dim3(nb), dim3(kBucketThreads), s, src, bk, bv, Mc, (const uint32_t *)counts,
                   (const uint32_t *)gsum, uint32_t(kGroup), (const uint32_t *)dbase,
@@ -2072,108 +1956,42 @@ struct EngineDevice {
     FH_HIP(hipMemsetAsync(scal.get(), 0, 2 * sizeof(uint32_t), stream));
     uint32_t *ecnt = views && S >= 8 ? edge_cnt.ensure(n + 1) : (uint32_t *)nullptr;
     // rows of <= kRegSlots slots: count, scan, and the union writes the
-    // committed-deps CSR directly; wider rows go through fixed-stride rows
+    // committed-deps CSR directly; wider rows go through fixed-stride rows.
+    // (Tried, round 3: the committed dots -- an output nothing later in the
+    // step reads -- on a second stream beside the graph stage, which needs
+    // only the edges.  The graph kernels slowed down more than the union's
+    // 3.3 ms they would hide: 21.8 against 21.6 ms per C4 step.)
     deps_direct = S <= kRegSlots;
-    // The committed dots (count, scan, dot gathers, CSR rows) are an output
-    // nothing later in the step reads: with FH_UNION_SIDE=1 they
-    // run on a second stream beside the graph stage, which needs only the
-    // edges (decoded from the codes alone).  The graph kernels are latency
-    // bound with one workgroup per CU; the union's gathers fill the idle
-    // SIMDs.  The side stream joins before the executed clock moves.
-    // Measured on C4: the graph kernel slows down more than the union's 3.3
-    // ms it would hide (21.8 against 21.6 ms per step; with the side launch
-    // capped at 256 / 512 workgroups, 24.0 / 22.8), so it is opt-in
-    // (FH_UNION_SIDE=1).
-    static const bool side_on = [] {
-      const char *e = getenv("FH_UNION_SIDE");
-      return e && *e == '1';
-    }();
-    union_side = side_on && deps_direct && !deps_only;
-    hipStream_t us = stream;
-    if (union_side) {
-      ensure_prev_stream();
-      us = s_prev;
-    }
     uint64_t *ddot = nullptr;
     const uint32_t *doff = nullptr;
-    // the count + scan that size the CSR rows (on `us`)
-    auto count_rows = [&]() {
-      if (views)
-        k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, us>>>(
-            n, S, (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(), bbase, dcnt);
-      else
-        k_cmd_count<uint64_t><<<grid_for(n, B), B, 0, us>>>(
-            n, S, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(), bbase, dcnt);
-      exclusive_scan_u32(dcnt, o_dep_off.get(), n, union_side ? scan_ws_side : scan_ws, us);
-    };
     if (deps_direct) {
       doff = o_dep_off.ensure(n + 1);
       ddot = o_dep.ensure(M + 1);
-      if (!union_side) {
-        count_rows();
-        mark("keydeps_count");
-      }
+      if (views)
+        k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, stream>>>(
+            n, S, (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(), bbase, dcnt);
+      else
+        k_cmd_count<uint64_t><<<grid_for(n, B), B, 0, stream>>>(
+            n, S, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(), bbase, dcnt);
+      exclusive_scan_u32(dcnt, o_dep_off.get(), n, scan_ws, stream);
+      mark("keydeps_count");
     } else {
       ddot = dep_dot.ensure(M + 1);
     }
-    // FH_UNION_XCD=0: the capped grid-stride launch
-    static const bool xcd_union = [] {
-      const char *e = getenv("FH_UNION_XCD");
-      return !(e && *e == '0');
-    }();
-    // FH_UNION_CHUNK (commands per launch, 0 = one launch): launches over
-    // consecutive command ranges keep the dots of recent dependencies within
-    // a window the Infinity Cache can hold; FH_UNION_NT=1: the streamed
-    // codes and outputs bypass cache residency
-    static const uint32_t union_chunk = [] {
-      const char *e = getenv("FH_UNION_CHUNK");
-      return e ? uint32_t(atol(e)) : 0u;
-    }();
-    static const int union_nt = [] {
-      const char *e = getenv("FH_UNION_NT");
-      return e && *e == '1' ? 1 : 0;
-    }();
-    const uint32_t uc = union_chunk ? union_chunk : n;
-    // one union launch per command range: mode 0 both outputs, 1 the edges,
-    // 2 the committed dots (on `hs`)
-    // FH_UNION_SIDE_WG: workgroups of the side stream's launch (0: the full
-    // grid); a small grid leaves the CUs' wave slots to the graph kernels
-    static const uint32_t side_wg = [] {
-      const char *e = getenv("FH_UNION_SIDE_WG");
-      return e ? uint32_t(atol(e)) / 8 * 8 : 0u;
-    }();
-    auto union_launch = [&](int mode, hipStream_t hs) {
-      for (uint32_t c0 = 0; c0 < n; c0 += uc) {
-        const uint32_t c1 = std::min<uint32_t>(n, c0 + uc), cn = c1 - c0;
-        const char *nm = mode == 1 ? "cmd_edges" : "cmd_union";
-        uint32_t g = S <= 4 && xcd_union ? (grid_for(cn, B, 1u << 22) + 7) / 8 * 8 : grid_for(cn, B);
-        if (mode == 2 && side_wg) g = std::min(g, side_wg);
-        if (views)
-          probed_launch(nm, double(cn) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
-                        k_cmd_engine<uint32_t>, dim3(g),
-                        dim3(B), hs, n, S, bdot,
-                        (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
-                        (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                        scal.get(), ecnt, bbase, doff, scal.get() + 1, c0, c1, union_nt, mode);
-        else
-          probed_launch(nm, double(cn) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
-                        k_cmd_engine<uint64_t>, dim3(mode == 2 && side_wg ? std::min(grid_for(cn, B), side_wg) : grid_for(cn, B)), dim3(B), hs, n, S,
-                        bdot, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
-                        (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                        scal.get(), ecnt, bbase, doff, scal.get() + 1, c0, c1, union_nt, mode);
-      }
-    };
-    if (union_side) {
-      // the edges first (the graph waits for them), then the side stream
-      union_launch(1, stream);
-      FH_HIP(hipEventRecord(ev_start, stream));
-      FH_HIP(hipStreamWaitEvent(us, ev_start, 0));
-      count_rows();
-      union_launch(2, us);
-      FH_HIP(hipEventRecord(ev_join, us));
-    } else {
-      union_launch(0, stream);
-    }
+    // rows of <= 4 slots: XCD-contiguous blocks (k_cmd_engine)
+    const uint32_t g = S <= 4 ? (grid_for(n, B, 1u << 22) + 7) / 8 * 8 : grid_for(n, B);
+    if (views)
+      probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
+                    k_cmd_engine<uint32_t>, dim3(g), dim3(B), stream, n, S, bdot,
+                    (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
+                    (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
+                    scal.get(), ecnt, bbase, doff, scal.get() + 1);
+    else
+      probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
+                    k_cmd_engine<uint64_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
+                    (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
+                    (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
+                    scal.get(), ecnt, bbase, doff, scal.get() + 1);
     mark("keydeps_union");
     if (deps_only) return;  // the committed deps are the output (partial replication)
     const uint32_t *gdst = dd, *goff = nullptr;
@@ -2218,11 +2036,6 @@ struct EngineDevice {
       k_seq_dots<<<grid_for(gout.nelem, B), B, 0, stream>>>(gout.nelem, gout.pk_vid, bdot, sq);
       o_seq = sq;
       mark("per_key_dots");
-    }
-    if (union_side) {  // the committed dots (side stream) before the clock moves
-      FH_HIP(hipStreamWaitEvent(stream, ev_join, 0));
-      union_side = false;
-      mark("union_join");
     }
     // executed clock: the whole batch executed
     unsigned long long *st = srcstats.get();

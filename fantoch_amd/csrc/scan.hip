@@ -201,13 +201,6 @@ struct Mailbox {
 
 void fetch_u32(const uint32_t *dev, uint32_t *host, int n, hipStream_t s) {
   FH_CHECK(n >= 0 && n <= 14, FH_EINVAL, "fetch_u32: at most 14 words");
-  static const char *ab = getenv("FH_FETCH_MEMCPY");  // A/B measurement
-  static const bool use_memcpy = ab && *ab && *ab != '0';
-  if (use_memcpy) {
-    FH_HIP(hipMemcpyAsync(host, dev, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    FH_HIP(hipStreamSynchronize(s));
-    return;
-  }
   // one mailbox per thread and device (handles are single-threaded)
   thread_local Mailbox mb[16];
   int d = 0;

@@ -19,7 +19,7 @@
 namespace fh {
 
 namespace {
-constexpr int kWideMax = 11;  // widest digit (R = 2048)
+constexpr int kWideMax = 9;  // widest digit (R = 512: the code placement's buckets)
 }  // namespace
 
 size_t SortWorkspace::meta_words(size_t n, int) const {
@@ -34,22 +34,15 @@ void SortWorkspace::prepare(size_t tiles, int, hipStream_t) {
 }
 
 // Digit plan: sort_digit_bits (sort_impl.h), balanced digits of <= 8 bits.
-// FH_SORT_WIDE=1 sorts keys of 17..22 bits in two
-// passes of 10 or 11 bits instead of three of 8 (the per-tile count matrix
-// grows 4-8x, one whole read + write of the pairs goes away).  Measured on
-// C4 (20-bit keys): no faster -- KeyDeps 15.75 vs 15.53 ms, per-key 3.40 vs
-// 3.29 ms: the wide k_down holds 57-74 KB of LDS (2 workgroups per CU
-// instead of 4) and matches 10 ballots per item, so a pass costs ~1.5x.
+// (Tried: keys of 17..22 bits in two passes of 10 or 11 bits instead of
+// three of 8.  No faster on C4 -- KeyDeps 15.75 vs 15.53 ms, per-key 3.40 vs
+// 3.29 ms: the wide k_down holds 57-74 KB of LDS, 2 workgroups per CU
+// instead of 4, and matches 10 ballots per item.)
 template <class K, class VT>
 void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *vb, size_t n,
                 int key_bits, SortWorkspace &ws, hipStream_t s, K **kout, VT **vout) {
   FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "sort: too many elements (>= 2^30)");
-  static const bool wide = [] {
-    const char *e = getenv("FH_SORT_WIDE");
-    return e && *e && *e != '0';
-  }();
-  int db = sort_digit_bits(key_bits, int(sizeof(K)));
-  if (wide && key_bits > 16 && key_bits <= 2 * kWideMax) db = key_bits <= 20 ? 10 : 11;
+  const int db = sort_digit_bits(key_bits, int(sizeof(K)));
   int passes = (key_bits + db - 1) / db;
   if (passes < 1) passes = 1;
   if (db == 8 && passes > int(sizeof(K))) passes = int(sizeof(K));
@@ -71,11 +64,7 @@ void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *v
     sort_passes<K, VT, DBV, ArraySrc<K, VT, false>>(ArraySrc<K, VT, false>{keys_in, vals_in},   \
                                                     true, ka, va, kb, vb, alias_a, n, passes,  \
                                                     db, ws, s, kout, vout);
-  if (db == 10) {
-    FH_SORT_RUN(10)
-  } else if (db == 11) {
-    FH_SORT_RUN(11)
-  } else if (db == 6) {
+  if (db == 6) {
     FH_SORT_RUN(6)
   } else if (db == 7) {
     FH_SORT_RUN(7)

@@ -55,9 +55,14 @@ __device__ __forceinline__ uint32_t elem_index(uint32_t base, int w, int i, int 
   return base + uint32_t(w) * 64 * kItems + uint32_t(i) * 64 + uint32_t(lane);
 }
 
+// Tile digit counts.  Runs of equal digits in adjacent lanes (passes after
+// the first see each key's elements contiguous: a hot key fills whole waves)
+// add their length with one LDS atomic from the run's first lane.  (Tried:
+// one atomic per item, 35 against 16 us per pass on a C4 chunk; wave64
+// ballot matching, slower on Zipf streams than either.)
 template <class K, class VT, int DB, class Src>
 __global__ void __launch_bounds__(kThreads)
-    k_up(Src src, uint32_t n, int shift, uint32_t *__restrict__ counts, int atomic_up) {
+    k_up(Src src, uint32_t n, int shift, uint32_t *__restrict__ counts) {
   constexpr int R = 1 << DB;
   __shared__ uint32_t s_h[kWaves][R];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -74,40 +79,17 @@ __global__ void __launch_bounds__(kThreads)
     }
   }
   __syncthreads();
-  const uint64_t lt = (uint64_t(1) << lane) - 1;
-  if (atomic_up == 2) {
-    // runs of equal digits in adjacent lanes (passes after the first see
-    // each key's elements contiguous: a hot key fills whole waves) add their
-    // length with one atomic from the run's first lane
 #pragma unroll
-    for (int i = 0; i < kItems; i++) {
-      const uint32_t idx = elem_index(base, w, i, lane);
-      const uint32_t d = idx < n ? uint32_t((key[i] >> shift) & (R - 1)) : ~0u;
-      const uint32_t dp = __shfl_up(d, 1, 64);
-      const bool head = lane == 0 || d != dp;
-      const uint64_t heads = __ballot(head);
-      if (head && d != ~0u) {
-        const uint64_t after = lane == 63 ? 0ull : heads >> (lane + 1);
-        const uint32_t len = after ? uint32_t(__builtin_ctzll(after)) + 1u : uint32_t(64 - lane);
-        atomicAdd(&s_h[w][d], len);
-      }
-    }
-  } else if (atomic_up) {
-    // one LDS atomic per item into the wave's histogram (same-digit lanes of
-    // one instruction serialise on their bin)
-#pragma unroll
-    for (int i = 0; i < kItems; i++) {
-      const uint32_t idx = elem_index(base, w, i, lane);
-      if (idx < n) atomicAdd(&s_h[w][uint32_t((key[i] >> shift) & (R - 1))], 1u);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < kItems; i++) {
-      const uint32_t idx = elem_index(base, w, i, lane);
-      const bool valid = idx < n;
-      const uint32_t d = uint32_t((key[i] >> shift) & (R - 1));
-      const uint64_t peers = match_digit<DB>(d, valid);
-      if (valid && (peers & lt) == 0) s_h[w][d] += uint32_t(__popcll(peers));  // wave-private
+  for (int i = 0; i < kItems; i++) {
+    const uint32_t idx = elem_index(base, w, i, lane);
+    const uint32_t d = idx < n ? uint32_t((key[i] >> shift) & (R - 1)) : ~0u;
+    const uint32_t dp = __shfl_up(d, 1, 64);
+    const bool head = lane == 0 || d != dp;
+    const uint64_t heads = __ballot(head);
+    if (head && d != ~0u) {
+      const uint64_t after = lane == 63 ? 0ull : heads >> (lane + 1);
+      const uint32_t len = after ? uint32_t(__builtin_ctzll(after)) + 1u : uint32_t(64 - lane);
+      atomicAdd(&s_h[w][d], len);
     }
   }
   __syncthreads();
@@ -235,24 +217,14 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
-// k_scan_b, or its 1024-thread form (FH_SCAN_WIDE=0: the 256-thread one)
+// the second scan level: k_scan_b_wide up to 1024 digits (the 256-thread
+// k_scan_b took 5.9 against 5.0 us for 8-bit digits, 9.5 against 6.3 for 9)
 template <int DB>
 inline void scan_b(uint32_t *gsum, uint32_t groups, uint32_t *dbase, hipStream_t s) {
-  static const bool wide = [] {
-    const char *e = getenv("FH_SCAN_WIDE");
-    return !(e && *e == '0');
-  }();
-  if constexpr (DB < 8) {  // (k_scan_b assumes at least 256 digits)
+  if constexpr (DB <= 10)
     k_scan_b_wide<DB><<<1, 1024, 0, s>>>(gsum, groups, dbase);
-  } else {
-    if constexpr (DB <= 10) {
-      if (wide) {
-        k_scan_b_wide<DB><<<1, 1024, 0, s>>>(gsum, groups, dbase);
-        return;
-      }
-    }
+  else
     k_scan_b<DB><<<1, 256, 0, s>>>(gsum, groups, dbase);
-  }
 }
 
 // Small sorts (tiles <= kFusedMaxTiles): one 1024-thread workgroup does both
@@ -452,20 +424,8 @@ template <class K, class VT, int DB, class Src>
 void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tiles,
                uint32_t groups, uint32_t *counts, uint32_t *gsum, uint32_t *dbase, hipStream_t s,
                bool probe, bool have_counts = false) {
-  // tile counts by LDS atomics (FH_SORT_UP_ATOMIC=0: wave64 ballot matching).
-  // Measured on C4 (Zipf 0.99, 20-bit keys): KeyDeps 15.44 -> 14.98 ms,
-  // per-key 3.40 -> 3.32 -- the 8 ballots per item cost more than the
-  // same-bin serialisation of hot digits.  Counts only: k_down's ranks stay
-  // ballot-matched (stable without relying on the order in which one
-  // instruction's same-address atomics return).
-  // FH_SORT_UP_ATOMIC=1: an atomic per item; default 2: per run of equal
-  // digits in adjacent lanes
-  static const int atomic_up = [] {
-    const char *e = getenv("FH_SORT_UP_ATOMIC");
-    return e && *e == '0' ? 0 : e && *e == '1' ? 1 : 2;
-  }();
   if (!have_counts)  // (else the producer of the input wrote the tile counts)
-    k_up<K, VT, DB, Src><<<tiles, kThreads, 0, s>>>(src, uint32_t(n), shift, counts, atomic_up);
+    k_up<K, VT, DB, Src><<<tiles, kThreads, 0, s>>>(src, uint32_t(n), shift, counts);
   uint32_t gsize = kGroup;
   if (DB <= 8 && tiles <= kFusedMaxTiles) {
     gsize = (tiles + 3) / 4;
@@ -474,12 +434,9 @@ void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tile
     k_scan_a<DB><<<groups, 256, 0, s>>>(counts, tiles, gsum);
     scan_b<DB>(gsum, groups, dbase, s);
   }
-  // the 512-thread scatter (k_down; FH_SORT_DOWN_THREADS=256: 256 threads).
-  // Measured on C4, u64 values: 613 -> 592 us per 100M-element pass
-  static const int down_th = [] {
-    const char *e = getenv("FH_SORT_DOWN_THREADS");
-    return e && atoi(e) == 256 ? kThreads : 512;
-  }();
+  // the 512-thread scatter (k_down).  Measured on C4, u64 values: 613 -> 592
+  // us per 100M-element pass against 256 threads
+  constexpr int down_th = 512;
   auto down = [&](auto kern, int th) {
     if (!probe) {
       kern<<<tiles, th, 0, s>>>(src, ko, vo, uint32_t(n), shift, counts, gsum, gsize, dbase);
@@ -557,15 +514,10 @@ void sort_pairs_src(const Src &src, K *ka, VT *va, K *kb, VT *vb, size_t n, int 
 // over them (20-bit keys: 7 + 7 + 6 instead of 8 + 8 + 4).  A narrower digit
 // means fewer ballots per item in k_down and longer same-digit runs per tile
 // (32 instead of 16 elements on average at 7 bits: 128-B writes instead of
-// 64-B ones).  FH_SORT_BALANCED=0: 8-bit digits throughout.
+// 64-B ones).
 inline int sort_digit_bits(int key_bits, int key_bytes) {
-  static const bool balanced = [] {
-    const char *e = getenv("FH_SORT_BALANCED");
-    return !(e && *e == '0');
-  }();
   int passes = std::max(1, (key_bits + 7) / 8);
   if (passes > key_bytes) passes = key_bytes;
-  if (!balanced) return 8;
   const int db = (key_bits + passes - 1) / passes;
   return db >= 8 ? 8 : db <= 6 ? 6 : 7;
 }

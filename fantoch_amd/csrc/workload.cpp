@@ -25,6 +25,22 @@
 //    (i+d)*W + d with d = 0 for the coordinator and d uniform in [0, W)
 //    otherwise (the analogue of the simulator's reorder_messages,
 //    fantoch/src/sim/runner.rs:513-518).
+// Partial replication (shards >= 2, BASELINE config C5): shard h holds the
+// processes n·h + 1 ... n·h + n (fantoch/src/util.rs:115-122) and the keys
+// with key % shards == h.
+//  - the command's target shard t is the shard of its first key (the client
+//    submits to it, fantoch/src/client/workload.rs:172-176); its coordinator
+//    there is process n·t + 1 + (i mod n), and the dot is that process's next
+//    id (DotGen::next_id, id.rs:88-91), so Dot::target_shard (id.rs:59-61)
+//    is t;
+//  - every shard h the command touches runs its own collect (the forwarded
+//    submit, protocol/partial.rs:8-34, then atlas.rs:214-328): its
+//    coordinator is n·h + 1 + (i mod n) (closest_process, the same local
+//    index) and its fast quorum the next fq-1 processes of shard h, each with
+//    a delay seeded by (i, h, j) -- shards see the command in independent
+//    orders;
+//  - a command's committed deps are the union of its shards' reports
+//    (MShardCommit, atlas.rs:559-639).
 #include <algorithm>
 #include <cmath>
 #include <map>
@@ -126,7 +142,11 @@ void validate(const fh_workload &w) {
     }
   }
   FH_CHECK(w.views <= w.n && w.views <= 16, FH_EINVAL, "workload: views must be <= n");
+  FH_CHECK(w.shards <= 64 && uint64_t(w.n) * std::max(1u, w.shards) <= 255, FH_EINVAL,
+           "workload: shards <= 64 and n * shards <= 255 (ProcessId is a u8)");
 }
+
+inline uint32_t nshards(const fh_workload &w) { return w.shards > 1 ? w.shards : 1; }
 
 inline uint64_t gen_key(const fh_workload &w, const Alias *za, uint64_t i, uint32_t slot,
                         uint32_t attempt) {
@@ -148,34 +168,80 @@ inline uint64_t gen_key(const fh_workload &w, const Alias *za, uint64_t i, uint3
   }
 }
 
-void gen_range(const fh_workload &w, const Alias *za, uint64_t first, size_t lo, size_t hi,
-               uint64_t *dot, uint64_t *key_id, uint8_t *fq_proc, uint64_t *fq_time) {
-  const uint32_t k = w.keys_per_cmd;
+// the command's keys (unique within the command)
+inline void gen_keys(const fh_workload &w, const Alias *za, uint64_t i, uint64_t *ks) {
+  for (uint32_t s = 0; s < w.keys_per_cmd; s++) {
+    uint64_t key = 0;
+    for (uint32_t a = 0;; a++) {
+      key = gen_key(w, za, i, s, a);
+      bool dup = false;
+      for (uint32_t t = 0; t < s; t++) dup |= ks[t] == key;
+      if (!dup) break;
+    }
+    ks[s] = key;
+  }
+}
+
+// Delay of view j of command i in shard h (0 for the shard's coordinator);
+// h = 0 is the unsharded stream's seeding.
+inline uint32_t member_delay(const fh_workload &w, uint64_t i, uint32_t h, uint32_t j) {
   const uint64_t W = w.window ? w.window : 1;
+  return j == 0 ? 0u : uint32_t(rnd(w.seed, i, 1000 + 64 * uint64_t(h) + j) % W);
+}
+
+// Partial replication: the dot of command i is the next id of its target
+// shard's coordinator, so sequences count the earlier commands with the same
+// (target shard, coordinator index).  seq[n·shards] holds those counts for the
+// commands before `first + lo` and is advanced over the range.
+void gen_range(const fh_workload &w, const Alias *za, uint64_t first, size_t lo, size_t hi,
+               uint64_t *dot, uint64_t *key_id, uint8_t *fq_proc, uint64_t *fq_time,
+               uint64_t *seq) {
+  const uint32_t k = w.keys_per_cmd, S = nshards(w);
+  const uint64_t W = w.window ? w.window : 1;
+  uint64_t ks[8];
   for (size_t c = lo; c < hi; c++) {
     const uint64_t i = first + c;
-    const uint32_t p = 1 + uint32_t(i % w.n);
-    if (dot) dot[c] = make_dot(p, i / w.n + 1);
-    if (key_id) {
-      uint64_t *ks = key_id + c * k;
-      for (uint32_t s = 0; s < k; s++) {
-        uint64_t key = 0;
-        for (uint32_t a = 0;; a++) {
-          key = gen_key(w, za, i, s, a);
-          bool dup = false;
-          for (uint32_t t = 0; t < s; t++) dup |= ks[t] == key;
-          if (!dup) break;
+    const uint32_t l = uint32_t(i % w.n);
+    gen_keys(w, za, i, ks);
+    if (key_id)
+      for (uint32_t s = 0; s < k; s++) key_id[c * k + s] = ks[s];
+    if (S == 1) {
+      if (dot) dot[c] = make_dot(1 + l, i / w.n + 1);
+      if (w.views && (fq_proc || fq_time)) {
+        for (uint32_t j = 0; j < w.views; j++) {
+          const uint64_t d = member_delay(w, i, 0, j);
+          if (fq_proc) fq_proc[c * w.views + j] = uint8_t(1 + (l + j) % w.n);
+          if (fq_time) fq_time[c * w.views + j] = (i + d) * W + d;
         }
-        ks[s] = key;
       }
+      continue;
     }
+    const uint32_t t = uint32_t(ks[0] % S);
+    const uint64_t q = ++seq[t * w.n + l];
+    if (dot) dot[c] = make_dot(w.n * t + 1 + l, q);
+    // views per key slot: those of the slot's shard, [(c·k + s)·views + j]
     if (w.views && (fq_proc || fq_time)) {
-      for (uint32_t j = 0; j < w.views; j++) {
-        const uint64_t d = j == 0 ? 0 : rnd(w.seed, i, 1000 + j) % W;
-        if (fq_proc) fq_proc[c * w.views + j] = uint8_t(1 + (p - 1 + j) % w.n);
-        if (fq_time) fq_time[c * w.views + j] = (i + d) * W + d;
+      for (uint32_t s = 0; s < k; s++) {
+        const uint32_t h = uint32_t(ks[s] % S);
+        for (uint32_t j = 0; j < w.views; j++) {
+          const uint64_t d = member_delay(w, i, h, j);
+          const size_t x = (c * k + s) * w.views + j;
+          if (fq_proc) fq_proc[x] = uint8_t(w.n * h + 1 + (l + j) % w.n);
+          if (fq_time) fq_time[x] = (i + d) * W + d;
+        }
       }
     }
+  }
+}
+
+// Per-(target shard, coordinator index) command counts over [lo, hi) of the
+// stream (partial replication's dot sequences).
+void seq_counts(const fh_workload &w, const Alias *za, uint64_t lo, uint64_t hi, uint64_t *cnt) {
+  const uint32_t S = nshards(w);
+  uint64_t ks[8];
+  for (uint64_t i = lo; i < hi; i++) {
+    gen_keys(w, za, i, ks);
+    cnt[uint32_t(ks[0] % S) * w.n + uint32_t(i % w.n)]++;
   }
 }
 
@@ -183,10 +249,6 @@ void gen_range(const fh_workload &w, const Alias *za, uint64_t first, size_t lo,
 // j = (r - (p_i - 1)) mod n when j < views, at time (i + d)·W + d (gen_range).
 // Its arrival order is (T = i + d, d) ascending: a counting sort over the
 // bucket T, filled in decreasing i so that within a bucket d ascends.
-uint32_t member_delay(const fh_workload &w, uint64_t i, uint32_t j) {
-  const uint64_t W = w.window ? w.window : 1;
-  return j == 0 ? 0u : uint32_t(rnd(w.seed, i, 1000 + j) % W);
-}
 
 // `keep` (may be null): batch-local index of each command in the output, or
 // ~0u for commands left out (a key shard of the stream)
@@ -203,13 +265,13 @@ void gen_log(const fh_workload &w, uint64_t first, size_t count, uint32_t r, uin
   };
   for (size_t c = 0; c < count; c++) {
     uint32_t j;
-    if (member(c, &j)) cnt[c + member_delay(w, first + c, j) + 1]++;
+    if (member(c, &j)) cnt[c + member_delay(w, first + c, 0, j) + 1]++;
   }
   for (size_t t = 1; t < cnt.size(); t++) cnt[t] += cnt[t - 1];
   FH_CHECK(cnt.back() <= cap, FH_EINVARIANT, "log capacity");
   for (size_t c = count; c-- > 0;) {
     uint32_t j;
-    if (member(c, &j)) out[cnt[c + member_delay(w, first + c, j)]++] = keep ? keep[c] : uint32_t(c);
+    if (member(c, &j)) out[cnt[c + member_delay(w, first + c, 0, j)]++] = keep ? keep[c] : uint32_t(c);
   }
 }
 
@@ -228,6 +290,44 @@ void parallel_chunks(size_t count, F f) {
   for (auto &t : ts) t.join();
 }
 
+// [0, count) in up to 16 chunks of >= 2^16 commands (generation threads)
+std::vector<size_t> chunk_bounds(size_t count) {
+  size_t threads = std::min<size_t>(16, std::max<size_t>(1, count / (1 << 16)));
+  unsigned hc = std::thread::hardware_concurrency();
+  if (hc) threads = std::min<size_t>(threads, hc);
+  std::vector<size_t> b(threads + 1);
+  for (size_t t = 0; t <= threads; t++) b[t] = count * t / threads;
+  return b;
+}
+
+// Partial replication: per generation chunk, the (target shard, coordinator)
+// counts of every command before it -- the sequences its dots continue from.
+std::vector<std::vector<uint64_t>> seq_bases(const fh_workload &w, const Alias *za,
+                                             uint64_t first, const std::vector<size_t> &bounds) {
+  const size_t T = bounds.size() - 1, C = size_t(w.n) * nshards(w);
+  // commands before `first`, then each chunk's own counts
+  const std::vector<size_t> pre = chunk_bounds(first);
+  const size_t P = pre.size() - 1;
+  std::vector<std::vector<uint64_t>> cnt(P + T, std::vector<uint64_t>(C, 0));
+  std::vector<std::thread> ts;
+  for (size_t t = 0; t < P; t++)
+    ts.emplace_back([&, t] { seq_counts(w, za, pre[t], pre[t + 1], cnt[t].data()); });
+  for (size_t t = 0; t < T; t++)
+    ts.emplace_back([&, t] {
+      seq_counts(w, za, first + bounds[t], first + bounds[t + 1], cnt[P + t].data());
+    });
+  for (auto &t : ts) t.join();
+  std::vector<std::vector<uint64_t>> base(T, std::vector<uint64_t>(C, 0));
+  std::vector<uint64_t> run(C, 0);
+  for (size_t t = 0; t < P; t++)
+    for (size_t x = 0; x < C; x++) run[x] += cnt[t][x];
+  for (size_t t = 0; t < T; t++) {
+    base[t] = run;
+    for (size_t x = 0; x < C; x++) run[x] += cnt[P + t][x];
+  }
+  return base;
+}
+
 }  // namespace
 }  // namespace fh
 
@@ -241,6 +341,8 @@ fh_status fh_workload_generate_shard(const fh_workload *w, uint64_t first, size_
   FH_CHECK(w && n_out, FH_EINVAL, "null argument");
   fh::validate(*w);
   FH_CHECK(nshards >= 1 && shard < nshards, FH_EINVAL, "workload: shard must be < nshards");
+  FH_CHECK(fh::nshards(*w) == 1, FH_EINVAL,
+           "workload: key shards of a partially replicated stream: use element logs");
   FH_CHECK(count < (size_t(1) << 32), FH_EINVAL, "workload: count must be < 2^32");
   const fh::Alias *za = w->kind == 0 ? &fh::zipf_alias(w->zipf_s, w->key_count) : nullptr;
   const uint32_t k = w->keys_per_cmd;
@@ -251,7 +353,7 @@ fh_status fh_workload_generate_shard(const fh_workload *w, uint64_t first, size_
     std::vector<uint64_t> ks(k);
     size_t m = 0;
     for (size_t c = lo; c < hi; c++) {
-      fh::gen_range(*w, za, first + c, 0, 1, nullptr, ks.data(), nullptr, nullptr);
+      fh::gen_range(*w, za, first + c, 0, 1, nullptr, ks.data(), nullptr, nullptr, nullptr);
       const bool mine = ks[0] % nshards == shard;
       keep[c] = mine ? 1u : ~0u;
       m += mine;
@@ -268,7 +370,7 @@ fh_status fh_workload_generate_shard(const fh_workload *w, uint64_t first, size_
     for (size_t c = lo; c < hi; c++) {
       if (keep[c] == ~0u) continue;
       keep[c] = uint32_t(o);
-      fh::gen_range(*w, za, first + c, 0, 1, dot + o, key_id + o * k, nullptr, nullptr);
+      fh::gen_range(*w, za, first + c, 0, 1, dot + o, key_id + o * k, nullptr, nullptr, nullptr);
       o++;
     }
   });
@@ -305,6 +407,9 @@ fh_status fh_workload_generate_logs(const fh_workload *w, uint64_t first, size_t
   fh::validate(*w);
   FH_CHECK(w->views >= 1, FH_EINVAL, "workload: logs need replica views (views >= 1)");
   FH_CHECK(count < (size_t(1) << 32), FH_EINVAL, "workload: count must be < 2^32");
+  FH_CHECK(fh::nshards(*w) == 1, FH_EINVAL,
+           "workload: a partially replicated stream's replicas log elements "
+           "(fh_workload_generate_element_logs)");
   // replica r holds exactly the commands whose fast quorum includes r + 1
   std::vector<size_t> per(w->n, 0);
   for (uint32_t r = 0; r < w->n; r++) {
@@ -342,22 +447,115 @@ fh_status fh_workload_generate(const fh_workload *w, uint64_t first, size_t coun
   FH_CHECK(w, FH_EINVAL, "null workload");
   fh::validate(*w);
   const fh::Alias *za = w->kind == 0 ? &fh::zipf_alias(w->zipf_s, w->key_count) : nullptr;
-  size_t threads = std::min<size_t>(16, std::max<size_t>(1, count / (1 << 16)));
-  unsigned hc = std::thread::hardware_concurrency();
-  if (hc) threads = std::min<size_t>(threads, hc);
-  if (threads <= 1) {
-    fh::gen_range(*w, za, first, 0, count, dot, key_id, fq_proc, fq_time);
-  } else {
-    std::vector<std::thread> ts;
-    const size_t chunk = (count + threads - 1) / threads;
-    for (size_t t = 0; t < threads; t++) {
-      const size_t lo = t * chunk, hi = std::min(count, lo + chunk);
-      if (lo >= hi) break;
-      ts.emplace_back(fh::gen_range, std::cref(*w), za, first, lo, hi, dot, key_id, fq_proc,
-                      fq_time);
+  const std::vector<size_t> bounds = fh::chunk_bounds(count);
+  const size_t T = bounds.size() - 1;
+  std::vector<std::vector<uint64_t>> seq(T);
+  if (fh::nshards(*w) > 1) seq = fh::seq_bases(*w, za, first, bounds);
+  std::vector<std::thread> ts;
+  for (size_t t = 0; t < T; t++)
+    ts.emplace_back(fh::gen_range, std::cref(*w), za, first, bounds[t], bounds[t + 1], dot, key_id,
+                    fq_proc, fq_time, seq[t].empty() ? nullptr : seq[t].data());
+  for (auto &t : ts) t.join();
+  FH_API_END
+}
+
+fh_status fh_workload_generate_element_logs(const fh_workload *w, uint64_t first, size_t count,
+                                            uint64_t *log_off, uint32_t *log_elem) {
+  FH_API_BEGIN
+  FH_CHECK(w && log_off && log_elem, FH_EINVAL, "null argument");
+  fh::validate(*w);
+  FH_CHECK(w->views >= 1, FH_EINVAL, "workload: logs need replica views (views >= 1)");
+  const uint32_t k = w->keys_per_cmd, V = w->views, n = w->n, S = fh::nshards(*w);
+  const uint32_t nlog = n * S, per = k * V;
+  FH_CHECK(uint64_t(count) * per < (uint64_t(1) << 31), FH_EINVAL,
+           "workload: element positions must be < 2^31");
+  const fh::Alias *za = w->kind == 0 ? &fh::zipf_alias(w->zipf_s, w->key_count) : nullptr;
+  const std::vector<size_t> bounds = fh::chunk_bounds(count);
+  const size_t T = bounds.size() - 1;
+  // element (c, s, j) -> its replica's log: shard h of key slot s, the
+  // shard's process (i + j) mod n
+  auto each = [&](size_t lo, size_t hi, auto f) {
+    uint64_t ks[8];
+    for (size_t c = lo; c < hi; c++) {
+      const uint64_t i = first + c;
+      const uint32_t l = uint32_t(i % n);
+      fh::gen_keys(*w, za, i, ks);
+      for (uint32_t s = 0; s < k; s++) {
+        const uint32_t h = uint32_t(ks[s] % S);
+        for (uint32_t j = 0; j < V; j++)
+          f(n * h + (l + j) % n, uint32_t((c * V + j) * k + s), fh::member_delay(*w, i, h, j));
+      }
     }
+  };
+  std::vector<std::vector<uint64_t>> cnt(T, std::vector<uint64_t>(nlog, 0));
+  {
+    std::vector<std::thread> ts;
+    for (size_t t = 0; t < T; t++)
+      ts.emplace_back([&, t] { each(bounds[t], bounds[t + 1], [&](uint32_t r, uint32_t, uint32_t) {
+                                 cnt[t][r]++;
+                               }); });
     for (auto &t : ts) t.join();
   }
+  // log r's entries of chunk t start at its offset plus the earlier chunks'
+  log_off[0] = 0;
+  for (uint32_t r = 0; r < nlog; r++) {
+    uint64_t tot = 0;
+    for (size_t t = 0; t < T; t++) tot += cnt[t][r];
+    log_off[r + 1] = log_off[r] + tot;
+  }
+  FH_CHECK(log_off[nlog] == uint64_t(count) * per, FH_EINVARIANT, "element log count");
+  std::vector<uint8_t> dly(count * per);
+  {
+    std::vector<std::vector<uint64_t>> pos(T, std::vector<uint64_t>(nlog));
+    for (uint32_t r = 0; r < nlog; r++) {
+      uint64_t o = log_off[r];
+      for (size_t t = 0; t < T; t++) {
+        pos[t][r] = o;
+        o += cnt[t][r];
+      }
+    }
+    std::vector<std::thread> ts;
+    for (size_t t = 0; t < T; t++)
+      ts.emplace_back([&, t] {
+        each(bounds[t], bounds[t + 1], [&](uint32_t r, uint32_t p, uint32_t d) {
+          const uint64_t o = pos[t][r]++;
+          log_elem[o] = p;
+          dly[o] = uint8_t(d);
+        });
+      });
+    for (auto &t : ts) t.join();
+  }
+  // each log in arrival order (time (c + d)·W + d, then position: one
+  // command's elements at a replica arrive together, slot order): the
+  // entries are in command order, displaced by less than the window, so an
+  // insertion sort is near linear
+  std::vector<std::thread> ts;
+  const uint32_t nt = std::min<uint32_t>(nlog, 16);
+  for (uint32_t t = 0; t < nt; t++)
+    ts.emplace_back([&, t] {
+      for (uint32_t r = t; r < nlog; r += nt) {
+        const uint64_t a = log_off[r], b = log_off[r + 1];
+        auto key = [&](uint64_t x) {
+          return ((uint64_t(log_elem[x] / per) + dly[x]) << 8) | dly[x];
+        };
+        for (uint64_t x = a + 1; x < b; x++) {
+          const uint32_t p = log_elem[x];
+          const uint8_t d = dly[x];
+          const uint64_t kx = key(x);
+          uint64_t y = x;
+          while (y > a) {
+            const uint64_t ky = key(y - 1);
+            if (ky < kx || (ky == kx && log_elem[y - 1] < p)) break;
+            log_elem[y] = log_elem[y - 1];
+            dly[y] = dly[y - 1];
+            y--;
+          }
+          log_elem[y] = p;
+          dly[y] = d;
+        }
+      }
+    });
+  for (auto &t : ts) t.join();
   FH_API_END
 }
 

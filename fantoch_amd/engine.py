@@ -77,11 +77,11 @@ class Engine:
     def stage(self, stream, nproc: int = 5):
         """stream: fantoch_amd.workload.Stream (views taken from it; its
         per-replica logs if generated, else fq_proc / fq_time)."""
-        if stream.log_cmd is not None:
+        if stream.log_cmd is not None or stream.log_elem is not None:
             return self.stage_logs([stream], nproc)
         views = 0 if stream.fq_proc is None else stream.fq_proc.shape[1]
         d = L.fh_stream_desc(n=stream.n, keys_per_cmd=stream.k, views=views,
-                             nproc=nproc if views else 0, pad=0)
+                             nproc=nproc if views else 0, flags=0)
         dots = np.ascontiguousarray(stream.dots, dtype=np.uint64)
         keys = np.ascontiguousarray(stream.keys, dtype=np.uint64)
         proc = None if not views else np.ascontiguousarray(stream.fq_proc, dtype=np.uint8)
@@ -95,7 +95,7 @@ class Engine:
         first = batches[0]
         views = 0 if first.fq_proc is None else first.fq_proc.shape[1]
         d = L.fh_stream_desc(n=first.n, keys_per_cmd=first.k, views=views,
-                             nproc=nproc if views else 0, pad=0)
+                             nproc=nproc if views else 0, flags=0)
         assert all(b.n == first.n and b.k == first.k for b in batches)
         dots = np.ascontiguousarray(np.concatenate([b.dots for b in batches]), dtype=np.uint64)
         keys = np.ascontiguousarray(np.concatenate([b.keys for b in batches]), dtype=np.uint64)
@@ -109,11 +109,16 @@ class Engine:
 
     def stage_logs(self, batches, nproc: int = 5):
         """Stage Streams that carry per-replica arrival logs (equal sizes);
-        each run() processes the next."""
+        each run() processes the next.  Element logs (partial replication)
+        carry their own process count, len(log_off) - 1."""
         first = batches[0]
         views = first.views
+        elem = first.log_elem is not None
+        if elem:
+            nproc = len(first.log_off) - 1
         assert views >= 1 and all(b.n == first.n and b.k == first.k for b in batches)
-        d = L.fh_stream_desc(n=first.n, keys_per_cmd=first.k, views=views, nproc=nproc, pad=0)
+        d = L.fh_stream_desc(n=first.n, keys_per_cmd=first.k, views=views, nproc=nproc,
+                             flags=L.FH_STREAM_ELEMENT_LOGS if elem else 0)
         one = len(batches) == 1
         dots = np.ascontiguousarray(first.dots if one else np.concatenate([b.dots for b in batches]),
                                     dtype=np.uint64)
@@ -121,14 +126,14 @@ class Engine:
                                     dtype=np.uint64)
         offs, base = [np.zeros(1, dtype=np.uint64)], 0
         for b in batches:
-            assert len(b.log_off) == nproc + 1
+            assert len(b.log_off) == nproc + 1 and (b.log_elem is not None) == elem
             offs.append(b.log_off[1:].astype(np.uint64) + np.uint64(base))
             base += int(b.log_off[-1])
         off = np.concatenate(offs)
-        cmd = first.log_cmd if one else np.concatenate([b.log_cmd for b in batches])
-        cmd = np.ascontiguousarray(cmd, dtype=np.uint32)
+        ent = [b.log_elem if elem else b.log_cmd for b in batches]
+        ent = np.ascontiguousarray(ent[0] if one else np.concatenate(ent), dtype=np.uint32)
         L.check(self._lib.fh_engine_stage_logs(self._h, C.byref(d), len(batches), L.ptr(dots),
-                                               L.ptr(keys), L.ptr(off), L.ptr(cmd)))
+                                               L.ptr(keys), L.ptr(off), L.ptr(ent)))
         self.n, self.k = first.n, first.k
 
     def run(self, sync: bool = True) -> float:

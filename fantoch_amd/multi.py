@@ -32,7 +32,7 @@ class MultiEngine:
 
     def stage(self, s, nproc: int = 5):
         """s: a Stream with per-replica logs (Workload.generate(logs=True))."""
-        d = L.fh_stream_desc(n=s.n, keys_per_cmd=s.k, views=s.views, nproc=nproc, pad=0)
+        d = L.fh_stream_desc(n=s.n, keys_per_cmd=s.k, views=s.views, nproc=nproc, flags=0)
         dots = np.ascontiguousarray(s.dots, dtype=np.uint64)
         keys = np.ascontiguousarray(s.keys, dtype=np.uint64)
         off = np.ascontiguousarray(s.log_off, dtype=np.uint64)

@@ -20,14 +20,19 @@ ZIPF, CONFLICT_RATE, CONFLICT_POOL = 0, 1, 2
 class Stream:
     dots: np.ndarray          # u64[n]
     keys: np.ndarray          # u64[n, k]
-    fq_proc: np.ndarray       # u8[n, views] or None
-    fq_time: np.ndarray       # u64[n, views] or None
+    fq_proc: np.ndarray       # u8[n, views] (partial replication: [n, k, views]) or None
+    fq_time: np.ndarray       # u64, shaped as fq_proc, or None
     key_space: int
     # replica views as per-replica arrival logs (fh_engine_stage_logs layout):
     # log_off u64[nproc+1], log_cmd u32[n*views]; None if not generated
     log_off: np.ndarray = None
     log_cmd: np.ndarray = None
     views_n: int = 0          # fast-quorum size when only the logs are held
+    # element logs (FH_STREAM_ELEMENT_LOGS): log_off u64[n_proc*shards+1],
+    # log_elem u32[n*k*views] positions (c*views + j)*k + s
+    log_elem: np.ndarray = None
+    shards: int = 1           # partial replication over `shards` key shards
+    nproc: int = 5            # processes per shard
 
     @property
     def n(self):
@@ -40,8 +45,23 @@ class Stream:
     @property
     def views(self):
         if self.fq_proc is not None:
-            return self.fq_proc.shape[1]
+            return self.fq_proc.shape[-1]
         return self.views_n
+
+    def shard_views(self, shard: int):
+        """Partial replication: shard `shard`'s part of the stream -- the
+        commands with a key on it (global indices), their keys on it
+        (key_off CSR + keys, Command::keys(shard), command.rs:95-100) and the
+        views of the shard's collect (fq_proc / fq_time [m, views])."""
+        assert self.fq_proc is not None and self.fq_proc.ndim == 3, "needs per-slot views"
+        on = self.keys % np.uint64(self.shards) == np.uint64(shard)
+        cnt = on.sum(axis=1)
+        cmds = np.nonzero(cnt)[0]
+        key_off = np.zeros(len(cmds) + 1, dtype=np.uint32)
+        np.cumsum(cnt[cmds], out=key_off[1:])
+        slot = np.argmax(on[cmds], axis=1)  # first slot on the shard: its views
+        return (cmds, key_off, self.keys[cmds][on[cmds]], self.fq_proc[cmds, slot],
+                self.fq_time[cmds, slot])
 
     def key_off(self):
         return (np.arange(self.n + 1, dtype=np.uint64) * self.k).astype(np.uint32)
@@ -60,6 +80,7 @@ class Workload:
     key_count: int = 1 << 20
     views: int = 0              # fast quorum size (0 = single view)
     window: int = 64            # reorder window W
+    shards: int = 1             # >= 2: partial replication (include/fantoch_hip.h fh_workload)
 
     @classmethod
     def zipf(cls, s, key_count, k=1, **kw):
@@ -77,32 +98,49 @@ class Workload:
         return L.fh_workload(seed=self.seed, n=self.n, keys_per_cmd=self.keys_per_cmd,
                              kind=self.kind, conflict_rate=self.conflict_rate,
                              pool_size=self.pool_size, clients=self.clients, zipf_s=self.zipf_s,
-                             key_count=self.key_count, views=self.views, window=self.window)
+                             key_count=self.key_count, views=self.views, window=self.window,
+                             shards=self.shards)
 
     def key_space(self) -> int:
         w = self._c()
         return int(L.load().fh_workload_key_space(C.byref(w)))
 
     def generate(self, count: int, first: int = 0, logs: bool = False,
-                 times: bool = True) -> Stream:
+                 times: bool = True, element_logs: bool = None) -> Stream:
         """Commands [first, first + count).  With views: fq_proc / fq_time if
-        `times`, the per-replica arrival logs if `logs` (the same arrivals)."""
+        `times` (per key slot under partial replication), the per-replica
+        arrival logs if `logs` (the same arrivals): command logs, or element
+        logs (fh_workload_generate_element_logs) for a partially replicated
+        stream or with `element_logs`."""
         lib = L.load()
         w = self._c()
+        sh = max(1, self.shards)
         dots = np.zeros(count, dtype=np.uint64)
         keys = np.zeros((count, self.keys_per_cmd), dtype=np.uint64)
         fq_proc = fq_time = None
         if self.views and times:
-            fq_proc = np.zeros((count, self.views), dtype=np.uint8)
-            fq_time = np.zeros((count, self.views), dtype=np.uint64)
+            shape = (count, self.views) if sh == 1 else (count, self.keys_per_cmd, self.views)
+            fq_proc = np.zeros(shape, dtype=np.uint8)
+            fq_time = np.zeros(shape, dtype=np.uint64)
         L.check(lib.fh_workload_generate(C.byref(w), first, count, L.ptr(dots), L.ptr(keys),
                                          L.ptr(fq_proc), L.ptr(fq_time)))
-        s = Stream(dots, keys, fq_proc, fq_time, self.key_space(), views_n=self.views)
+        s = Stream(dots, keys, fq_proc, fq_time, self.key_space(), views_n=self.views, shards=sh,
+                   nproc=self.n)
         if self.views and logs:
-            s.log_off = np.zeros(self.n + 1, dtype=np.uint64)
-            s.log_cmd = np.zeros(count * self.views, dtype=np.uint32)
-            L.check(lib.fh_workload_generate_logs(C.byref(w), first, count, L.ptr(s.log_off),
-                                                  L.ptr(s.log_cmd)))
+            if element_logs is None:
+                element_logs = sh > 1
+            if element_logs:
+                s.log_off = np.zeros(self.n * sh + 1, dtype=np.uint64)
+                s.log_elem = np.zeros(max(1, count * self.keys_per_cmd * self.views),
+                                      dtype=np.uint32)
+                L.check(lib.fh_workload_generate_element_logs(C.byref(w), first, count,
+                                                              L.ptr(s.log_off), L.ptr(s.log_elem)))
+                s.log_elem = s.log_elem[:count * self.keys_per_cmd * self.views]
+            else:
+                s.log_off = np.zeros(self.n + 1, dtype=np.uint64)
+                s.log_cmd = np.zeros(count * self.views, dtype=np.uint32)
+                L.check(lib.fh_workload_generate_logs(C.byref(w), first, count, L.ptr(s.log_off),
+                                                      L.ptr(s.log_cmd)))
         return s
 
     def generate_shard(self, count: int, nshards: int, shard: int, first: int = 0,

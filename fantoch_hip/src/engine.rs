@@ -49,12 +49,26 @@ impl Engine {
     /// batch-local commands replica r + 1's KeyDeps processes, in order.
     pub fn stage_logs(&mut self, nproc: u32, views: u32, dots: &[u64], keys: &[u64], k: usize,
                       log_off: &[u64], log_cmd: &[u32]) {
+        self.stage_logs_flags(nproc, views, dots, keys, k, log_off, log_cmd, 0);
+    }
+
+    /// Partial replication: element logs (FH_STREAM_ELEMENT_LOGS), entry =
+    /// element position (c * views + j) * k + s; nproc = processes of every
+    /// shard (log r = process r + 1).
+    pub fn stage_element_logs(&mut self, nproc: u32, views: u32, dots: &[u64], keys: &[u64],
+                              k: usize, log_off: &[u64], log_elem: &[u32]) {
+        self.stage_logs_flags(nproc, views, dots, keys, k, log_off, log_elem,
+                              ffi::FH_STREAM_ELEMENT_LOGS);
+    }
+
+    fn stage_logs_flags(&mut self, nproc: u32, views: u32, dots: &[u64], keys: &[u64], k: usize,
+                        log_off: &[u64], log_cmd: &[u32], flags: u32) {
         let desc = ffi::FhStreamDesc {
             n: dots.len(),
             keys_per_cmd: k as u32,
             views,
             nproc,
-            pad: 0,
+            flags,
         };
         check(unsafe {
             ffi::fh_engine_stage_logs(self.h, &desc, 1, dots.as_ptr(), keys.as_ptr(),

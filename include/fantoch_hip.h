@@ -423,8 +423,16 @@ typedef struct fh_stream_desc {
   uint32_t views;         /* 0 = single replica view (stream order);
                              >0 = fast-quorum size fq (replica views)      */
   uint32_t nproc;         /* processes (replica ids 1..nproc) when views>0 */
-  uint32_t pad;
+  uint32_t flags;         /* FH_STREAM_ELEMENT_LOGS: fh_engine_stage_logs'
+                             entries are element positions               */
 } fh_stream_desc;
+/* fh_engine_stage_logs: log entries are elements, not commands -- position
+ * (c*views + j)*k + s = key slot s of command c as fast-quorum member j of
+ * that slot's collect.  This is how partial replication stages (each shard's
+ * replicas see only the command's keys on their shard, Command::keys(shard),
+ * command.rs:95-100); every position of a batch appears in exactly one log,
+ * and nproc may reach 64. */
+#define FH_STREAM_ELEMENT_LOGS 1u
 
 fh_status fh_engine_create(const fh_config *cfg, fh_engine **out);
 fh_status fh_engine_destroy(fh_engine *h);
@@ -567,12 +575,25 @@ typedef struct fh_workload {
   uint64_t key_count;     /* kind 0: keys ranked 1..key_count -> ids 0..   */
   uint32_t views;         /* fast quorum size (0 = single view)            */
   uint32_t window;        /* reorder window W for replica views            */
+  uint32_t shards;        /* 0 or 1 = full replication; >= 2 = partial
+                             replication over `shards` key shards (key %
+                             shards), n processes each (n * shards <= 255):
+                             shard h = processes n*h+1 .. n*h+n
+                             (fantoch/src/util.rs:115-122); a command's dot
+                             comes from its first key's shard (its target
+                             shard, client/workload.rs:172-176, id.rs:59-61),
+                             and every shard it touches collects it with
+                             its own fast quorum and arrival delays
+                             (atlas.rs:214-328; union atlas.rs:559-639)    */
+  uint32_t pad;
 } fh_workload;
 
 /* Key space the workload's ids live in. */
 uint64_t fh_workload_key_space(const fh_workload *w);
 /* Generate commands [first, first+count): dot[count], key_id[count*k] and,
- * if views>0, fq_proc[count*views], fq_time[count*views]. */
+ * if views>0, fq_proc[count*views], fq_time[count*views].  Partial
+ * replication (shards >= 2): fq_proc / fq_time are per key slot,
+ * [(c*k + s)*views + j] = view j of the collect in key slot s's shard. */
 fh_status fh_workload_generate(const fh_workload *w, uint64_t first,
                                size_t count, uint64_t *dot, uint64_t *key_id,
                                uint8_t *fq_proc, uint64_t *fq_time);
@@ -583,6 +604,15 @@ fh_status fh_workload_generate(const fh_workload *w, uint64_t first,
 fh_status fh_workload_generate_logs(const fh_workload *w, uint64_t first,
                                     size_t count, uint64_t *log_off,
                                     uint32_t *log_cmd);
+/* The same commands' replica views as element logs (the fh_engine_stage_logs
+ * layout with FH_STREAM_ELEMENT_LOGS, one batch): log_off[n*S+1] (S = shards,
+ * 1 when unsharded; log r = process r+1), log_elem[count*k*views] element
+ * positions (c*views + j)*k + s: process r's KeyDeps sees key slot s of
+ * command c as member j of the slot's shard's fast quorum, in (time, c, s)
+ * order.  Every element appears in exactly one log. */
+fh_status fh_workload_generate_element_logs(const fh_workload *w, uint64_t first,
+                                            size_t count, uint64_t *log_off,
+                                            uint32_t *log_elem);
 /* Key shard `shard` of nshards of commands [first, first+count): the
  * commands whose first key k0 has k0 % nshards == shard (the key's owner,
  * SURVEY §8e), in stream order with their global dots; *n_out = how many.

@@ -22,8 +22,12 @@ Configurations (seeds as tools/bench_configs.py):
   c3        EPaxos ConflictPool 100% (key 0 + 16-key pool), 2 keys: deps at the
             full 10M, everything on the first 50k (the incremental Tarjan is
             quadratic on its one stream-wide SCC)
-  c5        Zipf 0.99 over 2^20 keys, 4 keys: deps at the full 12.5M shard
-            size, everything on the first 30k
+  c5_12m    Zipf 0.99 over 2^20 keys, 4 keys, unsharded: deps at 12.5M,
+            everything on the first 30k
+  c5        Atlas partial replication over 8 key shards (processes 5h+1..5h+5,
+            dots from the target shard, every shard's own collect and arrival
+            delays): deps at the full 100M (fullsize.shard_union), everything
+            on the first 20k
 Usage: python tests/golden/make_digests.py [--only c1,c4] (c4 needs ~30 GB RAM)
 """
 from __future__ import annotations
@@ -41,8 +45,8 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(HERE))
 
-from fullsize import (CONFIGS, cmd_index, digest_deps, digest_labels, digest_perkey,  # noqa: E402
-                      shard_stream)
+from fullsize import (CONFIGS, DotIndex, digest_deps, digest_labels, digest_perkey,  # noqa: E402
+                      shard_union)
 
 OUT = os.path.join(HERE, "digests.json")
 
@@ -57,52 +61,21 @@ def oracle_all(s):
     return off, deps, ex, lab, kso, ks
 
 
-def sharded_union(s, nshards):
-    """Partial replication (C5): every shard's replicas run the oracle's
-    per-replica SequentialKeyDeps + fast-quorum union over the commands' keys
-    on that shard (fo_views_run on the shard's part, tests/fullsize.py
-    shard_stream); a command's committed deps are the union over the shards
-    that replicate it (MShardCommit, atlas.rs:559-639, union :580-583).
-    Records are packed as command << 32 | source << 28 | sequence (the
-    generator's dots: source <= 5, sequence < 2^28), so one u64 sort + unique
-    is the union and leaves each row in ascending dot order."""
-    from oracle import oracle as O
-    n = s.n
-    assert n < (1 << 31) and int((s.dots & np.uint64((1 << 56) - 1)).max()) < (1 << 28)
-    assert int((s.dots >> np.uint64(56)).max()) < 8
-    recs = []
-    for sh in range(nshards):
-        t0 = time.time()
-        cmds, ko, kk = shard_stream(s, nshards, sh)
-        off, deps = O.views_run(0, 5, s.dots[cmds], ko, kk, s.fq_proc[cmds], s.fq_time[cmds])
-        per = np.diff(off.astype(np.int64))
-        r = np.repeat(cmds.astype(np.uint64), per) << np.uint64(32)
-        r |= (deps >> np.uint64(56)) << np.uint64(28)
-        r |= deps & np.uint64((1 << 28) - 1)
-        recs.append(r)
-        del off, deps, per, cmds, ko, kk
-        print(f"  shard {sh}: {len(r)} records, {time.time() - t0:.0f}s", flush=True)
-    rec = np.concatenate(recs)
-    del recs
-    rec.sort()
-    keep = np.ones(len(rec), dtype=bool)
-    keep[1:] = rec[1:] != rec[:-1]
-    rec = rec[keep]
-    del keep
-    cmd = (rec >> np.uint64(32)).astype(np.int64)
-    off = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(np.bincount(cmd, minlength=n), out=off[1:])
-    del cmd
-    lo = rec & np.uint64(0xFFFFFFFF)
-    del rec
-    deps = ((lo >> np.uint64(28)) << np.uint64(56)) | (lo & np.uint64((1 << 28) - 1))
-    return off.astype(np.uint32), deps
-
-
-def labels_in_command_order(s, ex, lab, first=0):
+def labels_in_command_order(s, ex, lab):
     out = np.zeros(s.n, dtype=np.uint64)
-    out[cmd_index(ex, 5, first)] = lab
+    out[DotIndex(s.dots)(ex)] = lab
     return out
+
+
+def oracle_sharded(s):
+    """Partial replication: the shards' union (fullsize.shard_union), then
+    one GraphExecutor over every command with all its keys."""
+    from oracle import oracle as O
+    off, deps = shard_union(s)
+    ko = s.key_off()
+    ex, lab, kso, ks = O.graph_run(s.dots, ko, s.keys.reshape(-1), off, deps, s.key_space)
+    assert len(ex) == s.n
+    return off, deps, ex, lab, kso, ks
 
 
 def main():
@@ -133,9 +106,18 @@ def main():
             entry.update(n=int(s.n), deps=digest_deps(off, deps), labels=digest_labels(labels),
                          perkey=digest_perkey(kso, ks))
         elif "shards" in c:
-            off, deps = sharded_union(w.generate(c["n"]), c["shards"])
+            off, deps = shard_union(lambda: w.generate(c["n"]), lean=True,
+                                    log=lambda m: print(" ", m, flush=True))
             entry.update(n=int(c["n"]), shards=c["shards"], deps=digest_deps(off, deps),
                          ndeps=int(off[-1]))
+            del off, deps
+            p = c["prefix"]
+            sp = w.generate(p)
+            off, deps, ex, lab, kso, ks = oracle_sharded(sp)
+            entry["prefix"] = {"n": p, "deps": digest_deps(off, deps),
+                               "labels": digest_labels(labels_in_command_order(sp, ex, lab)),
+                               "perkey": digest_perkey(kso, ks),
+                               "sccs": int(len(np.unique(lab))), "ndeps": int(off[-1])}
         elif "prefix" in c:
             s = w.generate(c["n"])
             ko = s.key_off()

@@ -350,26 +350,16 @@ print("ok")
 @pytest.mark.parametrize("env", [
     {},
     {"FH_VIEW_CMD": "0"},
-    {"FH_VIEW_CMD": "0", "FH_TAIL_FUSED": "0", "FH_SORT_UP_ATOMIC": "1", "FH_SCAN_WIDE": "0"},
-    {"FH_VIEW_CMD": "0", "FH_SORT_UP_ATOMIC": "0"},
-    {"FH_UNION_SIDE": "1", "FH_SORT_DOWN_THREADS": "256", "FH_TILE_BATCH_LOAD": "0"},
-    {"FH_UNION_SIDE": "1", "FH_UNION_SIDE_WG": "256", "FH_REC_WIN": "8192", "FH_SRCH_THREADS": "256",
-     "FH_SRCH_DIAG": "16"},
+    {"FH_VIEW_CMD": "0", "FH_PLACE_SLACK": "0"},
 ])
 def test_views_kernel_variants_match_oracle(env):
-    """The replica-view path's kernel variants (read once per process: a
-    child process): the command-level path (default) and the chunked one
-    (FH_VIEW_CMD=0), each against the oracle on a hot-key stream cut into
-    chunks of 20,000 elements, so that segments cross the bucketing
-    workgroups and chunks: the segment tails written by k_bucket_codes (the
-    first segment's deferred to k_place) or by k_tail_engine
-    (FH_TAIL_FUSED=0); the radix tile counts by runs of equal digits
-    (default), one atomic per item (FH_SORT_UP_ATOMIC=1) or ballot matching
-    (=0); the 1024- or 256-thread second scan level (FH_SCAN_WIDE).  Round
-    3: the committed dots on a second stream beside the graph stage
-    (FH_UNION_SIDE, with a capped grid), the 256-thread radix scatter, the
-    tile kernel's per-vertex edge loads, 8K record windows, 256-thread search
-    workgroups and non-temporal code stores (FH_SRCH_DIAG=16, exact)."""
+    """The replica-view paths (read once per process: a child process): the
+    command-level path (default) and the chunked one (FH_VIEW_CMD=0), each
+    against the oracle on a hot-key stream cut into chunks of 20,000
+    elements, so that segments cross the bucketing workgroups and chunks: the
+    segment tails written by k_bucket_codes in place or, for a segment begun
+    in an earlier workgroup, deferred to k_place; with a zero placement
+    slack every reordered arrival is a stray."""
     import subprocess, sys, os
     code = f"""
 import numpy as np, sys

@@ -65,10 +65,10 @@ def test_c4_key_shard_digest():
     check_digests(g, run_engine(s))
 
 
-@pytest.mark.parametrize("name", ["c3", "c5_12m"])
+@pytest.mark.parametrize("name", ["c3", "c5_12m", "c5"])
 def test_prefix_digest(name):
-    """C3 / the 4-key stream: everything against the oracle on the largest
-    prefix it finishes."""
+    """C3 / the unsharded 4-key stream / C5's partial replication: everything
+    against the oracle on the largest prefix it finishes."""
     g = gold(name)["prefix"]
     s = CONFIGS[name]["workload"]().generate(g["n"], logs=True, times=False)
     check_digests(g, run_engine(s))
@@ -93,16 +93,20 @@ def test_c4_full_properties():
 
 
 def test_c5_100m_partial_replication():
-    """C5 at its stated size: 100M commands of 4 keys over 8 key shards, all on
-    this GPU.  The committed deps must equal the oracle's shard-by-shard
-    computation -- every shard's replicas running SequentialKeyDeps over the
-    command's keys on that shard, unioned across shards (MShardCommit,
-    atlas.rs:580-583; tests/golden/make_digests.py sharded_union) -- and the
-    SCC partition, execution order and per-key sequences pass the full-size
-    properties (scipy SCC over the 856M committed deps)."""
+    """C5 at its stated size: 100M commands of 4 keys, Atlas partial
+    replication over 8 key shards, all on this GPU.  Shard h's processes are
+    5h+1..5h+5, a dot comes from its target shard, and every shard collects
+    with its own fast quorum and arrival order; the engine stages the 40
+    processes' element logs (each sees only the command's keys on its shard).
+    The committed deps must equal the oracle's shard-by-shard computation
+    unioned across shards (MShardCommit, atlas.rs:559-639;
+    tests/fullsize.py shard_union), and the SCC partition, execution order
+    and per-key sequences pass the full-size properties (scipy SCC over the
+    committed deps)."""
     g = gold("c5")
     assert g.get("shards") == 8
     s = CONFIGS["c5"]["workload"]().generate(g["n"], logs=True, times=False)
+    assert s.log_elem is not None and len(s.log_off) == 41
     r = run_engine(s)
     print("c5 100M: engine done", flush=True)
     assert int(r["dep_off"][-1]) == g["ndeps"], "committed dep count"

@@ -56,3 +56,71 @@ def test_shard_generator_partitions_the_stream():
             fl = full.log_cmd[full.log_off[r]:full.log_off[r + 1]].astype(np.int64)
             want = local[fl][local[fl] >= 0]
             assert np.array_equal(p.log_cmd[p.log_off[r]:p.log_off[r + 1]], want)
+
+
+# ---- partial replication (fh_workload.shards, BASELINE config C5) ----------
+
+@pytest.mark.parametrize("shards,k,first", [(8, 4, 0), (8, 4, 31_337), (3, 2, 5), (1, 3, 0)])
+def test_partial_stream_dots_views_and_element_logs(shards, k, first):
+    """Shard h holds processes 5h+1..5h+5 (fantoch/src/util.rs:115-122); a
+    command's dot is the next id of its target shard's coordinator (first
+    key's shard, client/workload.rs:172-176; id.rs:59-61, 88-91); each key
+    slot's views are its shard's collect; the element logs are each
+    process's (time, command, slot) order of exactly those views."""
+    w = Workload.zipf(0.99, 1 << 12, k=k, views=3, window=64, seed=77, n=5, shards=shards)
+    whole = w.generate(first + 20_000)
+    s = w.generate(20_000, first=first, logs=True, element_logs=True)
+    assert np.array_equal(s.dots, whole.dots[first:]) and np.array_equal(s.keys, whole.keys[first:])
+    src = (whole.dots >> np.uint64(56)).astype(np.int64)
+    seq = (whole.dots & np.uint64((1 << 56) - 1)).astype(np.int64)
+    i = np.arange(whole.n)
+    if shards > 1:
+        t = (whole.keys[:, 0] % np.uint64(shards)).astype(np.int64)
+        assert np.array_equal(src, 5 * t + 1 + i % 5), "coordinator of the target shard"
+        for p in np.unique(src):
+            assert np.array_equal(seq[src == p], np.arange(1, (src == p).sum() + 1)), "DotGen"
+        h = (s.keys % np.uint64(shards)).astype(np.int64)
+        assert np.array_equal((s.fq_proc[:, :, 0].astype(np.int64) - 1) // 5, h), "slot's shard"
+        fp = s.fq_proc.reshape(s.n, k, 3)
+        ft = s.fq_time.reshape(s.n, k, 3)
+    else:
+        assert np.array_equal(src, 1 + i % 5) and np.array_equal(seq, i // 5 + 1)
+        fp = np.repeat(s.fq_proc[:, None, :], k, axis=1)
+        ft = np.repeat(s.fq_time[:, None, :], k, axis=1)
+    assert len(s.log_off) == 5 * shards + 1 and s.log_off[-1] == s.n * k * 3
+    pos = s.log_elem.astype(np.int64)
+    assert np.array_equal(np.sort(pos), np.arange(s.n * k * 3)), "every element once"
+    for r in range(5 * shards):
+        e = pos[s.log_off[r]:s.log_off[r + 1]]
+        c, j, sl = e // (3 * k), (e // k) % 3, e % k
+        assert np.all(fp[c, sl, j] == r + 1), "element of this process"
+        tt = ft[c, sl, j].astype(np.int64)
+        order = np.lexsort((e, tt))
+        assert np.array_equal(order, np.arange(len(e))), "(time, position) order"
+    want = sum(int(((fp == r + 1)).sum()) for r in range(5 * shards))
+    assert want == s.n * k * 3
+
+
+def test_partial_union_differs_from_one_shard():
+    """The oracle's partial-replication union (every shard's own collect,
+    unioned) is not what one fully replicated KeyDeps gives on the same
+    commands: independent per-shard arrival orders create cross-shard
+    cycles (SCCs grow)."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from fullsize import shard_union
+    from oracle import oracle as O
+    s = Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64, seed=58, shards=8).generate(3000)
+    off, deps = shard_union(s)
+    t_slot = np.argmax((s.keys % np.uint64(8)) == (s.keys[:, :1] % np.uint64(8)), axis=1)
+    idx = np.arange(s.n)
+    proc = ((s.fq_proc[idx, t_slot].astype(np.int64) - 1) % 5 + 1).astype(np.uint8)
+    off1, deps1 = O.views_run(0, 5, s.dots, s.key_off(), s.keys.reshape(-1), proc,
+                              s.fq_time[idx, t_slot])
+    a = np.split(deps, off[1:-1].astype(np.int64))
+    b = np.split(deps1, off1[1:-1].astype(np.int64))
+    assert sum(not np.array_equal(x, y) for x, y in zip(a, b)) > s.n // 10
+    ko, kk = s.key_off(), s.keys.reshape(-1)
+    _, lab, _, _ = O.graph_run(s.dots, ko, kk, off, deps, s.key_space)
+    _, lab1, _, _ = O.graph_run(s.dots, ko, kk, off1, deps1, s.key_space)
+    assert np.unique(lab, return_counts=True)[1].max() > np.unique(lab1, return_counts=True)[1].max()
