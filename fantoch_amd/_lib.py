@@ -125,6 +125,21 @@ SIGNATURES = {
     "fh_workload_generate_element_logs": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V]),
     "fh_workload_generate_shard": (C.c_int, [P(fh_workload), C.c_uint64, S, C.c_uint32,
                                              C.c_uint32, P(S), V, V, V, V]),
+    "fh_dgraph_create": (C.c_int, [P(fh_config), C.c_uint32, C.c_uint32, P(V)]),
+    "fh_dgraph_destroy": (C.c_int, [V]),
+    "fh_dgraph_stage": (C.c_int, [V, P(fh_stream_desc), C.c_uint32, V, V, V, V, V, V, V]),
+    "fh_dgraph_keydeps": (C.c_int, [V, V]),
+    "fh_dgraph_local": (C.c_int, [V, V, V]),
+    "fh_dgraph_queries": (C.c_int, [V, V]),
+    "fh_dgraph_answer": (C.c_int, [V, S, V, V]),
+    "fh_dgraph_condense": (C.c_int, [V, V, P(C.c_uint64), P(C.c_uint64)]),
+    "fh_dgraph_condensed_part": (C.c_int, [V, V, V]),
+    "fh_dgraph_solve": (C.c_int, [V, S, V, S, V, V]),
+    "fh_dgraph_elements": (C.c_int, [V, V]),
+    "fh_dgraph_per_key": (C.c_int, [V, S, V]),
+    "fh_dgraph_results": (C.c_int, [V, V, V, S, P(S), V, V, V, P(S)]),
+    "fh_dgraph_set_profiling": (C.c_int, [V, C.c_int]),
+    "fh_dgraph_stage_times": (C.c_int, [V, P(C.c_char_p), P(C.c_float), S, P(S)]),
     "fh_engine_rewind": (C.c_int, [V]),
     "fh_engine_sync": (C.c_int, [V]),
 }

@@ -23,6 +23,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "engine_internal.h"
 #include "graph_core.h"
 #include "keybucket.h"
 #include "sort_impl.h"
@@ -790,7 +791,7 @@ __device__ __forceinline__ void cmd_union_regs(
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n,
-    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err) {
+    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, uint32_t vbase) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
@@ -872,7 +873,7 @@ __device__ __forceinline__ void cmd_union_regs(
       if (!dup) ds[nv++] = vv[t];
     }
   }
-  for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
+  for (uint32_t q = nv; q < S; q++) ds[q] = vbase + i;  // padding: self loops are ignored
   if (nv_out) nv_out[i] = nv;
 }
 
@@ -889,7 +890,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
                              uint64_t bbase, const uint32_t *__restrict__ out_off,
-                             uint32_t *__restrict__ err) {
+                             uint32_t *__restrict__ err, uint32_t vbase) {
   // uniform: the register path, with a sorting network sized to the row
   const uint32_t cn = n;
   if (S <= 4) {
@@ -901,20 +902,20 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     const uint32_t lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
     for (size_t j = size_t(lb) * blockDim.x + threadIdx.x; j < cn; j += size_t(nb) * blockDim.x)
       cmd_union_regs<4>(uint32_t(j), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                        blocked0, nblocked, nv_out, bbase, n, out_off, err);
+                        blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase);
     return;
   }
   if (S <= 8) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<8>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n, out_off, err);
+                        nblocked, nv_out, bbase, n, out_off, err, vbase);
     }
     return;
   }
   if (S <= kRegSlots) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<kRegSlots>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                                blocked0, nblocked, nv_out, bbase, n, out_off, err);
+                                blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase);
     }
     return;
   }
@@ -941,7 +942,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
         }
       }
     }
-    for (uint32_t q = nv; q < S; q++) ds[q] = i;  // padding: self loops are ignored
+    for (uint32_t q = nv; q < S; q++) ds[q] = vbase + i;  // padding: self loops are ignored
     if (nv_out) nv_out[i] = nv;
     const uint32_t m = S == 1 ? nd : sort_unique_u64(dd, nd);
     for (uint32_t q = m; q < S; q++) dd[q] = 0;
@@ -1299,6 +1300,7 @@ struct EngineDevice {
   DBuf<uint64_t> cv64a, cv64b;  // command-level views path: packed sort values
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
   bool deps_only = false;     // fh_engine_set_deps_only: stop after the committed deps
+  bool codes_only = false;    // subset logs (fh_dgraph): stop after KeyDeps, codes in dep32
   bool last_deps_only = false;
   DBuf<unsigned long long> srcstats;
   SortWorkspace sort_ws;
@@ -1505,8 +1507,12 @@ struct EngineDevice {
   // log_off[nb·nproc + 1] (global offsets into log_cmd), log_cmd[] batch-local
   // command indices; every command appears in exactly `views` logs, at most
   // once per log
+  // subset (fh_dgraph, element logs only): the logs hold a subset of the
+  // batch's positions, each at most once -- one key shard's processes; runs
+  // then stop after KeyDeps (codes_only)
   void stage_logs(const fh_stream_desc &d, size_t nb, const uint64_t *h_dot,
-                  const uint64_t *h_key, const uint64_t *h_off, const uint32_t *h_cmd) {
+                  const uint64_t *h_key, const uint64_t *h_off, const uint32_t *h_cmd,
+                  bool subset = false) {
     FH_CHECK(h_dot && h_key && nb >= 1, FH_EINVAL, "null argument");
     FH_CHECK(d.keys_per_cmd >= 1 && d.keys_per_cmd <= 8, FH_EINVAL, "keys_per_cmd in [1, 8]");
     const uint32_t fq = d.views ? d.views : 1;
@@ -1521,6 +1527,7 @@ struct EngineDevice {
     FH_CHECK((d.flags & ~FH_STREAM_ELEMENT_LOGS) == 0, FH_EINVAL, "stream desc: unknown flags");
     FH_CHECK(!elem || (d.views && d.nproc <= uint32_t(kMaxLogs)), FH_EINVAL,
              "element logs need replica views and nproc <= 64");
+    FH_CHECK(!subset || (elem && nb == 1), FH_EINVAL, "subset logs: element logs, one batch");
     FH_CHECK(!d.views || uint64_t(d.nproc + 1) * key_space <= 0xFFFFFFFFull, FH_ENOTIMPL,
              "replica views: (nproc + 1) * key_space must fit 32 bits");
     FH_HIP(hipSetDevice(device));
@@ -1540,16 +1547,16 @@ struct EngineDevice {
       // element logs: every position (c·fq + j)·k + s of a batch in exactly
       // one log (a replica may hold several of a command's key slots)
       const size_t np = d.nproc, per_b = n * fq * d.keys_per_cmd;
-      FH_CHECK(h_off[0] == 0 && h_off[nb * np] == per_b * nb, FH_EINVAL,
-               "element logs: every element position must appear in exactly one log");
-      ent.resize(per_b * nb);
+      FH_CHECK(h_off[0] == 0 && (subset ? h_off[np] <= per_b : h_off[nb * np] == per_b * nb),
+               FH_EINVAL, "element logs: every element position must appear in exactly one log");
+      ent.resize(subset ? size_t(h_off[np]) : per_b * nb);
       lo.resize(nb * (np + 1));
       std::vector<uint8_t> seen(per_b);
       h_win.assign(nb, 0);
       for (size_t b = 0; b < nb; b++) {
         std::fill(seen.begin(), seen.end(), 0);
         const uint64_t base = h_off[b * np];
-        FH_CHECK(h_off[(b + 1) * np] - base == per_b, FH_EINVAL,
+        FH_CHECK(subset || h_off[(b + 1) * np] - base == per_b, FH_EINVAL,
                  "element logs: a batch's logs must hold n * views * keys_per_cmd entries");
         for (size_t r = 0; r < np; r++) {
           lo[b * (np + 1) + r] = uint32_t(h_off[b * np + r] - base);
@@ -1562,7 +1569,7 @@ struct EngineDevice {
             ent[q] = p;
           }
         }
-        lo[b * (np + 1) + np] = uint32_t(per_b);
+        lo[b * (np + 1) + np] = uint32_t(h_off[(b + 1) * np] - base);
       }
     } else if (d.views) {
       const size_t np = d.nproc;
@@ -1636,6 +1643,7 @@ struct EngineDevice {
     nbatches = nb;
     cursor = 0;
     staged = true;
+    codes_only = subset;
   }
 
   // The device run of one batch: everything below is the timed hot path.
@@ -1784,7 +1792,7 @@ struct EngineDevice {
       const bool pow2 = (key_space & (key_space - 1)) == 0;
       const int bits = pow2 ? bits_for(key_space) : bits_for(uint64_t(np + 1) * key_space);
       const uint32_t per_entry = elem ? 1u : k;  // elements per log entry
-      const uint32_t *bent = lent.get() + b * size_t(n) * fq * (elem ? k : 1);
+      const uint32_t *bent = lent.get() + (codes_only ? 0 : b * size_t(n) * fq * (elem ? k : 1));
       for (uint32_t c = 0; c < nch; c++) {
         LogChunk lc;
         lc.cum[0] = 0;
@@ -1813,6 +1821,16 @@ struct EngineDevice {
         place_codes(Mc, ks, vs, S, pbase + c, bk, bv, dep32.ensure(M + 1), stream, bbase);
       }
       mark("keydeps_views");
+    }
+    if (codes_only) {
+      // fh_dgraph: the codes of the staged positions are the output (dep32)
+      if (ms || profile) FH_HIP(hipEventRecord(ev1, stream));
+      if (ms) {
+        FH_HIP(hipEventSynchronize(ev1));
+        FH_HIP(hipEventElapsedTime(ms, ev0, ev1));
+      }
+      if (profile) collect_times();
+      return;
     }
     if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bdot, bbase);
     materialize(n, S, bdot);
@@ -1985,13 +2003,13 @@ struct EngineDevice {
                     k_cmd_engine<uint32_t>, dim3(g), dim3(B), stream, n, S, bdot,
                     (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                    scal.get(), ecnt, bbase, doff, scal.get() + 1);
+                    scal.get(), ecnt, bbase, doff, scal.get() + 1, 0u);
     else
       probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
                     k_cmd_engine<uint64_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
                     (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                    scal.get(), ecnt, bbase, doff, scal.get() + 1);
+                    scal.get(), ecnt, bbase, doff, scal.get() + 1, 0u);
     mark("keydeps_union");
     if (deps_only) return;  // the committed deps are the output (partial replication)
     const uint32_t *gdst = dd, *goff = nullptr;
@@ -2129,6 +2147,7 @@ struct EngineDevice {
                uint64_t *scc_label, uint32_t *exec_rank, uint32_t *key_off, uint64_t *key_seq) {
     FH_HIP(hipSetDevice(device));
     FH_CHECK(staged && cursor > 0, FH_EINVAL, "no run to read results from");
+    FH_CHECK(!codes_only, FH_EINVAL, "subset logs: the run computed KeyDeps codes only");
     FH_CHECK(!last_deps_only || (!scc_label && !exec_rank && !key_off && !key_seq), FH_EINVAL,
              "deps-only run: only the committed deps are materialised");
     FH_HIP(hipStreamSynchronize(stream));
@@ -2167,6 +2186,37 @@ struct EngineDevice {
     FH_HIP(hipStreamSynchronize(stream));
   }
 };
+
+// ---- internal interface for fh_dgraph (engine_internal.h) ------------------
+EngineDevice *engine_new(const fh_config &cfg) { return new EngineDevice(cfg); }
+void engine_free(EngineDevice *e) { delete e; }
+void engine_stage_subset(EngineDevice *e, const fh_stream_desc &d, const uint64_t *dot,
+                         const uint64_t *key, const uint64_t *off, const uint32_t *ent) {
+  e->stage_logs(d, 1, dot, key, off, ent, true);
+}
+const uint32_t *engine_run_codes(EngineDevice *e, float *ms) {
+  FH_HIP(hipSetDevice(e->device));
+  e->rewind();
+  e->run(ms);
+  return e->dep32.get();
+}
+hipStream_t engine_stream(EngineDevice *e) { return e->stream; }
+void engine_set_profiling(EngineDevice *e, bool on) { e->profile = on; }
+std::vector<std::pair<std::string, float>> engine_times(EngineDevice *e) { return e->last_times; }
+
+void union_rows(uint32_t n, uint32_t S, const uint32_t *codes, const uint64_t *dot,
+                uint32_t vbase, uint32_t *dcnt, uint32_t *dep_off, uint64_t *dep_dot,
+                uint32_t *dst, uint32_t *ecnt, uint32_t *scal, ScanWorkspace &ws, hipStream_t s) {
+  FH_CHECK(S <= kRegSlots, FH_ENOTIMPL, "range union: at most 16 slots per command");
+  FH_HIP(hipMemsetAsync(scal, 0, 2 * sizeof(uint32_t), s));
+  k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, s>>>(n, S, codes, dot, 0, dcnt);
+  exclusive_scan_u32(dcnt, dep_off, n, ws, s);
+  const uint32_t g = S <= 4 ? (grid_for(n, B, 1u << 22) + 7) / 8 * 8 : grid_for(n, B);
+  probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
+                k_cmd_engine<uint32_t>, dim3(g), dim3(B), s, n, S, dot, codes, dot,
+                (const uint64_t *)nullptr, dep_dot, dcnt, dst, (uint8_t *)nullptr, scal, ecnt,
+                uint64_t(0), (const uint32_t *)dep_off, scal + 1, vbase);
+}
 
 }  // namespace fh
 

@@ -56,6 +56,8 @@ struct GraphInput {
   const uint32_t *sorted_vid = nullptr;   // [M] vid of each sorted element
   bool no_forward_hint = false;           // edges all point backwards
   bool want_per_key = true;               // build the per-key sequence
+  bool global_only = false;               // skip the tile path (fh_dgraph: rep + kap wanted)
+  bool want_orders = true;                // false: SCCs, kappa and labels only (out.kap)
   bool per_key_dots = false;              // ... of dots (pk_dot) instead of vids
   // optional: per-source (max seq, count) of the executed dots, accumulated
   // by a pass that reads every dot anyway (GraphOutput::src_stats_done)
@@ -80,6 +82,8 @@ struct GraphOutput {
   uint32_t *pk_vid = nullptr;     // [nelem] vids in per-key execution order
   uint64_t *pk_dot = nullptr;     // [nelem] their dots (per_key_dots: pk_vid null)
   bool src_stats_done = false;    // src_mx / src_cnt accumulated
+  uint64_t *kap = nullptr;        // [V] by representative: (ready time << 32) | depth
+                                  // (global path only)
 };
 
 struct TileOut;  // graph_tile.hip

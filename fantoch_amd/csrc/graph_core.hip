@@ -1305,7 +1305,7 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   }
   // replica views with a bounded reorder window: everything in tile-local LDS
   // passes, certified (graph_tile.hip); else the global path below
-  if (!in.no_forward_hint && tiles_eligible(in)) {
+  if (!in.no_forward_hint && !in.global_only && tiles_eligible(in)) {
     if (run_tiles(in, out)) {  // (labels come from the tiles)
       dbg_tile_ok++;
       build_per_key(in, out);
@@ -1327,7 +1327,7 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     any_blocked = ne != V;
   }
   const uint64_t nfwd = in.no_forward_hint ? 0 : count_forward(in);
-  if (nfwd == 0 && !any_blocked && in.sorted_keys && in.sorted_vid) {
+  if (nfwd == 0 && !any_blocked && in.sorted_keys && in.sorted_vid && in.want_orders) {
     // every SCC is a singleton and the execution order is the arrival order:
     // nothing to materialise (rep[v] = v, label = own dot, rank = v)
     out.trivial = true;
@@ -1398,6 +1398,11 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
             dbg_restricted, dbg_rounds, dbg_hprop, dbg_reach, dbg_left, out.fallback_used ? iters : 0u,
             dbg_kap_list,
             dbg_sync_n, dbg_sync_us);
+  if (!in.want_orders) {
+    build_labels(in, out);
+    out.kap = kap.get();
+    return;
+  }
   build_orders(in, out);
 }
 

@@ -558,6 +558,81 @@ fh_status fh_multi_results(fh_multi *h, uint32_t *dep_off, uint64_t *dep_dot,
 fh_status fh_multi_shard_size(fh_multi *h, size_t shard, size_t *n);
 
 /* ======================================================================
+ * Partial replication across GPUs (BASELINE config C5): one
+ * process per GPU, rank q of N; the exchanges between the steps are the
+ * caller's (torch.distributed / RCCL over xGMI), every buffer argument named
+ * _dev is a device pointer on the handle's device, and every call returns
+ * with the handle's stream idle.  Replaces, for a whole committed stream,
+ * the shards' collects and MShardCommit union (atlas.rs:214-328, 559-639)
+ * and the GraphExecutors that reach other shards' vertices through
+ * requests and replies (executor/graph/mod.rs:279-408, index.rs:171-205).
+ *   1. KeyDeps by key shard: rank q runs the processes of the shards h with
+ *      h % N == q (element logs, Command::keys(shard), command.rs:95-100).
+ *   2. Union by stream position: rank q owns commands [a_q, a_q+1) (a_q =
+ *      n*q/N); each element's dependency code goes to its command's owner
+ *      (all-to-all), which unions each command's keys x views.
+ *   3. Local SCCs of the range (cross-range edges cut); vertices reaching a
+ *      cross-range edge are contracted to their local SCCs.
+ *   4. The condensed graph (those super vertices, plus the ready times of
+ *      settled vertices they reach): cross-range targets resolved by their
+ *      owners (all-to-all of queries and answers), every rank's part
+ *      gathered (all-gather) and solved on every rank.
+ *   5. Each (key, command) element goes to the key's owner ((key % shards)
+ *      % N, all-to-all) with its order key; per-key sequences are sorted
+ *      there.
+ * Outputs per rank: the committed deps and SCC labels of its range, the
+ * per-key execution sequences of its keys (ExecutionOrderMonitor,
+ * fantoch/src/executor/monitor.rs:20-28).
+ * ==================================================================== */
+typedef struct fh_dgraph fh_dgraph;
+fh_status fh_dgraph_create(const fh_config *cfg, uint32_t rank, uint32_t world,
+                           fh_dgraph **out);
+fh_status fh_dgraph_destroy(fh_dgraph *h);
+/* The whole stream's dot[n] / key_id[n*k] (host) and this rank's processes'
+ * element logs (desc->flags has FH_STREAM_ELEMENT_LOGS, desc->nproc = its
+ * logs: the processes of its shards, shard order).  send_counts[world] /
+ * recv_counts[world] = elements of the code exchange; range[2] = (a_q,
+ * commands in the range). */
+fh_status fh_dgraph_stage(fh_dgraph *h, const fh_stream_desc *desc, uint32_t shards,
+                          const uint64_t *dot, const uint64_t *key_id,
+                          const uint64_t *log_off, const uint32_t *log_elem,
+                          uint64_t *send_counts, uint64_t *recv_counts,
+                          uint64_t *range);
+/* Step 1: this rank's KeyDeps; its elements' codes, by destination. */
+fh_status fh_dgraph_keydeps(fh_dgraph *h, uint32_t *send_dev);
+/* Steps 2-3: the range's codes (by source) -> union, local SCCs, escaping
+ * set; query_counts[world] = cross-range targets to resolve per owner. */
+fh_status fh_dgraph_local(fh_dgraph *h, const uint32_t *recv_dev,
+                          uint64_t *query_counts);
+fh_status fh_dgraph_queries(fh_dgraph *h, uint32_t *query_dev);
+/* An owner's answers to n queried vertices of its range. */
+fh_status fh_dgraph_answer(fh_dgraph *h, size_t n, const uint32_t *in_dev,
+                           uint32_t *out_dev);
+/* Step 4: with the answers, this rank's part of the condensed graph: nv
+ * vertices (2 x u64 each), ne edges (u64 each). */
+fh_status fh_dgraph_condense(fh_dgraph *h, const uint32_t *answers_dev, uint64_t *nv,
+                             uint64_t *ne);
+fh_status fh_dgraph_condensed_part(fh_dgraph *h, uint64_t *verts_dev, uint64_t *edges_dev);
+/* Step 5: every rank's parts (gathered) -> solve, order keys of the range;
+ * elem_counts[world] = per-key elements for each key owner. */
+fh_status fh_dgraph_solve(fh_dgraph *h, size_t nv, const uint64_t *verts_dev, size_t ne,
+                          const uint64_t *edges_dev, uint64_t *elem_counts);
+fh_status fh_dgraph_elements(fh_dgraph *h, uint64_t *elem_dev);
+/* The n elements of this rank's keys (2 x u64 each) -> per-key sequences. */
+fh_status fh_dgraph_per_key(fh_dgraph *h, size_t n, const uint64_t *elem_dev);
+/* Host copies (any pointer may be NULL): the range's committed deps
+ * (dep_off[count+1], dep_dot), SCC labels (min dot) of the range's commands,
+ * and the per-key elements of this rank's keys, by key then execution
+ * order (pk_key[*pk_len], pk_dot[*pk_len]). */
+fh_status fh_dgraph_results(fh_dgraph *h, uint32_t *dep_off, uint64_t *dep_dot,
+                            size_t dep_cap, size_t *dep_len, uint64_t *scc_label,
+                            uint32_t *pk_key, uint64_t *pk_dot, size_t *pk_len);
+/* Device time of each step of the last run (profiling on). */
+fh_status fh_dgraph_set_profiling(fh_dgraph *h, int on);
+fh_status fh_dgraph_stage_times(fh_dgraph *h, const char **names, float *ms, size_t cap,
+                                size_t *len);
+
+/* ======================================================================
  * Synthetic workload (fantoch/src/client/{workload,key_gen}.rs semantics,
  * seeded and counter-based so every consumer sees the same stream).
  * ==================================================================== */
