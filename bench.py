@@ -86,6 +86,13 @@ def parse():
                     help="skip the other BASELINE configurations (C1, C3, C4 key shard, C5 12.5M)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 100M line")
     ap.add_argument("--c5-commands", type=int, default=100_000_000)
+    ap.add_argument("--c5-steps", type=int, default=3)
+    ap.add_argument("--one-gpu", action="store_true",
+                    help="every rank on GPU 0 over gloo (a dry run of the N > 1 paths on a "
+                         "one-GPU box; not a measurement)")
+    ap.add_argument("--c5-backend", default="",
+                    help="N > 1: exchange backend of the C5 leg (default: the process group's, "
+                         "RCCL; gloo for a dry run of N ranks sharing one GPU)")
     ap.add_argument("--no-cpu-sharded", action="store_true",
                     help="skip the key-sharded multi-process CPU baseline")
     return ap.parse_args()
@@ -328,6 +335,57 @@ def c5_line(args, local):
     return r
 
 
+def c5_dist_line(args, rank, world, local, group):
+    """C5 across GPUs: fantoch_amd.dgraph.DistPartial -- KeyDeps by key shard
+    (shard h on rank h % N), the per-command union and local SCCs by stream-
+    position range, cross-range queries / answers, the condensed graph
+    all-gathered and solved on every rank, per-key sequences at the keys'
+    owners; exchanges over `group` (RCCL, or gloo for a dry run of N ranks
+    sharing one GPU).  value = 100M x steps / max-over-ranks time."""
+    import torch
+    import torch.distributed as dist
+    from fantoch_amd.dgraph import DistPartial
+    n = args.c5_commands
+    t_gen = time.perf_counter()
+    s = c5_workload().generate(n, logs=True, times=False)
+    t_gen = time.perf_counter() - t_gen
+    p = DistPartial(rank, world, s.key_space, group=group, device=local)
+    t_stage = time.perf_counter()
+    p.stage(s)
+    t_stage = time.perf_counter() - t_stage
+    del s
+    p.run()  # warmup
+    steps = args.c5_steps
+    dist.barrier(group=group)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        p.run()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    dist.barrier(group=group)
+    t = torch.tensor([el], dtype=torch.float64)
+    if dist.get_backend(group) == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    el = float(t.item())
+    p.stages.set_profiling(True)
+    p.run()
+    stage_ms = p.stages.stage_times()
+    p.stages.set_profiling(False)
+    p.stages.close()
+    v = n * steps / el
+    return {"workload": "C5 across GPUs: Atlas partial replication, 8 key shards (key mod 8; shard "
+                        "h = processes 5h+1..5h+5 on rank h % N), Zipf 0.99 over 2^20 keys, 4 "
+                        "keys/cmd, fast quorum 3, 100M commands; every step orders the whole "
+                        "stream (committed deps, SCC labels, per-key sequences)",
+            "commands": n, "n_gpus": world, "steps": steps, "warmup": 1,
+            "ms_per_step": round(el / steps * 1e3, 3), "commands_per_s": v, "scaling": "strong",
+            "parallelism": f"KeyDeps by key shard x{world}; union + SCC by stream range x{world}",
+            "backend": dist.get_backend(group), "generate_s": round(t_gen, 2),
+            "stage_s": round(t_stage, 2), "rank0_stage_ms": stage_ms}
+
+
 def cpu_sharded_worker(arg):
     keys, nsh, sh, sample = arg
     import numpy as np
@@ -374,7 +432,10 @@ def secondary_c2(args, local):
     el = timed_steps(eng, steps, lambda: None, rewind=False)
     r = eng.results()
     eng.close()
-    return {"metric": METRIC, "value": batch * steps / el, "unit": "commands/s",
+    v = batch * steps / el
+    d = int(r["dep_off"][-1]) / batch
+    return {"metric": METRIC, "value": v, "unit": "commands/s",
+            "path_roofline": path_roofline(v, 1, 1, d),
             "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warm,
             "config": {"workload": "C2: Zipf s=0.7 over 2^20 keys, 1 key/cmd, single replica view, "
                                    "1M-command batches of one stream, every output materialised",
@@ -389,11 +450,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     import torch
+    if args.one_gpu:  # a dry run of N ranks on one GPU (gloo): the box has one
+        local = 0
     if world > 1 or "RANK" in os.environ:
         import torch.distributed as dist_mod
         dist = dist_mod
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if args.one_gpu:
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
     from fantoch_amd.engine import Engine
 
@@ -421,7 +487,8 @@ def main():
     eng.sync()
     elapsed = timed_steps(eng, args.steps, barrier)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cpu" if args.one_gpu else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = args.commands * args.steps / elapsed
@@ -494,6 +561,9 @@ def main():
                           f"{ts:.2f}s"}
     if rank == 0 and world == 1 and not args.no_c5:
         result["c5"] = c5_line(args, local)
+    if world > 1 and not args.no_c5:
+        grp = dist.new_group(backend=args.c5_backend) if args.c5_backend else dist.group.WORLD
+        result["c5"] = c5_dist_line(args, rank, world, local, grp)
     if rank == 0 and world == 1 and not args.no_secondary:
         result["secondary"] = secondary_c2(args, local)
     if rank == 0 and world == 1 and not args.no_configs:

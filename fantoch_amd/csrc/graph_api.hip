@@ -520,6 +520,22 @@ struct GraphDevice {
     W.P = W.KP = W.DP = 0;
     cur = 1 - cur;
     FH_HIP(hipStreamSynchronize(stream));
+    // every drained dot is a carried vertex or one of this batch's executed
+    // vertices (the reference panics otherwise): the batch part is checked by
+    // count and by a sum of mixed dots over both sides (O(n), no set)
+    auto mix = [](uint64_t x) {
+      x ^= x >> 33;
+      x *= 0xff51afd7ed558ccdull;
+      x ^= x >> 33;
+      x *= 0xc4ceb9fe1a85ec53ull;
+      return x ^ (x >> 33);
+    };
+    uint64_t want_n = 0, want_h = 0, got_n = 0, got_h = 0;
+    for (size_t i = 0; i < n; i++)
+      if (!bflag[i]) {
+        want_n++;
+        want_h += mix(dot[i]);
+      }
     for (uint32_t j = 0; j < nexec; j++) {
       const uint64_t d = xdot[j];
       ready.emplace_back(d, xlab[j]);
@@ -535,8 +551,12 @@ struct GraphDevice {
         pend.erase(it);
       } else {  // a vertex of this batch (stamped now)
         m_delay.push_back(0);
+        got_n++;
+        got_h += mix(d);
       }
     }
+    FH_CHECK(got_n == want_n && got_h == want_h, FH_EINVARIANT,
+             "graph: an executed dot was neither a pending vertex nor one of the batch");
     // the batch's survivors join the host's pending metadata, in arrival
     // order (after the pass: a failed pass leaves host and device sets equal)
     for (size_t i = 0; i < n; i++) {

@@ -21,12 +21,42 @@ impl Drop for Handle {
     }
 }
 
+type Shards = Option<BTreeSet<ShardId>>;
+
 struct State {
     h: Handle,
     keys: Interner,
-    // Dependency::shards of every dot seen: a function of the dot (the
-    // command's shard set, or None for a noop), deps/keys/mod.rs:24-35
-    shards: fantoch::HashMap<Dot, Option<BTreeSet<ShardId>>>,
+    // Dependency::shards (a function of the dot: the command's shard set, or
+    // None for a noop, deps/keys/mod.rs:24-35) of the dots the device state
+    // can still return -- the latest dot of each (key, read/write) slot and
+    // the latest noop -- with the number of slots holding each.  A dot leaves
+    // when no slot holds it, so the map is bounded by the keys, as the
+    // reference's latest table is (keys/sequential.rs:7-12, locked.rs:10-15).
+    live: fantoch::HashMap<Dot, (Shards, u32)>,
+    slots: fantoch::HashMap<(u64, bool), Dot>, // (key id, read slot) -> latest dot
+    noop: Option<Dot>,
+}
+
+impl State {
+    fn hold(&mut self, dot: Dot, shards: &Shards) {
+        self.live.entry(dot).or_insert_with(|| (shards.clone(), 0)).1 += 1;
+    }
+
+    fn release(&mut self, dot: Dot) {
+        if let Some(e) = self.live.get_mut(&dot) {
+            e.1 -= 1;
+            if e.1 == 0 {
+                self.live.remove(&dot);
+            }
+        }
+    }
+
+    fn set_slot(&mut self, slot: (u64, bool), dot: Dot, shards: &Shards) {
+        self.hold(dot, shards);
+        if let Some(old) = self.slots.insert(slot, dot) {
+            self.release(old);
+        }
+    }
 }
 
 /// `SequentialKeyDeps` (keys/sequential.rs:7-144) on the device.  `Clone`
@@ -52,7 +82,9 @@ impl HipKeyDeps {
         let state = State {
             h: Handle(h),
             keys: Interner::default(),
-            shards: Default::default(),
+            live: Default::default(),
+            slots: Default::default(),
+            noop: None,
         };
         Self {
             shard_id,
@@ -100,11 +132,17 @@ impl HipKeyDeps {
         }
     }
 
-    fn to_deps(st: &State, dots: Vec<u64>) -> HashSet<Dependency> {
+    /// Output dots -> Dependency: shards from the live slots, or from the
+    /// call's `past` (deps the caller handed in, returned in this call only).
+    fn to_deps(st: &State, past: &fantoch::HashMap<Dot, Shards>, dots: Vec<u64>)
+        -> HashSet<Dependency> {
         dots.into_iter()
             .map(|x| {
                 let dot = unpack(x);
-                let shards = st.shards.get(&dot).cloned().unwrap_or(None);
+                let shards = match st.live.get(&dot) {
+                    Some((s, _)) => s.clone(),
+                    None => past.get(&dot).cloned().unwrap_or(None),
+                };
                 Dependency { dot, shards }
             })
             .collect()
@@ -113,25 +151,39 @@ impl HipKeyDeps {
     fn add(&mut self, dot: Dot, cmd: &Command, past: Option<HashSet<Dependency>>)
         -> HashSet<Dependency> {
         let mut st = self.inner.lock().unwrap();
-        st.shards.insert(dot, Some(cmd.shards().cloned().collect()));
         let keys: Vec<u64> = cmd.keys(self.shard_id).map(|k| st.keys.id(k)).collect();
+        let mut past_shards = fantoch::HashMap::default();
         let past: Option<Vec<u64>> = past.map(|p| {
             p.into_iter()
                 .map(|d| {
-                    st.shards.entry(d.dot).or_insert(d.shards);
+                    past_shards.insert(d.dot, d.shards);
                     pack(d.dot)
                 })
                 .collect()
         });
-        let out = self.call(&mut st, dot, &keys, cmd.read_only(), false, past.as_deref());
-        Self::to_deps(&st, out)
+        let read_only = cmd.read_only();
+        let out = self.call(&mut st, dot, &keys, read_only, false, past.as_deref());
+        let deps = Self::to_deps(&st, &past_shards, out);
+        // the command becomes its keys' latest (the read slot for a read-only
+        // command under LockedKeyDeps, locked.rs:100-117; else the write slot)
+        let shards: Shards = Some(cmd.shards().cloned().collect());
+        let read_slot = self.read_write && read_only;
+        for k in keys {
+            st.set_slot((k, read_slot), dot, &shards);
+        }
+        deps
     }
 
     fn noop(&mut self, dot: Dot) -> HashSet<Dependency> {
         let mut st = self.inner.lock().unwrap();
-        st.shards.insert(dot, None);
         let out = self.call(&mut st, dot, &[], false, true, None);
-        Self::to_deps(&st, out)
+        let deps = Self::to_deps(&st, &Default::default(), out);
+        // the latest noop (sequential.rs:66-70); keys' slots are unchanged
+        st.hold(dot, &None);
+        if let Some(old) = st.noop.replace(dot) {
+            st.release(old);
+        }
+        deps
     }
 
     /// KeyDeps::cmd_deps (keys/mod.rs:54-56; sequential.rs:44-50): latest

@@ -1,0 +1,88 @@
+"""Partial replication across ranks on the GPU: DistPartial with the HIP
+stages (fh_dgraph_*, csrc/dgraph.hip).  The box has one GPU, so the ranks
+share it and exchange over gloo (host copies); the 8-GPU bench runs the same
+steps over RCCL.  The assembled outputs must equal the single-process oracle
+on the same partially replicated stream: committed deps, SCC partition and
+every key's execution sequence."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def make_stream(n, seed, keys, k=4, shards=8):
+    from fantoch_amd.workload import Workload
+    w = Workload.zipf(0.99, keys, k=k, views=3, window=64, seed=seed, n=5, shards=shards)
+    return w.generate(n, logs=True)
+
+
+def _worker(rank, world, port, n, seed, keys, q):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    torch.cuda.set_device(0)
+    torch.zeros(1, device="cuda")  # torch's HIP runtime first (tests/conftest.py)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fantoch_amd.dgraph import DistPartial
+    s = make_stream(n, seed, keys)
+    p = DistPartial(rank, world, s.key_space, device=0)
+    p.stage(s)
+    for _ in range(2):  # a second run on the same staged stream (rewind inside)
+        p.run()
+    out = p.results()
+    gathered = [None] * world
+    dist.all_gather_object(gathered, out)
+    if rank == 0:
+        q.put(gathered)
+    dist.barrier()
+    p.stages.close()
+    dist.destroy_process_group()
+
+
+def run_ranks(world, n, seed, keys):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, keys, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return parts
+
+
+@pytest.mark.parametrize("world,n,seed,keys", [(1, 6000, 71, 4096), (2, 8000, 72, 4096),
+                                               (4, 8000, 73, 1 << 20), (2, 12_000, 74, 1 << 16)])
+def test_dgraph_hip_ranks_match_oracle(world, n, seed, keys):
+    sys.path.insert(0, HERE)
+    from fantoch_amd.dgraph import assemble
+    from fullsize import shard_union
+    from oracle import oracle as O
+    parts = run_ranks(world, n, seed, keys)
+    s = make_stream(n, seed, keys)
+    got = assemble(parts, s.n, s.key_space)
+    off, deps = shard_union(s)
+    assert np.array_equal(got["dep_off"], off) and np.array_equal(got["deps"], deps), "deps"
+    ex, lab, kso, ks = O.graph_run(s.dots, s.key_off(), s.keys.reshape(-1), off, deps, s.key_space)
+    want = dict(zip(ex.tolist(), lab.tolist()))
+    assert dict(zip(s.dots.tolist(), got["scc_label"].tolist())) == want, "SCC partition"
+    assert np.array_equal(got["key_off"], kso), "per-key lengths"
+    assert np.array_equal(got["key_seq"], ks), "per-key sequences"

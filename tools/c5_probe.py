@@ -1,6 +1,8 @@
 #!/usr/bin/env python
-"""C5 probe: the 4-key Zipf stream (seed as tests/fullsize.py) at a given size
-through the fused engine on one GPU; wall ms per step and the phase profile."""
+"""C5 probe: the partially replicated 4-key Zipf stream (seed as
+tests/fullsize.py, 8 shards) at a given size through the fused engine on one
+GPU; wall ms per step and the phase profile (FH_GRAPH_DEBUG=1 adds the graph
+stage's rounds on stderr)."""
 import argparse
 import json
 import os
@@ -18,10 +20,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100_000_000)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--shards", type=int, default=8)
     a = ap.parse_args()
     t = time.time()
     s = Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64, seed=0xFA170C4000000005,
-                      n=5).generate(a.n, logs=True, times=False)
+                      n=5, shards=a.shards).generate(a.n, logs=True, times=False)
     print(json.dumps({"gen_s": round(time.time() - t, 1)}), flush=True)
     eng = Engine(s.key_space, n=5, device=0)
     t = time.time()

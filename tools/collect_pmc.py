@@ -32,30 +32,36 @@ from collections import defaultdict
 
 # probe name (fh_engine_set_probe) -> kernel-name pattern
 PROBES = {
-    # k_down<K, VT, DB, Src>: pass 0 of an IOTA sort reads ArraySrc<..., true>
-    "sort_scatter": r"k_down<unsigned int, unsigned int, 8, fh::(anonymous namespace)::ArraySrc<unsigned int, unsigned int, false>",
-    "sort_scatter_iota": r"k_down<unsigned int, unsigned int, 8, fh::(anonymous namespace)::ArraySrc<unsigned int, unsigned int, true>",
-    "sort_scatter_dots": r"k_down<unsigned int, unsigned long, 8",
+    # k_down<K, VT, DB, Src>: u32 or u64 values, any digit width (the balanced
+    # 7 / 7 / 6-bit plan of 20-bit keys)
+    "sort_scatter": r"k_down<unsigned int, unsigned int,",
+    "sort_scatter_dots": r"k_down<unsigned int, unsigned long,",
+    "sort_scatter_u64": r"k_down<unsigned long, unsigned int,",
+    "sort_up": r"k_up<",
     "graph_tile": r"k_graph_tile<",
-    "prev_engine": r"k_prev_views",
     "prev_bucket": r"k_bucket_codes",
     "place": r"k_place",
     "cmd_union": r"k_cmd_engine<unsigned int>",
     "cmd_count": r"k_cmd_count<unsigned int>",
+    "cmd_search": r"k_cmd_search<",
+    "view_records": r"k_view_records<",
+    "cmd_pack": r"k_cmd_pack",
+    "cmd_tails": r"k_cmd_tails",
     "log_keys": r"k_log_keys",
     "tail_engine": r"k_tail_engine<unsigned int>",
+    "exec_fill_dots": r"k_exec_fill_dots",
     "elem_fill_dots": r"k_elem_fill_dots",
     "exec_from_groups": r"k_exec_from_groups",
-    # global graph path (C3 / C5 shards: tools/gpu_pmc.sh CFG=c5)
+    # global graph path (C3 / C5)
     "kap_relax": r"k_kap_relax",
     "kap_init": r"k_kap_init",
     "fb_hprop": r"k_fb_hprop",
     "fb_reach": r"k_fb_reach",
     "fb_init": r"k_fb_init",
+    "fb_merge": r"k_fb_merge",
     "windows": r"k_windows",
     "edge_rep": r"k_edge_rep",
-    "sort_scatter_u64": r"k_down<unsigned long, unsigned int, 8",
-    "sort_up": r"k_up<unsigned int, unsigned int, 8",
+    "edges_csr": r"k_edges_csr",
     "sort_scan": r"k_scan_fused",
     "sv_deps": r"k_sv_deps",
     "sv_tails": r"k_sv_tails",
