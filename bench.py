@@ -82,6 +82,8 @@ def parse():
                     help="kernels whose launches are timed in the probe pass")
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase profile pass")
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary C2 line")
+    ap.add_argument("--no-streaming", action="store_true",
+                    help="skip the small-batch executor line (tools/stream_bench)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other BASELINE configurations (C1, C3, C4 key shard, C5 12.5M)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 100M line")
@@ -386,6 +388,24 @@ def c5_dist_line(args, rank, world, local, group):
             "stage_s": round(t_stage, 2), "rank0_stage_ms": stage_ms}
 
 
+def streaming_line():
+    """The executor drop-in at small batches (tools/stream_bench.cpp, built by
+    tools/build_tools.sh): a C4-shaped committed stream fed to one fh_graph
+    in stream order, `batch` Adds per call, drained after every call --
+    GraphExecutor::handle + fetch_actions (executor.rs:76-145) as the runners
+    call them (run/task/executor.rs:150-175); host arrays in and out, PCIe
+    included.  None if the tool is not built."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "stream_bench")
+    if not os.path.exists(exe):
+        return None
+    p = subprocess.run([exe, "1", "20000", "10", "100000", "1000", "2000000", "1000000",
+                        "10000000"], capture_output=True, text=True, timeout=300)
+    if p.returncode != 0:
+        return {"error": p.stderr[-400:]}
+    return [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+
+
 def cpu_sharded_worker(arg):
     keys, nsh, sh, sample = arg
     import numpy as np
@@ -566,6 +586,8 @@ def main():
         result["c5"] = c5_dist_line(args, rank, world, local, grp)
     if rank == 0 and world == 1 and not args.no_secondary:
         result["secondary"] = secondary_c2(args, local)
+    if rank == 0 and world == 1 and not args.no_streaming:
+        result["streaming"] = streaming_line()
     if rank == 0 and world == 1 and not args.no_configs:
         result["configs"] = other_configs(local)
     if rank == 0:

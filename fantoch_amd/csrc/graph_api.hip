@@ -22,6 +22,7 @@
 #include "dotindex.h"
 #include "execlog.h"
 #include "graph_core.h"
+#include "graph_small.h"
 
 namespace fh {
 
@@ -255,6 +256,7 @@ struct GraphDevice {
   }
   ~GraphDevice() {
     (void)hipSetDevice(device);
+    if (h_small) (void)hipHostFree(h_small);
     if (stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
@@ -406,6 +408,16 @@ struct GraphDevice {
     }
     const std::vector<uint64_t> &exc = exc_sorted;
     uint64_t *dexc = d_exc.ensure(exc.size() + 1);
+    // FH_GRAPH_SMALL=0 (tests): every pass through the general path
+    static const bool small_on = [] {
+      const char *e = getenv("FH_GRAPH_SMALL");
+      return !(e && *e == '0');
+    }();
+    if (small_on && V <= size_t(kSmallV) && size_t(W.DP) + DB <= size_t(kSmallE)) {
+      small_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, V, KB, DB, ddot_v, dko, dk,
+                 ddo, dd, dexc, uint32_t(exc.size()));
+      return;
+    }
     // dot -> vid index
     uint64_t *sd = nullptr;
     uint32_t *sv = nullptr;
@@ -520,6 +532,92 @@ struct GraphDevice {
     W.P = W.KP = W.DP = 0;
     cur = 1 - cur;
     FH_HIP(hipStreamSynchronize(stream));
+    finish_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, xdot, xlab, bflag, mlist, P2);
+  }
+
+  // A small graph's pass (graph_small.hip): one launch, one read-back.
+  DBuf<uint8_t> d_small;
+  uint8_t *h_small = nullptr;
+  size_t h_small_cap = 0;
+  void small_pass(size_t n, const uint64_t *dot, const uint32_t *dep_off, const uint64_t *dep_dot,
+                  const uint64_t *cmd_shards, const uint64_t *dep_shards, size_t V, size_t KB,
+                  size_t DB, const uint64_t *ddot_v, const uint32_t *dko, const uint32_t *dk,
+                  const uint32_t *ddo, const uint64_t *dd, const uint64_t *dexc, uint32_t nexc) {
+    DSet &W = ds[cur];
+    DSet &N = ds[1 - cur];
+    // the next set holds at most every current vertex, key and dependency
+    const size_t KT = size_t(W.KP) + KB, DT = size_t(W.DP) + DB;
+    uint64_t *ndot = grow_keep(N.dot, V + 1, 0, stream);
+    uint32_t *nkoff = grow_keep(N.koff, V + 2, 0, stream);
+    uint32_t *nkey = grow_keep(N.key32, KT + 1, 0, stream);
+    uint32_t *ndoff = grow_keep(N.doff, V + 2, 0, stream);
+    uint64_t *nddot = grow_keep(N.ddot, DT + 1, 0, stream);
+    // read-back block: header, executed dots, labels, missing dots, flags
+    const size_t hdr = 64, bytes = hdr + V * 16 + DT * 8 + V;
+    uint8_t *blk = d_small.ensure(bytes);
+    if (h_small_cap < bytes) {
+      if (h_small) FH_HIP(hipHostFree(h_small));
+      h_small = nullptr;
+      h_small_cap = 0;
+      FH_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_small), bytes * 2, hipHostMallocDefault));
+      h_small_cap = bytes * 2;
+    }
+    SmallPass sp;
+    sp.V = uint32_t(V);
+    sp.dot = ddot_v;
+    sp.koff = dko;
+    sp.key32 = dk;
+    sp.doff = ddo;
+    sp.ddot = dd;
+    sp.frontier = d_frontier.get();
+    sp.exc = dexc;
+    sp.nexc = nexc;
+    sp.header = reinterpret_cast<uint32_t *>(blk);
+    sp.xdot = reinterpret_cast<uint64_t *>(blk + hdr);
+    sp.xlab = sp.xdot + V;
+    sp.miss = sp.xlab + V;
+    sp.miss_cap = uint32_t(DT);
+    sp.blocked = reinterpret_cast<uint8_t *>(sp.miss + DT);
+    sp.ndot = ndot;
+    sp.nkoff = nkoff;
+    sp.nkey32 = nkey;
+    sp.ndoff = ndoff;
+    sp.nddot = nddot;
+    launch_graph_small(sp, stream);
+    FH_HIP(hipMemcpyAsync(h_small, blk, bytes, hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    const uint32_t *hh = reinterpret_cast<const uint32_t *>(h_small);
+    const uint32_t nexec = hh[0], nmiss = std::min<uint32_t>(hh[1], uint32_t(DT));
+    // mod.rs:235-240 (state unchanged: the next set is not taken, the
+    // appended rows are ignored)
+    FH_CHECK(hh[2] == 0, FH_EINVARIANT, "Graph::handle_add tried to index already indexed dot");
+    batch_seq0 = next_seq;
+    index_requests(n, dot, dep_off, dep_dot, dep_shards);
+    batch_seq0 = ~uint64_t(0);
+    const uint64_t *hx = reinterpret_cast<const uint64_t *>(h_small + hdr);
+    std::vector<uint64_t> xdot(hx, hx + nexec), xlab(hx + V, hx + V + nexec);
+    std::vector<uint64_t> mlist(hx + 2 * V, hx + 2 * V + nmiss);
+    const uint8_t *hb = reinterpret_cast<const uint8_t *>(hx + 2 * V + DT);
+    std::vector<uint8_t> bflag(hb + (V - n), hb + V);
+    const uint32_t P2 = hh[3];
+    FH_CHECK(P2 == V - nexec, FH_EINVARIANT, "graph: small pass counts");
+    N.P = P2;
+    N.KP = hh[4];
+    N.DP = hh[5];
+    W.P = W.KP = W.DP = 0;
+    cur = 1 - cur;
+    passes_small++;
+    finish_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, xdot, xlab, bflag, mlist, P2);
+  }
+  uint64_t passes_small = 0;
+
+  // The host side of a pass: the drained vertices, executed clock, metrics,
+  // the survivors' pending metadata and the missing dependencies.
+  void finish_pass(size_t n, const uint64_t *dot, const uint32_t *dep_off, const uint64_t *dep_dot,
+                   const uint64_t *cmd_shards, const uint64_t *dep_shards,
+                   const std::vector<uint64_t> &xdot, const std::vector<uint64_t> &xlab,
+                   const std::vector<uint8_t> &bflag, std::vector<uint64_t> &mlist, uint32_t P2) {
+    const size_t nexec = xdot.size();
     // every drained dot is a carried vertex or one of this batch's executed
     // vertices (the reference panics otherwise): the batch part is checked by
     // count and by a sum of mixed dots over both sides (O(n), no set)

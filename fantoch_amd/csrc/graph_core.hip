@@ -572,7 +572,12 @@ __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
                            uint8_t *__restrict__ pushed, const uint32_t *__restrict__ prev,
                            int nodone) {
   if (prev && ld_u32(prev) == 0) return;  // converged (see converge())
-  GRID_STRIDE(j, n) {
+  GRID_STRIDE(jj, n) {
+    // descending positions: dependencies mostly point to earlier arrivals,
+    // so a push lands on a vertex a later-dispatched workgroup still has to
+    // visit, and the reach cascades down a backward chain inside one launch
+    // instead of one hop per launch
+    const uint32_t j = n - 1 - jj;
     const uint32_t v = FB_VID(j);
     // a vertex pushes its edges once, in the launch after its class is
     // reached (later launches would repeat the same pushes: the reach loop

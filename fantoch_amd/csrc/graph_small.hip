@@ -1,0 +1,367 @@
+// graph_small.hip -- one executor pass of a small graph in one workgroup
+// (fh_graph streaming at small batches: SURVEY §8f rank 1).
+//
+// GraphExecutor::handle(Add) runs per command inside the simulator and the
+// runner (fantoch/src/sim/runner.rs:407-413, run/task/executor.rs:150-175),
+// so a drop-in must take batches of one.  The general pass (graph_api.hip:
+// dot sort, resolve, GraphCore's fixpoints, compaction) is a few dozen
+// launches with several host round trips; for V <= kSmallV vertices and
+// E <= kSmallE dependency entries everything happens here, in LDS, in one
+// launch, and the host reads one block back:
+//  1. vertex dots sorted (bitonic, LDS): duplicate check (mod.rs:235-240)
+//     and the dot -> vid index;
+//  2. dependencies resolved: self and executed ones ignored (tarjan.rs:131-
+//     148), others are vertices or missing (the vertex is blocked, tarjan.rs:
+//     150-170); missing dots listed;
+//  3. blocked closure: a vertex reaching a missing dependency stays pending
+//     (check_pending, mod.rs:558-644);
+//  4. the rest as GraphCore orders it (graph_core.h): H = max vid reachable
+//     (pointer jumping), SCCs by rounds of reach from each ready group's root
+//     (an SCC's representative is its minimum vid), depth over same-H edges,
+//     execution order by (H, depth, representative, dot), labels = min dot;
+//  5. the survivors compacted, in arrival order, into the next vertex set.
+#include "graph_small.h"
+
+#include "dotindex.h"
+
+namespace fh {
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr uint16_t kNone = 0xFFFF;
+
+// exclusive scan of one value per thread over the block
+__device__ uint32_t block_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kThreads / 64; i++) {
+    const uint32_t c = s_w[i];
+    if (i < w) pre += c;
+    tot += c;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+// bitonic sort of n2 (a power of two <= 2 * kThreads) keys ascending, with
+// an optional u16 payload
+__device__ void bitonic(uint64_t *key, uint16_t *val, int n2) {
+  for (int k = 2; k <= n2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int x = threadIdx.x; x < n2; x += kThreads) {
+        const int p = x ^ j;
+        if (p > x) {
+          const uint64_t a = key[x], b = key[p];
+          const bool up = (x & k) == 0;
+          if (up ? a > b : a < b) {
+            key[x] = b;
+            key[p] = a;
+            if (val) {
+              const uint16_t t = val[x];
+              val[x] = val[p];
+              val[p] = t;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+__device__ int find_lds(const uint64_t *sd, int n, uint64_t d) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (sd[mid] < d)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < n && sd[lo] == d ? lo : -1;
+}
+
+// sweep to the fixpoint: body(x) returns true on a change
+template <class F>
+__device__ void sweep(int n, uint32_t *s_ch, F body) {
+  for (int it = 0;; it++) {
+    bool ch = false;
+    for (int x = threadIdx.x; x < n; x += kThreads) ch |= body(x);
+    if (ch) s_ch[it % 3] = 1;
+    if (threadIdx.x == 0) s_ch[(it + 1) % 3] = 0;
+    __syncthreads();
+    if (!s_ch[it % 3]) break;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) s_ch[threadIdx.x] = 0;
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kThreads)
+    k_graph_small(SmallPass p) {
+  __shared__ uint64_t s_dot[kSmallV], s_sd[kSmallV], s_key[kSmallV];
+  __shared__ uint16_t s_sv[kSmallV], s_rank[kSmallV];
+  __shared__ uint16_t s_off[kSmallV + 1], s_dst[kSmallE];
+  __shared__ uint16_t s_H[kSmallV], s_R[kSmallV], s_W[kSmallV], s_min[kSmallV];
+  __shared__ uint32_t s_D[kSmallV];
+  __shared__ uint8_t s_blk[kSmallV], s_F[kSmallV];
+  __shared__ uint32_t s_w[kThreads / 64], s_ch[3], s_nmiss, s_err;
+  const int tid = threadIdx.x, V = int(p.V);
+  int n2 = 1;
+  while (n2 < V) n2 <<= 1;
+  if (tid < 3) s_ch[tid] = 0;
+  if (tid == 0) s_nmiss = s_err = 0;
+  for (int x = tid; x < n2; x += kThreads) {
+    const uint64_t d = x < V ? p.dot[x] : ~0ull;
+    s_dot[x] = d;
+    s_sd[x] = d;
+    s_sv[x] = uint16_t(x);
+  }
+  __syncthreads();
+  // 1. dot -> vid index; a dot indexed twice (mod.rs:235-240)
+  bitonic(s_sd, s_sv, n2);
+  for (int x = tid; x < V; x += kThreads) {
+    s_rank[s_sv[x]] = uint16_t(x);
+    if (x > 0 && s_sd[x] == s_sd[x - 1]) s_err = 1;
+  }
+  __syncthreads();
+  // 2. resolve: count, scan, fill
+  uint32_t cnt[2] = {0, 0};
+  for (int j = 0; j < 2; j++) {
+    const int v = tid + j * kThreads;
+    if (v >= V) continue;
+    bool missing = false;
+    const uint64_t self = s_dot[v];
+    for (uint32_t e = p.doff[v]; e < p.doff[v + 1]; e++) {
+      const uint64_t d = p.ddot[e];
+      if (d == self || executed_dev(d, p.frontier, p.exc, p.nexc)) continue;
+      if (find_lds(s_sd, V, d) >= 0) {
+        cnt[j]++;
+      } else {
+        missing = true;
+        const uint32_t q = atomicAdd(&s_nmiss, 1u);
+        if (q < p.miss_cap) p.miss[q] = d;
+      }
+    }
+    s_blk[v] = missing;
+  }
+  uint32_t etot = 0;
+  const uint32_t o0 = block_scan(cnt[0] + cnt[1], s_w, &etot);
+  {
+    uint32_t o = o0;
+    for (int j = 0; j < 2; j++) {
+      const int v = tid + j * kThreads;
+      if (v >= V) continue;
+      s_off[v] = uint16_t(o);
+      const uint64_t self = s_dot[v];
+      for (uint32_t e = p.doff[v]; e < p.doff[v + 1]; e++) {
+        const uint64_t d = p.ddot[e];
+        if (d == self || executed_dev(d, p.frontier, p.exc, p.nexc)) continue;
+        const int u = find_lds(s_sd, V, d);
+        if (u >= 0) s_dst[o++] = s_sv[u];
+      }
+    }
+    if (tid == 0) s_off[V] = uint16_t(etot);
+  }
+  __syncthreads();
+  // 3. blocked closure
+  sweep(V, s_ch, [&](int v) {
+    if (s_blk[v]) return false;
+    for (int e = s_off[v]; e < s_off[v + 1]; e++)
+      if (s_blk[s_dst[e]]) {
+        s_blk[v] = 1;
+        return true;
+      }
+    return false;
+  });
+  // 4. H = max vid reachable (executable vertices reach only executable ones)
+  for (int v = tid; v < V; v += kThreads) {
+    s_H[v] = uint16_t(v);
+    s_R[v] = kNone;
+    s_F[v] = 0;
+  }
+  __syncthreads();
+  sweep(V, s_ch, [&](int v) {
+    if (s_blk[v]) return false;
+    uint32_t h = s_H[v];
+    const uint32_t h0 = h;
+    for (int e = s_off[v]; e < s_off[v + 1]; e++) h = max(h, uint32_t(s_H[s_dst[e]]));
+    h = max(h, uint32_t(s_H[h]));
+    if (h > h0) {
+      s_H[v] = uint16_t(h);
+      return true;
+    }
+    return false;
+  });
+  // SCC rounds over the unassigned vertices: W = max unassigned vid reachable
+  // through unassigned vertices; roots (W(v) = v) reach their class members
+  for (int round = 0;; round++) {
+    uint32_t left = 0;
+    {
+      uint32_t mine = 0;
+      for (int v = tid; v < V; v += kThreads)
+        if (!s_blk[v] && s_R[v] == kNone) {
+          mine++;
+          s_W[v] = uint16_t(v);
+          s_F[v] = 0;
+        }
+      block_scan(mine, s_w, &left);
+    }
+    if (!left) break;
+    sweep(V, s_ch, [&](int v) {
+      if (s_blk[v] || s_R[v] != kNone) return false;
+      uint32_t h = s_W[v];
+      const uint32_t h0 = h;
+      for (int e = s_off[v]; e < s_off[v + 1]; e++) {
+        const uint16_t y = s_dst[e];
+        if (s_R[y] == kNone) h = max(h, uint32_t(s_W[y]));
+      }
+      h = max(h, uint32_t(s_W[h]));
+      if (h > h0) {
+        s_W[v] = uint16_t(h);
+        return true;
+      }
+      return false;
+    });
+    for (int v = tid; v < V; v += kThreads)
+      if (!s_blk[v] && s_R[v] == kNone && s_W[v] == v) s_F[v] = 1;
+    __syncthreads();
+    sweep(V, s_ch, [&](int v) {
+      if (s_F[v] != 1) return false;
+      s_F[v] = 2;
+      const uint16_t g = s_W[v];
+      for (int e = s_off[v]; e < s_off[v + 1]; e++) {
+        const uint16_t y = s_dst[e];
+        if (s_R[y] == kNone && s_F[y] == 0 && s_W[y] == g) s_F[y] = 1;
+      }
+      return true;
+    });
+    for (int v = tid; v < V; v += kThreads)
+      if (!s_blk[v] && s_R[v] == kNone && s_F[v]) s_R[v] = s_W[v];
+    __syncthreads();
+  }
+  // representative = min member; labels = min dot; depth over same-H edges
+  for (int v = tid; v < V; v += kThreads) {
+    s_min[v] = kNone;
+    s_D[v] = 0;
+    s_key[v] = ~0ull;  // per representative: min dot (label)
+  }
+  __syncthreads();
+  for (int v = tid; v < V; v += kThreads)
+    if (!s_blk[v]) {
+      // 16-bit min through the 32-bit word: s_min is reread after the barrier
+      uint32_t *w = reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(&s_min[s_R[v]]) & ~uintptr_t(3));
+      const int sh = int(reinterpret_cast<uintptr_t>(&s_min[s_R[v]]) & 2) * 8;
+      uint32_t old = *w;
+      for (;;) {
+        if (uint16_t(old >> sh) <= uint16_t(v)) break;
+        const uint32_t nw = (old & ~(0xFFFFu << sh)) | (uint32_t(v) << sh);
+        const uint32_t prev = atomicCAS(w, old, nw);
+        if (prev == old) break;
+        old = prev;
+      }
+    }
+  __syncthreads();
+  for (int v = tid; v < V; v += kThreads)
+    if (!s_blk[v]) {
+      s_R[v] = s_min[s_R[v]];
+      atomicMin(reinterpret_cast<unsigned long long *>(&s_key[s_R[v]]),
+                (unsigned long long)s_dot[v]);
+    }
+  __syncthreads();
+  sweep(V, s_ch, [&](int v) {
+    if (s_blk[v]) return false;
+    const uint16_t r = s_R[v], h = s_H[v];
+    uint32_t best = 0;
+    for (int e = s_off[v]; e < s_off[v + 1]; e++) {
+      const uint16_t y = s_dst[e];
+      if (s_H[y] == h && s_R[y] != r) best = max(best, s_D[s_R[y]] + 1);
+    }
+    return best > s_D[r] && atomicMax(&s_D[r], best) < best;
+  });
+  // 5. execution order: (H, depth, representative, dot rank); labels
+  uint64_t *ok = s_sd;  // the sorted dots are no longer needed: order keys
+  uint64_t lab[2];
+  for (int j = 0; j < 2; j++) {
+    const int v = tid + j * kThreads;
+    lab[j] = v < V && !s_blk[v] ? s_key[s_R[v]] : 0ull;
+  }
+  __syncthreads();
+  for (int v = tid; v < n2; v += kThreads) {
+    if (v < V && !s_blk[v])
+      ok[v] = (uint64_t(s_H[v]) << 33) | (uint64_t(s_D[s_R[v]]) << 22) |
+              (uint64_t(s_R[v]) << 11) | s_rank[v];
+    else
+      ok[v] = ~0ull;
+  }
+  for (int j = 0; j < 2; j++) {
+    const int v = tid + j * kThreads;
+    if (v < V) s_key[v] = lab[j];  // label per vertex
+  }
+  __syncthreads();
+  bitonic(ok, nullptr, n2);
+  uint32_t nexec = 0;
+  {
+    uint32_t mine = 0;
+    for (int v = tid; v < V; v += kThreads) mine += s_blk[v] ? 0u : 1u;
+    block_scan(mine, s_w, &nexec);
+  }
+  for (uint32_t i = tid; i < nexec; i += kThreads) {
+    const uint16_t v = s_sv[ok[i] & 0x7FF];
+    p.xdot[i] = s_dot[v];
+    p.xlab[i] = s_key[v];
+  }
+  for (int v = tid; v < V; v += kThreads) p.blocked[v] = s_blk[v];
+  // survivors, compacted in arrival order into the next vertex set
+  uint32_t kc[2] = {0, 0}, dc[2] = {0, 0}, kv[2] = {0, 0};
+  for (int j = 0; j < 2; j++) {
+    const int v = tid + j * kThreads;
+    if (v < V && s_blk[v]) {
+      kv[j] = 1;
+      kc[j] = p.koff[v + 1] - p.koff[v];
+      dc[j] = p.doff[v + 1] - p.doff[v];
+    }
+  }
+  uint32_t tv = 0, tk = 0, td = 0;
+  uint32_t ov = block_scan(kv[0] + kv[1], s_w, &tv);
+  uint32_t okk = block_scan(kc[0] + kc[1], s_w, &tk);
+  uint32_t od = block_scan(dc[0] + dc[1], s_w, &td);
+  for (int j = 0; j < 2; j++) {
+    const int v = tid + j * kThreads;
+    if (!kv[j]) continue;
+    p.ndot[ov] = s_dot[v];
+    p.nkoff[ov] = okk;
+    p.ndoff[ov] = od;
+    for (uint32_t e = p.koff[v]; e < p.koff[v + 1]; e++) p.nkey32[okk++] = p.key32[e];
+    for (uint32_t e = p.doff[v]; e < p.doff[v + 1]; e++) p.nddot[od++] = p.ddot[e];
+    ov++;
+  }
+  if (tid == 0) {
+    p.nkoff[tv] = tk;
+    p.ndoff[tv] = td;
+    p.header[0] = nexec;
+    p.header[1] = s_nmiss;
+    p.header[2] = s_err;
+    p.header[3] = tv;
+    p.header[4] = tk;
+    p.header[5] = td;
+  }
+}
+
+}  // namespace
+
+void launch_graph_small(const SmallPass &p, hipStream_t s) {
+  FH_CHECK(p.V >= 1 && p.V <= uint32_t(kSmallV), FH_EINVARIANT, "graph_small: vertex count");
+  k_graph_small<<<1, kThreads, 0, s>>>(p);
+}
+
+}  // namespace fh

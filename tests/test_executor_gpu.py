@@ -288,3 +288,55 @@ def test_kv_results_follow_the_oracle_order():
     # the store holds each key's last Put
     for k in np.nonzero(np.diff(kso))[0]:
         assert ex.store.execute(str(int(k)), KVOp.get()) == str(int(ks[kso[k + 1] - 1]))
+
+
+def test_small_pass_equals_general_pass():
+    """The one-launch small-graph pass (csrc/graph_small.hip, V <= 2048)
+    against the general pass (FH_GRAPH_SMALL=0, read once per process: child
+    processes) on the same shuffled C4-shaped stream in batches of 1, 5 and
+    300 with a held-back backlog: identical drained dots and SCC labels, in
+    the same order, and identical pending counts after every batch."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import json, sys
+import numpy as np
+sys.path.insert(0, {root!r})
+from fantoch_amd.engine import Engine
+from fantoch_amd.executor import HipGraphExecutor, GraphExecutionInfo
+from fantoch_amd.workload import Workload
+s = Workload.zipf(0.99, 512, k=1, views=3, window=64, seed=91).generate(6000)
+eng = Engine(s.key_space, n=5)
+eng.stage(s); eng.run()
+r = eng.results()
+rng = np.random.default_rng(5)
+order = [int(i) for i in np.argsort(np.arange(s.n) + rng.integers(0, 200, s.n), kind="stable")]
+order = order[:17] + order[18:] + [order[17]]  # one command held back: a backlog
+out = []
+for batch in (1, 5, 300):
+    ex = HipGraphExecutor(1, 0, 5, 1, key_space=s.key_space)
+    pend = []
+    for b0 in range(0, len(order), batch):
+        ex.handle_batch([GraphExecutionInfo.add(int(s.dots[j]), [int(s.keys[j, 0])],
+                         [int(x) for x in r["deps"][r["dep_off"][j]:r["dep_off"][j + 1]]])
+                         for j in order[b0:b0 + batch]])
+        pend.append(ex.pending())
+    seq = []
+    while True:
+        x = ex.to_clients()
+        if x is None:
+            break
+        seq.append(int(x.rifl))
+    out.append([seq, sorted(ex.last_labels.items()), pend])
+print(json.dumps(out))
+"""
+    res = []
+    for env in ({}, {"FH_GRAPH_SMALL": "0"}):
+        e = dict(os.environ, **env)
+        p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                           timeout=300, env=e)
+        assert p.returncode == 0, p.stdout + p.stderr
+        res.append(p.stdout.strip().splitlines()[-1])
+    assert res[0] == res[1]
