@@ -1299,6 +1299,9 @@ struct EngineDevice {
   DBuf<uint8_t> tailm;        // command-level views path: tail views per sorted command
   DBuf<uint64_t> cv64a, cv64b;  // command-level views path: packed sort values
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
+  // per batch: (seq bits, packed bits) of its dots, src << sb | seq (0: wider
+  // than 32 bits), so the per-key sort can move 4-byte dots
+  std::vector<std::pair<int, int>> h_dpack;
   bool deps_only = false;     // fh_engine_set_deps_only: stop after the committed deps
   bool codes_only = false;    // subset logs (fh_dgraph): stop after KeyDeps, codes in dep32
   bool last_deps_only = false;
@@ -1626,6 +1629,16 @@ struct EngineDevice {
              "replica views: command log exceeds 2^31 commands (32-bit dependency codes)");
     FH_HIP(hipMemcpyAsync(dot.get() + log_len, h_dot, n * nb * sizeof(uint64_t),
                           hipMemcpyHostToDevice, stream));
+    h_dpack.assign(nb, {0, 0});
+    for (size_t b = 0; b < nb; b++) {
+      uint64_t ms = 0, mq = 0;
+      for (size_t i = b * n; i < (b + 1) * n; i++) {
+        ms = std::max<uint64_t>(ms, h_dot[i] >> 56);
+        mq = std::max<uint64_t>(mq, h_dot[i] & 0x00FFFFFFFFFFFFFFull);
+      }
+      const int sb = bits_for(mq + 1), pb = sb + bits_for(ms + 1);
+      h_dpack[b] = pb <= 32 ? std::make_pair(sb, pb) : std::make_pair(0, 0);
+    }
     stage_base = log_len;
     log_len += n * nb;
     FH_HIP(hipMemcpyAsync(key32.ensure(nk * nb + 1), k32.data(), nk * nb * sizeof(uint32_t),
@@ -2039,6 +2052,10 @@ struct EngineDevice {
       gin.sorted_vid = svid;
     }
     gin.per_key_dots = true;
+    if (cursor >= 1 && cursor - 1 < h_dpack.size()) {
+      gin.dot_sb = h_dpack[cursor - 1].first;
+      gin.dot_pbits = h_dpack[cursor - 1].second;
+    }
     // the executed-clock stats ride on the per-key pass's dot reads
     unsigned long long *stt = srcstats.ensure(4 * 256);
     FH_HIP(hipMemsetAsync(stt + 256, 0, 512 * sizeof(unsigned long long), stream));

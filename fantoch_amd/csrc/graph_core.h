@@ -59,6 +59,9 @@ struct GraphInput {
   bool global_only = false;               // skip the tile path (fh_dgraph: rep + kap wanted)
   bool want_orders = true;                // false: SCCs, kappa and labels only (out.kap)
   bool per_key_dots = false;              // ... of dots (pk_dot) instead of vids
+  // dots packable as src << dot_sb | seq in dot_pbits <= 32 bits (0: not
+  // known / not packable): the per-key sort then moves 4-byte values
+  int dot_sb = 0, dot_pbits = 0;
   // optional: per-source (max seq, count) of the executed dots, accumulated
   // by a pass that reads every dot anyway (GraphOutput::src_stats_done)
   unsigned long long *src_mx = nullptr;   // [256]

@@ -797,12 +797,26 @@ __global__ void k_elem_fill(uint32_t n, const uint32_t *__restrict__ order, uint
   }
 }
 
+// dot of an element value: the whole u64, or (src, seq) packed into the
+// batch's bits (DotPack: src << sb | seq, when that fits 32 bits) so the
+// per-key sort moves 4-byte values
+struct DotWide {
+  __device__ uint64_t operator()(uint64_t d) const { return d; }
+};
+struct DotPack {
+  int sb;
+  __device__ uint32_t operator()(uint64_t d) const {
+    return uint32_t(((d >> 56) << sb) | (d & 0x00FFFFFFFFFFFFFFull));
+  }
+};
+
 // one key per command: the element of exec position j is (key, dot) of
 // order[j] (the gather follows the execution order, close to arrival order)
+template <class P, class VD>
 __global__ void __launch_bounds__(256)
     k_elem_fill_dots(uint32_t n, uint32_t k, const uint32_t *__restrict__ order,
-                     const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot,
-                     uint32_t *__restrict__ ek, uint64_t *__restrict__ ed,
+                     const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot, P pack,
+                     uint32_t *__restrict__ ek, VD *__restrict__ ed,
                      unsigned long long *__restrict__ src_mx, unsigned int *__restrict__ src_cnt) {
   __shared__ unsigned long long s_mx[256];
   __shared__ unsigned int s_cnt[256];
@@ -812,9 +826,10 @@ __global__ void __launch_bounds__(256)
   GRID_STRIDE(j, n) {
     const uint32_t v = order[j];
     const uint64_t d = dot[v];
+    const VD pd = pack(d);
     for (uint32_t s = 0; s < k; s++) {
       ek[size_t(j) * k + s] = key32[size_t(v) * k + s];
-      ed[size_t(j) * k + s] = d;
+      ed[size_t(j) * k + s] = pd;
     }
     if (src_mx) acc.add(d);
   }
@@ -824,12 +839,13 @@ __global__ void __launch_bounds__(256)
 // the same from the tile kernel's groups, one thread per vertex: its rank
 // r = start[H] + rank in group is written, and (key, dot) go to element r
 // (r stays within the reach bound of v, so the writes stay coalesced)
+template <class P, class VD>
 __global__ void __launch_bounds__(256)
     k_exec_fill_dots(uint32_t n, uint32_t k, const uint32_t *__restrict__ hgrp,
                      const uint32_t *__restrict__ grank, const uint32_t *__restrict__ gstart,
-                     const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot,
+                     const uint32_t *__restrict__ key32, const uint64_t *__restrict__ dot, P pack,
                      uint32_t *__restrict__ rank, uint32_t *__restrict__ ek,
-                     uint64_t *__restrict__ ed, unsigned long long *__restrict__ src_mx,
+                     VD *__restrict__ ed, unsigned long long *__restrict__ src_mx,
                      unsigned int *__restrict__ src_cnt) {
   __shared__ unsigned long long s_mx[256];
   __shared__ unsigned int s_cnt[256];
@@ -840,13 +856,24 @@ __global__ void __launch_bounds__(256)
     const uint32_t r = gstart[hgrp[v]] + grank[v];
     rank[v] = r;
     const uint64_t d = dot[v];
+    const VD pd = pack(d);
     for (uint32_t s = 0; s < k; s++) {
       ek[size_t(r) * k + s] = key32[size_t(v) * k + s];
-      ed[size_t(r) * k + s] = d;
+      ed[size_t(r) * k + s] = pd;
     }
     if (src_mx) acc.add(d);
   }
   if (src_mx) acc.commit(src_mx, src_cnt);  // (src_mx is uniform)
+}
+
+// packed dots back to u64 after the per-key sort
+__global__ void k_unpack_dots(uint32_t n, const uint32_t *__restrict__ pd, int sb,
+                              uint64_t *__restrict__ out) {
+  const uint32_t m = (1u << sb) - 1;
+  GRID_STRIDE(j, n) {
+    const uint32_t x = pd[j];
+    out[j] = (uint64_t(x >> sb) << 56) | (x & m);
+  }
 }
 
 __global__ void k_copy_dot(uint32_t V, const uint64_t *__restrict__ dot, uint64_t *__restrict__ out) {
@@ -970,8 +997,7 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
   const uint32_t V = in.V;
   FH_HIP(hipMemsetAsync(kap.get(), 0, size_t(V) * sizeof(uint64_t), stream));
   FH_HIP(hipMemsetAsync(kraise.ensure(V + 1), 0, size_t(V) * sizeof(uint32_t), stream));
-  static const bool no_hseed = getenv("FH_NO_HSEED") != nullptr;
-  const bool seeded = hseed_ok && !no_hseed;
+  const bool seeded = hseed_ok;
   k_kap_init<<<agg_blocks(V), B, 0, stream>>>(V, blocked.get(), rep.get(),
                                               seeded ? hseed.get() : nullptr,
                                               kap.get());
@@ -1246,20 +1272,42 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
     const uint32_t ne = nexec * in.k;
     uint32_t *ek = tmp32a.ensure(ne + 1), *k2 = flags.ensure(ne + 1);
     uint64_t *ed = pk_da.ensure(ne + 1), *d2 = pk_db.ensure(ne + 1);
-    if (fill_from_groups) {
-      fill_from_groups = false;
-      k_exec_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(
-          nexec, in.k, t_h.get(), t_rank.get(), t_start.get(), in.key32, in.dot, out.exec_rank,
-          ek, ed, in.src_mx, in.src_cnt);
-    } else {
-      k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, in.k, ord, in.key32, in.dot,
-                                                             ek, ed, in.src_mx, in.src_cnt);
-    }
-    out.src_stats_done = in.src_mx != nullptr;
     uint32_t *ko = nullptr;
     uint64_t *dout = nullptr;
-    sort_pairs<uint32_t, uint64_t>(ek, ed, k2, d2, ek, ed, ne, in.key_bits, sort_ws, stream,
-                                   &ko, &dout);
+    const bool packed = in.dot_pbits > 0 && in.dot_pbits <= 32;
+    if (packed) {
+      // 4-byte packed dots through the sort (its buffers inside pk_db, whose
+      // ne + 1 u64 hold both), unpacked into pk_da at the end
+      uint32_t *pa = reinterpret_cast<uint32_t *>(d2), *pb = pa + (ne + 1);
+      const DotPack pk{in.dot_sb};
+      if (fill_from_groups) {
+        k_exec_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(
+            nexec, in.k, t_h.get(), t_rank.get(), t_start.get(), in.key32, in.dot, pk,
+            out.exec_rank, ek, pa, in.src_mx, in.src_cnt);
+      } else {
+        k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, in.k, ord, in.key32, in.dot, pk,
+                                                               ek, pa, in.src_mx, in.src_cnt);
+      }
+      uint32_t *po = nullptr;
+      sort_pairs<uint32_t, uint32_t>(ek, pa, k2, pb, ek, pa, ne, in.key_bits, sort_ws, stream, &ko,
+                                     &po);
+      k_unpack_dots<<<grid_for(ne, B), B, 0, stream>>>(ne, po, in.dot_sb, ed);
+      dout = ed;
+    } else {
+      if (fill_from_groups) {
+        k_exec_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(
+            nexec, in.k, t_h.get(), t_rank.get(), t_start.get(), in.key32, in.dot, DotWide{},
+            out.exec_rank, ek, ed, in.src_mx, in.src_cnt);
+      } else {
+        k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, in.k, ord, in.key32, in.dot,
+                                                               DotWide{}, ek, ed, in.src_mx,
+                                                               in.src_cnt);
+      }
+      sort_pairs<uint32_t, uint64_t>(ek, ed, k2, d2, ek, ed, ne, in.key_bits, sort_ws, stream,
+                                     &ko, &dout);
+    }
+    fill_from_groups = false;
+    out.src_stats_done = in.src_mx != nullptr;
     out.pk_key = ko;
     out.pk_vid = nullptr;
     out.pk_dot = dout;
@@ -1363,8 +1411,7 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   // same shape (C5: a 1.2M-member SCC) goes there directly, without the
   // bounded kappa run and the restricted attempt (their only product here
   // would be the coloring's seed, worth less than the 3 relax passes)
-  static const char *pf_env = getenv("FH_PREFER_FULL");  // 0 = never, 1 = always
-  const bool direct_full = pf_env ? *pf_env == '1' : prefer_full;
+  const bool direct_full = prefer_full;
   bool ok = false;
   dbg_cand = dbg_restricted = 0;
   if (direct_full) {
@@ -1384,8 +1431,7 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     // first the vertices still being raised (the missed cycles are among
     // them), certified by a bounded kappa run; if a cycle is left, the exact
     // coloring over every vertex
-    static const bool full_only = getenv("FH_FB_FULL") != nullptr;
-    if (!full_only && coloring_fallback(in, 1)) ok = order_kappa(in, give_up, iters, true);
+    if (coloring_fallback(in, 1)) ok = order_kappa(in, give_up, iters, true);
     if (!ok) {
       coloring_fallback(in, 0);
       ok = order_kappa(in, 1u << 30, iters);

@@ -52,15 +52,7 @@ constexpr int kTileThreads = 1024;
 constexpr int kTileC = 10240;  // max context vertices (LDS: 15 B per vertex)
 constexpr uint16_t kNone = 0xFFFF;
 constexpr int kMaxCore = 8;     // core vertices per thread (T <= 8192)
-constexpr uint32_t kMixR1 = 512;  // pass-1 reach bound of the mixed tiling (FH_TILE_R1)
-static uint32_t mix_r1() {
-  static const uint32_t r = [] {
-    const char *e = getenv("FH_TILE_R1");
-    const uint32_t v = e ? uint32_t(atoi(e)) : kMixR1;
-    return v >= 256 && v <= 1024 && v % 64 == 0 ? v : kMixR1;
-  }();
-  return r;
-}
+constexpr uint32_t kMixR1 = 512;  // pass-1 reach bound of the mixed tiling
 
 // R0 rounded up to a multiple of 64 (at least 256)
 static uint32_t round_r0(uint32_t x) { return std::max<uint32_t>(256, (x + 63) & ~63u); }
@@ -153,11 +145,6 @@ struct TileOut {
   unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
   int r0;      // certified reach bound R0 (L = 2·R0)
   int core;    // core vertices per tile T (T + 2L <= kTileC, T <= kMaxCore·1024)
-  int batch_load;  // 1: the load phase issues all of a thread's edge loads first
-  int hblock;  // H sweeps: 1 = each wave walks a contiguous block in ascending
-               // steps of 64 (updates of a block's earlier vertices are seen by
-               // its later ones in the same sweep), 2 = the same in batches of
-               // 5 vertices per lane (loads first), 0 = block-strided
 };
 
 namespace {
@@ -210,46 +197,18 @@ __global__ void __launch_bounds__(kTileThreads)
   }
 
   // 1. context edges; certificate part 2: forward spans of core vertices
-  // (batch_load: every edge load of the thread issued before the first is
-  // used)
   uint32_t nlong = 0;
-  if (!out.batch_load) {
-    for (int x = tid; x < C; x += kTileThreads) {
-      const uint32_t v = lo + x;
+  for (int x = tid; x < C; x += kTileThreads) {
+    const uint32_t v = lo + x;
 #pragma unroll
-      for (int s = 0; s < S; s++) {
-        const uint32_t u = dst[size_t(v) * S + s];
-        uint16_t l = kNone;
-        if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
-        if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
-        eL[s][x] = l;
-      }
-      sH[x] = uint16_t(x);
+    for (int s = 0; s < S; s++) {
+      const uint32_t u = dst[size_t(v) * S + s];
+      uint16_t l = kNone;
+      if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
+      if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
+      eL[s][x] = l;
     }
-  } else {
-    constexpr int kLd = kTileC / kTileThreads;
-    uint32_t uu[kLd][S];
-#pragma unroll
-    for (int i = 0; i < kLd; i++) {
-      const int x = tid + i * kTileThreads;
-#pragma unroll
-      for (int s = 0; s < S; s++) uu[i][s] = x < C ? dst[size_t(lo + x) * S + s] : 0u;
-    }
-#pragma unroll
-    for (int i = 0; i < kLd; i++) {
-      const int x = tid + i * kTileThreads;
-      if (x >= C) break;
-      const uint32_t v = lo + x;
-#pragma unroll
-      for (int s = 0; s < S; s++) {
-        const uint32_t u = uu[i][s];
-        uint16_t l = kNone;
-        if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
-        if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
-        eL[s][x] = l;
-      }
-      sH[x] = uint16_t(x);
-    }
+    sH[x] = uint16_t(x);
   }
   __syncthreads();
   phase(0);
@@ -277,62 +236,9 @@ __global__ void __launch_bounds__(kTileThreads)
   // vertex x reaches, so H(H(x)) is reachable too: pointer jumping collapses
   // chains of forward dependencies in logarithmically many sweeps.
   const int hP = 64 * ((C + kTileThreads - 1) / kTileThreads);  // per-wave block
-  // hblock 2: each wave walks its block kHB vertices per lane at a time, all
-  // loads of a batch issued before any store (one dependent LDS round trip
-  // chain per batch instead of per vertex).  Measured on C4: no faster per
-  // sweep (2.65 vs 2.53 us: the sweep is bound by LDS bank conflicts of the
-  // random sH[y] reads, not by latency) and one sweep more (less in-sweep
-  // propagation), so hblock 1 stays the default.
-  auto h_sweeps_batched = [&]() {
-    constexpr int kHB = 5;
-    const int w = tid >> 6, lane = tid & 63, nk = hP / 64;
-    int it = 0;
-    for (;; it++) {
-      bool ch = false;
-      for (int k0 = 0; k0 < nk; k0 += kHB) {
-        int xs[kHB];
-        uint32_t h[kHB], h0[kHB];
-        uint16_t ys[kHB][S];
-#pragma unroll
-        for (int u = 0; u < kHB; u++) {
-          const int x = w * hP + (k0 + u) * 64 + lane;
-          xs[u] = (k0 + u < nk && x < C) ? x : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < kHB; u++) {
-          h0[u] = xs[u] >= 0 ? uint32_t(sH[xs[u]]) : 0u;
-#pragma unroll
-          for (int q = 0; q < S; q++) ys[u][q] = xs[u] >= 0 ? eL[q][xs[u]] : kNone;
-        }
-#pragma unroll
-        for (int u = 0; u < kHB; u++) {
-          h[u] = h0[u];
-#pragma unroll
-          for (int q = 0; q < S; q++)
-            if (ys[u][q] != kNone) h[u] = max(h[u], uint32_t(sH[ys[u][q]]));
-        }
-#pragma unroll
-        for (int u = 0; u < kHB; u++)
-          if (xs[u] >= 0) h[u] = max(h[u], uint32_t(sH[h[u]]));
-#pragma unroll
-        for (int u = 0; u < kHB; u++)
-          if (xs[u] >= 0 && h[u] > h0[u]) {
-            sH[xs[u]] = uint16_t(h[u]);
-            ch = true;
-          }
-      }
-      if (ch) s_ch[it % 3] = 1;
-      if (tid == 0) s_ch[(it + 1) % 3] = 0;
-      __syncthreads();
-      if (!s_ch[it % 3]) break;
-    }
-    __syncthreads();
-    if (tid < 3) s_ch[tid] = 0;
-    __syncthreads();
-    return it + 1;
-  };
-  // hblock 1 (default) with each thread's vertices' context edges and own H
-  // in registers: the thread owning x is the only writer of sH[x], so its
+  // Each wave walks a contiguous block in ascending steps of 64 (updates of a
+  // block's earlier vertices are seen by its later ones in the same sweep),
+  // with each thread's vertices' context edges and own H in registers: the thread owning x is the only writer of sH[x], so its
   // register copy stays exact, and a sweep's LDS traffic is the random
   // sH[y] / sH[H] reads alone (the edge rows and own H were conflict-free
   // re-reads of the same words every sweep)
@@ -377,26 +283,7 @@ __global__ void __launch_bounds__(kTileThreads)
     __syncthreads();
     return it + 1;
   };
-  const int hs = out.hblock == 2 ? h_sweeps_batched() : out.hblock == 1 ? h_sweeps_regs() : sweeps(
-      [&](int i) {
-        const int x = out.hblock ? ((i & (kTileThreads - 1)) >> 6) * hP + (i >> 10) * 64 + (i & 63)
-                                 : i;
-        if (x >= C) return false;
-        uint32_t h = sH[x];
-        const uint32_t h0 = h;
-#pragma unroll
-        for (int s = 0; s < S; s++) {
-          const uint16_t y = eL[s][x];
-          if (y != kNone) h = max(h, uint32_t(sH[y]));
-        }
-        h = max(h, uint32_t(sH[h]));
-        if (h > h0) {
-          sH[x] = uint16_t(h);
-          return true;
-        }
-        return false;
-      },
-      out.hblock ? (kTileThreads / 64) * hP : C, nullptr);
+  const int hs = h_sweeps_regs();
   phase(1);
 
   // 3. certificate part 1: core excess < R0
@@ -768,7 +655,7 @@ static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint
 // only certified cores; pass 2 overwrites its cores.
 bool GraphCore::tiles_mixed(const GraphInput &in, TileOut &to, uint32_t r2, uint32_t *st) {
   const uint32_t V = in.V;
-  const uint32_t r1 = mix_r1();
+  const uint32_t r1 = kMixR1;
   uint32_t *stat = to.stat;
   to.r0 = int(r1);
   to.core = std::min(kTileC - 4 * int(r1), kMaxCore * kTileThreads);
@@ -841,12 +728,6 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.redo = nullptr;
   to.cores = nullptr;
   to.failf = nullptr;
-  static const int hblock = getenv("FH_TILE_HBLOCK") ? atoi(getenv("FH_TILE_HBLOCK")) : 1;
-  to.hblock = hblock;
-  // FH_TILE_BATCH_LOAD=1: measured slower on C4 (2610 against 2529 us per
-  // launch: the 30 live loads cost more than the round trips they overlap)
-  static const int batch_load = getenv("FH_TILE_BATCH_LOAD") ? atoi(getenv("FH_TILE_BATCH_LOAD")) : 0;
-  to.batch_load = batch_load;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   to.prof = nullptr;
   if (debug) {
@@ -860,23 +741,18 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   // R0 = 2048, then the global path.
   bool ok = false;
   uint32_t st[7] = {0, 0, 0, 0, 0, 0, 0};
-  static const uint32_t r0_env = getenv("FH_TILE_R0") ? uint32_t(atoi(getenv("FH_TILE_R0"))) : 0;
-  uint32_t r0 = r0_env ? round_r0(r0_env) : tile_r0;  // (env: first bound, measurement)
-  // mixed bounds (FH_TILE_MIXED=0: off): when the last run needed a bound
-  // above kMixR1, every tile first runs at kMixR1 (longer cores) and only the
-  // failed tiles and their neighbours run again at the larger bound
-  static const bool mixed_on = [] {
-    const char *e = getenv("FH_TILE_MIXED");
-    return !(e && *e == '0');
-  }();
-  if (mixed_on && !r0_env && tile_r0 > mix_r1()) {
+  uint32_t r0 = tile_r0;
+  // mixed bounds: when the last run needed a bound above kMixR1, every tile
+  // first runs at kMixR1 (longer cores) and only the failed tiles and their
+  // neighbours run again at the larger bound
+  if (tile_r0 > kMixR1) {
     dbg_mixed_redo = 0;
     ok = tiles_mixed(in, to, tile_r0, st);
     if (debug)
       fprintf(stderr,
               "fh graph_tile mixed: V=%u R1=%u R2=%u redo_cores=%u ok=%d max_excess=%u "
               "max_sweeps=%u max_rounds=%u max_group=%u\n",
-              V, mix_r1(), uint32_t(to.r0), dbg_mixed_redo, int(ok), st[1], st[4], st[5], st[6]);
+              V, kMixR1, uint32_t(to.r0), dbg_mixed_redo, int(ok), st[1], st[4], st[5], st[6]);
   }
   for (int attempt = 0; attempt < 4 && !ok; attempt++) {
     to.r0 = int(r0);
@@ -940,8 +816,7 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
 }
 
 bool GraphCore::tiles_eligible(const GraphInput &in) const {
-  return !in.off && !in.blocked0 && in.stride >= 2 && in.stride <= 3 && in.V >= 1 &&
-         !getenv("FH_NO_TILES");
+  return !in.off && !in.blocked0 && in.stride >= 2 && in.stride <= 3 && in.V >= 1;
 }
 
 }  // namespace fh

@@ -3,7 +3,5 @@
 set -e
 cd "$(dirname "$0")/.."
 python -m fantoch_amd.build
-/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ifantoch_amd/csrc \
-  tools/sortbench.hip -o tools/sortbench -Lfantoch_amd -lfantoch_hip -Wl,-rpath,'$ORIGIN/../fantoch_amd'
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 tools/pmc_calib.hip -o tools/pmc_calib
 /opt/rocm/bin/hipcc -O3 -std=c++17 -Iinclude tools/stream_bench.cpp -o tools/stream_bench -Lfantoch_amd -lfantoch_hip -Wl,-rpath,'$ORIGIN/../fantoch_amd'
