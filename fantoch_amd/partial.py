@@ -24,6 +24,10 @@ per-key sequences are its keys' commands in stream order.
 The stages are injectable (`keydeps`, `union`) so the world-size-2 CPU test
 can run the exchange with the oracle standing in for the GPU stages; the
 defaults are the HIP ones and fail loudly without the library.
+
+This is the single-view KeyDeps drop-in for partial replication (SURVEY §8
+a8).  The C5 pipeline with replica views, SCCs and per-key order across GPUs
+is fantoch_amd.dgraph (csrc/dgraph.hip).
 """
 from __future__ import annotations
 
@@ -233,211 +237,3 @@ class PartialShard:
         pos = np.searchsorted(owned, g_cmd)
         dep_off, dep_set = self.union(len(owned), pos, g_dep)
         return owned, dep_off, dep_set
-
-
-# ------------------------------------------------- full pipeline over ranks
-# Partial replication with replica views (config C5 across GPUs): every rank
-# is a key shard and produces the per-key execution sequences of its keys.
-#
-#   1. KeyDeps      -- the shard's replicas run SequentialKeyDeps over the
-#      command's owned keys only (Command::keys(shard), command.rs:95-100),
-#      in their arrival order.  Each owned (command, key) pair is staged as a
-#      single-key pseudo command (unique pseudo dot, the real command's
-#      arrivals), so the fused engine runs unchanged in deps-only mode: the
-#      deps of a key do not depend on the command's other keys, and the
-#      union over a command's pairs, views and shards is the command's
-#      committed dep set (plain union, quorum.rs:28-98 / atlas.rs:580-583).
-#   2. exchange     -- (command, dep) records to the command's owner (the
-#      shard of its first key): one all-to-all.
-#   3. union        -- the owner merges them (fh_dep_union).
-#   4. graph        -- the committed dep rows are all-gathered, and every
-#      rank orders the whole graph (SCCs, execution order).  With cross-shard
-#      commands on every key, a shard's closure is nearly the whole stream
-#      (C5: a 1.19M-member SCC spanning all shards), so the graph exchange is
-#      the whole edge set; the reference reaches the same vertices one request
-#      at a time (executor/graph/mod.rs:279-408).
-#   5. per-key      -- each rank cuts the sequences of its own keys out of the
-#      execution order.
-
-PSEUDO_SOURCE = 1
-
-
-def pseudo_stream(s, rank: int, world: int):
-    """The shard's KeyDeps input (stage 1) from a Stream with replica logs:
-    (pseudo Stream of k = 1 commands over local key ids, pseudo -> command
-    index).  Pseudo p has dot (PSEUDO_SOURCE, p + 1); replica r's log lists a
-    command's pseudo commands where it lists the command."""
-    from .workload import Stream
-
-    if s.log_cmd is None or s.log_off is None:
-        raise ValueError("pseudo_stream: the stream needs its replica logs (generate(logs=True))")
-    fq = s.views
-    mine = s.keys % np.uint64(world) == np.uint64(rank)
-    c, t = np.nonzero(mine)  # command order, then key slot order
-    p2c = c.astype(np.int64)
-    npair = len(p2c)
-    pkeys = (s.keys[c, t] // np.uint64(world)).astype(np.uint64).reshape(-1, 1)
-    pdots = (np.uint64(PSEUDO_SOURCE) << np.uint64(56)) | np.arange(1, npair + 1, dtype=np.uint64)
-    cnt = np.bincount(p2c, minlength=s.n).astype(np.int64)
-    first = np.zeros(s.n + 1, dtype=np.int64)
-    np.cumsum(cnt, out=first[1:])
-    cmd = s.log_cmd.astype(np.int64)  # replica logs list command indices
-    reps = cnt[cmd]
-    ends = np.cumsum(reps)
-    within = np.arange(int(ends[-1]) if len(ends) else 0, dtype=np.int64) - np.repeat(ends - reps, reps)
-    plog = (first[np.repeat(cmd, reps)] + within).astype(np.uint32)
-    cum = np.concatenate([[0], ends]).astype(np.uint64)
-    plo = cum[s.log_off.astype(np.int64)]
-    key_space = (s.key_space + world - 1) // world
-    fq_proc = None if s.fq_proc is None else s.fq_proc[p2c]
-    fq_time = None if s.fq_time is None else s.fq_time[p2c]
-    ps = Stream(pdots, pkeys, fq_proc, fq_time, key_space, log_off=plo, log_cmd=plog,
-                views_n=fq)
-    return ps, p2c
-
-
-def pseudo_records(p2c, dots, dep_off, deps):
-    """Stage-1 output in pseudo dots -> (command index, real dep dot) records."""
-    dep_off = np.asarray(dep_off, dtype=np.int64)
-    per = np.diff(dep_off)
-    rec_cmd = np.repeat(p2c, per)
-    p = (np.asarray(deps, dtype=np.uint64) & np.uint64((1 << 56) - 1)).astype(np.int64) - 1
-    return rec_cmd, dots[p2c[p]]
-
-
-def hip_views_keydeps(device: int = -1, nproc: int = 5):
-    """Stage 1 on the GPU: the fused engine in deps-only mode over a pseudo
-    stream -> (dep_off, deps) in pseudo dots."""
-    from .engine import Engine
-
-    def run(ps):
-        eng = Engine(ps.key_space, n=nproc, device=device)
-        try:
-            eng.set_deps_only(True)
-            eng.stage_logs([ps], nproc=nproc)
-            eng.run()
-            return eng.deps()
-        finally:
-            eng.close()
-
-    return run
-
-
-def hip_order(device: int = -1):
-    """Stage 4 on the GPU: the graph executor (fh_graph) over a whole
-    committed graph -> (execution-ordered dots, SCC label per command)."""
-    from .keydeps import make_config
-
-    lib = L.load()
-
-    def run(dots, dep_off, deps):
-        n = len(dots)
-        cfg = make_config(n=1, f=0, device=device, key_space=1)
-        h = C.c_void_p()
-        L.check(lib.fh_graph_create(1, 0, C.byref(cfg), C.byref(h)))
-        try:
-            d = np.ascontiguousarray(dots, dtype=np.uint64)
-            ko = np.zeros(n + 1, dtype=np.uint32)
-            do = np.ascontiguousarray(dep_off, dtype=np.uint32)
-            dp = np.ascontiguousarray(deps, dtype=np.uint64)
-            L.check(lib.fh_graph_add_batch(h, n, L.ptr(d), L.ptr(ko), None, L.ptr(do),
-                                           L.ptr(dp) if len(dp) else None))
-            ex = np.zeros(max(1, n), dtype=np.uint64)
-            lab = np.zeros(max(1, n), dtype=np.uint64)
-            ln = C.c_size_t(0)
-            L.check(lib.fh_graph_drain(h, L.ptr(ex), L.ptr(lab), len(ex), C.byref(ln)))
-            if ln.value != n:
-                raise L.FhError(L.FH_EINVARIANT, f"graph left {n - ln.value} commands pending")
-        finally:
-            lib.fh_graph_destroy(h)
-        pos = np.searchsorted(dots, ex[:n], sorter=np.argsort(dots, kind="stable"))
-        order = np.argsort(dots, kind="stable")[pos]
-        label = np.zeros(n, dtype=np.uint64)
-        label[order] = lab[:n]
-        return ex[:n], label
-
-    return run
-
-
-def _allgather_rows(group, owned, dep_off, deps, n: int):
-    """Every rank's owned rows -> the whole committed CSR (command order)."""
-    import torch
-    import torch.distributed as dist
-
-    world = dist.get_world_size(group)
-    on_gpu = dist.get_backend(group) == "nccl"
-    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
-    cnt = np.diff(np.asarray(dep_off, dtype=np.int64))
-    mine = np.stack([np.asarray(owned, np.int64), cnt], 1) if len(owned) else np.zeros((0, 2), np.int64)
-    payload = [mine.reshape(-1), np.asarray(deps, dtype=np.uint64).view(np.int64)]
-    out = []
-    for arr in payload:
-        sz = torch.tensor([len(arr)], dtype=torch.int64, device=dev)
-        sizes = [torch.zeros_like(sz) for _ in range(world)]
-        dist.all_gather(sizes, sz, group=group)
-        sizes = [int(x.item()) for x in sizes]
-        mx = max(1, max(sizes))
-        buf = torch.zeros(mx, dtype=torch.int64, device=dev)
-        buf[:len(arr)] = torch.from_numpy(arr).to(dev)
-        bufs = [torch.zeros_like(buf) for _ in range(world)]
-        dist.all_gather(bufs, buf, group=group)
-        out.append([b[:sz_].cpu().numpy() for b, sz_ in zip(bufs, sizes)])
-    rows = np.concatenate([r.reshape(-1, 2) for r in out[0]])
-    dep_all = np.concatenate(out[1]).view(np.uint64)
-    counts = np.zeros(n, dtype=np.int64)
-    counts[rows[:, 0]] = rows[:, 1]
-    off = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(counts, out=off[1:])
-    # the gathered deps are row blocks in (rank, owned command) order
-    starts = np.repeat(off[rows[:, 0]], rows[:, 1])
-    within = np.arange(len(dep_all)) - np.repeat(np.cumsum(rows[:, 1]) - rows[:, 1], rows[:, 1])
-    full = np.zeros(len(dep_all), dtype=np.uint64)
-    full[starts + within] = dep_all
-    return off.astype(np.uint32), full
-
-
-class PartialPipeline:
-    """One rank (one GPU) of the partial-replication pipeline above.
-
-    Stages are injectable so the world-size-2 CPU test runs the exchange
-    logic with the oracle in place of the GPU stages:
-      keydeps(pseudo_stream) -> (dep_off, deps in pseudo dots)
-      union(n_cmd, cmd, dep) -> (dep_off, deps)
-      order(dots, dep_off, deps) -> (execution-ordered dots, label per command)
-    The defaults are the HIP stages and fail loudly without the library."""
-
-    def __init__(self, rank: int, world: int, group=None, device: int = -1,
-                 keydeps: Optional[Callable] = None, union: Optional[Callable] = None,
-                 order: Optional[Callable] = None, nproc: int = 5):
-        self.rank, self.world, self.group = rank, world, group
-        self.keydeps = keydeps if keydeps is not None else hip_views_keydeps(device, nproc)
-        self.union = union if union is not None else hip_union(device)
-        self.order = order if order is not None else hip_order(device)
-
-    def run(self, s):
-        """One stream with replica logs (every rank holds the same stream).
-        Returns a dict: committed deps of the whole stream (dep_off, deps),
-        the SCC label of every command, and this shard's per-key sequences
-        {global key: [dots in execution order]}."""
-        ps, p2c = pseudo_stream(s, self.rank, self.world)
-        pofs, pdeps = self.keydeps(ps)
-        rec_cmd, rec_dep = pseudo_records(p2c, s.dots, pofs, pdeps)
-        owner = command_owner(s.keys, self.world)
-        g_cmd, g_dep = exchange_records(self.group, self.world, owner[rec_cmd], rec_cmd, rec_dep)
-        owned = np.nonzero(owner == self.rank)[0]
-        pos = np.searchsorted(owned, g_cmd)
-        odo, odeps = self.union(len(owned), pos, g_dep)
-        dep_off, deps = _allgather_rows(self.group, owned, odo, odeps, s.n)
-        ex, label = self.order(s.dots, dep_off, deps)
-        # this shard's per-key sequences, cut out of the execution order
-        rank_of = np.empty(s.n, dtype=np.int64)
-        srt = np.argsort(s.dots, kind="stable")
-        rank_of[srt[np.searchsorted(s.dots, ex, sorter=srt)]] = np.arange(s.n)
-        mine = s.keys % np.uint64(self.world) == np.uint64(self.rank)
-        c, t = np.nonzero(mine)
-        key = s.keys[c, t]
-        o = np.lexsort((rank_of[c], key))
-        seq = {}
-        for kk, dd in zip(key[o].tolist(), s.dots[c[o]].tolist()):
-            seq.setdefault(kk, []).append(dd)
-        return {"dep_off": dep_off, "deps": deps, "scc_label": label, "key_seq": seq}
