@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(kThreads)
   // 2. resolve: count, scan, fill
   uint32_t cnt[2] = {0, 0};
   for (int j = 0; j < 2; j++) {
-    const int v = tid + j * kThreads;
+    const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     if (v >= V) continue;
     bool missing = false;
     const uint64_t self = s_dot[v];
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(kThreads)
   {
     uint32_t o = o0;
     for (int j = 0; j < 2; j++) {
-      const int v = tid + j * kThreads;
+      const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
       if (v >= V) continue;
       s_off[v] = uint16_t(o);
       const uint64_t self = s_dot[v];
@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(kThreads)
   uint64_t *ok = s_sd;  // the sorted dots are no longer needed: order keys
   uint64_t lab[2];
   for (int j = 0; j < 2; j++) {
-    const int v = tid + j * kThreads;
+    const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     lab[j] = v < V && !s_blk[v] ? s_key[s_R[v]] : 0ull;
   }
   __syncthreads();
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(kThreads)
       ok[v] = ~0ull;
   }
   for (int j = 0; j < 2; j++) {
-    const int v = tid + j * kThreads;
+    const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     if (v < V) s_key[v] = lab[j];  // label per vertex
   }
   __syncthreads();
@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(kThreads)
   // survivors, compacted in arrival order into the next vertex set
   uint32_t kc[2] = {0, 0}, dc[2] = {0, 0}, kv[2] = {0, 0};
   for (int j = 0; j < 2; j++) {
-    const int v = tid + j * kThreads;
+    const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     if (v < V && s_blk[v]) {
       kv[j] = 1;
       kc[j] = p.koff[v + 1] - p.koff[v];
@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(kThreads)
   uint32_t okk = block_scan(kc[0] + kc[1], s_w, &tk);
   uint32_t od = block_scan(dc[0] + dc[1], s_w, &td);
   for (int j = 0; j < 2; j++) {
-    const int v = tid + j * kThreads;
+    const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     if (!kv[j]) continue;
     p.ndot[ov] = s_dot[v];
     p.nkoff[ov] = okk;

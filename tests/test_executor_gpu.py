@@ -2,6 +2,7 @@
 reference's known-answer tests (executor/graph/mod.rs:716-1350) and against
 the oracle's incremental DependencyGraph on shuffled arrival orders."""
 import itertools
+import json
 import random
 
 import numpy as np
@@ -293,9 +294,11 @@ def test_kv_results_follow_the_oracle_order():
 def test_small_pass_equals_general_pass():
     """The one-launch small-graph pass (csrc/graph_small.hip, V <= 2048)
     against the general pass (FH_GRAPH_SMALL=0, read once per process: child
-    processes) on the same shuffled C4-shaped stream in batches of 1, 5 and
-    300 with a held-back backlog: identical drained dots and SCC labels, in
-    the same order, and identical pending counts after every batch."""
+    processes) on shuffled streams in batches of 1, 5 and 300 with a held-back
+    backlog: identical drained dots and SCC labels, in the same order, and
+    identical pending counts after every batch.  The 2-key stream keeps more
+    than 1024 commands pending, so passes with 1024 < V <= 2048 (two vertices
+    per thread) run small."""
     import os
     import subprocess
     import sys
@@ -307,29 +310,30 @@ sys.path.insert(0, {root!r})
 from fantoch_amd.engine import Engine
 from fantoch_amd.executor import HipGraphExecutor, GraphExecutionInfo
 from fantoch_amd.workload import Workload
-s = Workload.zipf(0.99, 512, k=1, views=3, window=64, seed=91).generate(6000)
-eng = Engine(s.key_space, n=5)
-eng.stage(s); eng.run()
-r = eng.results()
-rng = np.random.default_rng(5)
-order = [int(i) for i in np.argsort(np.arange(s.n) + rng.integers(0, 200, s.n), kind="stable")]
-order = order[:17] + order[18:] + [order[17]]  # one command held back: a backlog
 out = []
-for batch in (1, 5, 300):
-    ex = HipGraphExecutor(1, 0, 5, 1, key_space=s.key_space)
-    pend = []
-    for b0 in range(0, len(order), batch):
-        ex.handle_batch([GraphExecutionInfo.add(int(s.dots[j]), [int(s.keys[j, 0])],
-                         [int(x) for x in r["deps"][r["dep_off"][j]:r["dep_off"][j + 1]]])
-                         for j in order[b0:b0 + batch]])
-        pend.append(ex.pending())
-    seq = []
-    while True:
-        x = ex.to_clients()
-        if x is None:
-            break
-        seq.append(int(x.rifl))
-    out.append([seq, sorted(ex.last_labels.items()), pend])
+for k, seed in ((1, 91), (2, 92)):
+    s = Workload.zipf(0.99, 512, k=k, views=3, window=64, seed=seed).generate(6000)
+    eng = Engine(s.key_space, n=5)
+    eng.stage(s); eng.run()
+    r = eng.results()
+    rng = np.random.default_rng(5)
+    order = [int(i) for i in np.argsort(np.arange(s.n) + rng.integers(0, 200, s.n), kind="stable")]
+    order = order[:17] + order[18:] + [order[17]]  # one command held back: a backlog
+    for batch in (1, 5, 300):
+        ex = HipGraphExecutor(1, 0, 5, 1, key_space=s.key_space)
+        pend = []
+        for b0 in range(0, len(order), batch):
+            ex.handle_batch([GraphExecutionInfo.add(int(s.dots[j]), [int(x) for x in s.keys[j]],
+                             [int(x) for x in r["deps"][r["dep_off"][j]:r["dep_off"][j + 1]]])
+                             for j in order[b0:b0 + batch]])
+            pend.append(ex.pending())
+        seq = []
+        while True:
+            x = ex.to_clients()
+            if x is None:
+                break
+            seq.append([int(x.rifl), int(x.key)])
+        out.append([seq, sorted(ex.last_labels.items()), pend, ex.passes()])
 print(json.dumps(out))
 """
     res = []
@@ -338,5 +342,8 @@ print(json.dumps(out))
         p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
                            timeout=300, env=e)
         assert p.returncode == 0, p.stdout + p.stderr
-        res.append(p.stdout.strip().splitlines()[-1])
-    assert res[0] == res[1]
+        res.append(json.loads(p.stdout.strip().splitlines()[-1]))
+    assert [r[:3] for r in res[0]] == [r[:3] for r in res[1]]
+    # the 2-key stream at batch 1 crosses 1024 pending while below 2048
+    pend = res[0][3][2]
+    assert any(1024 < x < 2047 for x in pend), max(pend)
