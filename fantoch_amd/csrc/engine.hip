@@ -791,7 +791,8 @@ __device__ __forceinline__ void cmd_union_regs(
     const uint64_t *__restrict__ frontier, uint64_t *__restrict__ dep_dot,
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n,
-    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, uint32_t vbase) {
+    const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, uint32_t vbase,
+    bool edges_at_deps, uint32_t &fwd) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
@@ -862,7 +863,12 @@ __device__ __forceinline__ void cmd_union_regs(
   }
   dep_cnt[i] = m;
   }
-  uint32_t *ds = dst + size_t(i) * S;
+  // graph edges: a fixed-stride row of S, or (edges_at_deps) the command's
+  // committed-deps row of the CSR (its in-batch deps are a subset), both
+  // padded with the vertex itself (self loops are ignored); forward edges
+  // (a dependency that arrived later) are counted for the graph stage
+  uint32_t *ds = edges_at_deps ? dst + out_off[i] : dst + size_t(i) * S;
+  const uint32_t ecap = edges_at_deps ? out_off[i + 1] - out_off[i] : S;
   uint32_t nv = 0;
 #pragma unroll
   for (uint32_t t = 0; t < kRegSlots; t++) {
@@ -870,10 +876,14 @@ __device__ __forceinline__ void cmd_union_regs(
       bool dup = false;
 #pragma unroll
       for (uint32_t q = 0; q < t; q++) dup |= vv[q] == vv[t];
-      if (!dup) ds[nv++] = vv[t];
+      if (!dup) {
+        if (nv < ecap) ds[nv] = vv[t];
+        nv++;
+        fwd += vv[t] > vbase + i;
+      }
     }
   }
-  for (uint32_t q = nv; q < S; q++) ds[q] = vbase + i;  // padding: self loops are ignored
+  for (uint32_t q = nv; q < ecap; q++) ds[q] = vbase + i;
   if (nv_out) nv_out[i] = nv;
 }
 
@@ -890,9 +900,12 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
                              uint64_t bbase, const uint32_t *__restrict__ out_off,
-                             uint32_t *__restrict__ err, uint32_t vbase) {
+                             uint32_t *__restrict__ err, uint32_t vbase, uint32_t edges_at_deps,
+                             unsigned long long *__restrict__ nfwd) {
   // uniform: the register path, with a sorting network sized to the row
   const uint32_t cn = n;
+  const bool ead = edges_at_deps != 0 && out_off != nullptr;
+  uint32_t fwd = 0;
   if (S <= 4) {
     // XCD-contiguous blocks (grid a multiple of 8): workgroup b runs on XCD
     // b mod 8, which takes the b/8-th block of its own eighth of the
@@ -902,53 +915,61 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     const uint32_t lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
     for (size_t j = size_t(lb) * blockDim.x + threadIdx.x; j < cn; j += size_t(nb) * blockDim.x)
       cmd_union_regs<4>(uint32_t(j), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                        blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase);
-    return;
-  }
-  if (S <= 8) {
+                        blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd);
+  } else if (S <= 8) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<8>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n, out_off, err, vbase);
+                        nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd);
     }
-    return;
-  }
-  if (S <= kRegSlots) {
+  } else if (S <= kRegSlots) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<kRegSlots>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                                blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase);
+                                blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase, ead,
+                                fwd);
     }
-    return;
-  }
-  GRID_STRIDE(i, cn) {
-    uint64_t *dd = dep_dot + size_t(i) * S;
-    uint32_t *ds = dst + size_t(i) * S;
-    uint32_t nv = 0, nd = 0;
-    bool missing = false;
-    for (uint32_t t = 0; t < S; t++) {
-      uint64_t x = 0;
-      uint32_t v = 0;
-      const int kind = decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
-      if (kind == 1) {
-        bool dup = false;
-        for (uint32_t q = 0; q < nv; q++) dup |= ds[q] == v;
-        if (!dup) ds[nv++] = v;
-        dd[nd++] = dot[v];
-      } else if (kind == 2) {
-        {
-          dd[nd++] = x;
-          // executed? (AEClock frontier; exceptions are not carried by the
-          // fused engine: every earlier batch executed completely)
-          if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
+  } else {
+    GRID_STRIDE(i, cn) {
+      uint64_t *dd = dep_dot + size_t(i) * S;
+      uint32_t *ds = dst + size_t(i) * S;
+      uint32_t nv = 0, nd = 0;
+      bool missing = false;
+      for (uint32_t t = 0; t < S; t++) {
+        uint64_t x = 0;
+        uint32_t v = 0;
+        const int kind = decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
+        if (kind == 1) {
+          bool dup = false;
+          for (uint32_t q = 0; q < nv; q++) dup |= ds[q] == v;
+          if (!dup) {
+            ds[nv++] = v;
+            fwd += v > vbase + i;
+          }
+          dd[nd++] = dot[v];
+        } else if (kind == 2) {
+          {
+            dd[nd++] = x;
+            // executed? (AEClock frontier; exceptions are not carried by the
+            // fused engine: every earlier batch executed completely)
+            if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
+          }
         }
       }
+      for (uint32_t q = nv; q < S; q++) ds[q] = vbase + i;  // padding: self loops are ignored
+      if (nv_out) nv_out[i] = nv;
+      const uint32_t m = S == 1 ? nd : sort_unique_u64(dd, nd);
+      for (uint32_t q = m; q < S; q++) dd[q] = 0;
+      dep_cnt[i] = m;
+      if (blocked0) blocked0[i] = missing;
+      if (missing) atomicAdd(nblocked, 1u);
     }
-    for (uint32_t q = nv; q < S; q++) ds[q] = vbase + i;  // padding: self loops are ignored
-    if (nv_out) nv_out[i] = nv;
-    const uint32_t m = S == 1 ? nd : sort_unique_u64(dd, nd);
-    for (uint32_t q = m; q < S; q++) dd[q] = 0;
-    dep_cnt[i] = m;
-    if (blocked0) blocked0[i] = missing;
-    if (missing) atomicAdd(nblocked, 1u);
+  }
+  // forward-edge count over 64 counters (one hot word would serialise)
+  if (nfwd) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) fwd += __shfl_xor(fwd, o, 64);
+    if ((threadIdx.x & 63) == 0 && fwd)
+      atomicAdd(&nfwd[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & 63],
+                (unsigned long long)fwd);
   }
 }
 
@@ -1291,6 +1312,7 @@ struct EngineDevice {
   uint32_t o_nelem = 0;               // per-key sequence length (key_offs, o_seq)
   const uint64_t *o_seq = nullptr;    // [o_nelem] per-key sequences of dots
   DBuf<uint32_t> edge_cnt, edge_off, edge_csr;  // replica views: in-batch edges as CSR
+  DBuf<unsigned long long> fwd_ctr;  // [64] forward edges counted by the union
   DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
   DBuf<uint32_t> place_base;  // replica views: per-chunk smallest element position
@@ -2011,22 +2033,32 @@ struct EngineDevice {
     }
     // rows of <= 4 slots: XCD-contiguous blocks (k_cmd_engine)
     const uint32_t g = S <= 4 ? (grid_for(n, B, 1u << 22) + 7) / 8 * 8 : grid_for(n, B);
+    // wide rows (C5: 12 slots) write their edges into the committed-deps CSR
+    // rows (the in-batch deps are a subset), so no edge compaction pass; the
+    // union also counts the forward edges for the graph stage
+    const bool edges_at_deps = views && S >= 8 && deps_direct;
+    unsigned long long *fwd = views ? fwd_ctr.ensure(64) : nullptr;
+    if (fwd) FH_HIP(hipMemsetAsync(fwd, 0, 64 * sizeof(unsigned long long), stream));
     if (views)
       probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
                     k_cmd_engine<uint32_t>, dim3(g), dim3(B), stream, n, S, bdot,
                     (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                    scal.get(), ecnt, bbase, doff, scal.get() + 1, 0u);
+                    scal.get(), edges_at_deps ? (uint32_t *)nullptr : ecnt, bbase, doff,
+                    scal.get() + 1, 0u, uint32_t(edges_at_deps), fwd);
     else
       probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
                     k_cmd_engine<uint64_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
                     (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
-                    scal.get(), ecnt, bbase, doff, scal.get() + 1, 0u);
+                    scal.get(), ecnt, bbase, doff, scal.get() + 1, 0u, 0u,
+                    (unsigned long long *)nullptr);
     mark("keydeps_union");
     if (deps_only) return;  // the committed deps are the output (partial replication)
     const uint32_t *gdst = dd, *goff = nullptr;
-    if (views && S >= 8) {  // measured: a win at S = 12 (C5), flat or worse at 3 and 6
+    if (edges_at_deps) {
+      goff = doff;
+    } else if (views && S >= 8) {  // measured: a win at S = 12 (C5), flat or worse at 3 and 6
       uint32_t *eo = edge_off.ensure(n + 1);
       exclusive_scan_u32(edge_cnt.get(), eo, n, scan_ws, stream);
       uint32_t *ec = edge_csr.ensure(size_t(n) * S + 1);
@@ -2042,6 +2074,7 @@ struct EngineDevice {
     gin.stride = goff ? 0 : S;
     gin.dst = gdst;
     gin.blocked0 = nullptr;  // see k_cmd_engine: no pending carried by the fused engine
+    gin.fwd_counts = fwd;    // forward edges, counted by the union
     gin.dot = bdot;
     gin.k = k;
     gin.key32 = bkey;
@@ -2232,7 +2265,8 @@ void union_rows(uint32_t n, uint32_t S, const uint32_t *codes, const uint64_t *d
   probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
                 k_cmd_engine<uint32_t>, dim3(g), dim3(B), s, n, S, dot, codes, dot,
                 (const uint64_t *)nullptr, dep_dot, dcnt, dst, (uint8_t *)nullptr, scal, ecnt,
-                uint64_t(0), (const uint32_t *)dep_off, scal + 1, vbase);
+                uint64_t(0), (const uint32_t *)dep_off, scal + 1, vbase, 0u,
+                (unsigned long long *)nullptr);
 }
 
 }  // namespace fh

@@ -55,6 +55,9 @@ struct GraphInput {
   const uint32_t *sorted_keys = nullptr;  // [M]
   const uint32_t *sorted_vid = nullptr;   // [M] vid of each sorted element
   bool no_forward_hint = false;           // edges all point backwards
+  // [64] or null: the forward edges, counted by the producer of the edges
+  // (the sum is count_forward's result, without its pass)
+  const unsigned long long *fwd_counts = nullptr;
   bool want_per_key = true;               // build the per-key sequence
   bool global_only = false;               // skip the tile path (fh_dgraph: rep + kap wanted)
   bool want_orders = true;                // false: SCCs, kappa and labels only (out.kap)
@@ -98,6 +101,11 @@ struct GraphCore {
   DBuf<uint32_t> rep, cnt, pos, order, rank, tmp32a, tmp32b, tmp32c, tmp32d, flags;
   DBuf<uint32_t> kraise;  // [V] last kappa iteration that raised kap[rep]
   DBuf<uint32_t> erep;    // [E] rep[dst[e]] (refresh_edge_rep)
+  // class edges after the windows (k_class_edges): the edge array's rows,
+  // targets as representatives (ce_rep_ok while the global path reads them)
+  DBuf<uint32_t> ce_dst;
+  bool ce_rep_ok = false;
+  bool ce_fresh = false;  // no class merged since the class edges were written
   uint64_t nedges = 0;
   DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c, pk_da, pk_db;
   DBuf<uint8_t> blocked;

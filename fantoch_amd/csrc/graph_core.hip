@@ -240,7 +240,10 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int lane) {
 // smallest vertex it mutually reaches.
 __global__ void __launch_bounds__(256)
     k_windows(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride, const uint32_t *__restrict__ dst,
-              const uint8_t *__restrict__ blocked, uint32_t *parent, uint32_t nwin) {
+              const uint8_t *__restrict__ blocked, uint32_t *parent, uint32_t nwin,
+              int any_blocked) {
+  // any_blocked == 0: no vertex is pending, so the per-edge blocked[u]
+  // gathers (a random byte per edge, C5: most of the kernel's traffic) go
   __shared__ uint64_t s_rows[4][128][2];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t win = blockIdx.x * 4 + wv;
@@ -251,10 +254,10 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const uint32_t v = base + h * 64 + lane;
-    if (v < V && !blocked[v]) {
+    if (v < V && !(any_blocked && blocked[v])) {
       for (uint32_t e = EB(v); e < EE(v); e++) {
         const uint32_t u = dst[e];
-        if (u >= base && u < base + 128 && u != v && !blocked[u]) {
+        if (u >= base && u < base + 128 && u != v && !(any_blocked && blocked[u])) {
           const uint32_t bit = u - base;
           r[h][bit >> 6] |= uint64_t(1) << (bit & 63);
           fwd |= u > v;
@@ -309,6 +312,38 @@ __global__ void __launch_bounds__(256)
       }
       if (found) break;
     }
+  }
+}
+
+// ---------------------------------------------------------------- class edges
+// After the windows, the coloring and kappa follow only edges between
+// classes.  One pass writes each vertex's dependency targets as their
+// classes' representatives into a copy of the edge array (same rows), its
+// own class and repeats replaced by its own representative -- which every
+// kernel below skips without a gather (the first 16 targets of a row are
+// compared pairwise in registers, the rest kept as they come).  This is the
+// table refresh_edge_rep would write (rep[dst[e]]), with the repeats gone:
+// on C5 ~60 % of the entries need no gather any more.  Classes only merge
+// later, so rep[target rep] stays the current representative.
+constexpr int kCeDedup = 16;
+__global__ void __launch_bounds__(256)
+    k_class_edges(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
+                  const uint32_t *__restrict__ dst, const uint32_t *__restrict__ rep,
+                  uint32_t *__restrict__ cdst) {
+  GRID_STRIDE(v, V) {
+    const uint32_t r = rep[v];
+    const uint32_t eb = EB(v), ee = EE(v);
+    uint32_t rr[kCeDedup];
+#pragma unroll
+    for (int j = 0; j < kCeDedup; j++) rr[j] = eb + j < ee ? rep[dst[eb + j]] : r;
+#pragma unroll
+    for (int j = 0; j < kCeDedup; j++) {
+      bool keep = rr[j] != r;
+#pragma unroll
+      for (int i = 0; i < j; i++) keep = keep && rr[i] != rr[j];
+      if (eb + j < ee) cdst[eb + j] = keep ? rr[j] : r;
+    }
+    for (uint32_t e = eb + kCeDedup; e < ee; e++) cdst[e] = rep[dst[e]];
   }
 }
 
@@ -979,7 +1014,8 @@ void GraphCore::find_sccs(const GraphInput &in) {
   const uint32_t V = in.V;
   k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
   const uint32_t nwin = (V + 63) / 64;
-  k_windows<<<(nwin + 3) / 4, 256, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), rep.get(), nwin);
+  k_windows<<<(nwin + 3) / 4, 256, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), rep.get(), nwin,
+                                                int(in.blocked0 != nullptr));
   mark("scc_windows");
   k_uf_compress<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
   mark("scc_compress");
@@ -1001,8 +1037,11 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
   k_kap_init<<<agg_blocks(V), B, 0, stream>>>(V, blocked.get(), rep.get(),
                                               seeded ? hseed.get() : nullptr,
                                               kap.get());
-  if (!seeded) refresh_edge_rep(in);
-  const uint32_t *er = seeded ? nullptr : erep.get();
+  // unseeded: the edge targets' representatives -- the class edges while no
+  // coloring has merged classes since they were written, else a refresh
+  const bool fresh = ce_rep_ok && ce_fresh;
+  if (!seeded && !fresh) refresh_edge_rep(in);
+  const uint32_t *er = seeded ? nullptr : fresh ? in.dst : erep.get();
   if (!give_up_early) {
     // to the fixpoint: device-side convergence, no per-iteration read-back
     uint32_t launched = 0;
@@ -1112,8 +1151,12 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
   const bool full = list == nullptr;
   const uint32_t *er = nullptr;
   if (full) {
-    refresh_edge_rep(in);
-    er = erep.get();
+    if (ce_rep_ok && ce_fresh) {
+      er = in.dst;  // class edges: the targets are representatives already
+    } else {
+      refresh_edge_rep(in);
+      er = erep.get();
+    }
   }
   bool first_full = full;  // round 1 over every vertex: done[] is all zero
   for (;;) {
@@ -1147,6 +1190,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     k_fb_merge<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached, parent,
                                      scalars.get() + 1);
     k_fb_compress<<<G, B, 0, stream>>>(n, list, parent, rep.get());
+    ce_fresh = false;  // classes merged: the class edges' targets may be stale
     if (!read_scalar(1)) break;
     first_full = false;
     if (full) {
@@ -1379,7 +1423,17 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     FH_HIP(hipStreamSynchronize(stream));
     any_blocked = ne != V;
   }
-  const uint64_t nfwd = in.no_forward_hint ? 0 : count_forward(in);
+  uint64_t nfwd = 0;
+  if (in.no_forward_hint) {
+    nfwd = 0;
+  } else if (in.fwd_counts && !any_blocked) {
+    unsigned long long c[64];
+    FH_HIP(hipMemcpyAsync(c, in.fwd_counts, sizeof(c), hipMemcpyDeviceToHost, stream));
+    FH_HIP(hipStreamSynchronize(stream));
+    for (int i = 0; i < 64; i++) nfwd += c[i];
+  } else {
+    nfwd = count_forward(in);
+  }
   if (nfwd == 0 && !any_blocked && in.sorted_keys && in.sorted_vid && in.want_orders) {
     // every SCC is a singleton and the execution order is the arrival order:
     // nothing to materialise (rep[v] = v, label = own dot, rank = v)
@@ -1394,8 +1448,21 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     mark("trivial_order");
     return;
   }
+  // the coloring and kappa below read `cin`: after the windows, the class
+  // edges (class_targets) instead of every dependency
+  GraphInput cin = in;
   if (nfwd) {
     find_sccs(in);
+    uint32_t *cd = ce_dst.ensure(nedges + 1);
+    {
+      const uint64_t blocks = (uint64_t(V) + B - 1) / B;
+      k_class_edges<<<unsigned(blocks < 65536 ? blocks : 65536), B, 0, stream>>>(
+          V, in.off, in.stride, in.dst, rep.get(), cd);
+    }
+    cin.dst = cd;
+    ce_rep_ok = true;  // cd holds representatives: the coloring's erep
+    ce_fresh = true;
+    mark("class_edges");
   } else {
     k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
   }
@@ -1417,12 +1484,12 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   if (direct_full) {
     out.fallback_used = true;
     kap_seed_ok = false;
-    coloring_fallback(in, 0);
+    coloring_fallback(cin, 0);
     kap_seed_ok = true;
-    ok = order_kappa(in, 1u << 30, iters);
+    ok = order_kappa(cin, 1u << 30, iters);
     iters1 = 0;
   } else {
-    ok = order_kappa(in, give_up, iters, true);
+    ok = order_kappa(cin, give_up, iters, true);
     iters1 = iters;
   }
   bool used_full = direct_full;
@@ -1431,14 +1498,15 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     // first the vertices still being raised (the missed cycles are among
     // them), certified by a bounded kappa run; if a cycle is left, the exact
     // coloring over every vertex
-    if (coloring_fallback(in, 1)) ok = order_kappa(in, give_up, iters, true);
+    if (coloring_fallback(cin, 1)) ok = order_kappa(cin, give_up, iters, true);
     if (!ok) {
-      coloring_fallback(in, 0);
-      ok = order_kappa(in, 1u << 30, iters);
+      coloring_fallback(cin, 0);
+      ok = order_kappa(cin, 1u << 30, iters);
       used_full = true;
     }
   }
   prefer_full = used_full;
+  ce_rep_ok = false;
   out.kappa_iters = iters;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   if (debug)
