@@ -11,6 +11,7 @@
 // AEClock<ProcessId> (frontier + exceptions, threshold crate) kept on the
 // host and mirrored to the device per batch.
 #include <algorithm>
+#include <cstring>
 #include <deque>
 #include <map>
 #include <set>
@@ -82,12 +83,29 @@ __global__ void k_resolve_fill(uint32_t V, const uint64_t *__restrict__ dot,
   }
 }
 
-// appended batch rows: offsets rebased past the carried prefix
-__global__ void k_rebase(uint32_t n, uint32_t *__restrict__ koff, uint32_t kbase,
-                         uint32_t *__restrict__ doff, uint32_t dbase) {
-  GRID_STRIDE(i, n) {
-    koff[i] += kbase;
-    doff[i] += dbase;
+// The batch's rows, uploaded as one block, appended after the carried
+// prefix (offsets rebased past it); the executed-clock mirror rides along
+// when it changed (nf = 256 frontier words, then ne exceptions).
+struct Upload {
+  const uint64_t *dot, *dep, *clk;
+  const uint32_t *key, *koff, *doff;
+  uint32_t n, nk, nd, nf, ne;
+};
+__global__ void k_append(Upload u, uint64_t *__restrict__ vdot, uint32_t *__restrict__ koff,
+                         uint32_t *__restrict__ key, uint32_t *__restrict__ doff,
+                         uint64_t *__restrict__ dep, uint32_t kbase, uint32_t dbase,
+                         uint64_t *__restrict__ frontier, uint64_t *__restrict__ exc) {
+  const uint32_t m = max(max(u.n + 1, u.nk), max(u.nd, u.nf + u.ne));
+  GRID_STRIDE(i, m) {
+    if (i < u.n) vdot[i] = u.dot[i];
+    if (i <= u.n) {
+      koff[i] = u.koff[i] + kbase;
+      doff[i] = u.doff[i] + dbase;
+    }
+    if (i < u.nk) key[i] = u.key[i];
+    if (i < u.nd) dep[i] = u.dep[i];
+    if (i < u.nf) frontier[i] = u.clk[i];
+    else if (i < u.nf + u.ne) exc[i - u.nf] = u.clk[i];
   }
 }
 
@@ -230,6 +248,9 @@ struct GraphDevice {
   uint64_t passes = 0, skipped = 0;
   // device buffers
   DBuf<uint64_t> d_sd, d_sd2, d_frontier, d_exc, d_xdot, d_xlab, d_miss;
+  DBuf<uint8_t> d_up;        // the batch's upload block (k_append)
+  uint8_t *h_up = nullptr;   // its pinned host side
+  size_t h_up_cap = 0;
   DBuf<uint32_t> d_cnt, d_off, d_dst, d_sv, d_sv2, d_err, d_kv, d_kk, d_kd, d_pv, d_pk, d_pd;
   DBuf<uint8_t> d_blocked0;
   SortWorkspace sort_ws;
@@ -257,6 +278,7 @@ struct GraphDevice {
   ~GraphDevice() {
     (void)hipSetDevice(device);
     if (h_small) (void)hipHostFree(h_small);
+    if (h_up) (void)hipHostFree(h_up);
     if (stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
@@ -367,44 +389,66 @@ struct GraphDevice {
     const size_t KB = n ? key_off[n] : 0, DB = n ? dep_off[n] : 0;
     FH_CHECK(size_t(W.KP) + KB < (size_t(1) << 32) && size_t(W.DP) + DB < (size_t(1) << 32),
              FH_EINVAL, "too many keys / dependencies");
-    std::vector<uint32_t> k32(KB);
-    for (size_t e = 0; e < KB; e++) {
+    for (size_t e = 0; e < KB; e++)
       FH_CHECK(key_id[e] < cfg.key_space, FH_EINVAL, "key id >= key_space");
-      k32[e] = uint32_t(key_id[e]);
-    }
     if (V == 0) return;
     uint64_t *ddot_v = grow_keep(W.dot, V + 1, P, stream);
     uint32_t *dko = grow_keep(W.koff, V + 2, P + 1, stream);
     uint32_t *dk = grow_keep(W.key32, W.KP + KB + 1, W.KP, stream);
     uint32_t *ddo = grow_keep(W.doff, V + 2, P + 1, stream);
     uint64_t *dd = grow_keep(W.ddot, W.DP + DB + 1, W.DP, stream);
-    if (n) {
-      FH_HIP(hipMemcpyAsync(ddot_v + P, dot, n * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
-      FH_HIP(hipMemcpyAsync(dko + P, key_off, (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
-                            stream));
-      FH_HIP(hipMemcpyAsync(ddo + P, dep_off, (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
-                            stream));
-      if (KB)
-        FH_HIP(hipMemcpyAsync(dk + W.KP, k32.data(), KB * sizeof(uint32_t), hipMemcpyHostToDevice,
-                              stream));
-      if (DB)
-        FH_HIP(hipMemcpyAsync(dd + W.DP, dep_dot, DB * sizeof(uint64_t), hipMemcpyHostToDevice,
-                              stream));
-      k_rebase<<<grid_for(n + 1, B), B, 0, stream>>>(uint32_t(n + 1), dko + P, W.KP, ddo + P,
-                                                      W.DP);
-    }
-    // executed clock mirror: re-sorted and re-uploaded only when the clock
+    // executed clock mirror: re-sorted and re-sent only when the clock
     // changed since the last pass
-    if (clock.version != exc_version) {
+    const bool clk = clock.version != exc_version;
+    if (clk) {
       exc_sorted.assign(clock.exc.begin(), clock.exc.end());
       std::sort(exc_sorted.begin(), exc_sorted.end());
-      FH_HIP(hipMemcpyAsync(d_frontier.get(), clock.frontier, sizeof(clock.frontier),
-                            hipMemcpyHostToDevice, stream));
       d_exc.ensure(exc_sorted.size() + 1);
-      if (!exc_sorted.empty())
-        FH_HIP(hipMemcpyAsync(d_exc.get(), exc_sorted.data(), exc_sorted.size() * sizeof(uint64_t),
-                              hipMemcpyHostToDevice, stream));
       exc_version = clock.version;
+    }
+    // one pinned block, one copy, one append launch (separate pageable
+    // copies cost several microseconds each: the floor of a small batch)
+    Upload u{};
+    u.n = uint32_t(n);
+    u.nk = uint32_t(KB);
+    u.nd = uint32_t(DB);
+    u.nf = clk ? 256u : 0u;
+    u.ne = clk ? uint32_t(exc_sorted.size()) : 0u;
+    if (n || clk) {
+      const size_t o_dot = 0, o_dep = o_dot + n * 8, o_clk = o_dep + DB * 8,
+                   o_key = o_clk + (size_t(u.nf) + u.ne) * 8, o_ko = o_key + KB * 4,
+                   o_do = o_ko + (n + 1) * 4, bytes = o_do + (n + 1) * 4;
+      if (h_up_cap < bytes) {
+        if (h_up) FH_HIP(hipHostFree(h_up));
+        h_up = nullptr;
+        h_up_cap = 0;
+        FH_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_up), bytes * 2, hipHostMallocDefault));
+        h_up_cap = bytes * 2;
+      }
+      uint8_t *dup = d_up.ensure(bytes + 8);
+      if (n) {
+        std::memcpy(h_up + o_dot, dot, n * 8);
+        if (DB) std::memcpy(h_up + o_dep, dep_dot, DB * 8);
+        uint32_t *hk = reinterpret_cast<uint32_t *>(h_up + o_key);
+        for (size_t e = 0; e < KB; e++) hk[e] = uint32_t(key_id[e]);
+        std::memcpy(h_up + o_ko, key_off, (n + 1) * 4);
+        std::memcpy(h_up + o_do, dep_off, (n + 1) * 4);
+      }
+      if (clk) {
+        std::memcpy(h_up + o_clk, clock.frontier, 256 * 8);
+        if (u.ne) std::memcpy(h_up + o_clk + 256 * 8, exc_sorted.data(), size_t(u.ne) * 8);
+      }
+      FH_HIP(hipMemcpyAsync(dup, h_up, bytes, hipMemcpyHostToDevice, stream));
+      u.dot = reinterpret_cast<const uint64_t *>(dup + o_dot);
+      u.dep = reinterpret_cast<const uint64_t *>(dup + o_dep);
+      u.clk = reinterpret_cast<const uint64_t *>(dup + o_clk);
+      u.key = reinterpret_cast<const uint32_t *>(dup + o_key);
+      u.koff = reinterpret_cast<const uint32_t *>(dup + o_ko);
+      u.doff = reinterpret_cast<const uint32_t *>(dup + o_do);
+      const uint32_t m = std::max(std::max(u.n + 1, u.nk), std::max(u.nd, u.nf + u.ne));
+      k_append<<<grid_for(m, B), B, 0, stream>>>(u, ddot_v + P, dko + P, dk + W.KP, ddo + P,
+                                                 dd + W.DP, W.KP, W.DP, d_frontier.get(),
+                                                 d_exc.get());
     }
     const std::vector<uint64_t> &exc = exc_sorted;
     uint64_t *dexc = d_exc.ensure(exc.size() + 1);
