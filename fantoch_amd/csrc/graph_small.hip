@@ -56,7 +56,7 @@ __device__ uint32_t block_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
 // bitonic sort of n2 (a power of two <= 2 * kThreads) keys ascending, with
 // an optional u16 payload.  Thread t owns elements t and t + kThreads, so a
 // stage whose partners are under 64 apart stays inside one wave's 64-element
-// blocks: it needs only a wave barrier; a block barrier precedes the stages
+// blocks: it needs only a wave barrier; block barriers surround the stages
 // with wider partners (51 of a 2048-element sort's 66 stages are wave-local)
 __device__ void bitonic(uint64_t *key, uint16_t *val, int n2) {
   for (int k = 2; k <= n2; k <<= 1)
@@ -78,9 +78,13 @@ __device__ void bitonic(uint64_t *key, uint16_t *val, int n2) {
           }
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (j >= 64) {
+        __syncthreads();  // this stage wrote other waves' elements
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
     }
   __syncthreads();
 }
