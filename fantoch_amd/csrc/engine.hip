@@ -1266,6 +1266,27 @@ __global__ void k_identity_labels(uint32_t n, const uint64_t *__restrict__ dot,
 // contiguous): a run's head records its start, its tail the count.  One
 // write per distinct key -- an atomic histogram serialises on Zipf-hot keys
 // (key 0 of C4 holds 6.5% of the stream: 4 ms of same-address atomics).
+// one pass over the per-key sort's output: each key's run start and end, and
+// the packed dots unpacked (src << sb | seq -> the u64 dot) into the
+// sequence output
+__global__ void k_run_bounds_unpack(uint32_t m, const uint32_t *__restrict__ keys,
+                                    const uint32_t *__restrict__ pd, int sb,
+                                    uint32_t *__restrict__ start, uint32_t *__restrict__ end,
+                                    uint64_t *__restrict__ seq) {
+  const uint32_t msk = (1u << sb) - 1;
+  GRID_STRIDE(j, m) {
+    const uint32_t k = keys[j];
+    if (j == 0 || keys[j - 1] != k) start[k] = j;
+    if (j + 1 == m || keys[j + 1] != k) end[k] = j + 1;
+    const uint32_t x = pd[j];
+    seq[j] = (uint64_t(x >> sb) << 56) | (x & msk);
+  }
+}
+__global__ void k_run_len(uint32_t K, const uint32_t *__restrict__ start,
+                          uint32_t *__restrict__ end) {
+  GRID_STRIDE(k, K) end[k] -= start[k];
+}
+
 __global__ void k_run_start(uint32_t m, const uint32_t *__restrict__ keys,
                             uint32_t *__restrict__ start) {
   GRID_STRIDE(j, m) if (j == 0 || keys[j - 1] != keys[j]) start[keys[j]] = j;
@@ -1370,6 +1391,7 @@ struct EngineDevice {
   // path's slots, the packed dots' sequence bits (-1: no inline dots)
   uint32_t code_stride = 0;
   int code_isb = -1;
+  int pk_sb = 0;  // the per-key sort's packed dots: sequence bits
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
   // per batch: (seq bits, packed bits) of its dots, src << sb | seq (0: wider
   // than 32 bits), so the per-key sort can move 4-byte dots
@@ -2155,7 +2177,9 @@ struct EngineDevice {
     graph.run(gin, gout);
     FH_CHECK(gout.npending == 0, FH_EINVARIANT, "fused engine batch left pending vertices");
     // per-key sequence of dots (ExecutionOrderMonitor::add order)
-    if (gout.pk_dot) {
+    if (gout.pk_dot32) {
+      pk_sb = gin.dot_sb;  // unpacked by materialize's pass over the runs
+    } else if (gout.pk_dot) {
       o_seq = gout.pk_dot;
     } else {
       uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
@@ -2223,8 +2247,18 @@ struct EngineDevice {
     uint32_t *o = key_offs.ensure(key_space + 2);
     uint32_t *hp = headpos.ensure(key_space + 1);
     FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
-    k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
-    k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
+    if (gout.pk_dot32) {
+      // packed per-key dots: run bounds and the unpacked sequence in one pass
+      FH_HIP(hipMemsetAsync(hp, 0, key_space * sizeof(uint32_t), stream));
+      uint64_t *sq = seq_dot.ensure(o_nelem + 1);
+      k_run_bounds_unpack<<<grid_for(o_nelem, B), B, 0, stream>>>(
+          o_nelem, gout.pk_key, gout.pk_dot32, pk_sb, hp, h, sq);
+      k_run_len<<<grid_for(uint32_t(key_space), B), B, 0, stream>>>(uint32_t(key_space), hp, h);
+      o_seq = sq;
+    } else {
+      k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
+      k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
+    }
     exclusive_scan_u32(h, o, key_space, scan_ws, stream);
     if (sv_fused) {
       uint64_t *sq = seq_dot.ensure(o_nelem + 1);
