@@ -102,11 +102,6 @@ struct GraphCore {
   DBuf<uint32_t> rep, cnt, pos, order, rank, tmp32a, tmp32b, tmp32c, tmp32d, flags;
   DBuf<uint32_t> kraise;  // [V] last kappa iteration that raised kap[rep]
   DBuf<uint32_t> erep;    // [E] rep[dst[e]] (refresh_edge_rep)
-  // class edges after the windows (k_class_edges): the edge array's rows,
-  // targets as representatives (ce_rep_ok while the global path reads them)
-  DBuf<uint32_t> ce_dst;
-  bool ce_rep_ok = false;
-  bool ce_fresh = false;  // no class merged since the class edges were written
   uint64_t nedges = 0;
   DBuf<uint64_t> kap, label, tmp64a, tmp64b, tmp64c, pk_da, pk_db;
   DBuf<uint8_t> blocked;

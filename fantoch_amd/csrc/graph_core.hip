@@ -315,38 +315,6 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// ---------------------------------------------------------------- class edges
-// After the windows, the coloring and kappa follow only edges between
-// classes.  One pass writes each vertex's dependency targets as their
-// classes' representatives into a copy of the edge array (same rows), its
-// own class and repeats replaced by its own representative -- which every
-// kernel below skips without a gather (the first 16 targets of a row are
-// compared pairwise in registers, the rest kept as they come).  This is the
-// table refresh_edge_rep would write (rep[dst[e]]), with the repeats gone:
-// on C5 ~60 % of the entries need no gather any more.  Classes only merge
-// later, so rep[target rep] stays the current representative.
-constexpr int kCeDedup = 16;
-__global__ void __launch_bounds__(256)
-    k_class_edges(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
-                  const uint32_t *__restrict__ dst, const uint32_t *__restrict__ rep,
-                  uint32_t *__restrict__ cdst) {
-  GRID_STRIDE(v, V) {
-    const uint32_t r = rep[v];
-    const uint32_t eb = EB(v), ee = EE(v);
-    uint32_t rr[kCeDedup];
-#pragma unroll
-    for (int j = 0; j < kCeDedup; j++) rr[j] = eb + j < ee ? rep[dst[eb + j]] : r;
-#pragma unroll
-    for (int j = 0; j < kCeDedup; j++) {
-      bool keep = rr[j] != r;
-#pragma unroll
-      for (int i = 0; i < j; i++) keep = keep && rr[i] != rr[j];
-      if (eb + j < ee) cdst[eb + j] = keep ? rr[j] : r;
-    }
-    for (uint32_t e = eb + kCeDedup; e < ee; e++) cdst[e] = rep[dst[e]];
-  }
-}
-
 // ---------------------------------------------------------------- kappa
 __global__ void __launch_bounds__(256)
     k_kap_init(uint32_t V, const uint8_t *__restrict__ blocked, const uint32_t *__restrict__ rep,
@@ -1027,11 +995,8 @@ bool GraphCore::order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &
   k_kap_init<<<agg_blocks(V), B, 0, stream>>>(V, blocked.get(), rep.get(),
                                               seeded ? hseed.get() : nullptr,
                                               kap.get());
-  // unseeded: the edge targets' representatives -- the class edges while no
-  // coloring has merged classes since they were written, else a refresh
-  const bool fresh = ce_rep_ok && ce_fresh;
-  if (!seeded && !fresh) refresh_edge_rep(in);
-  const uint32_t *er = seeded ? nullptr : fresh ? in.dst : erep.get();
+  if (!seeded) refresh_edge_rep(in);
+  const uint32_t *er = seeded ? nullptr : erep.get();
   if (!give_up_early) {
     // to the fixpoint: device-side convergence, no per-iteration read-back
     uint32_t launched = 0;
@@ -1141,12 +1106,8 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
   const bool full = list == nullptr;
   const uint32_t *er = nullptr;
   if (full) {
-    if (ce_rep_ok && ce_fresh) {
-      er = in.dst;  // class edges: the targets are representatives already
-    } else {
-      refresh_edge_rep(in);
-      er = erep.get();
-    }
+    refresh_edge_rep(in);
+    er = erep.get();
   }
   bool first_full = full;  // round 1 over every vertex: done[] is all zero
   for (;;) {
@@ -1180,7 +1141,6 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     k_fb_merge<<<G, B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached, parent,
                                      scalars.get() + 1);
     k_fb_compress<<<G, B, 0, stream>>>(n, list, parent, rep.get());
-    ce_fresh = false;  // classes merged: the class edges' targets may be stale
     if (!read_scalar(1)) break;
     first_full = false;
     if (full) {
@@ -1438,21 +1398,8 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     mark("trivial_order");
     return;
   }
-  // the coloring and kappa below read `cin`: after the windows, the class
-  // edges (class_targets) instead of every dependency
-  GraphInput cin = in;
   if (nfwd) {
     find_sccs(in);
-    uint32_t *cd = ce_dst.ensure(nedges + 1);
-    {
-      const uint64_t blocks = (uint64_t(V) + B - 1) / B;
-      k_class_edges<<<unsigned(blocks < 65536 ? blocks : 65536), B, 0, stream>>>(
-          V, in.off, in.stride, in.dst, rep.get(), cd);
-    }
-    cin.dst = cd;
-    ce_rep_ok = true;  // cd holds representatives: the coloring's erep
-    ce_fresh = true;
-    mark("class_edges");
   } else {
     k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
   }
@@ -1474,12 +1421,12 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   if (direct_full) {
     out.fallback_used = true;
     kap_seed_ok = false;
-    coloring_fallback(cin, 0);
+    coloring_fallback(in, 0);
     kap_seed_ok = true;
-    ok = order_kappa(cin, 1u << 30, iters);
+    ok = order_kappa(in, 1u << 30, iters);
     iters1 = 0;
   } else {
-    ok = order_kappa(cin, give_up, iters, true);
+    ok = order_kappa(in, give_up, iters, true);
     iters1 = iters;
   }
   bool used_full = direct_full;
@@ -1488,15 +1435,14 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
     // first the vertices still being raised (the missed cycles are among
     // them), certified by a bounded kappa run; if a cycle is left, the exact
     // coloring over every vertex
-    if (coloring_fallback(cin, 1)) ok = order_kappa(cin, give_up, iters, true);
+    if (coloring_fallback(in, 1)) ok = order_kappa(in, give_up, iters, true);
     if (!ok) {
-      coloring_fallback(cin, 0);
-      ok = order_kappa(cin, 1u << 30, iters);
+      coloring_fallback(in, 0);
+      ok = order_kappa(in, 1u << 30, iters);
       used_full = true;
     }
   }
   prefer_full = used_full;
-  ce_rep_ok = false;
   out.kappa_iters = iters;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   if (debug)
