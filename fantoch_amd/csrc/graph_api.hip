@@ -596,8 +596,9 @@ struct GraphDevice {
     uint32_t *nkey = grow_keep(N.key32, KT + 1, 0, stream);
     uint32_t *ndoff = grow_keep(N.doff, V + 2, 0, stream);
     uint64_t *nddot = grow_keep(N.ddot, DT + 1, 0, stream);
-    // read-back block: header, executed dots, labels, missing dots, flags
-    const size_t hdr = 64, bytes = hdr + V * 16 + DT * 8 + V;
+    // read-back block: header, executed dots, labels, missing dots, pending
+    // flags, carried flags of the executed
+    const size_t hdr = 64, bytes = hdr + V * 16 + DT * 8 + 2 * V;
     uint8_t *blk = d_small.ensure(bytes);
     if (h_small_cap < bytes) {
       if (h_small) FH_HIP(hipHostFree(h_small));
@@ -608,6 +609,7 @@ struct GraphDevice {
     }
     SmallPass sp;
     sp.V = uint32_t(V);
+    sp.P = uint32_t(V - n);
     sp.dot = ddot_v;
     sp.koff = dko;
     sp.key32 = dk;
@@ -622,6 +624,7 @@ struct GraphDevice {
     sp.miss = sp.xlab + V;
     sp.miss_cap = uint32_t(DT);
     sp.blocked = reinterpret_cast<uint8_t *>(sp.miss + DT);
+    sp.xcar = sp.blocked + V;
     sp.ndot = ndot;
     sp.nkoff = nkoff;
     sp.nkey32 = nkey;
@@ -651,7 +654,8 @@ struct GraphDevice {
     W.P = W.KP = W.DP = 0;
     cur = 1 - cur;
     passes_small++;
-    finish_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, xdot, xlab, bflag, mlist, P2);
+    finish_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, xdot, xlab, bflag, mlist, P2,
+                hb + V);
   }
   uint64_t passes_small = 0;
 
@@ -660,7 +664,10 @@ struct GraphDevice {
   void finish_pass(size_t n, const uint64_t *dot, const uint32_t *dep_off, const uint64_t *dep_dot,
                    const uint64_t *cmd_shards, const uint64_t *dep_shards,
                    const std::vector<uint64_t> &xdot, const std::vector<uint64_t> &xlab,
-                   const std::vector<uint8_t> &bflag, std::vector<uint64_t> &mlist, uint32_t P2) {
+                   const std::vector<uint8_t> &bflag, std::vector<uint64_t> &mlist, uint32_t P2,
+                   const uint8_t *xcar = nullptr) {
+    // xcar (the small pass): per executed vertex, carried or not -- only the
+    // carried ones have host metadata to look up
     const size_t nexec = xdot.size();
     // every drained dot is a carried vertex or one of this batch's executed
     // vertices (the reference panics otherwise): the batch part is checked by
@@ -686,7 +693,7 @@ struct GraphDevice {
       // execution order), one ExecutionDelay per command
       if (j == 0 || xlab[j - 1] != xlab[j]) m_chain.push_back(0);
       m_chain.back()++;
-      auto it = pend.find(d);
+      auto it = (!xcar || xcar[j]) ? pend.find(d) : pend.end();
       if (it != pend.end()) {  // a carried vertex
         m_delay.push_back(now_ms >= it->second.time ? now_ms - it->second.time : 0);
         porder.erase(it->second.seq);

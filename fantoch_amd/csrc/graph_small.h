@@ -11,6 +11,7 @@ constexpr int kSmallE = 8192;  // dependency entries of those vertices
 
 struct SmallPass {
   uint32_t V;
+  uint32_t P;  // the first P vertices are carried pending ones
   // vertices (carried pending, then the batch): dots, key lists, dependency
   // lists (CSR offsets over the key / dependency arrays)
   const uint64_t *dot;
@@ -22,6 +23,7 @@ struct SmallPass {
   // outputs: executed dots and labels in execution order, per-vertex pending
   // flags, missing dependency dots (repeats allowed, up to miss_cap)
   uint64_t *xdot, *xlab;
+  uint8_t *xcar;  // per executed vertex: 1 if carried (host metadata to drop)
   uint8_t *blocked;
   uint64_t *miss;
   uint32_t miss_cap;

@@ -228,6 +228,13 @@ __global__ void __launch_bounds__(kThreads)
       block_scan(mine, s_w, &left);
     }
     if (!left) break;
+    // round 0: nothing is assigned yet, so W over the unassigned vertices is
+    // H itself
+    if (round == 0) {
+      for (int v = tid; v < V; v += kThreads)
+        if (!s_blk[v]) s_W[v] = s_H[v];
+      __syncthreads();
+    } else
     sweep(V, s_ch, [&](int v) {
       if (s_blk[v] || s_R[v] != kNone) return false;
       uint32_t h = s_W[v];
@@ -330,6 +337,7 @@ __global__ void __launch_bounds__(kThreads)
     const uint16_t v = s_sv[ok[i] & 0x7FF];
     p.xdot[i] = s_dot[v];
     p.xlab[i] = s_key[v];
+    p.xcar[i] = v < p.P ? 1 : 0;
   }
   for (int v = tid; v < V; v += kThreads) p.blocked[v] = s_blk[v];
   // survivors, compacted in arrival order into the next vertex set
