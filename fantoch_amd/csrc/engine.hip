@@ -100,9 +100,10 @@ __global__ void __launch_bounds__(kThreads)
                const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
                uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
                uint32_t *__restrict__ emin, uint32_t slack, uint32_t *__restrict__ counts,
-               uint32_t dmask) {
-  __shared__ uint32_t s_h[256];
+               uint32_t dmask, uint32_t shift0) {
+  __shared__ uint32_t s_h[512];  // the sort's first digit (up to 9 bits, from bit shift0)
   s_h[threadIdx.x] = 0;
+  s_h[threadIdx.x + 256] = 0;
   __syncthreads();
   const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(M, base + uint32_t(kTile));
   const uint32_t per = fq * k;
@@ -121,10 +122,11 @@ __global__ void __launch_bounds__(kThreads)
     }
     keys[x] = key;
     vals[x] = val;
-    atomicAdd(&s_h[key & dmask], 1u);
+    atomicAdd(&s_h[(key >> shift0) & dmask], 1u);
   }
   __syncthreads();
-  if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
+  for (uint32_t d = threadIdx.x; d <= dmask; d += kThreads)
+    counts[size_t(blockIdx.x) * (dmask + 1) + d] = s_h[d];
   // placement base: the smallest first entry of the replicas' slices, less a
   // slack for entries that arrive before earlier commands.  Only a hint (see
   // above).  An exact minimum by atomics serialised the kernel on one word:
@@ -1393,6 +1395,10 @@ struct EngineDevice {
   int code_isb = -1;
   int pk_sb = 0;  // the per-key sort's packed dots: sequence bits
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
+  // per batch: low key bits every log holds constant (partial replication: a
+  // process sees only its shard's keys, key mod shards = h), which the
+  // chunked path's sort skips -- a (log, key) segment stays contiguous
+  std::vector<uint32_t> h_kshift;
   // per batch: (seq bits, packed bits) of its dots, src << sb | seq (0: wider
   // than 32 bits), so the per-key sort can move 4-byte dots
   std::vector<std::pair<int, int>> h_dpack;
@@ -1640,6 +1646,7 @@ struct EngineDevice {
       FH_CHECK(h_dot[i] != ~0ull && (h_dot[i] >> 56) != 0, FH_EINVAL,
                "stage: dot (255, 2^56 - 1) is reserved and ProcessId 0 is not a process");
     std::vector<uint32_t> ent, lo;
+    h_kshift.assign(nb, 0);
     if (d.views && elem) {
       // element logs: every position (c·fq + j)·k + s of a batch in exactly
       // one log (a replica may hold several of a command's key slots)
@@ -1655,18 +1662,33 @@ struct EngineDevice {
         const uint64_t base = h_off[b * np];
         FH_CHECK(subset || h_off[(b + 1) * np] - base == per_b, FH_EINVAL,
                  "element logs: a batch's logs must hold n * views * keys_per_cmd entries");
+        uint32_t kdiff = 0;  // OR over logs of the keys' differences from the log's first
+        const uint32_t kk = d.keys_per_cmd, pc = uint32_t(fq) * kk;
         for (size_t r = 0; r < np; r++) {
           lo[b * (np + 1) + r] = uint32_t(h_off[b * np + r] - base);
           FH_CHECK(h_off[b * np + r + 1] >= h_off[b * np + r], FH_EINVAL, "logs: offsets");
+          uint32_t k0 = ~0u;
           for (uint64_t q = h_off[b * np + r]; q < h_off[b * np + r + 1]; q++) {
             const uint32_t p = h_cmd[q];
             FH_CHECK(p < per_b && !seen[p], FH_EINVAL,
                      "element logs: every element position must appear in exactly one log");
+            if (p < per_b) {
+              const uint32_t key = k32[b * nk + size_t(p / pc) * kk + p % kk];
+              if (k0 == ~0u) k0 = key;
+              kdiff |= key ^ k0;
+            }
             seen[p] = 1;
             ent[q] = p;
           }
         }
         lo[b * (np + 1) + np] = uint32_t(h_off[(b + 1) * np] - base);
+        // up to 4 constant low bits (the shard of key mod 2^jb); a power-of-
+        // two key space keeps them below the replica bits of the composite
+        const int kb = bits_for(key_space);
+        const bool pow2 = (key_space & (key_space - 1)) == 0;
+        uint32_t jb = kdiff ? uint32_t(__builtin_ctz(kdiff)) : 4u;
+        jb = std::min<uint32_t>(jb, 4);
+        h_kshift[b] = pow2 && int(jb) < kb ? jb : 0u;
       }
     } else if (d.views) {
       const size_t np = d.nproc;
@@ -1902,6 +1924,12 @@ struct EngineDevice {
       // 23-bit composite)
       const bool pow2 = (key_space & (key_space - 1)) == 0;
       const int bits = pow2 ? bits_for(key_space) : bits_for(uint64_t(np + 1) * key_space);
+      // low key bits every log holds constant (partial replication) are not
+      // sorted: equal higher bits within one log mean equal keys, so the
+      // (log, key) segments stay contiguous; 17 bits sort in two 9-bit passes
+      const uint32_t jb = pow2 && b < h_kshift.size() ? h_kshift[b] : 0u;
+      const int sbits = bits - int(jb);
+      const int sdb = sbits > 16 && sbits <= 18 ? 9 : sort_digit_bits(sbits, 4);
       const uint32_t per_entry = elem ? 1u : k;  // elements per log entry
       const uint32_t *bent = lent.get() + (codes_only ? 0 : b * size_t(n) * fq * (elem ? k : 1));
       for (uint32_t c = 0; c < nch; c++) {
@@ -1918,13 +1946,13 @@ struct EngineDevice {
         uint32_t *ks = nullptr;
         const uint32_t tiles = (Mc + kTile - 1) / kTile;
         sort_ws.prepare(tiles, 1, stream);
-        const int db = sort_digit_bits(bits, 4);
+        const int db = sdb;
         probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys, dim3(tiles),
                       dim3(kThreads), stream, Mc, k, fq, np, uint32_t(elem), lc, bent, bkey,
                       uint32_t(key_space), lk, lv, pbase + c, place_slack, sort_ws.meta.get(),
-                      (1u << db) - 1);
+                      (1u << db) - 1, jb);
         sort_pairs_counted<uint32_t, uint32_t>(lk, lv, sk32b.ensure(Mc + 1), svb.ensure(Mc + 1), Mc,
-                                               bits, sort_ws, stream, &ks, &vs, db);
+                                               sbits, sort_ws, stream, &ks, &vs, db, int(jb));
         // heads read the latest table, tails then make the chunk's last
         // commands the latest (command-log references); the sort's other
         // buffer pair takes the bucketed (position, code)
