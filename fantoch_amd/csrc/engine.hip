@@ -416,20 +416,6 @@ __global__ void __launch_bounds__(1024)
 // positions differ by at most 3W + 1 < 2^(qb-1): the sign of the difference
 // modulo 2^qb decides.  The host checks 3W + 1 < 2^(qb-1) before taking
 // this path.
-// command-level KeyDeps code slots: kSlotWords u32 per command, the fq <= 4
-// codes first, the in-batch deps' packed dots (src << sb | seq) from word
-// kSlotDots -- one 32-B store per command, so the union gathers no dots
-constexpr uint32_t kSlotWords = 8, kSlotDots = 4;
-
-// the key sort's value in the command-level path: command | meta (u64, as
-// two words) and the command's packed dot, carried to the search's LDS tile
-struct CmdVal {
-  uint32_t lo, hi, dot;
-  CmdVal() = default;
-  __host__ __device__ constexpr CmdVal(int) : lo(0), hi(0), dot(0) {}
-  __host__ __device__ uint64_t v() const { return (uint64_t(hi) << 32) | lo; }
-};
-
 struct CmdMeta {
   uint32_t fq, rb, qb, vb;  // views; bits per view: replica, arrival, both
   uint32_t kb, cb;          // key word: meta from bit kb; value: command in [0, cb)
@@ -467,9 +453,8 @@ struct CmdMeta {
 // counts for the sort's first pass (sort_pairs_counted).
 __global__ void __launch_bounds__(kThreads)
     k_cmd_pack(uint32_t n, CmdMeta cm, const uint32_t *__restrict__ key32,
-               const uint32_t *__restrict__ rec, const uint64_t *__restrict__ dot, int sb,
-               uint32_t *__restrict__ kw, CmdVal *__restrict__ val,
-               uint32_t *__restrict__ counts, uint32_t dmask) {
+               const uint32_t *__restrict__ rec, uint32_t *__restrict__ kw,
+               uint64_t *__restrict__ val, uint32_t *__restrict__ counts, uint32_t dmask) {
   __shared__ uint32_t s_h[256];
   s_h[threadIdx.x] = 0;
   __syncthreads();
@@ -481,13 +466,7 @@ __global__ void __launch_bounds__(kThreads)
       const uint32_t r = rec[size_t(x) * cm.fq + j];
       m |= ((uint64_t(r >> kRecT) << cm.qb) | (r & cm.qmask)) << (j * cm.vb);
     }
-    const uint64_t v = uint64_t(x) | (m << cm.cb);
-    const uint64_t d = dot[x];
-    CmdVal cv;
-    cv.lo = uint32_t(v);
-    cv.hi = uint32_t(v >> 32);
-    cv.dot = uint32_t(((d >> 56) << sb) | (d & 0x00FFFFFFFFFFFFFFull));
-    val[x] = cv;
+    val[x] = uint64_t(x) | (m << cm.cb);
     kw[x] = key | uint32_t((m >> (64 - cm.cb)) << cm.kb);
     atomicAdd(&s_h[key & dmask], 1u);
   }
@@ -558,10 +537,10 @@ struct ViewScan {
 template <uint32_t FQ, int TH>
 __global__ void __launch_bounds__(TH)
     k_cmd_search(uint32_t n, CmdMeta cm, uint32_t K, uint32_t np, const uint32_t *__restrict__ kws,
-                 const CmdVal *__restrict__ vals, const uint64_t *__restrict__ latest,
+                 const uint64_t *__restrict__ vals, const uint64_t *__restrict__ latest,
                  uint32_t *__restrict__ code, uint8_t *__restrict__ tailm) {
   constexpr int kSpan = TH + 2 * kSrchHalo;
-  __shared__ uint32_t s_key[kSpan], s_c[kSpan], s_d[kSpan];
+  __shared__ uint32_t s_key[kSpan], s_c[kSpan];
   __shared__ uint32_t s_q[kSpan * kSrchMaxRep];
   const uint32_t tid = threadIdx.x, core = blockIdx.x * TH, i = core + tid;
   const uint32_t lo = core > uint32_t(kSrchHalo) ? core - kSrchHalo : 0u;
@@ -571,12 +550,10 @@ __global__ void __launch_bounds__(TH)
   __syncthreads();
   for (uint32_t x = tid; x < span; x += TH) {
     const uint32_t kw = kws[lo + x];
-    const CmdVal cv = vals[lo + x];
-    const uint64_t v = cv.v();
+    const uint64_t v = vals[lo + x];
     const uint64_t m = cm.meta(kw, v);
     s_key[x] = kw & cm.kmask;
     s_c[x] = uint32_t(v & cm.cmask);
-    s_d[x] = cv.dot;
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) s_q[x * np + cm.rep(m, j)] = cm.arr(m, j);
   }
@@ -584,7 +561,7 @@ __global__ void __launch_bounds__(TH)
   if (i >= n) return;
   const uint32_t me = i - lo;
   const uint32_t key = s_key[me], c = s_c[me];
-  const uint64_t m0 = cm.meta(kws[i], vals[i].v());
+  const uint64_t m0 = cm.meta(kws[i], vals[i]);
   // all views in one pass over the neighbours (shared key and command
   // loads); each view's scan stops on its own
   ViewScan vs[FQ];
@@ -602,29 +579,21 @@ __global__ void __launch_bounds__(TH)
   }
   // backward: the staged span, then global memory (a neighbour outside the
   // span is unpacked from the packed arrays)
-  // the best candidate's dot rides along (candidates come from both
-  // directions: a later command may reach the replica earlier)
-  uint32_t bd[FQ];
-#pragma unroll
-  for (uint32_t j = 0; j < FQ; j++) bd[j] = 0;
   bool go = true;
   for (uint32_t x = me; go && x > 0;) {
     x--;
     const bool sk = s_key[x] == key;
-    const uint32_t cc = s_c[x], dd = s_d[x];
+    const uint32_t cc = s_c[x];
     go = false;
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) {
-      const uint32_t b0 = vs[j].bc;
       on[j] = vs[j].back(sk & on[j], cc, s_q[x * np + rr[j]]);
-      bd[j] = vs[j].bc != b0 ? dd : bd[j];
       go |= on[j];
     }
   }
   for (uint32_t ip = lo; go && ip-- > 0;) {
     const uint32_t kw = kws[ip];
-    const CmdVal cv = vals[ip];
-    const uint64_t v = cv.v();
+    const uint64_t v = vals[ip];
     const uint64_t m = cm.meta(kw, v);
     const bool sk = (kw & cm.kmask) == key;
     const uint32_t cc = uint32_t(v & cm.cmask);
@@ -633,9 +602,7 @@ __global__ void __launch_bounds__(TH)
     for (uint32_t j = 0; j < FQ; j++) {
       uint32_t t = kNoArr;
       cm.find(m, rr[j], &t);
-      const uint32_t b0 = vs[j].bc;
       on[j] = vs[j].back(sk & on[j], cc, t);
-      bd[j] = vs[j].bc != b0 ? cv.dot : bd[j];
       go |= on[j];
     }
   }
@@ -645,20 +612,17 @@ __global__ void __launch_bounds__(TH)
   for (uint32_t j = 0; j < FQ; j++) on[j] = true;
   for (uint32_t x = me + 1; go && x < span; x++) {
     const bool sk = s_key[x] == key;
-    const uint32_t cc = s_c[x], dd = s_d[x];
+    const uint32_t cc = s_c[x];
     go = false;
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) {
-      const uint32_t b0 = vs[j].bc;
       on[j] = vs[j].fwd(sk & on[j], cc, s_q[x * np + rr[j]]);
-      bd[j] = vs[j].bc != b0 ? dd : bd[j];
       go |= on[j];
     }
   }
   for (uint32_t ip = hi; go && ip < n; ip++) {
     const uint32_t kw = kws[ip];
-    const CmdVal cv = vals[ip];
-    const uint64_t v = cv.v();
+    const uint64_t v = vals[ip];
     const uint64_t m = cm.meta(kw, v);
     const bool sk = (kw & cm.kmask) == key;
     const uint32_t cc = uint32_t(v & cm.cmask);
@@ -667,9 +631,7 @@ __global__ void __launch_bounds__(TH)
     for (uint32_t j = 0; j < FQ; j++) {
       uint32_t t = kNoArr;
       cm.find(m, rr[j], &t);
-      const uint32_t b0 = vs[j].bc;
       on[j] = vs[j].fwd(sk & on[j], cc, t);
-      bd[j] = vs[j].bc != b0 ? cv.dot : bd[j];
       go |= on[j];
     }
   }
@@ -685,29 +647,30 @@ __global__ void __launch_bounds__(TH)
     }
     msk |= vs[j].tail ? 1u << j : 0u;
   }
-  // the views' codes and their in-batch deps' dots leave in one 32-B slot
-  // per command (one line: a random store costs a line whatever its size)
-  uint32_t w[kSlotWords];
+  // the views' codes leave in one store per command (tried: 16-B aligned
+  // stores and non-temporal stores, both flat; round 3)
+  uint32_t *o = code + size_t(c) * FQ;
+  if constexpr (FQ == 3) {
+    *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(o) =
+        HIP_vector_type<uint32_t, 3>(cds[0], cds[1], cds[2]);
+  } else if constexpr (FQ == 4) {
+    *reinterpret_cast<uint4 *>(o) = make_uint4(cds[0], cds[1], cds[2], cds[3]);
+  } else {
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    w[j] = j < FQ ? cds[j] : 0u;
-    w[kSlotDots + j] = j < FQ ? bd[j] : 0u;
+    for (uint32_t j = 0; j < FQ; j++) o[j] = cds[j];
   }
-  uint4 *o = reinterpret_cast<uint4 *>(code + size_t(c) * kSlotWords);
-  o[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  o[1] = make_uint4(w[4], w[5], w[6], w[7]);
   tailm[i] = uint8_t(msk);
 }
 
 // the tails become the replicas' latest entries (after every head's read)
 __global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *__restrict__ kws,
-                            const CmdVal *__restrict__ vals, const uint8_t *__restrict__ tailm,
+                            const uint64_t *__restrict__ vals, const uint8_t *__restrict__ tailm,
                             uint64_t *__restrict__ latest, uint64_t log_base) {
   GRID_STRIDE(i, n) {
     const uint32_t msk = tailm[i];
     if (!msk) continue;
     const uint32_t kw = kws[i];
-    const uint64_t v = vals[i].v();
+    const uint64_t v = vals[i];
     const uint64_t m = cm.meta(kw, v);
     const uint32_t key = kw & cm.kmask, c = uint32_t(v & cm.cmask);
     for (uint32_t j = 0; j < cm.fq; j++)
@@ -831,27 +794,21 @@ __device__ __forceinline__ void cmd_union_regs(
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n,
     const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, uint32_t vbase,
-    bool edges_at_deps, uint32_t &fwd, uint32_t cs, int isb) {
+    bool edges_at_deps, uint32_t &fwd) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
-  uint64_t inl[kRegSlots];  // isb >= 0: the in-batch deps' dots, from the code slot
   bool missing = false;
 #pragma unroll
   for (uint32_t t = 0; t < kRegSlots; t++) {
     r[t] = ~0ull;
     vv[t] = ~0u;
-    inl[t] = 0;
     if (t < S) {
       uint64_t x = 0;
       uint32_t v = 0;
       const int kind =
-          decode_dep(dep_code[size_t(i) * cs + t], &v, &x, dlog, bbase, n);
+          decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
       if (kind == 1) {
         vv[t] = v;
-        if (isb >= 0) {
-          const uint32_t pd = uint32_t(dep_code[size_t(i) * cs + kSlotDots + t]);
-          inl[t] = (uint64_t(pd >> isb) << 56) | (pd & ((1u << isb) - 1));
-        }
       } else if (kind == 2) {
         r[t] = x;
         if ((x & 0x00FFFFFFFFFFFFFFull) > frontier[x >> 56]) missing = true;
@@ -868,7 +825,7 @@ __device__ __forceinline__ void cmd_union_regs(
     bool dup = vv[t] == ~0u;
 #pragma unroll
     for (uint32_t q = 0; q < t; q++) dup |= vv[q] == vv[t];
-    if (!dup) r[t] = isb >= 0 ? inl[t] : dot[vv[t]];
+    if (!dup) r[t] = dot[vv[t]];
   }
   // bitonic sort of the 16 register slots, ascending
 #pragma unroll
@@ -946,9 +903,7 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
                              uint64_t bbase, const uint32_t *__restrict__ out_off,
                              uint32_t *__restrict__ err, uint32_t vbase, uint32_t edges_at_deps,
-                             unsigned long long *__restrict__ nfwd, uint32_t cs, int isb) {
-  // cs: the code row stride (S, or kSlotWords for the command-level path's
-  // slots); isb >= 0: the slots carry the in-batch deps' packed dots
+                             unsigned long long *__restrict__ nfwd) {
   // uniform: the register path, with a sorting network sized to the row
   const uint32_t cn = n;
   const bool ead = edges_at_deps != 0 && out_off != nullptr;
@@ -962,18 +917,17 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     const uint32_t lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
     for (size_t j = size_t(lb) * blockDim.x + threadIdx.x; j < cn; j += size_t(nb) * blockDim.x)
       cmd_union_regs<4>(uint32_t(j), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                        blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd, cs,
-                        isb);
+                        blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd);
   } else if (S <= 8) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<8>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd, cs, isb);
+                        nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd);
     }
   } else if (S <= kRegSlots) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<kRegSlots>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
                                 blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase, ead,
-                                fwd, cs, isb);
+                                fwd);
     }
   } else {
     GRID_STRIDE(i, cn) {
@@ -1029,7 +983,7 @@ template <uint32_t kSlots, class CT>
 __device__ __forceinline__ uint32_t cmd_count_regs(uint32_t i, uint32_t S,
                                                    const CT *__restrict__ dep_code,
                                                    const uint64_t *__restrict__ dlog,
-                                                   uint64_t bbase, uint32_t n, uint32_t cs) {
+                                                   uint64_t bbase, uint32_t n) {
   uint64_t r[kSlots];
 #pragma unroll
   for (uint32_t t = 0; t < kSlots; t++) {
@@ -1037,7 +991,7 @@ __device__ __forceinline__ uint32_t cmd_count_regs(uint32_t i, uint32_t S,
     if (t < S) {
       uint64_t x = 0;
       uint32_t v = 0;
-      const int kind = decode_dep(dep_code[size_t(i) * cs + t], &v, &x, dlog, bbase, n);
+      const int kind = decode_dep(dep_code[size_t(i) * S + t], &v, &x, dlog, bbase, n);
       r[t] = kind == 1 ? uint64_t(v) : kind == 2 ? x : ~0ull;  // dots >= 2^56 > vids
     }
   }
@@ -1055,13 +1009,13 @@ __device__ __forceinline__ uint32_t cmd_count_regs(uint32_t i, uint32_t S,
 template <class CT>
 __global__ void k_cmd_count(uint32_t n, uint32_t S, const CT *__restrict__ dep_code,
                             const uint64_t *__restrict__ dlog, uint64_t bbase,
-                            uint32_t *__restrict__ cnt, uint32_t cs) {
+                            uint32_t *__restrict__ cnt) {
   if (S <= 4) {
-    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<4>(i, S, dep_code, dlog, bbase, n, cs);
+    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<4>(i, S, dep_code, dlog, bbase, n);
   } else if (S <= 8) {
-    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<8>(i, S, dep_code, dlog, bbase, n, cs);
+    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<8>(i, S, dep_code, dlog, bbase, n);
   } else {
-    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<kRegSlots>(i, S, dep_code, dlog, bbase, n, cs);
+    GRID_STRIDE(i, n) cnt[i] = cmd_count_regs<kRegSlots>(i, S, dep_code, dlog, bbase, n);
   }
 }
 
@@ -1388,11 +1342,7 @@ struct EngineDevice {
   DBuf<uint32_t> tail_defer;  // k_bucket_codes: deferred (segment, command) per workgroup
   DBuf<uint32_t> vrec;        // command-level views path: replica | arrival per element
   DBuf<uint8_t> tailm;        // command-level views path: tail views per sorted command
-  DBuf<CmdVal> cv64a, cv64b;  // command-level views path: packed sort values
-  // this run's dependency-code rows: stride and, for the command-level
-  // path's slots, the packed dots' sequence bits (-1: no inline dots)
-  uint32_t code_stride = 0;
-  int code_isb = -1;
+  DBuf<uint64_t> cv64a, cv64b;  // command-level views path: packed sort values
   int pk_sb = 0;  // the per-key sort's packed dots: sequence bits
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
   // per batch: low key bits every log holds constant (partial replication: a
@@ -1882,14 +1832,10 @@ struct EngineDevice {
       sorted_keys32 = ks;
     } else if (CmdMeta cm; cmd_meta(b, k, fq, n, &cm)) {
       sv_fused = false;
-      cmd_views(b, n, fq, M, bkey, bdot, bbase, cm);
-      code_stride = kSlotWords;
-      code_isb = h_dpack[b].first;
+      cmd_views(b, n, fq, M, bkey, bbase, cm);
       mark("keydeps_views");
     } else {
       sv_fused = false;
-      code_stride = S;
-      code_isb = -1;
       // every replica's KeyDeps over its arrival log, in chunks: chunk c
       // takes the c-th slice of each log (a replica's slices stay in arrival
       // order, so the latest table carries each (replica, key) segment across
@@ -1990,9 +1936,7 @@ struct EngineDevice {
       const char *e = getenv("FH_VIEW_CMD");
       return !(e && *e == '0');
     }();
-    // (the code slots carry the dots packed to 32 bits: h_dpack)
     if (!on || k != 1 || fq > 4 || desc.nproc > uint32_t(kSrchMaxRep) || b >= h_win.size() ||
-        b >= h_dpack.size() || h_dpack[b].second == 0 ||
         (desc.flags & FH_STREAM_ELEMENT_LOGS) ||
         n >= (1u << kRecT) || n < 2)
       return false;
@@ -2020,7 +1964,7 @@ struct EngineDevice {
   }
 
   void cmd_views(size_t b, uint32_t n, uint32_t fq, uint32_t M, const uint32_t *bkey,
-                 const uint64_t *bdot, uint64_t bbase, const CmdMeta &cm) {
+                 uint64_t bbase, const CmdMeta &cm) {
     const uint32_t np = desc.nproc;
     LogOffs lo{};
     const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
@@ -2037,28 +1981,27 @@ struct EngineDevice {
     sort_ws.prepare(tiles, 1, stream);
     const int db = sort_digit_bits(key_bits, 4);
     uint32_t *kwa = sk32a.ensure(n + 1);
-    CmdVal *va = cv64a.ensure(n + 1);
-    // reads the key, fq records and the dot, writes the key word and the
-    // value (command | meta, packed dot)
-    probed_launch("cmd_pack", double(n) * (4.0 + 4.0 * fq + 8.0 + 4.0 + 12.0), k_cmd_pack,
-                  dim3(tiles), dim3(kThreads), stream, n, cm, bkey, (const uint32_t *)rec, bdot,
-                  h_dpack[b].first, kwa, va, sort_ws.meta.get(), (1u << db) - 1);
+    uint64_t *va = cv64a.ensure(n + 1);
+    // reads the key and fq records, writes the key word and the value
+    probed_launch("cmd_pack", double(n) * (4.0 + 4.0 * fq + 4.0 + 8.0), k_cmd_pack, dim3(tiles),
+                  dim3(kThreads), stream, n, cm, bkey, (const uint32_t *)rec, kwa, va,
+                  sort_ws.meta.get(), (1u << db) - 1);
     uint32_t *ks = nullptr;
-    CmdVal *vs = nullptr;
-    sort_pairs_counted<uint32_t, CmdVal>(kwa, va, sk32b.ensure(n + 1), cv64b.ensure(n + 1), n,
-                                         key_bits, sort_ws, stream, &ks, &vs, db);
+    uint64_t *vs = nullptr;
+    sort_pairs_counted<uint32_t, uint64_t>(kwa, va, sk32b.ensure(n + 1), cv64b.ensure(n + 1), n,
+                                           key_bits, sort_ws, stream, &ks, &vs, db);
     uint8_t *tm = tailm.ensure(n + 1);
     // reads the sorted key words and values (12 B, neighbours from LDS) and
     // the heads' latest entries, writes fq codes and the tail mask.  1024
     // threads (tried 256 / 512: flat)
-    uint32_t *codes = dep32.ensure(size_t(n) * kSlotWords + 1);
-    const double sb = double(n) * (16.0 + 4.0 * kSlotWords + 1.0);
+    uint32_t *codes = dep32.ensure(size_t(M) + 1);
+    const double sb = double(n) * (12.0 + fq * 4.0 + 1.0);
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
     auto go = [&](auto kern) {
       probed_launch("cmd_search", sb, kern, dim3((n + kSrchThreads - 1) / kSrchThreads),
                     dim3(kSrchThreads), stream, n, cm, K, np, (const uint32_t *)ks,
-                    (const CmdVal *)vs, lat, codes, tm);
+                    (const uint64_t *)vs, lat, codes, tm);
     };
     switch (fq) {
       case 1: go(k_cmd_search<1, kSrchThreads>); break;
@@ -2066,8 +2009,8 @@ struct EngineDevice {
       case 3: go(k_cmd_search<3, kSrchThreads>); break;
       default: go(k_cmd_search<4, kSrchThreads>); break;
     }
-    k_cmd_tails<<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks,
-                                                  (const CmdVal *)vs, tm, views_latest(), bbase);
+    k_cmd_tails<<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks, vs, tm,
+                                                  views_latest(), bbase);
   }
 
   // The chunk's dependency codes -> dep32 through the placement pass: bucket
@@ -2129,11 +2072,10 @@ struct EngineDevice {
       ddot = o_dep.ensure(M + 1);
       if (views)
         k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, stream>>>(
-            n, S, (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(), bbase, dcnt,
-            code_stride);
+            n, S, (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(), bbase, dcnt);
       else
         k_cmd_count<uint64_t><<<grid_for(n, B), B, 0, stream>>>(
-            n, S, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(), bbase, dcnt, S);
+            n, S, (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(), bbase, dcnt);
       exclusive_scan_u32(dcnt, o_dep_off.get(), n, scan_ws, stream);
       mark("keydeps_count");
     } else {
@@ -2153,14 +2095,14 @@ struct EngineDevice {
                     (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
                     scal.get(), edges_at_deps ? (uint32_t *)nullptr : ecnt, bbase, doff,
-                    scal.get() + 1, 0u, uint32_t(edges_at_deps), fwd, code_stride, code_isb);
+                    scal.get() + 1, 0u, uint32_t(edges_at_deps), fwd);
     else
       probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
                     k_cmd_engine<uint64_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
                     (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
                     scal.get(), ecnt, bbase, doff, scal.get() + 1, 0u, 0u,
-                    (unsigned long long *)nullptr, S, -1);
+                    (unsigned long long *)nullptr);
     mark("keydeps_union");
     if (deps_only) return;  // the committed deps are the output (partial replication)
     const uint32_t *gdst = dd, *goff = nullptr;
@@ -2379,14 +2321,14 @@ void union_rows(uint32_t n, uint32_t S, const uint32_t *codes, const uint64_t *d
                 uint32_t *dst, uint32_t *ecnt, uint32_t *scal, ScanWorkspace &ws, hipStream_t s) {
   FH_CHECK(S <= kRegSlots, FH_ENOTIMPL, "range union: at most 16 slots per command");
   FH_HIP(hipMemsetAsync(scal, 0, 2 * sizeof(uint32_t), s));
-  k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, s>>>(n, S, codes, dot, 0, dcnt, S);
+  k_cmd_count<uint32_t><<<grid_for(n, B), B, 0, s>>>(n, S, codes, dot, 0, dcnt);
   exclusive_scan_u32(dcnt, dep_off, n, ws, s);
   const uint32_t g = S <= 4 ? (grid_for(n, B, 1u << 22) + 7) / 8 * 8 : grid_for(n, B);
   probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
                 k_cmd_engine<uint32_t>, dim3(g), dim3(B), s, n, S, dot, codes, dot,
                 (const uint64_t *)nullptr, dep_dot, dcnt, dst, (uint8_t *)nullptr, scal, ecnt,
                 uint64_t(0), (const uint32_t *)dep_off, scal + 1, vbase, 0u,
-                (unsigned long long *)nullptr, S, -1);
+                (unsigned long long *)nullptr);
 }
 
 }  // namespace fh
