@@ -89,6 +89,63 @@ __device__ void bitonic(uint64_t *key, uint16_t *val, int n2) {
   __syncthreads();
 }
 
+// Each 64-element block of key[0, n2) sorted ascending in place, with an
+// optional u16 payload: bitonic levels up to 64 only, so every stage stays
+// inside one wave's elements (wave barriers; the last level merges every
+// block upwards).
+__device__ void sort_blocks64(uint64_t *key, uint16_t *val, int n2) {
+  for (int k = 2; k <= 64; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int x = threadIdx.x; x < n2; x += kThreads) {
+        const int p = x ^ j;
+        if (p > x) {
+          const uint64_t a = key[x], b = key[p];
+          const bool up = k == 64 || (x & k) == 0;
+          if (up ? a > b : a < b) {
+            key[x] = b;
+            key[p] = a;
+            if (val) {
+              const uint16_t t = val[x];
+              val[x] = val[p];
+              val[p] = t;
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  __syncthreads();
+}
+
+// Global rank of element x of the block-sorted key[0, n2): its index in its
+// block plus, per other block, the elements before it there (binary search;
+// equal keys order by block, so ranks are unique and the order stable).
+__device__ uint32_t merge_rank(const uint64_t *key, int n2, int x) {
+  const uint64_t kx = key[x];
+  const int bx = x >> 6;
+  uint32_t r = uint32_t(x & 63);
+  for (int b = 0; b < (n2 >> 6); b++) {
+    if (b == bx) continue;
+    const uint64_t *blk = key + (b << 6);
+    int lo = 0, hi = 64;
+    if (b < bx) {  // upper bound: equal keys of earlier blocks come first
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (blk[mid] <= kx) lo = mid + 1; else hi = mid;
+      }
+    } else {  // lower bound
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (blk[mid] < kx) lo = mid + 1; else hi = mid;
+      }
+    }
+    r += uint32_t(lo);
+  }
+  return r;
+}
+
 __device__ int find_lds(const uint64_t *sd, int n, uint64_t d) {
   int lo = 0, hi = n;
   while (lo < hi) {
@@ -138,8 +195,25 @@ __global__ void __launch_bounds__(kThreads)
     s_sv[x] = uint16_t(x);
   }
   __syncthreads();
-  // 1. dot -> vid index; a dot indexed twice (mod.rs:235-240)
-  bitonic(s_sd, s_sv, n2);
+  // 1. dot -> vid index; a dot indexed twice (mod.rs:235-240).  Blocks of 64
+  // sorted per wave (in s_key / s_W, free until the SCC phases), then every
+  // dot placed at its merge rank
+  if (n2 >= 128) {
+    for (int x = tid; x < n2; x += kThreads) {
+      s_key[x] = s_sd[x];
+      s_W[x] = s_sv[x];
+    }
+    __syncthreads();
+    sort_blocks64(s_key, s_W, n2);
+    for (int x = tid; x < n2; x += kThreads) {
+      const uint32_t r = merge_rank(s_key, n2, x);
+      s_sd[r] = s_key[x];
+      s_sv[r] = s_W[x];
+    }
+    __syncthreads();
+  } else {
+    bitonic(s_sd, s_sv, n2);
+  }
   for (int x = tid; x < V; x += kThreads) {
     s_rank[s_sv[x]] = uint16_t(x);
     if (x > 0 && s_sd[x] == s_sd[x - 1]) s_err = 1;
@@ -326,18 +400,30 @@ __global__ void __launch_bounds__(kThreads)
     if (v < V) s_key[v] = lab[j];  // label per vertex
   }
   __syncthreads();
-  bitonic(ok, nullptr, n2);
   uint32_t nexec = 0;
   {
     uint32_t mine = 0;
     for (int v = tid; v < V; v += kThreads) mine += s_blk[v] ? 0u : 1u;
     block_scan(mine, s_w, &nexec);
   }
-  for (uint32_t i = tid; i < nexec; i += kThreads) {
-    const uint16_t v = s_sv[ok[i] & 0x7FF];
+  // the order keys are unique (the dot rank): each executed vertex is written
+  // at its key's rank (blocks of 64 per wave, then merge ranks; the pending
+  // ones' all-ones keys rank last)
+  auto emit = [&](uint32_t i, uint64_t key) {
+    const uint16_t v = s_sv[key & 0x7FF];
     p.xdot[i] = s_dot[v];
     p.xlab[i] = s_key[v];
     p.xcar[i] = v < p.P ? 1 : 0;
+  };
+  if (n2 >= 128) {
+    sort_blocks64(ok, nullptr, n2);
+    for (int x = tid; x < n2; x += kThreads) {
+      const uint32_t r = merge_rank(ok, n2, x);
+      if (r < nexec) emit(r, ok[x]);
+    }
+  } else {
+    bitonic(ok, nullptr, n2);
+    for (uint32_t i = tid; i < nexec; i += kThreads) emit(i, ok[i]);
   }
   for (int v = tid; v < V; v += kThreads) p.blocked[v] = s_blk[v];
   // survivors, compacted in arrival order into the next vertex set
