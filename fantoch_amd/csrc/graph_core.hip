@@ -237,14 +237,13 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int lane) {
 // One wave per window [64w, 64w+128): lane l owns rows l and 64+l of the
 // window's reachability bit-matrix (two u64 words per row).  Warshall over
 // the 128 pivots, broadcast by readlane; then each vertex unites with the
-// smallest vertex it mutually reaches.
+// smallest vertex it mutually reaches (its row AND its column).
 __global__ void __launch_bounds__(256)
     k_windows(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride, const uint32_t *__restrict__ dst,
               const uint8_t *__restrict__ blocked, uint32_t *parent, uint32_t nwin,
               int any_blocked) {
   // any_blocked == 0: no vertex is pending, so the per-edge blocked[u]
   // gathers (a random byte per edge, C5: most of the kernel's traffic) go
-  __shared__ uint64_t s_rows[4][128][2];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t win = blockIdx.x * 4 + wv;
   if (win >= nwin) return;
@@ -285,33 +284,35 @@ __global__ void __launch_bounds__(256)
   FH_WARSHALL_HALF(0)
   FH_WARSHALL_HALF(1)
 #undef FH_WARSHALL_HALF
-  s_rows[wv][lane][0] = r[0][0];
-  s_rows[wv][lane][1] = r[0][1];
-  s_rows[wv][64 + lane][0] = r[1][0];
-  s_rows[wv][64 + lane][1] = r[1][1];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // columns of the closure (who reaches x), by ballots: lane l takes the
+  // columns of its vertices l and 64 + l; then the vertices x mutually
+  // reaches are row AND column, and the smallest of them below x is x's
+  // local SCC minimum -- no LDS, no per-candidate loop
+  uint64_t col[2][2] = {{0, 0}, {0, 0}};
+  for (int xl = 0; xl < 64; xl++) {
+    const uint64_t c00 = __ballot((r[0][0] >> xl) & 1);
+    const uint64_t c01 = __ballot((r[1][0] >> xl) & 1);
+    const uint64_t c10 = __ballot((r[0][1] >> xl) & 1);
+    const uint64_t c11 = __ballot((r[1][1] >> xl) & 1);
+    if (lane == xl) {
+      col[0][0] = c00;
+      col[0][1] = c01;
+      col[1][0] = c10;
+      col[1][1] = c11;
+    }
+  }
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const uint32_t x = h * 64 + lane;
     if (base + x >= V) continue;
-    // smallest u < x with x ->+ u and u ->+ x
-    for (int wd = 0; wd <= h; wd++) {
-      uint64_t cand = r[h][wd];
-      if (wd == h) cand &= (uint64_t(1) << (x & 63)) - 1;
-      bool found = false;
-      while (cand) {
-        const int b = __builtin_ctzll(cand);
-        cand &= cand - 1;
-        const uint32_t u = wd * 64 + b;
-        if ((s_rows[wv][u][x >> 6] >> (x & 63)) & 1) {
-          uf_union(parent, base + x, base + u);
-          found = true;
-          break;
-        }
-      }
-      if (found) break;
-    }
+    // u < x: word 0 (u < 64) and, for h = 1, word 1 below lane
+    uint64_t m0 = r[h][0] & col[h][0];
+    uint64_t m1 = h ? (r[h][1] & col[h][1]) & ((uint64_t(1) << lane) - 1) : 0ull;
+    if (!h) m0 &= (uint64_t(1) << lane) - 1;
+    if (m0)
+      uf_union(parent, base + x, base + uint32_t(__builtin_ctzll(m0)));
+    else if (m1)
+      uf_union(parent, base + x, base + 64 + uint32_t(__builtin_ctzll(m1)));
   }
 }
 
