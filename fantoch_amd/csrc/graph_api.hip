@@ -95,10 +95,12 @@ __global__ void k_append(Upload u, uint64_t *__restrict__ vdot, uint32_t *__rest
                          uint32_t *__restrict__ key, uint32_t *__restrict__ doff,
                          uint64_t *__restrict__ dep, uint32_t kbase, uint32_t dbase,
                          uint64_t *__restrict__ frontier, uint64_t *__restrict__ exc) {
-  const uint32_t m = max(max(u.n + 1, u.nk), max(u.nd, u.nf + u.ne));
+  const uint32_t m = max(max(u.n ? u.n + 1 : 0u, u.nk), max(u.nd, u.nf + u.ne));
   GRID_STRIDE(i, m) {
+    // rows only for a non-empty batch: with n == 0 the carried set's end
+    // offsets (koff[0] = koff[P] of the set) must stay as they are
     if (i < u.n) vdot[i] = u.dot[i];
-    if (i <= u.n) {
+    if (u.n && i <= u.n) {
       koff[i] = u.koff[i] + kbase;
       doff[i] = u.doff[i] + dbase;
     }
@@ -445,7 +447,7 @@ struct GraphDevice {
       u.key = reinterpret_cast<const uint32_t *>(dup + o_key);
       u.koff = reinterpret_cast<const uint32_t *>(dup + o_ko);
       u.doff = reinterpret_cast<const uint32_t *>(dup + o_do);
-      const uint32_t m = std::max(std::max(u.n + 1, u.nk), std::max(u.nd, u.nf + u.ne));
+      const uint32_t m = std::max(std::max(u.n ? u.n + 1 : 0u, u.nk), std::max(u.nd, u.nf + u.ne));
       k_append<<<grid_for(m, B), B, 0, stream>>>(u, ddot_v + P, dko + P, dk + W.KP, ddo + P,
                                                  dd + W.DP, W.KP, W.DP, d_frontier.get(),
                                                  d_exc.get());

@@ -8,6 +8,11 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 TAG=${TAG:-r04}
 mkdir -p $OUT
+if [ -n "$PRE_TESTS" ]; then
+  echo "== pre-tests $(date +%T)"
+  timeout -k 10 300 python -u -m pytest $PRE_TESTS -m gpu -x -q --timeout 240 --timeout-method thread > $OUT/pytest_pre_$TAG.log 2>&1 || { tail -30 $OUT/pytest_pre_$TAG.log; exit 1; }
+  tail -2 $OUT/pytest_pre_$TAG.log
+fi
 SMOKE=1 TESTS="${TESTS:-tests}" TAG=$TAG bash tools/gpu_r04.sh || exit 1
 echo "== c4 bench $(date +%T)"
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-configs --no-secondary --no-c5 --no-streaming > $OUT/bench_c4_$TAG.json 2> $OUT/bench_c4_$TAG.err || { tail -20 $OUT/bench_c4_$TAG.err; exit 1; }
