@@ -490,16 +490,20 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            uint32_t *H, uint32_t *changed, const uint32_t *__restrict__ prev,
-                           int nodone) {
+                           int nodone, int desc) {
   // nodone: the first round of the full coloring (nothing done yet): the
-  // done[] gathers per edge are skipped
+  // done[] gathers per edge are skipped.
+  // desc: blocks take the positions in descending order.  Ready times flow
+  // up along backward dependencies (an ascending launch cascades them) and
+  // down along forward ones (a descending launch does); launches alternate.
   // the previous launch of the group changed nothing: converged, return
   if (prev && ld_u32(prev) == 0) return;
   __shared__ AggTable<uint32_t> tb;
   agg_init<uint32_t, true>(tb);
   __syncthreads();
   {
-    const uint32_t j = blockIdx.x * B + threadIdx.x;
+    const uint32_t bj = desc ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+    const uint32_t j = bj * B + threadIdx.x;
     const uint32_t v = j < n ? FB_VID(j) : 0u;
     const bool act = j < n && !blocked[v] && !done[v];
     const uint32_t r = act ? rep[v] : 0u;
@@ -1123,7 +1127,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     converge(1, dbg_hprop, [&](uint32_t *changed, const uint32_t *prev) {
       k_fb_hprop<<<agg_blocks(n), B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er,
                                                   blocked.get(), done, rep.get(), H, changed, prev,
-                                                  int(first_full));
+                                                  int(first_full), int(dbg_hprop & 1));
     });
     if (!list && !recent_iter) {
       k_fb_save_h<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), H, hseed.ensure(V));
