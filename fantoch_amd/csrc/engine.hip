@@ -100,10 +100,9 @@ __global__ void __launch_bounds__(kThreads)
                const uint32_t *__restrict__ ent, const uint32_t *__restrict__ key32,
                uint32_t K, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
                uint32_t *__restrict__ emin, uint32_t slack, uint32_t *__restrict__ counts,
-               uint32_t dmask, uint32_t shift0) {
-  __shared__ uint32_t s_h[512];  // the sort's first digit (up to 9 bits, from bit shift0)
+               uint32_t dmask) {
+  __shared__ uint32_t s_h[256];
   s_h[threadIdx.x] = 0;
-  s_h[threadIdx.x + 256] = 0;
   __syncthreads();
   const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(M, base + uint32_t(kTile));
   const uint32_t per = fq * k;
@@ -122,11 +121,10 @@ __global__ void __launch_bounds__(kThreads)
     }
     keys[x] = key;
     vals[x] = val;
-    atomicAdd(&s_h[(key >> shift0) & dmask], 1u);
+    atomicAdd(&s_h[key & dmask], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d <= dmask; d += kThreads)
-    counts[size_t(blockIdx.x) * (dmask + 1) + d] = s_h[d];
+  if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
   // placement base: the smallest first entry of the replicas' slices, less a
   // slack for entries that arrive before earlier commands.  Only a hint (see
   // above).  An exact minimum by atomics serialised the kernel on one word:
@@ -965,13 +963,20 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
       if (missing) atomicAdd(nblocked, 1u);
     }
   }
-  // forward-edge count over 64 counters (one hot word would serialise)
+  // forward-edge count: a block sum, one atomic per block over 64 counters
+  // (per-wave atomics into them cost C4 1.2 ms of union time; the count is
+  // asked for only where the tile path does not apply, wide rows)
   if (nfwd) {
+    __shared__ uint32_t s_f[8];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) fwd += __shfl_xor(fwd, o, 64);
-    if ((threadIdx.x & 63) == 0 && fwd)
-      atomicAdd(&nfwd[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & 63],
-                (unsigned long long)fwd);
+    if ((threadIdx.x & 63) == 0) s_f[threadIdx.x >> 6] = fwd;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (uint32_t w = 0; w < (blockDim.x >> 6); w++) t += s_f[w];
+      if (t) atomicAdd(&nfwd[blockIdx.x & 63], (unsigned long long)t);
+    }
   }
 }
 
@@ -1222,27 +1227,6 @@ __global__ void k_identity_labels(uint32_t n, const uint64_t *__restrict__ dot,
 // contiguous): a run's head records its start, its tail the count.  One
 // write per distinct key -- an atomic histogram serialises on Zipf-hot keys
 // (key 0 of C4 holds 6.5% of the stream: 4 ms of same-address atomics).
-// one pass over the per-key sort's output: each key's run start and end, and
-// the packed dots unpacked (src << sb | seq -> the u64 dot) into the
-// sequence output
-__global__ void k_run_bounds_unpack(uint32_t m, const uint32_t *__restrict__ keys,
-                                    const uint32_t *__restrict__ pd, int sb,
-                                    uint32_t *__restrict__ start, uint32_t *__restrict__ end,
-                                    uint64_t *__restrict__ seq) {
-  const uint32_t msk = (1u << sb) - 1;
-  GRID_STRIDE(j, m) {
-    const uint32_t k = keys[j];
-    if (j == 0 || keys[j - 1] != k) start[k] = j;
-    if (j + 1 == m || keys[j + 1] != k) end[k] = j + 1;
-    const uint32_t x = pd[j];
-    seq[j] = (uint64_t(x >> sb) << 56) | (x & msk);
-  }
-}
-__global__ void k_run_len(uint32_t K, const uint32_t *__restrict__ start,
-                          uint32_t *__restrict__ end) {
-  GRID_STRIDE(k, K) end[k] -= start[k];
-}
-
 __global__ void k_run_start(uint32_t m, const uint32_t *__restrict__ keys,
                             uint32_t *__restrict__ start) {
   GRID_STRIDE(j, m) if (j == 0 || keys[j - 1] != keys[j]) start[keys[j]] = j;
@@ -1343,12 +1327,7 @@ struct EngineDevice {
   DBuf<uint32_t> vrec;        // command-level views path: replica | arrival per element
   DBuf<uint8_t> tailm;        // command-level views path: tail views per sorted command
   DBuf<uint64_t> cv64a, cv64b;  // command-level views path: packed sort values
-  int pk_sb = 0;  // the per-key sort's packed dots: sequence bits
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
-  // per batch: low key bits every log holds constant (partial replication: a
-  // process sees only its shard's keys, key mod shards = h), which the
-  // chunked path's sort skips -- a (log, key) segment stays contiguous
-  std::vector<uint32_t> h_kshift;
   // per batch: (seq bits, packed bits) of its dots, src << sb | seq (0: wider
   // than 32 bits), so the per-key sort can move 4-byte dots
   std::vector<std::pair<int, int>> h_dpack;
@@ -1596,7 +1575,6 @@ struct EngineDevice {
       FH_CHECK(h_dot[i] != ~0ull && (h_dot[i] >> 56) != 0, FH_EINVAL,
                "stage: dot (255, 2^56 - 1) is reserved and ProcessId 0 is not a process");
     std::vector<uint32_t> ent, lo;
-    h_kshift.assign(nb, 0);
     if (d.views && elem) {
       // element logs: every position (c·fq + j)·k + s of a batch in exactly
       // one log (a replica may hold several of a command's key slots)
@@ -1612,33 +1590,18 @@ struct EngineDevice {
         const uint64_t base = h_off[b * np];
         FH_CHECK(subset || h_off[(b + 1) * np] - base == per_b, FH_EINVAL,
                  "element logs: a batch's logs must hold n * views * keys_per_cmd entries");
-        uint32_t kdiff = 0;  // OR over logs of the keys' differences from the log's first
-        const uint32_t kk = d.keys_per_cmd, pc = uint32_t(fq) * kk;
         for (size_t r = 0; r < np; r++) {
           lo[b * (np + 1) + r] = uint32_t(h_off[b * np + r] - base);
           FH_CHECK(h_off[b * np + r + 1] >= h_off[b * np + r], FH_EINVAL, "logs: offsets");
-          uint32_t k0 = ~0u;
           for (uint64_t q = h_off[b * np + r]; q < h_off[b * np + r + 1]; q++) {
             const uint32_t p = h_cmd[q];
             FH_CHECK(p < per_b && !seen[p], FH_EINVAL,
                      "element logs: every element position must appear in exactly one log");
-            if (p < per_b) {
-              const uint32_t key = k32[b * nk + size_t(p / pc) * kk + p % kk];
-              if (k0 == ~0u) k0 = key;
-              kdiff |= key ^ k0;
-            }
             seen[p] = 1;
             ent[q] = p;
           }
         }
         lo[b * (np + 1) + np] = uint32_t(h_off[(b + 1) * np] - base);
-        // up to 4 constant low bits (the shard of key mod 2^jb); a power-of-
-        // two key space keeps them below the replica bits of the composite
-        const int kb = bits_for(key_space);
-        const bool pow2 = (key_space & (key_space - 1)) == 0;
-        uint32_t jb = kdiff ? uint32_t(__builtin_ctz(kdiff)) : 4u;
-        jb = std::min<uint32_t>(jb, 4);
-        h_kshift[b] = pow2 && int(jb) < kb ? jb : 0u;
       }
     } else if (d.views) {
       const size_t np = d.nproc;
@@ -1870,12 +1833,6 @@ struct EngineDevice {
       // 23-bit composite)
       const bool pow2 = (key_space & (key_space - 1)) == 0;
       const int bits = pow2 ? bits_for(key_space) : bits_for(uint64_t(np + 1) * key_space);
-      // low key bits every log holds constant (partial replication) are not
-      // sorted: equal higher bits within one log mean equal keys, so the
-      // (log, key) segments stay contiguous; 17 bits sort in two 9-bit passes
-      const uint32_t jb = pow2 && b < h_kshift.size() ? h_kshift[b] : 0u;
-      const int sbits = bits - int(jb);
-      const int sdb = sbits > 16 && sbits <= 18 ? 9 : sort_digit_bits(sbits, 4);
       const uint32_t per_entry = elem ? 1u : k;  // elements per log entry
       const uint32_t *bent = lent.get() + (codes_only ? 0 : b * size_t(n) * fq * (elem ? k : 1));
       for (uint32_t c = 0; c < nch; c++) {
@@ -1892,13 +1849,13 @@ struct EngineDevice {
         uint32_t *ks = nullptr;
         const uint32_t tiles = (Mc + kTile - 1) / kTile;
         sort_ws.prepare(tiles, 1, stream);
-        const int db = sdb;
+        const int db = sort_digit_bits(bits, 4);
         probed_launch("log_keys", double(Mc) * (4.0 + 4.0 + 8.0), k_log_keys, dim3(tiles),
                       dim3(kThreads), stream, Mc, k, fq, np, uint32_t(elem), lc, bent, bkey,
                       uint32_t(key_space), lk, lv, pbase + c, place_slack, sort_ws.meta.get(),
-                      (1u << db) - 1, jb);
+                      (1u << db) - 1);
         sort_pairs_counted<uint32_t, uint32_t>(lk, lv, sk32b.ensure(Mc + 1), svb.ensure(Mc + 1), Mc,
-                                               sbits, sort_ws, stream, &ks, &vs, db, int(jb));
+                                               bits, sort_ws, stream, &ks, &vs, db);
         // heads read the latest table, tails then make the chunk's last
         // commands the latest (command-log references); the sort's other
         // buffer pair takes the bucketed (position, code)
@@ -2087,7 +2044,7 @@ struct EngineDevice {
     // rows (the in-batch deps are a subset), so no edge compaction pass; the
     // union also counts the forward edges for the graph stage
     const bool edges_at_deps = views && S >= 8 && deps_direct;
-    unsigned long long *fwd = views ? fwd_ctr.ensure(64) : nullptr;
+    unsigned long long *fwd = views && S >= 8 ? fwd_ctr.ensure(64) : nullptr;
     if (fwd) FH_HIP(hipMemsetAsync(fwd, 0, 64 * sizeof(unsigned long long), stream));
     if (views)
       probed_launch("cmd_union", double(n) * (S * 4.0 + 8.0 * S + 4.0 * S + 4.0),
@@ -2147,9 +2104,7 @@ struct EngineDevice {
     graph.run(gin, gout);
     FH_CHECK(gout.npending == 0, FH_EINVARIANT, "fused engine batch left pending vertices");
     // per-key sequence of dots (ExecutionOrderMonitor::add order)
-    if (gout.pk_dot32) {
-      pk_sb = gin.dot_sb;  // unpacked by materialize's pass over the runs
-    } else if (gout.pk_dot) {
+    if (gout.pk_dot) {
       o_seq = gout.pk_dot;
     } else {
       uint64_t *sq = seq_dot.ensure(gout.nelem + 1);
@@ -2217,18 +2172,8 @@ struct EngineDevice {
     uint32_t *o = key_offs.ensure(key_space + 2);
     uint32_t *hp = headpos.ensure(key_space + 1);
     FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
-    if (gout.pk_dot32) {
-      // packed per-key dots: run bounds and the unpacked sequence in one pass
-      FH_HIP(hipMemsetAsync(hp, 0, key_space * sizeof(uint32_t), stream));
-      uint64_t *sq = seq_dot.ensure(o_nelem + 1);
-      k_run_bounds_unpack<<<grid_for(o_nelem, B), B, 0, stream>>>(
-          o_nelem, gout.pk_key, gout.pk_dot32, pk_sb, hp, h, sq);
-      k_run_len<<<grid_for(uint32_t(key_space), B), B, 0, stream>>>(uint32_t(key_space), hp, h);
-      o_seq = sq;
-    } else {
-      k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
-      k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
-    }
+    k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
+    k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
     exclusive_scan_u32(h, o, key_space, scan_ws, stream);
     if (sv_fused) {
       uint64_t *sq = seq_dot.ensure(o_nelem + 1);

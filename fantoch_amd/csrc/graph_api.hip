@@ -600,7 +600,7 @@ struct GraphDevice {
     uint64_t *nddot = grow_keep(N.ddot, DT + 1, 0, stream);
     // read-back block: header, executed dots, labels, missing dots, pending
     // flags, carried flags of the executed
-    const size_t hdr = 64, bytes = hdr + V * 16 + DT * 8 + 2 * V;
+    const size_t hdr = 128, bytes = hdr + V * 16 + DT * 8 + 2 * V;  // header: 32 words
     uint8_t *blk = d_small.ensure(bytes);
     if (h_small_cap < bytes) {
       if (h_small) FH_HIP(hipHostFree(h_small));
@@ -632,11 +632,21 @@ struct GraphDevice {
     sp.nkey32 = nkey;
     sp.ndoff = ndoff;
     sp.nddot = nddot;
+    static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
+    sp.stamps = debug ? 1 : 0;
     launch_graph_small(sp, stream);
     FH_HIP(hipMemcpyAsync(h_small, blk, bytes, hipMemcpyDeviceToHost, stream));
     FH_HIP(hipStreamSynchronize(stream));
     const uint32_t *hh = reinterpret_cast<const uint32_t *>(h_small);
     const uint32_t nexec = hh[0], nmiss = std::min<uint32_t>(hh[1], uint32_t(DT));
+    if (debug) {
+      auto at = [&](int i) { return (uint64_t(hh[9 + 2 * i]) << 32) | hh[8 + 2 * i]; };
+      fprintf(stderr, "fh graph_small V=%zu phases (us): sort %.1f resolve %.1f blocked %.1f "
+              "H %.1f rounds %.1f depth %.1f order %.1f survivors %.1f\n", V,
+              (at(1) - at(0)) * 0.01, (at(2) - at(1)) * 0.01, (at(3) - at(2)) * 0.01,
+              (at(4) - at(3)) * 0.01, (at(5) - at(4)) * 0.01, (at(6) - at(5)) * 0.01,
+              (at(7) - at(6)) * 0.01, (at(8) - at(7)) * 0.01);
+    }
     // mod.rs:235-240 (state unchanged: the next set is not taken, the
     // appended rows are ignored)
     FH_CHECK(hh[2] == 0, FH_EINVARIANT, "Graph::handle_add tried to index already indexed dot");

@@ -87,7 +87,6 @@ struct GraphOutput {
   uint32_t *pk_key = nullptr;     // [nelem] keys, ascending
   uint32_t *pk_vid = nullptr;     // [nelem] vids in per-key execution order
   uint64_t *pk_dot = nullptr;     // [nelem] their dots (per_key_dots: pk_vid null)
-  uint32_t *pk_dot32 = nullptr;   // or packed (dot_pbits): src << dot_sb | seq, pk_dot null
   bool src_stats_done = false;    // src_mx / src_cnt accumulated
   uint64_t *kap = nullptr;        // [V] by representative: (ready time << 32) | depth
                                   // (global path only)

@@ -875,6 +875,16 @@ __global__ void __launch_bounds__(256)
   if (src_mx) acc.commit(src_mx, src_cnt);  // (src_mx is uniform)
 }
 
+// packed dots back to u64 after the per-key sort
+__global__ void k_unpack_dots(uint32_t n, const uint32_t *__restrict__ pd, int sb,
+                              uint64_t *__restrict__ out) {
+  const uint32_t m = (1u << sb) - 1;
+  GRID_STRIDE(j, n) {
+    const uint32_t x = pd[j];
+    out[j] = (uint64_t(x >> sb) << 56) | (x & m);
+  }
+}
+
 __global__ void k_copy_dot(uint32_t V, const uint64_t *__restrict__ dot, uint64_t *__restrict__ out) {
   GRID_STRIDE(v, V) out[v] = dot[v];
 }
@@ -1278,7 +1288,7 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
     const bool packed = in.dot_pbits > 0 && in.dot_pbits <= 32;
     if (packed) {
       // 4-byte packed dots through the sort (its buffers inside pk_db, whose
-      // ne + 1 u64 hold both)
+      // ne + 1 u64 hold both), unpacked into pk_da at the end
       uint32_t *pa = reinterpret_cast<uint32_t *>(d2), *pb = pa + (ne + 1);
       const DotPack pk{in.dot_sb};
       if (fill_from_groups) {
@@ -1292,8 +1302,8 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
       uint32_t *po = nullptr;
       sort_pairs<uint32_t, uint32_t>(ek, pa, k2, pb, ek, pa, ne, in.key_bits, sort_ws, stream, &ko,
                                      &po);
-      // left packed: the consumer's pass over the sorted keys unpacks them
-      out.pk_dot32 = po;
+      k_unpack_dots<<<grid_for(ne, B), B, 0, stream>>>(ne, po, in.dot_sb, ed);
+      dout = ed;
     } else {
       if (fill_from_groups) {
         k_exec_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(

@@ -34,6 +34,7 @@ struct SmallPass {
   // [0] executed, [1] missing dots, [2] duplicate dot, [3] survivors,
   // [4] their key entries, [5] their dependency entries
   uint32_t *header;
+  int stamps;  // FH_GRAPH_DEBUG: phase clock stamps into header[8..25]
 };
 
 void launch_graph_small(const SmallPass &p, hipStream_t s);

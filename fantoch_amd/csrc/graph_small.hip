@@ -176,6 +176,16 @@ __device__ void sweep(int n, uint32_t *s_ch, F body) {
 
 __global__ void __launch_bounds__(kThreads)
     k_graph_small(SmallPass p) {
+  // phase stamps (FH_GRAPH_DEBUG): wall clock (100 MHz) at 8 points into
+  // header[8 + 2i] (host prints the phase times)
+  auto stamp = [&](int i) {
+    if (p.stamps && threadIdx.x == 0) {
+      const uint64_t t = wall_clock64();
+      p.header[8 + 2 * i] = uint32_t(t);
+      p.header[9 + 2 * i] = uint32_t(t >> 32);
+    }
+  };
+  stamp(0);
   __shared__ uint64_t s_dot[kSmallV], s_sd[kSmallV], s_key[kSmallV];
   __shared__ uint16_t s_sv[kSmallV], s_rank[kSmallV];
   __shared__ uint16_t s_off[kSmallV + 1], s_dst[kSmallE];
@@ -219,6 +229,7 @@ __global__ void __launch_bounds__(kThreads)
     if (x > 0 && s_sd[x] == s_sd[x - 1]) s_err = 1;
   }
   __syncthreads();
+  stamp(1);
   // 2. resolve: count, scan, fill
   uint32_t cnt[2] = {0, 0};
   for (int j = 0; j < 2; j++) {
@@ -258,6 +269,7 @@ __global__ void __launch_bounds__(kThreads)
     if (tid == 0) s_off[V] = uint16_t(etot);
   }
   __syncthreads();
+  stamp(2);
   // 3. blocked closure
   sweep(V, s_ch, [&](int v) {
     if (s_blk[v]) return false;
@@ -268,6 +280,7 @@ __global__ void __launch_bounds__(kThreads)
       }
     return false;
   });
+  stamp(3);
   // 4. H = max vid reachable (executable vertices reach only executable ones)
   for (int v = tid; v < V; v += kThreads) {
     s_H[v] = uint16_t(v);
@@ -287,6 +300,7 @@ __global__ void __launch_bounds__(kThreads)
     }
     return false;
   });
+  stamp(4);
   // SCC rounds over the unassigned vertices: W = max unassigned vid reachable
   // through unassigned vertices; roots (W(v) = v) reach their class members
   for (int round = 0;; round++) {
@@ -341,6 +355,7 @@ __global__ void __launch_bounds__(kThreads)
       if (!s_blk[v] && s_R[v] == kNone && s_F[v]) s_R[v] = s_W[v];
     __syncthreads();
   }
+  stamp(5);
   // representative = min member; labels = min dot; depth over same-H edges
   for (int v = tid; v < V; v += kThreads) {
     s_min[v] = kNone;
@@ -380,6 +395,7 @@ __global__ void __launch_bounds__(kThreads)
     }
     return best > s_D[r] && atomicMax(&s_D[r], best) < best;
   });
+  stamp(6);
   // 5. execution order: (H, depth, representative, dot rank); labels
   uint64_t *ok = s_sd;  // the sorted dots are no longer needed: order keys
   uint64_t lab[2];
@@ -426,6 +442,7 @@ __global__ void __launch_bounds__(kThreads)
     for (uint32_t i = tid; i < nexec; i += kThreads) emit(i, ok[i]);
   }
   for (int v = tid; v < V; v += kThreads) p.blocked[v] = s_blk[v];
+  stamp(7);
   // survivors, compacted in arrival order into the next vertex set
   uint32_t kc[2] = {0, 0}, dc[2] = {0, 0}, kv[2] = {0, 0};
   for (int j = 0; j < 2; j++) {
@@ -460,6 +477,7 @@ __global__ void __launch_bounds__(kThreads)
     p.header[4] = tk;
     p.header[5] = td;
   }
+  stamp(8);
 }
 
 }  // namespace

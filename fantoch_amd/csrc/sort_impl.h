@@ -460,8 +460,7 @@ void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tile
 template <class K, class VT, int DB, class Src0>
 void sort_passes(const Src0 &src0, bool probe0, K *ka, VT *va, K *kb, VT *vb, bool alias_a,
                  size_t n, int passes, int db, SortWorkspace &ws, hipStream_t s, K **kout,
-                 VT **vout, bool counts0 = false, int shift0 = 0) {
-  // shift0: the sort key's lowest bit (pass p sorts bits [shift0 + db·p, + db))
+                 VT **vout, bool counts0 = false) {
   const uint32_t tiles = uint32_t((n + kTile - 1) / kTile);
   const uint32_t groups = (tiles + kGroup - 1) / kGroup;
   ws.prepare(tiles, passes, s);
@@ -471,16 +470,16 @@ void sort_passes(const Src0 &src0, bool probe0, K *ka, VT *va, K *kb, VT *vb, bo
   uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
   K *ko = alias_a ? kb : ka;
   VT *vo = alias_a ? vb : va;
-  sort_pass<K, VT, DB, Src0>(src0, ko, vo, n, shift0, tiles, groups, counts, gsum, dbase, s,
-                            probe0, counts0);
+  sort_pass<K, VT, DB, Src0>(src0, ko, vo, n, 0, tiles, groups, counts, gsum, dbase, s, probe0,
+                            counts0);
   const K *ki = ko;
   const VT *vi = vo;
   for (int p = 1; p < passes; p++) {
     K *kn = ko == ka ? kb : ka;
     VT *vn = ko == ka ? vb : va;
     sort_pass<K, VT, DB, ArraySrc<K, VT, false>>(ArraySrc<K, VT, false>{ki, vi}, kn, vn, n,
-                                                 shift0 + db * p, tiles, groups, counts, gsum,
-                                                 dbase, s, true);
+                                                 db * p, tiles, groups, counts, gsum, dbase, s,
+                                                 true);
     ko = kn;
     vo = vn;
     ki = ko;
@@ -523,11 +522,9 @@ inline int sort_digit_bits(int key_bits, int key_bytes) {
   return db >= 8 ? 8 : db <= 6 ? 6 : 7;
 }
 
-// key_bits bits from bit shift0 (a caller whose segments are already
-// separated by the low bits skips them); db <= 9
 template <class K, class VT>
 void sort_pairs_counted(K *ka, VT *va, K *kb, VT *vb, size_t n, int key_bits, SortWorkspace &ws,
-                        hipStream_t s, K **kout, VT **vout, int db, int shift0 = 0) {
+                        hipStream_t s, K **kout, VT **vout, int db) {
   FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "sort: too many elements (>= 2^30)");
   const int passes = std::max(1, (key_bits + db - 1) / db);
   if (n == 0) {
@@ -538,16 +535,13 @@ void sort_pairs_counted(K *ka, VT *va, K *kb, VT *vb, size_t n, int key_bits, So
   using Src = ArraySrc<K, VT, false>;
   if (db == 6)
     sort_passes<K, VT, 6, Src>(Src{ka, va}, true, ka, va, kb, vb, true, n, passes, 6, ws, s, kout,
-                               vout, true, shift0);
+                               vout, true);
   else if (db == 7)
     sort_passes<K, VT, 7, Src>(Src{ka, va}, true, ka, va, kb, vb, true, n, passes, 7, ws, s, kout,
-                               vout, true, shift0);
-  else if (db == 8)
-    sort_passes<K, VT, 8, Src>(Src{ka, va}, true, ka, va, kb, vb, true, n, passes, 8, ws, s, kout,
-                               vout, true, shift0);
+                               vout, true);
   else
-    sort_passes<K, VT, 9, Src>(Src{ka, va}, true, ka, va, kb, vb, true, n, passes, 9, ws, s, kout,
-                               vout, true, shift0);
+    sort_passes<K, VT, 8, Src>(Src{ka, va}, true, ka, va, kb, vb, true, n, passes, 8, ws, s, kout,
+                               vout, true);
 }
 
 }  // namespace
