@@ -20,6 +20,8 @@ echo "== streaming $(date +%T)"
 timeout -k 10 120 tools/stream_bench 1 20000 10 100000 1000 2000000 > $OUT/stream_$TAG.txt 2>&1 || { cat $OUT/stream_$TAG.txt; exit 1; }
 cat $OUT/stream_$TAG.txt
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sbprof_$TAG -o sb -- tools/stream_bench 1 5000 1000 1000000 > $OUT/sbprof_$TAG.log 2>&1 || { tail -20 $OUT/sbprof_$TAG.log; exit 1; }
+FH_GRAPH_DEBUG=1 timeout -k 10 60 tools/stream_bench 1000 20000 > $OUT/stream_dbg_$TAG.txt 2> $OUT/stream_dbg_$TAG.err || { tail -5 $OUT/stream_dbg_$TAG.err; exit 1; }
+tail -3 $OUT/stream_dbg_$TAG.err
 echo "== c5 probe $(date +%T)"
 FH_GRAPH_DEBUG=1 timeout -k 10 300 python -u tools/c5_probe.py --steps 2 > $OUT/c5dbg_$TAG.log 2>&1 || { tail -20 $OUT/c5dbg_$TAG.log; exit 1; }
 grep -v "^\[W" $OUT/c5dbg_$TAG.log | tail -4
