@@ -792,7 +792,7 @@ __device__ __forceinline__ void cmd_union_regs(
     uint32_t *__restrict__ dep_cnt, uint32_t *__restrict__ dst, uint8_t *__restrict__ blocked0,
     uint32_t *nblocked, uint32_t *__restrict__ nv_out, uint64_t bbase, uint32_t n,
     const uint32_t *__restrict__ out_off, uint32_t *__restrict__ err, uint32_t vbase,
-    bool edges_at_deps, uint32_t &fwd) {
+    bool edges_at_deps, uint32_t &fwd, const uint32_t *__restrict__ dot32, int sb32) {
   uint64_t r[kRegSlots];
   uint32_t vv[kRegSlots];
   bool missing = false;
@@ -823,7 +823,14 @@ __device__ __forceinline__ void cmd_union_regs(
     bool dup = vv[t] == ~0u;
 #pragma unroll
     for (uint32_t q = 0; q < t; q++) dup |= vv[q] == vv[t];
-    if (!dup) r[t] = dot[vv[t]];
+    if (!dup) {
+      if (dot32) {  // the packed copy: half the bytes per gathered line
+        const uint32_t pd = dot32[vv[t]];
+        r[t] = (uint64_t(pd >> sb32) << 56) | (pd & ((1u << sb32) - 1));
+      } else {
+        r[t] = dot[vv[t]];
+      }
+    }
   }
   // bitonic sort of the 16 register slots, ascending
 #pragma unroll
@@ -901,7 +908,10 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
                              uint32_t *nblocked, uint32_t *__restrict__ nv_out,
                              uint64_t bbase, const uint32_t *__restrict__ out_off,
                              uint32_t *__restrict__ err, uint32_t vbase, uint32_t edges_at_deps,
-                             unsigned long long *__restrict__ nfwd) {
+                             unsigned long long *__restrict__ nfwd,
+                             const uint32_t *__restrict__ dot32, int sb32) {
+  // dot32 (or null): the batch's dots packed src << sb32 | seq, gathered
+  // instead of the u64 dots
   // uniform: the register path, with a sorting network sized to the row
   const uint32_t cn = n;
   const bool ead = edges_at_deps != 0 && out_off != nullptr;
@@ -915,17 +925,18 @@ __global__ void k_cmd_engine(uint32_t n, uint32_t S, const uint64_t *__restrict_
     const uint32_t lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
     for (size_t j = size_t(lb) * blockDim.x + threadIdx.x; j < cn; j += size_t(nb) * blockDim.x)
       cmd_union_regs<4>(uint32_t(j), S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
-                        blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd);
+                        blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd, dot32,
+                        sb32);
   } else if (S <= 8) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<8>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst, blocked0,
-                        nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd);
+                        nblocked, nv_out, bbase, n, out_off, err, vbase, ead, fwd, dot32, sb32);
     }
   } else if (S <= kRegSlots) {
     GRID_STRIDE(j, cn) {
       cmd_union_regs<kRegSlots>(j, S, dot, dep_code, dlog, frontier, dep_dot, dep_cnt, dst,
                                 blocked0, nblocked, nv_out, bbase, n, out_off, err, vbase, ead,
-                                fwd);
+                                fwd, dot32, sb32);
     }
   } else {
     GRID_STRIDE(i, cn) {
@@ -1227,6 +1238,14 @@ __global__ void k_identity_labels(uint32_t n, const uint64_t *__restrict__ dot,
 // contiguous): a run's head records its start, its tail the count.  One
 // write per distinct key -- an atomic histogram serialises on Zipf-hot keys
 // (key 0 of C4 holds 6.5% of the stream: 4 ms of same-address atomics).
+__global__ void k_pack_dots(uint32_t n, const uint64_t *__restrict__ dot, int sb,
+                            uint32_t *__restrict__ out) {
+  GRID_STRIDE(i, n) {
+    const uint64_t d = dot[i];
+    out[i] = uint32_t(((d >> 56) << sb) | (d & 0x00FFFFFFFFFFFFFFull));
+  }
+}
+
 __global__ void k_run_start(uint32_t m, const uint32_t *__restrict__ keys,
                             uint32_t *__restrict__ start) {
   GRID_STRIDE(j, m) if (j == 0 || keys[j - 1] != keys[j]) start[keys[j]] = j;
@@ -1320,6 +1339,7 @@ struct EngineDevice {
   const uint64_t *o_seq = nullptr;    // [o_nelem] per-key sequences of dots
   DBuf<uint32_t> edge_cnt, edge_off, edge_csr;  // replica views: in-batch edges as CSR
   DBuf<unsigned long long> fwd_ctr;  // [64] forward edges counted by the union
+  DBuf<uint32_t> dot32;  // staged batches' dots packed to 32 bits (h_dpack)
   DBuf<uint8_t> blocked0;
   DBuf<uint32_t> scal;
   DBuf<uint32_t> place_base;  // replica views: per-chunk smallest element position
@@ -1667,6 +1687,19 @@ struct EngineDevice {
       }
       const int sb = bits_for(mq + 1), pb = sb + bits_for(ms + 1);
       h_dpack[b] = pb <= 32 ? std::make_pair(sb, pb) : std::make_pair(0, 0);
+    }
+    // the union's gathers read a packed copy of each batch's dots (input
+    // layout, built here with the upload)
+    {
+      bool any = false;
+      for (size_t b = 0; b < nb; b++) any |= h_dpack[b].second > 0;
+      if (any) {
+        uint32_t *d32 = dot32.ensure(n * nb + 1);
+        for (size_t b = 0; b < nb; b++)
+          if (h_dpack[b].second > 0)
+            k_pack_dots<<<grid_for(uint32_t(n), B), B, 0, stream>>>(
+                uint32_t(n), dot.get() + log_len + b * n, h_dpack[b].first, d32 + b * n);
+      }
     }
     stage_base = log_len;
     log_len += n * nb;
@@ -2040,6 +2073,11 @@ struct EngineDevice {
     }
     // rows of <= 4 slots: XCD-contiguous blocks (k_cmd_engine)
     const uint32_t g = S <= 4 ? (grid_for(n, B, 1u << 22) + 7) / 8 * 8 : grid_for(n, B);
+    // the batch's packed dots (staged), when they fit 32 bits
+    const size_t bcur = cursor - 1;
+    const bool packed = bcur < h_dpack.size() && h_dpack[bcur].second > 0 && dot32.get();
+    const uint32_t *bdot32 = packed ? dot32.get() + bcur * size_t(n) : nullptr;
+    const int bsb32 = packed ? h_dpack[bcur].first : 0;
     // wide rows (C5: 12 slots) write their edges into the committed-deps CSR
     // rows (the in-batch deps are a subset), so no edge compaction pass; the
     // union also counts the forward edges for the graph stage
@@ -2052,14 +2090,14 @@ struct EngineDevice {
                     (const uint32_t *)dep32.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
                     scal.get(), edges_at_deps ? (uint32_t *)nullptr : ecnt, bbase, doff,
-                    scal.get() + 1, 0u, uint32_t(edges_at_deps), fwd);
+                    scal.get() + 1, 0u, uint32_t(edges_at_deps), fwd, bdot32, bsb32);
     else
       probed_launch("cmd_union", double(n) * (S * 8.0 + 8.0 * S + 4.0 * S + 4.0),
                     k_cmd_engine<uint64_t>, dim3(grid_for(n, B)), dim3(B), stream, n, S, bdot,
                     (const uint64_t *)dep_ext.get(), (const uint64_t *)dot.get(),
                     (const uint64_t *)frontier.get(), ddot, dcnt, dd, (uint8_t *)nullptr,
                     scal.get(), ecnt, bbase, doff, scal.get() + 1, 0u, 0u,
-                    (unsigned long long *)nullptr);
+                    (unsigned long long *)nullptr, (const uint32_t *)nullptr, 0);
     mark("keydeps_union");
     if (deps_only) return;  // the committed deps are the output (partial replication)
     const uint32_t *gdst = dd, *goff = nullptr;
@@ -2273,7 +2311,7 @@ void union_rows(uint32_t n, uint32_t S, const uint32_t *codes, const uint64_t *d
                 k_cmd_engine<uint32_t>, dim3(g), dim3(B), s, n, S, dot, codes, dot,
                 (const uint64_t *)nullptr, dep_dot, dcnt, dst, (uint8_t *)nullptr, scal, ecnt,
                 uint64_t(0), (const uint32_t *)dep_off, scal + 1, vbase, 0u,
-                (unsigned long long *)nullptr);
+                (unsigned long long *)nullptr, (const uint32_t *)nullptr, 0);
 }
 
 }  // namespace fh
