@@ -250,8 +250,8 @@ struct GraphDevice {
   uint64_t passes = 0, skipped = 0;
   // device buffers
   DBuf<uint64_t> d_sd, d_sd2, d_frontier, d_exc, d_xdot, d_xlab, d_miss;
-  DBuf<uint8_t> d_up;        // the batch's upload block (k_append)
-  uint8_t *h_up = nullptr;   // its pinned host side
+  uint8_t *h_up = nullptr;      // the batch's upload block: mapped pinned host memory
+  uint8_t *h_up_dev = nullptr;  // its device address (k_append reads it)
   size_t h_up_cap = 0;
   DBuf<uint32_t> d_cnt, d_off, d_dst, d_sv, d_sv2, d_err, d_kv, d_kk, d_kd, d_pv, d_pk, d_pd;
   DBuf<uint8_t> d_blocked0;
@@ -424,10 +424,13 @@ struct GraphDevice {
         if (h_up) FH_HIP(hipHostFree(h_up));
         h_up = nullptr;
         h_up_cap = 0;
-        FH_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_up), bytes * 2, hipHostMallocDefault));
+        FH_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_up), bytes * 2, hipHostMallocMapped));
+        FH_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&h_up_dev), h_up, 0));
         h_up_cap = bytes * 2;
       }
-      uint8_t *dup = d_up.ensure(bytes + 8);
+      // k_append reads the mapped block itself (no copy operation; the pass
+      // ends with a stream synchronize before the block is rewritten)
+      uint8_t *dup = h_up_dev;
       if (n) {
         std::memcpy(h_up + o_dot, dot, n * 8);
         if (DB) std::memcpy(h_up + o_dep, dep_dot, DB * 8);
@@ -440,7 +443,6 @@ struct GraphDevice {
         std::memcpy(h_up + o_clk, clock.frontier, 256 * 8);
         if (u.ne) std::memcpy(h_up + o_clk + 256 * 8, exc_sorted.data(), size_t(u.ne) * 8);
       }
-      FH_HIP(hipMemcpyAsync(dup, h_up, bytes, hipMemcpyHostToDevice, stream));
       u.dot = reinterpret_cast<const uint64_t *>(dup + o_dot);
       u.dep = reinterpret_cast<const uint64_t *>(dup + o_dep);
       u.clk = reinterpret_cast<const uint64_t *>(dup + o_clk);
@@ -582,8 +584,8 @@ struct GraphDevice {
   }
 
   // A small graph's pass (graph_small.hip): one launch, one read-back.
-  DBuf<uint8_t> d_small;
-  uint8_t *h_small = nullptr;
+  uint8_t *h_small = nullptr;      // the pass's results: mapped pinned host memory
+  uint8_t *h_small_dev = nullptr;  // its device address (k_graph_small writes it)
   size_t h_small_cap = 0;
   void small_pass(size_t n, const uint64_t *dot, const uint32_t *dep_off, const uint64_t *dep_dot,
                   const uint64_t *cmd_shards, const uint64_t *dep_shards, size_t V, size_t KB,
@@ -601,12 +603,13 @@ struct GraphDevice {
     // read-back block: header, executed dots, labels, missing dots, pending
     // flags, carried flags of the executed
     const size_t hdr = 128, bytes = hdr + V * 16 + DT * 8 + 2 * V;  // header: 32 words
-    uint8_t *blk = d_small.ensure(bytes);
+
     if (h_small_cap < bytes) {
       if (h_small) FH_HIP(hipHostFree(h_small));
       h_small = nullptr;
       h_small_cap = 0;
-      FH_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_small), bytes * 2, hipHostMallocDefault));
+      FH_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_small), bytes * 2, hipHostMallocMapped));
+      FH_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&h_small_dev), h_small, 0));
       h_small_cap = bytes * 2;
     }
     SmallPass sp;
@@ -620,6 +623,7 @@ struct GraphDevice {
     sp.frontier = d_frontier.get();
     sp.exc = dexc;
     sp.nexc = nexc;
+    uint8_t *blk = h_small_dev;
     sp.header = reinterpret_cast<uint32_t *>(blk);
     sp.xdot = reinterpret_cast<uint64_t *>(blk + hdr);
     sp.xlab = sp.xdot + V;
@@ -634,8 +638,7 @@ struct GraphDevice {
     sp.nddot = nddot;
     static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
     sp.stamps = debug ? 1 : 0;
-    launch_graph_small(sp, stream);
-    FH_HIP(hipMemcpyAsync(h_small, blk, bytes, hipMemcpyDeviceToHost, stream));
+    launch_graph_small(sp, stream);  // writes the mapped block: no read-back copy
     FH_HIP(hipStreamSynchronize(stream));
     const uint32_t *hh = reinterpret_cast<const uint32_t *>(h_small);
     const uint32_t nexec = hh[0], nmiss = std::min<uint32_t>(hh[1], uint32_t(DT));

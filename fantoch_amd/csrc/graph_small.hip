@@ -188,7 +188,8 @@ __global__ void __launch_bounds__(kThreads)
   stamp(0);
   __shared__ uint64_t s_dot[kSmallV], s_sd[kSmallV], s_key[kSmallV];
   __shared__ uint16_t s_sv[kSmallV], s_rank[kSmallV];
-  __shared__ uint16_t s_off[kSmallV + 1], s_dst[kSmallE];
+  __shared__ uint16_t s_off[kSmallV + 1], s_dst[kSmallE], s_tgt[kSmallE];
+  __shared__ uint64_t s_front[256];  // executed clock frontier (AEClock)
   __shared__ uint16_t s_H[kSmallV], s_R[kSmallV], s_W[kSmallV], s_min[kSmallV];
   __shared__ uint32_t s_D[kSmallV];
   __shared__ uint8_t s_blk[kSmallV], s_F[kSmallV];
@@ -198,6 +199,7 @@ __global__ void __launch_bounds__(kThreads)
   while (n2 < V) n2 <<= 1;
   if (tid < 3) s_ch[tid] = 0;
   if (tid == 0) s_nmiss = s_err = 0;
+  if (tid < 256) s_front[tid] = p.frontier[tid];
   for (int x = tid; x < n2; x += kThreads) {
     const uint64_t d = x < V ? p.dot[x] : ~0ull;
     s_dot[x] = d;
@@ -230,23 +232,32 @@ __global__ void __launch_bounds__(kThreads)
   }
   __syncthreads();
   stamp(1);
-  // 2. resolve: count, scan, fill
+  // 2. resolve: one pass over the dependency lists (the global loads)
+  // writes each entry's target vid, or kNone for self / executed / missing,
+  // into LDS at its list position; the scan then compacts from LDS
   uint32_t cnt[2] = {0, 0};
+  const uint32_t e0 = p.doff[0];
   for (int j = 0; j < 2; j++) {
     const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     if (v >= V) continue;
     bool missing = false;
     const uint64_t self = s_dot[v];
-    for (uint32_t e = p.doff[v]; e < p.doff[v + 1]; e++) {
+    const uint32_t eb = p.doff[v], ee = p.doff[v + 1];
+    for (uint32_t e = eb; e < ee; e++) {
       const uint64_t d = p.ddot[e];
-      if (d == self || executed_dev(d, p.frontier, p.exc, p.nexc)) continue;
-      if (find_lds(s_sd, V, d) >= 0) {
-        cnt[j]++;
-      } else {
-        missing = true;
-        const uint32_t q = atomicAdd(&s_nmiss, 1u);
-        if (q < p.miss_cap) p.miss[q] = d;
+      uint16_t t = kNone;
+      if (d != self && !executed_dev(d, s_front, p.exc, p.nexc)) {
+        const int u = find_lds(s_sd, V, d);
+        if (u >= 0) {
+          t = s_sv[u];
+          cnt[j]++;
+        } else {
+          missing = true;
+          const uint32_t q = atomicAdd(&s_nmiss, 1u);
+          if (q < p.miss_cap) p.miss[q] = d;
+        }
       }
+      s_tgt[e - e0] = t;
     }
     s_blk[v] = missing;
   }
@@ -255,15 +266,13 @@ __global__ void __launch_bounds__(kThreads)
   {
     uint32_t o = o0;
     for (int j = 0; j < 2; j++) {
-      const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
+      const int v = 2 * tid + j;
       if (v >= V) continue;
       s_off[v] = uint16_t(o);
-      const uint64_t self = s_dot[v];
-      for (uint32_t e = p.doff[v]; e < p.doff[v + 1]; e++) {
-        const uint64_t d = p.ddot[e];
-        if (d == self || executed_dev(d, p.frontier, p.exc, p.nexc)) continue;
-        const int u = find_lds(s_sd, V, d);
-        if (u >= 0) s_dst[o++] = s_sv[u];
+      const uint32_t eb = p.doff[v] - e0, ee = p.doff[v + 1] - e0;
+      for (uint32_t e = eb; e < ee; e++) {
+        const uint16_t t = s_tgt[e];
+        if (t != kNone) s_dst[o++] = t;
       }
     }
     if (tid == 0) s_off[V] = uint16_t(etot);
