@@ -405,50 +405,54 @@ __global__ void __launch_bounds__(kThreads)
     return best > s_D[r] && atomicMax(&s_D[r], best) < best;
   });
   stamp(6);
-  // 5. execution order: (H, depth, representative, dot rank); labels
-  uint64_t *ok = s_sd;  // the sorted dots are no longer needed: order keys
+  // 5. execution order: (H, depth, representative, dot) -- the executed
+  // vertices counting-sorted by ready time H (groups in H order), then each
+  // one's rank inside its group by (depth, representative, dot); labels
   uint64_t lab[2];
   for (int j = 0; j < 2; j++) {
     const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     lab[j] = v < V && !s_blk[v] ? s_key[s_R[v]] : 0ull;
   }
+  // group counts and cursors in s_sd's space (the sorted dots are done)
+  uint32_t *s_gs = reinterpret_cast<uint32_t *>(s_sd), *s_gc = s_gs + kSmallV;
+  for (int v = tid; v < V; v += kThreads) s_gs[v] = 0;
   __syncthreads();
-  for (int v = tid; v < n2; v += kThreads) {
-    if (v < V && !s_blk[v])
-      ok[v] = (uint64_t(s_H[v]) << 33) | (uint64_t(s_D[s_R[v]]) << 22) |
-              (uint64_t(s_R[v]) << 11) | s_rank[v];
-    else
-      ok[v] = ~0ull;
-  }
   for (int j = 0; j < 2; j++) {
-    const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
-    if (v < V) s_key[v] = lab[j];  // label per vertex
+    const int v = 2 * tid + j;
+    if (v < V) {
+      s_key[v] = lab[j];  // label per vertex
+      if (!s_blk[v]) atomicAdd(&s_gs[s_H[v]], 1u);
+    }
   }
   __syncthreads();
   uint32_t nexec = 0;
   {
-    uint32_t mine = 0;
-    for (int v = tid; v < V; v += kThreads) mine += s_blk[v] ? 0u : 1u;
-    block_scan(mine, s_w, &nexec);
+    const int v0 = 2 * tid;
+    const uint32_t c0 = v0 < V ? s_gs[v0] : 0u, c1 = v0 + 1 < V ? s_gs[v0 + 1] : 0u;
+    const uint32_t o = block_scan(c0 + c1, s_w, &nexec);
+    if (v0 < V) s_gs[v0] = s_gc[v0] = o;
+    if (v0 + 1 < V) s_gs[v0 + 1] = s_gc[v0 + 1] = o + c0;
   }
-  // the order keys are unique (the dot rank): each executed vertex is written
-  // at its key's rank (blocks of 64 per wave, then merge ranks; the pending
-  // ones' all-ones keys rank last)
-  auto emit = [&](uint32_t i, uint64_t key) {
-    const uint16_t v = s_sv[key & 0x7FF];
-    p.xdot[i] = s_dot[v];
-    p.xlab[i] = s_key[v];
-    p.xcar[i] = v < p.P ? 1 : 0;
-  };
-  if (n2 >= 128) {
-    sort_blocks64(ok, nullptr, n2);
-    for (int x = tid; x < n2; x += kThreads) {
-      const uint32_t r = merge_rank(ok, n2, x);
-      if (r < nexec) emit(r, ok[x]);
+  __syncthreads();
+  // members listed group by group (s_W: the SCC rounds are done)
+  for (int v = tid; v < V; v += kThreads)
+    if (!s_blk[v]) s_W[atomicAdd(&s_gc[s_H[v]], 1u)] = uint16_t(v);
+  __syncthreads();
+  for (int v = tid; v < V; v += kThreads) {
+    if (s_blk[v]) continue;
+    const uint32_t g = s_H[v], b0 = s_gs[g], b1 = s_gc[g];
+    const uint32_t rv = s_R[v], dv = s_D[rv];
+    const uint64_t xv = s_dot[v];
+    uint32_t rk = 0;
+    for (uint32_t i = b0; i < b1; i++) {
+      const uint32_t y = s_W[i];
+      const uint32_t ry = s_R[y], dy = s_D[ry];
+      rk += dy != dv ? dy < dv : ry != rv ? ry < rv : s_dot[y] < xv;
     }
-  } else {
-    bitonic(ok, nullptr, n2);
-    for (uint32_t i = tid; i < nexec; i += kThreads) emit(i, ok[i]);
+    const uint32_t pos = b0 + rk;
+    p.xdot[pos] = xv;
+    p.xlab[pos] = s_key[v];
+    p.xcar[pos] = uint32_t(v) < p.P ? 1 : 0;
   }
   for (int v = tid; v < V; v += kThreads) p.blocked[v] = s_blk[v];
   stamp(7);
