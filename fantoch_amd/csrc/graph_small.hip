@@ -7,19 +7,22 @@
 // dot sort, resolve, GraphCore's fixpoints, compaction) is a few dozen
 // launches with several host round trips; for V <= kSmallV vertices and
 // E <= kSmallE dependency entries everything happens here, in LDS, in one
-// launch, and the host reads one block back:
-//  1. vertex dots sorted (bitonic, LDS): duplicate check (mod.rs:235-240)
-//     and the dot -> vid index;
-//  2. dependencies resolved: self and executed ones ignored (tarjan.rs:131-
-//     148), others are vertices or missing (the vertex is blocked, tarjan.rs:
-//     150-170); missing dots listed;
+// launch, reading the batch from and writing its results to mapped pinned
+// host memory:
+//  1. the dot -> vid index: an LDS hash table (duplicate check,
+//     mod.rs:235-240);
+//  2. dependencies resolved once (the global loads): self and executed ones
+//     ignored (tarjan.rs:131-148), others are vertices or missing (the
+//     vertex is blocked, tarjan.rs:150-170); missing dots listed;
 //  3. blocked closure: a vertex reaching a missing dependency stays pending
 //     (check_pending, mod.rs:558-644);
 //  4. the rest as GraphCore orders it (graph_core.h): H = max vid reachable
 //     (pointer jumping), SCCs by rounds of reach from each ready group's root
 //     (an SCC's representative is its minimum vid), depth over same-H edges,
-//     execution order by (H, depth, representative, dot), labels = min dot;
-//  5. the survivors compacted, in arrival order, into the next vertex set.
+//     labels = min dot;
+//  5. execution order by (H, depth, representative, dot): a counting sort by
+//     H, then each vertex's rank inside its group;
+//  6. the survivors compacted, in arrival order, into the next vertex set.
 #include "graph_small.h"
 
 #include "dotindex.h"
@@ -53,109 +56,19 @@ __device__ uint32_t block_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
   return pre + x - v;
 }
 
-// bitonic sort of n2 (a power of two <= 2 * kThreads) keys ascending, with
-// an optional u16 payload.  Thread t owns elements t and t + kThreads, so a
-// stage whose partners are under 64 apart stays inside one wave's 64-element
-// blocks: it needs only a wave barrier; block barriers surround the stages
-// with wider partners (51 of a 2048-element sort's 66 stages are wave-local)
-__device__ void bitonic(uint64_t *key, uint16_t *val, int n2) {
-  for (int k = 2; k <= n2; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j >= 64) __syncthreads();
-      for (int x = threadIdx.x; x < n2; x += kThreads) {
-        const int p = x ^ j;
-        if (p > x) {
-          const uint64_t a = key[x], b = key[p];
-          const bool up = (x & k) == 0;
-          if (up ? a > b : a < b) {
-            key[x] = b;
-            key[p] = a;
-            if (val) {
-              const uint16_t t = val[x];
-              val[x] = val[p];
-              val[p] = t;
-            }
-          }
-        }
-      }
-      if (j >= 64) {
-        __syncthreads();  // this stage wrote other waves' elements
-      } else {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    }
-  __syncthreads();
+// dot -> vid hash index in LDS: 2 * kSmallV slots, linear probing; the
+// all-ones dot is reserved (the empty slot), as everywhere in the library
+constexpr int kHash = 2 * kSmallV;
+constexpr uint64_t kEmpty = ~0ull;
+__device__ __forceinline__ uint32_t hash_slot(uint64_t d) {
+  return uint32_t((d * 0x9E3779B97F4A7C15ull) >> 52) & (kHash - 1);
 }
-
-// Each 64-element block of key[0, n2) sorted ascending in place, with an
-// optional u16 payload: bitonic levels up to 64 only, so every stage stays
-// inside one wave's elements (wave barriers; the last level merges every
-// block upwards).
-__device__ void sort_blocks64(uint64_t *key, uint16_t *val, int n2) {
-  for (int k = 2; k <= 64; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int x = threadIdx.x; x < n2; x += kThreads) {
-        const int p = x ^ j;
-        if (p > x) {
-          const uint64_t a = key[x], b = key[p];
-          const bool up = k == 64 || (x & k) == 0;
-          if (up ? a > b : a < b) {
-            key[x] = b;
-            key[p] = a;
-            if (val) {
-              const uint16_t t = val[x];
-              val[x] = val[p];
-              val[p] = t;
-            }
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  __syncthreads();
-}
-
-// Global rank of element x of the block-sorted key[0, n2): its index in its
-// block plus, per other block, the elements before it there (binary search;
-// equal keys order by block, so ranks are unique and the order stable).
-__device__ uint32_t merge_rank(const uint64_t *key, int n2, int x) {
-  const uint64_t kx = key[x];
-  const int bx = x >> 6;
-  uint32_t r = uint32_t(x & 63);
-  for (int b = 0; b < (n2 >> 6); b++) {
-    if (b == bx) continue;
-    const uint64_t *blk = key + (b << 6);
-    int lo = 0, hi = 64;
-    if (b < bx) {  // upper bound: equal keys of earlier blocks come first
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (blk[mid] <= kx) lo = mid + 1; else hi = mid;
-      }
-    } else {  // lower bound
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (blk[mid] < kx) lo = mid + 1; else hi = mid;
-      }
-    }
-    r += uint32_t(lo);
+__device__ __forceinline__ int find_hash(const uint64_t *hk, const uint16_t *hv, uint64_t d) {
+  for (uint32_t h = hash_slot(d);; h = (h + 1) & (kHash - 1)) {
+    const uint64_t k = hk[h];
+    if (k == d) return hv[h];
+    if (k == kEmpty) return -1;
   }
-  return r;
-}
-
-__device__ int find_lds(const uint64_t *sd, int n, uint64_t d) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (sd[mid] < d)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return lo < n && sd[lo] == d ? lo : -1;
 }
 
 // sweep to the fixpoint: body(x) returns true on a change
@@ -186,8 +99,11 @@ __global__ void __launch_bounds__(kThreads)
     }
   };
   stamp(0);
-  __shared__ uint64_t s_dot[kSmallV], s_sd[kSmallV], s_key[kSmallV];
-  __shared__ uint16_t s_sv[kSmallV], s_rank[kSmallV];
+  __shared__ uint64_t s_dot[kSmallV], s_key[kSmallV];
+  // dot -> vid hash index (open addressing, load <= 1/2); after the resolve
+  // its key words are scratch for the order's group counts
+  __shared__ uint64_t s_hk[kHash];
+  __shared__ uint16_t s_hv[kHash];
   __shared__ uint16_t s_off[kSmallV + 1], s_dst[kSmallE], s_tgt[kSmallE];
   __shared__ uint64_t s_front[256];  // executed clock frontier (AEClock)
   __shared__ uint16_t s_H[kSmallV], s_R[kSmallV], s_W[kSmallV], s_min[kSmallV];
@@ -195,40 +111,27 @@ __global__ void __launch_bounds__(kThreads)
   __shared__ uint8_t s_blk[kSmallV], s_F[kSmallV];
   __shared__ uint32_t s_w[kThreads / 64], s_ch[3], s_nmiss, s_err;
   const int tid = threadIdx.x, V = int(p.V);
-  int n2 = 1;
-  while (n2 < V) n2 <<= 1;
   if (tid < 3) s_ch[tid] = 0;
   if (tid == 0) s_nmiss = s_err = 0;
   if (tid < 256) s_front[tid] = p.frontier[tid];
-  for (int x = tid; x < n2; x += kThreads) {
-    const uint64_t d = x < V ? p.dot[x] : ~0ull;
-    s_dot[x] = d;
-    s_sd[x] = d;
-    s_sv[x] = uint16_t(x);
-  }
+  for (int x = tid; x < kHash; x += kThreads) s_hk[x] = kEmpty;
+  for (int x = tid; x < V; x += kThreads) s_dot[x] = p.dot[x];
   __syncthreads();
-  // 1. dot -> vid index; a dot indexed twice (mod.rs:235-240).  Blocks of 64
-  // sorted per wave (in s_key / s_W, free until the SCC phases), then every
-  // dot placed at its merge rank
-  if (n2 >= 128) {
-    for (int x = tid; x < n2; x += kThreads) {
-      s_key[x] = s_sd[x];
-      s_W[x] = s_sv[x];
-    }
-    __syncthreads();
-    sort_blocks64(s_key, s_W, n2);
-    for (int x = tid; x < n2; x += kThreads) {
-      const uint32_t r = merge_rank(s_key, n2, x);
-      s_sd[r] = s_key[x];
-      s_sv[r] = s_W[x];
-    }
-    __syncthreads();
-  } else {
-    bitonic(s_sd, s_sv, n2);
-  }
+  // 1. dot -> vid index; a dot indexed twice (mod.rs:235-240)
   for (int x = tid; x < V; x += kThreads) {
-    s_rank[s_sv[x]] = uint16_t(x);
-    if (x > 0 && s_sd[x] == s_sd[x - 1]) s_err = 1;
+    const uint64_t d = s_dot[x];
+    for (uint32_t h = hash_slot(d);; h = (h + 1) & (kHash - 1)) {
+      const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long *>(&s_hk[h]),
+                                      (unsigned long long)kEmpty, (unsigned long long)d);
+      if (prev == kEmpty) {
+        s_hv[h] = uint16_t(x);
+        break;
+      }
+      if (prev == d) {
+        s_err = 1;
+        break;
+      }
+    }
   }
   __syncthreads();
   stamp(1);
@@ -247,9 +150,9 @@ __global__ void __launch_bounds__(kThreads)
       const uint64_t d = p.ddot[e];
       uint16_t t = kNone;
       if (d != self && !executed_dev(d, s_front, p.exc, p.nexc)) {
-        const int u = find_lds(s_sd, V, d);
+        const int u = find_hash(s_hk, s_hv, d);
         if (u >= 0) {
-          t = s_sv[u];
+          t = uint16_t(u);
           cnt[j]++;
         } else {
           missing = true;
@@ -413,8 +316,8 @@ __global__ void __launch_bounds__(kThreads)
     const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     lab[j] = v < V && !s_blk[v] ? s_key[s_R[v]] : 0ull;
   }
-  // group counts and cursors in s_sd's space (the sorted dots are done)
-  uint32_t *s_gs = reinterpret_cast<uint32_t *>(s_sd), *s_gc = s_gs + kSmallV;
+  // group counts and cursors in the hash keys' space (the resolve is done)
+  uint32_t *s_gs = reinterpret_cast<uint32_t *>(s_hk), *s_gc = s_gs + kSmallV;
   for (int v = tid; v < V; v += kThreads) s_gs[v] = 0;
   __syncthreads();
   for (int j = 0; j < 2; j++) {
