@@ -490,20 +490,16 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            uint32_t *H, uint32_t *changed, const uint32_t *__restrict__ prev,
-                           int nodone, int desc) {
+                           int nodone) {
   // nodone: the first round of the full coloring (nothing done yet): the
-  // done[] gathers per edge are skipped.
-  // desc: blocks take the positions in descending order.  Ready times flow
-  // up along backward dependencies (an ascending launch cascades them) and
-  // down along forward ones (a descending launch does); launches alternate.
+  // done[] gathers per edge are skipped
   // the previous launch of the group changed nothing: converged, return
   if (prev && ld_u32(prev) == 0) return;
   __shared__ AggTable<uint32_t> tb;
   agg_init<uint32_t, true>(tb);
   __syncthreads();
   {
-    const uint32_t bj = desc ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
-    const uint32_t j = bj * B + threadIdx.x;
+    const uint32_t j = blockIdx.x * B + threadIdx.x;
     const uint32_t v = j < n ? FB_VID(j) : 0u;
     const bool act = j < n && !blocked[v] && !done[v];
     const uint32_t r = act ? rep[v] : 0u;
@@ -578,15 +574,14 @@ __global__ void k_fb_reach(uint32_t n, const uint32_t *__restrict__ list,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            const uint32_t *__restrict__ H, uint8_t *reached, uint32_t *changed,
                            uint8_t *__restrict__ pushed, const uint32_t *__restrict__ prev,
-                           int nodone, int asc) {
+                           int nodone) {
   if (prev && ld_u32(prev) == 0) return;  // converged (see converge())
   GRID_STRIDE(jj, n) {
     // descending positions: dependencies mostly point to earlier arrivals,
     // so a push lands on a vertex a later-dispatched workgroup still has to
     // visit, and the reach cascades down a backward chain inside one launch
-    // instead of one hop per launch; every other launch ascends, for the
-    // pushes along forward dependencies
-    const uint32_t j = asc ? jj : n - 1 - jj;
+    // instead of one hop per launch
+    const uint32_t j = n - 1 - jj;
     const uint32_t v = FB_VID(j);
     // a vertex pushes its edges once, in the launch after its class is
     // reached (later launches would repeat the same pushes: the reach loop
@@ -1138,7 +1133,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     converge(1, dbg_hprop, [&](uint32_t *changed, const uint32_t *prev) {
       k_fb_hprop<<<agg_blocks(n), B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er,
                                                   blocked.get(), done, rep.get(), H, changed, prev,
-                                                  int(first_full), int(!(dbg_hprop & 1)));
+                                                  int(first_full));
     });
     if (!list && !recent_iter) {
       k_fb_save_h<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), H, hseed.ensure(V));
@@ -1148,8 +1143,7 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     FH_HIP(hipMemsetAsync(pushed, 0, V, stream));
     converge(1, dbg_reach, [&](uint32_t *changed, const uint32_t *prev) {
       k_fb_reach<<<G, B, 0, stream>>>(n, list, in.off, in.stride, in.dst, er, blocked.get(), done,
-                                       rep.get(), H, reached, changed, pushed, prev, int(first_full),
-                                       int(!(dbg_reach & 1)));
+                                       rep.get(), H, reached, changed, pushed, prev, int(first_full));
     });
     FH_HIP(hipMemsetAsync(scalars.get() + 1, 0, sizeof(uint32_t), stream));
     // unions go to a separate parent array (seeded from rep by k_fb_roots)
