@@ -102,12 +102,18 @@ __global__ void __launch_bounds__(kThreads)
                uint32_t *__restrict__ emin, uint32_t slack, uint32_t *__restrict__ counts,
                uint32_t dmask) {
   __shared__ uint32_t s_h[256];
+  __shared__ uint32_t s_r0;
   s_h[threadIdx.x] = 0;
-  __syncthreads();
   const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(M, base + uint32_t(kTile));
+  // the tile's first log, searched once: a tile spans a log or two, so each
+  // element advances from there (element logs: 40 logs, a search per element
+  // was half the kernel)
+  if (threadIdx.x == 0) s_r0 = base < M ? ch.replica(base, nlog) : 0u;
+  __syncthreads();
+  uint32_t r = s_r0;
   const uint32_t per = fq * k;
   for (uint32_t x = base + threadIdx.x; x < end; x += kThreads) {
-    const uint32_t r = ch.replica(x, nlog);
+    while (r + 1 < nlog && ch.cum[r + 1] <= x) r++;
     const uint32_t y = x - ch.cum[r];
     uint32_t key, val;
     if (elem) {
