@@ -1326,17 +1326,6 @@ struct EngineDevice {
   // outputs of the last run (materialised inside run(), copied by results())
   bool deps_direct = false;  // run_general wrote o_dep_off / o_dep (no compaction)
   bool sv_labels_done = false;  // k_sv_compact wrote the trivial labels / ranks
-  // replica views' KeyDeps pipeline (second stream, second buffer set)
-  hipStream_t s_prev = nullptr;
-  hipEvent_t ev_start = nullptr, ev_join = nullptr, ev_sorted[2] = {}, ev_freed[2] = {};
-  DBuf<uint32_t> sk32c, sk32d, svc, svd;
-  void ensure_prev_stream() {
-    if (s_prev) return;
-    FH_HIP(hipStreamCreateWithFlags(&s_prev, hipStreamNonBlocking));
-    for (hipEvent_t *e : {&ev_start, &ev_join, &ev_sorted[0], &ev_sorted[1], &ev_freed[0],
-                          &ev_freed[1]})
-      FH_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  }
   DBuf<uint32_t> o_dep_off;
   DBuf<uint64_t> o_dep;
   const uint64_t *o_label = nullptr;  // [n] min dot of each command's SCC
@@ -1363,8 +1352,6 @@ struct EngineDevice {
   DBuf<unsigned long long> srcstats;
   SortWorkspace sort_ws;
   ScanWorkspace scan_ws;
-  ScanWorkspace scan_ws_side;  // the side stream's scans (FH_UNION_SIDE)
-  bool union_side = false;    // this run's committed dots are on s_prev
   GraphCore graph;
   GraphOutput gout;
   Probe probe;
@@ -1417,12 +1404,6 @@ struct EngineDevice {
     clear_marks();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
-    if (s_prev) {
-      (void)hipStreamSynchronize(s_prev);
-      for (hipEvent_t e : {ev_start, ev_join, ev_sorted[0], ev_sorted[1], ev_freed[0], ev_freed[1]})
-        if (e) (void)hipEventDestroy(e);
-      (void)hipStreamDestroy(s_prev);
-    }
     if (stream) (void)hipStreamDestroy(stream);
   }
 

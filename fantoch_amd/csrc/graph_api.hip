@@ -644,7 +644,7 @@ struct GraphDevice {
     const uint32_t nexec = hh[0], nmiss = std::min<uint32_t>(hh[1], uint32_t(DT));
     if (debug) {
       auto at = [&](int i) { return (uint64_t(hh[9 + 2 * i]) << 32) | hh[8 + 2 * i]; };
-      fprintf(stderr, "fh graph_small V=%zu phases (us): sort %.1f resolve %.1f blocked %.1f "
+      fprintf(stderr, "fh graph_small V=%zu phases (us): index %.1f resolve %.1f blocked %.1f "
               "H %.1f rounds %.1f depth %.1f order %.1f survivors %.1f\n", V,
               (at(1) - at(0)) * 0.01, (at(2) - at(1)) * 0.01, (at(3) - at(2)) * 0.01,
               (at(4) - at(3)) * 0.01, (at(5) - at(4)) * 0.01, (at(6) - at(5)) * 0.01,
