@@ -11,6 +11,8 @@
 // AEClock<ProcessId> (frontier + exceptions, threshold crate) kept on the
 // host and mirrored to the device per batch.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -360,6 +362,7 @@ struct GraphDevice {
                  const uint32_t *dep_off, const uint64_t *dep_dot,
                  const uint64_t *cmd_shards = nullptr, const uint64_t *dep_shards = nullptr) {
     FH_CHECK(n == 0 || (dot && key_off && dep_off), FH_EINVAL, "null argument");
+    t_enter = std::chrono::steady_clock::now();
     FH_HIP(hipSetDevice(device));
     // check_pending (mod.rs:558-644) retries only the children of dots that
     // were just executed: a retry with no new vertex where none of the
@@ -403,8 +406,7 @@ struct GraphDevice {
     // changed since the last pass
     const bool clk = clock.version != exc_version;
     if (clk) {
-      exc_sorted.assign(clock.exc.begin(), clock.exc.end());
-      std::sort(exc_sorted.begin(), exc_sorted.end());
+      clock.exceptions(exc_sorted);
       d_exc.ensure(exc_sorted.size() + 1);
       exc_version = clock.version;
     }
@@ -638,11 +640,29 @@ struct GraphDevice {
     sp.nddot = nddot;
     static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
     sp.stamps = debug ? 1 : 0;
+    sp.seq = ++small_seq;
+    volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h_small) + 31;
+    *done = 0;
+    const auto t_launch = std::chrono::steady_clock::now();
     launch_graph_small(sp, stream);  // writes the mapped block: no read-back copy
-    FH_HIP(hipStreamSynchronize(stream));
+    // the kernel's last store is the completion word (polled: ~4 us sooner
+    // than a stream synchronize at a batch of one); the stream is queried now
+    // and then so that a failed launch cannot spin forever
+    for (uint32_t i = 1; *done != sp.seq; i++) {
+      if ((i & 1023) != 0) continue;
+      const hipError_t st = hipStreamQuery(stream);
+      if (st == hipErrorNotReady) continue;
+      FH_HIP(st);
+      FH_CHECK(*done == sp.seq, FH_EINVARIANT, "graph_small: pass ended without its completion word");
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const auto t_sync = std::chrono::steady_clock::now();
     const uint32_t *hh = reinterpret_cast<const uint32_t *>(h_small);
     const uint32_t nexec = hh[0], nmiss = std::min<uint32_t>(hh[1], uint32_t(DT));
     if (debug) {
+      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      fprintf(stderr, "fh graph_small host (us): upload %.1f launch+wait %.1f\n",
+              us(t_enter, t_launch), us(t_launch, t_sync));
       auto at = [&](int i) { return (uint64_t(hh[9 + 2 * i]) << 32) | hh[8 + 2 * i]; };
       fprintf(stderr, "fh graph_small V=%zu phases (us): index %.1f resolve %.1f blocked %.1f "
               "H %.1f rounds %.1f depth %.1f order %.1f survivors %.1f\n", V,
@@ -671,7 +691,13 @@ struct GraphDevice {
     passes_small++;
     finish_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, xdot, xlab, bflag, mlist, P2,
                 hb + V);
+    if (debug)
+      fprintf(stderr, "fh graph_small host (us): results %.1f\n",
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_sync)
+                  .count());
   }
+  std::chrono::steady_clock::time_point t_enter;  // add_batch entry (FH_GRAPH_DEBUG timings)
+  uint32_t small_seq = 0;
   uint64_t passes_small = 0;
 
   // The host side of a pass: the drained vertices, executed clock, metrics,
@@ -938,20 +964,7 @@ fh_status fh_graph_set_executed_frontier(fh_graph *h, uint32_t source, uint64_t 
   FH_CHECK(seq >= c.frontier[source], FH_EINVAL,
            "set_executed_frontier: the executed frontier cannot move backwards");
   if (seq == c.frontier[source]) return FH_OK;
-  c.frontier[source] = seq;
-  for (auto it = c.exc.begin(); it != c.exc.end();) {
-    if ((*it >> 56) == source && (*it & 0x00FFFFFFFFFFFFFFull) <= seq)
-      it = c.exc.erase(it);
-    else
-      ++it;
-  }
-  for (;;) {
-    auto it = c.exc.find(fh::make_dot(source, c.frontier[source] + 1));
-    if (it == c.exc.end()) break;
-    c.exc.erase(it);
-    c.frontier[source]++;
-  }
-  c.version++;
+  c.raise_frontier(source, seq);
   h->dev.clock_changed = true;
   FH_API_END
 }

@@ -35,6 +35,7 @@ struct SmallPass {
   // [4] their key entries, [5] their dependency entries
   uint32_t *header;
   int stamps;  // FH_GRAPH_DEBUG: phase clock stamps into header[8..25]
+  uint32_t seq;  // written to header[31] last (the host may poll it)
 };
 
 void launch_graph_small(const SmallPass &p, hipStream_t s);

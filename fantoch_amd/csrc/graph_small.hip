@@ -394,6 +394,11 @@ __global__ void __launch_bounds__(kThreads)
     p.header[5] = td;
   }
   stamp(8);
+  // completion word for a host that polls the mapped block: every thread's
+  // stores are made visible system-wide before it
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(&p.header[31], p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace

@@ -167,8 +167,8 @@ struct PredDevice {
       doff.push_back(uint32_t(deps.size()));
     }
     // executed set mirror
-    std::vector<uint64_t> exc(executed.exc.begin(), executed.exc.end());
-    std::sort(exc.begin(), exc.end());
+    std::vector<uint64_t> exc;
+    executed.exceptions(exc);
     FH_HIP(hipMemcpyAsync(d_frontier.get(), executed.frontier, sizeof(executed.frontier),
                           hipMemcpyHostToDevice, stream));
     uint64_t *dexc = d_exc.ensure(exc.size() + 1);
