@@ -88,6 +88,34 @@ struct AEClock {
     version++;
     return true;
   }
+  // add for a list of dots (one executor pass's executed dots): bits first,
+  // then each touched process's frontier advances once, by whole runs
+  void add_all(const uint64_t *dots, size_t n) {
+    bool changed = false;
+    uint64_t touched[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i < n; i++) {
+      const uint64_t d = dots[i];
+      const uint32_t s = uint32_t(d >> 56);
+      const uint64_t q = d & 0x00FFFFFFFFFFFFFFull;
+      if (q <= frontier[s]) continue;
+      if (q - frontier[s] <= kWin) {
+        uint64_t &w = words(s)[(q % kWin) >> 6];
+        const uint64_t b = uint64_t(1) << (q & 63);
+        if (w & b) continue;
+        if (!far.empty() && far.count(d)) continue;
+        w |= b;
+        nbits[s]++;
+        touched[s >> 6] |= uint64_t(1) << (s & 63);
+        changed = true;
+      } else if (far.insert(d).second) {
+        touched[s >> 6] |= uint64_t(1) << (s & 63);
+        changed = true;
+      }
+    }
+    for (uint32_t g = 0; g < 4; g++)
+      for (uint64_t m = touched[g]; m; m &= m - 1) advance(g * 64 + uint32_t(__builtin_ctzll(m)));
+    if (changed) version++;
+  }
   // Raise s's frontier to seq (>= the current one): exceptions at or below it
   // go, and exceptions right above it fold in
   void raise_frontier(uint32_t s, uint64_t seq) {
@@ -111,9 +139,15 @@ struct AEClock {
     out.clear();
     for (uint32_t s = 0; s < 256; s++) {
       if (!nbits[s]) continue;
+      // the ring's slot i holds q = the one in (frontier, frontier + kWin]
+      // with q mod kWin = i
       const uint64_t *w = ring[s].get();
-      for (uint64_t q = frontier[s] + 1; q <= frontier[s] + kWin; q++)
-        if ((w[(q % kWin) >> 6] >> (q & 63)) & 1) out.push_back(make_dot(s, q));
+      const uint64_t f = frontier[s];
+      for (uint64_t x = 0; x < kWin / 64; x++)
+        for (uint64_t m = w[x]; m; m &= m - 1) {
+          const uint64_t i = x * 64 + uint64_t(__builtin_ctzll(m));
+          out.push_back(make_dot(s, f + 1 + ((i - (f + 1)) & (kWin - 1))));
+        }
     }
     out.insert(out.end(), far.begin(), far.end());
     std::sort(out.begin(), out.end());
@@ -145,10 +179,18 @@ struct AEClock {
   void advance(uint32_t s) {
     for (;;) {
       const uint64_t q = frontier[s] + 1;
-      if (nbits[s] && test(s, q)) {
-        clear(s, q);
-        frontier[s] = q;
-        continue;
+      if (nbits[s]) {
+        // the run of set bits from q's slot to the end of its word
+        uint64_t &w = ring[s][(q % kWin) >> 6];
+        const uint64_t x = ~(w >> (q & 63));  // ones above the word's top: len <= 64 - (q & 63)
+        const uint64_t len = x ? uint64_t(__builtin_ctzll(x)) : 64;
+        if (len) {
+          const uint64_t mask = (len == 64 ? ~uint64_t(0) : ((uint64_t(1) << len) - 1)) << (q & 63);
+          w &= ~mask;
+          nbits[s] -= uint32_t(len);
+          frontier[s] += len;
+          continue;
+        }
       }
       if (!far.empty()) {
         auto it = far.find(make_dot(s, q));

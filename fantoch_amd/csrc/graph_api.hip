@@ -88,29 +88,9 @@ __global__ void k_resolve_fill(uint32_t V, const uint64_t *__restrict__ dot,
 // The batch's rows, uploaded as one block, appended after the carried
 // prefix (offsets rebased past it); the executed-clock mirror rides along
 // when it changed (nf = 256 frontier words, then ne exceptions).
-struct Upload {
-  const uint64_t *dot, *dep, *clk;
-  const uint32_t *key, *koff, *doff;
-  uint32_t n, nk, nd, nf, ne;
-};
-__global__ void k_append(Upload u, uint64_t *__restrict__ vdot, uint32_t *__restrict__ koff,
-                         uint32_t *__restrict__ key, uint32_t *__restrict__ doff,
-                         uint64_t *__restrict__ dep, uint32_t kbase, uint32_t dbase,
-                         uint64_t *__restrict__ frontier, uint64_t *__restrict__ exc) {
-  const uint32_t m = max(max(u.n ? u.n + 1 : 0u, u.nk), max(u.nd, u.nf + u.ne));
-  GRID_STRIDE(i, m) {
-    // rows only for a non-empty batch: with n == 0 the carried set's end
-    // offsets (koff[0] = koff[P] of the set) must stay as they are
-    if (i < u.n) vdot[i] = u.dot[i];
-    if (u.n && i <= u.n) {
-      koff[i] = u.koff[i] + kbase;
-      doff[i] = u.doff[i] + dbase;
-    }
-    if (i < u.nk) key[i] = u.key[i];
-    if (i < u.nd) dep[i] = u.dep[i];
-    if (i < u.nf) frontier[i] = u.clk[i];
-    else if (i < u.nf + u.ne) exc[i - u.nf] = u.clk[i];
-  }
+__global__ void k_append(Upload u, AppendDst a) {
+  const uint32_t m = append_items(u);
+  GRID_STRIDE(i, m) append_item(u, a, i);
 }
 
 // executed vertices in execution order: their dots and SCC labels
@@ -451,23 +431,25 @@ struct GraphDevice {
       u.key = reinterpret_cast<const uint32_t *>(dup + o_key);
       u.koff = reinterpret_cast<const uint32_t *>(dup + o_ko);
       u.doff = reinterpret_cast<const uint32_t *>(dup + o_do);
-      const uint32_t m = std::max(std::max(u.n ? u.n + 1 : 0u, u.nk), std::max(u.nd, u.nf + u.ne));
-      k_append<<<grid_for(m, B), B, 0, stream>>>(u, ddot_v + P, dko + P, dk + W.KP, ddo + P,
-                                                 dd + W.DP, W.KP, W.DP, d_frontier.get(),
-                                                 d_exc.get());
     }
     const std::vector<uint64_t> &exc = exc_sorted;
     uint64_t *dexc = d_exc.ensure(exc.size() + 1);
+    const AppendDst adst{ddot_v + P, dko + P, dk + W.KP, ddo + P, dd + W.DP, W.KP, W.DP,
+                         d_frontier.get(), dexc};
     // FH_GRAPH_SMALL=0 (tests): every pass through the general path
     static const bool small_on = [] {
       const char *e = getenv("FH_GRAPH_SMALL");
       return !(e && *e == '0');
     }();
     if (small_on && V <= size_t(kSmallV) && size_t(W.DP) + DB <= size_t(kSmallE)) {
+      // k_graph_small appends the rows itself
       small_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, V, KB, DB, ddot_v, dko, dk,
-                 ddo, dd, dexc, uint32_t(exc.size()));
+                 ddo, dd, dexc, uint32_t(exc.size()), u, adst);
       return;
     }
+    if (n || clk)
+      k_append<<<grid_for(std::max({u.n ? u.n + 1 : 0u, u.nk, u.nd, u.nf + u.ne}), B), B, 0,
+                 stream>>>(u, adst);
     // dot -> vid index
     uint64_t *sd = nullptr;
     uint32_t *sv = nullptr;
@@ -592,7 +574,8 @@ struct GraphDevice {
   void small_pass(size_t n, const uint64_t *dot, const uint32_t *dep_off, const uint64_t *dep_dot,
                   const uint64_t *cmd_shards, const uint64_t *dep_shards, size_t V, size_t KB,
                   size_t DB, const uint64_t *ddot_v, const uint32_t *dko, const uint32_t *dk,
-                  const uint32_t *ddo, const uint64_t *dd, const uint64_t *dexc, uint32_t nexc) {
+                  const uint32_t *ddo, const uint64_t *dd, const uint64_t *dexc, uint32_t nexc,
+                  const Upload &up, const AppendDst &adst) {
     DSet &W = ds[cur];
     DSet &N = ds[1 - cur];
     // the next set holds at most every current vertex, key and dependency
@@ -615,6 +598,8 @@ struct GraphDevice {
       h_small_cap = bytes * 2;
     }
     SmallPass sp;
+    sp.up = up;
+    sp.dst = adst;
     sp.V = uint32_t(V);
     sp.P = uint32_t(V - n);
     sp.dot = ddot_v;
@@ -664,9 +649,9 @@ struct GraphDevice {
       fprintf(stderr, "fh graph_small host (us): upload %.1f launch+wait %.1f\n",
               us(t_enter, t_launch), us(t_launch, t_sync));
       auto at = [&](int i) { return (uint64_t(hh[9 + 2 * i]) << 32) | hh[8 + 2 * i]; };
-      fprintf(stderr, "fh graph_small V=%zu phases (us): index %.1f resolve %.1f blocked %.1f "
+      fprintf(stderr, "fh graph_small V=%zu phases (us): append %.1f index %.1f resolve %.1f blocked %.1f "
               "H %.1f rounds %.1f depth %.1f order %.1f survivors %.1f\n", V,
-              (at(1) - at(0)) * 0.01, (at(2) - at(1)) * 0.01, (at(3) - at(2)) * 0.01,
+              (at(9) - at(0)) * 0.01, (at(1) - at(9)) * 0.01, (at(2) - at(1)) * 0.01, (at(3) - at(2)) * 0.01,
               (at(4) - at(3)) * 0.01, (at(5) - at(4)) * 0.01, (at(6) - at(5)) * 0.01,
               (at(7) - at(6)) * 0.01, (at(8) - at(7)) * 0.01);
     }
@@ -729,7 +714,6 @@ struct GraphDevice {
     for (uint32_t j = 0; j < nexec; j++) {
       const uint64_t d = xdot[j];
       ready.emplace_back(d, xlab[j]);
-      clock.add(d);  // executed clock update (tarjan.rs:296)
       // metrics: one ChainSize per SCC (members are contiguous in the
       // execution order), one ExecutionDelay per command
       if (j == 0 || xlab[j - 1] != xlab[j]) m_chain.push_back(0);
@@ -747,6 +731,7 @@ struct GraphDevice {
     }
     FH_CHECK(got_n == want_n && got_h == want_h, FH_EINVARIANT,
              "graph: an executed dot was neither a pending vertex nor one of the batch");
+    clock.add_all(xdot.data(), nexec);  // executed clock update (tarjan.rs:296)
     // the batch's survivors join the host's pending metadata, in arrival
     // order (after the pass: a failed pass leaves host and device sets equal)
     for (size_t i = 0; i < n; i++) {

@@ -60,6 +60,7 @@ __device__ uint32_t block_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
 // all-ones dot is reserved (the empty slot), as everywhere in the library
 constexpr int kHash = 2 * kSmallV;
 constexpr uint64_t kEmpty = ~0ull;
+constexpr int kSmallExc = 1024;  // executed-clock exceptions staged in LDS
 __device__ __forceinline__ uint32_t hash_slot(uint64_t d) {
   return uint32_t((d * 0x9E3779B97F4A7C15ull) >> 52) & (kHash - 1);
 }
@@ -89,7 +90,7 @@ __device__ void sweep(int n, uint32_t *s_ch, F body) {
 
 __global__ void __launch_bounds__(kThreads)
     k_graph_small(SmallPass p) {
-  // phase stamps (FH_GRAPH_DEBUG): wall clock (100 MHz) at 8 points into
+  // phase stamps (FH_GRAPH_DEBUG): wall clock (100 MHz) at 10 points into
   // header[8 + 2i] (host prints the phase times)
   auto stamp = [&](int i) {
     if (p.stamps && threadIdx.x == 0) {
@@ -99,6 +100,29 @@ __global__ void __launch_bounds__(kThreads)
     }
   };
   stamp(0);
+  // the batch's rows after the carried prefix, and the clock mirror
+  // (k_append's job on the general path); the pass below reads them back
+  // from global memory after the barrier
+  {
+    // four items per thread per round, every load issued before a store: one
+    // PCIe round trip per 4096 items instead of one per 1024
+    const uint32_t m = append_items(p.up);
+    for (uint32_t i0 = 0; i0 < m; i0 += 4 * kThreads) {
+      AppendVals av[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = i0 + uint32_t(k) * kThreads + threadIdx.x;
+        if (i < m) append_load(p.up, i, av[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = i0 + uint32_t(k) * kThreads + threadIdx.x;
+        if (i < m) append_store(p.up, p.dst, i, av[k]);
+      }
+    }
+  }
+  __syncthreads();
+  stamp(9);
   __shared__ uint64_t s_dot[kSmallV], s_key[kSmallV];
   // dot -> vid hash index (open addressing, load <= 1/2); after the resolve
   // its key words are scratch for the order's group counts
@@ -106,6 +130,9 @@ __global__ void __launch_bounds__(kThreads)
   __shared__ uint16_t s_hv[kHash];
   __shared__ uint16_t s_off[kSmallV + 1], s_dst[kSmallE], s_tgt[kSmallE];
   __shared__ uint64_t s_front[256];  // executed clock frontier (AEClock)
+  // its exceptions, staged when they fit: the resolve's binary search per
+  // dependency then runs in LDS instead of ~8 dependent global loads
+  __shared__ uint64_t s_exc[kSmallExc];
   __shared__ uint16_t s_H[kSmallV], s_R[kSmallV], s_W[kSmallV], s_min[kSmallV];
   __shared__ uint32_t s_D[kSmallV];
   __shared__ uint8_t s_blk[kSmallV], s_F[kSmallV];
@@ -116,6 +143,10 @@ __global__ void __launch_bounds__(kThreads)
   if (tid < 256) s_front[tid] = p.frontier[tid];
   for (int x = tid; x < kHash; x += kThreads) s_hk[x] = kEmpty;
   for (int x = tid; x < V; x += kThreads) s_dot[x] = p.dot[x];
+  const bool exc_lds = p.nexc <= uint32_t(kSmallExc);
+  if (exc_lds)
+    for (uint32_t x = tid; x < p.nexc; x += kThreads) s_exc[x] = p.exc[x];
+  const uint64_t *exc = exc_lds ? s_exc : p.exc;
   __syncthreads();
   // 1. dot -> vid index; a dot indexed twice (mod.rs:235-240)
   for (int x = tid; x < V; x += kThreads) {
@@ -135,32 +166,44 @@ __global__ void __launch_bounds__(kThreads)
   }
   __syncthreads();
   stamp(1);
-  // 2. resolve: one pass over the dependency lists (the global loads)
-  // writes each entry's target vid, or kNone for self / executed / missing,
-  // into LDS at its list position; the scan then compacts from LDS
+  // 2. resolve: one pass over the dependency entries, a thread per entry
+  // (coalesced loads, no per-vertex chains of dependent global loads),
+  // writes each entry's target vid into LDS at its list position: kNone for
+  // executed, kMiss for missing; an entry naming its own vertex is dropped
+  // by the per-vertex pass below (its own dot is always a vertex)
+  constexpr uint16_t kMiss = 0xFFFE;
+  const uint32_t e0 = p.doff[0], DT = p.doff[V] - e0;
+  for (uint32_t e = tid; e < DT; e += kThreads) {
+    const uint64_t d = p.ddot[e0 + e];
+    uint16_t t = kNone;
+    if (!executed_dev(d, s_front, exc, p.nexc)) {
+      const int u = find_hash(s_hk, s_hv, d);
+      if (u >= 0) {
+        t = uint16_t(u);
+      } else {
+        t = kMiss;
+        const uint32_t q = atomicAdd(&s_nmiss, 1u);
+        if (q < p.miss_cap) p.miss[q] = d;
+      }
+    }
+    s_tgt[e] = t;
+  }
+  __syncthreads();
   uint32_t cnt[2] = {0, 0};
-  const uint32_t e0 = p.doff[0];
   for (int j = 0; j < 2; j++) {
     const int v = 2 * tid + j;  // a thread's vertices are adjacent: scans follow vid order
     if (v >= V) continue;
     bool missing = false;
-    const uint64_t self = s_dot[v];
-    const uint32_t eb = p.doff[v], ee = p.doff[v + 1];
+    const uint32_t eb = p.doff[v] - e0, ee = p.doff[v + 1] - e0;
     for (uint32_t e = eb; e < ee; e++) {
-      const uint64_t d = p.ddot[e];
-      uint16_t t = kNone;
-      if (d != self && !executed_dev(d, s_front, p.exc, p.nexc)) {
-        const int u = find_hash(s_hk, s_hv, d);
-        if (u >= 0) {
-          t = uint16_t(u);
-          cnt[j]++;
-        } else {
-          missing = true;
-          const uint32_t q = atomicAdd(&s_nmiss, 1u);
-          if (q < p.miss_cap) p.miss[q] = d;
-        }
+      const uint16_t t = s_tgt[e];
+      if (t == uint16_t(v)) {
+        s_tgt[e] = kNone;  // self (graph/mod.rs skips the vertex's own dot)
+      } else if (t == kMiss) {
+        missing = true;
+      } else if (t != kNone) {
+        cnt[j]++;
       }
-      s_tgt[e - e0] = t;
     }
     s_blk[v] = missing;
   }
@@ -175,7 +218,7 @@ __global__ void __launch_bounds__(kThreads)
       const uint32_t eb = p.doff[v] - e0, ee = p.doff[v + 1] - e0;
       for (uint32_t e = eb; e < ee; e++) {
         const uint16_t t = s_tgt[e];
-        if (t != kNone) s_dst[o++] = t;
+        if (t < kMiss) s_dst[o++] = t;
       }
     }
     if (tid == 0) s_off[V] = uint16_t(etot);

@@ -210,6 +210,39 @@ def test_executed_frontier_never_moves_back_and_folds_exceptions():
         L.check(ex._lib.fh_graph_set_executed_frontier(ex._h, 2, 1))
 
 
+def test_many_and_far_clock_exceptions():
+    """AEClock with more exceptions than the small pass stages in LDS (1,500,
+    so its resolve searches the device list), exceptions beyond the bit ring
+    (4,096 above the frontier), and frontier raises folding both."""
+    ex = _ex()
+    ex.mark_executed([D((2, s)) for s in range(2, 3001, 2)] + [D((2, 10000))] +
+                     [D((3, s)) for s in range(5000, 5101)])
+    _add(ex, D((1, 1)), [D((2, 2000)), D((2, 10000)), D((3, 5050))])
+    assert ex.pending() == 0                      # every dependency executed
+    _add(ex, D((1, 2)), [D((2, 2001))])
+    assert ex.pending() == 1 and ex.missing() == [D((2, 2001))]
+    ex.mark_executed([D((2, 1))])                 # folds 1, 2; 3 is not executed
+    _add(ex, D((1, 3)), [D((2, 3))])
+    assert ex.pending() == 2
+    ex.mark_executed([D((2, 2001))])
+    ex.handle_batch([])
+    assert ex.pending() == 1                      # (1, 2) went, (1, 3) waits on (2, 3)
+    ex.set_executed_frontier(2, 2999)             # folds the even exceptions up to 3000
+    ex.handle_batch([])
+    assert ex.pending() == 0
+    _add(ex, D((1, 4)), [D((2, 3000)), D((3, 5100))])
+    _add(ex, D((1, 5)), [D((2, 3001)), D((3, 4999))])
+    assert ex.pending() == 1 and ex.missing() == [D((2, 3001)), D((3, 4999))]
+    ex.set_executed_frontier(3, 5200)             # far exceptions at or below it go
+    ex.mark_executed([D((2, 3001))])
+    ex.handle_batch([])
+    assert ex.pending() == 0
+    got = []
+    while (r := ex.to_clients()) is not None:
+        got.append(r[0])
+    assert got == [D((1, s)) for s in (1, 2, 3, 4, 5)]
+
+
 def test_device_resident_backlog_then_release_matches_oracle():
     """A command held back until the end leaves most of the stream pending
     behind it (carried on the device from batch to batch); the missing set is
