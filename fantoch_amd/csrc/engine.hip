@@ -1252,6 +1252,24 @@ __global__ void k_pack_dots(uint32_t n, const uint64_t *__restrict__ dot, int sb
   }
 }
 
+// per-key offsets straight from the sorted keys: o[k] = the number of
+// elements whose key is below k (lower bound), for k in [0, K] -- one launch
+// instead of a histogram (run starts, run counts) and its scan
+__global__ void k_key_offsets(uint32_t m, const uint32_t *__restrict__ keys, uint32_t K,
+                              uint32_t *__restrict__ o) {
+  GRID_STRIDE(k, K + 1) {
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1);
+      if (keys[mid] < k)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    o[k] = lo;
+  }
+}
+
 __global__ void k_run_start(uint32_t m, const uint32_t *__restrict__ keys,
                             uint32_t *__restrict__ start) {
   GRID_STRIDE(j, m) if (j == 0 || keys[j - 1] != keys[j]) start[keys[j]] = j;
@@ -2193,13 +2211,20 @@ struct EngineDevice {
     }
     // per-key offsets over the ascending key space (histogram + scan)
     o_nelem = gout.nelem;
-    uint32_t *h = key_hist.ensure(key_space + 1);
     uint32_t *o = key_offs.ensure(key_space + 2);
-    uint32_t *hp = headpos.ensure(key_space + 1);
-    FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
-    k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
-    k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
-    exclusive_scan_u32(h, o, key_space, scan_ws, stream);
+    uint32_t *hp = nullptr;
+    if (sv_fused && bucket_order) {
+      // key-grouped runs (not ascending): histogram of the runs and its scan
+      uint32_t *h = key_hist.ensure(key_space + 1);
+      hp = headpos.ensure(key_space + 1);
+      FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
+      k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
+      k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
+      exclusive_scan_u32(h, o, key_space, scan_ws, stream);
+    } else {
+      k_key_offsets<<<grid_for(uint32_t(key_space) + 1, B), B, 0, stream>>>(
+          o_nelem, gout.pk_key, uint32_t(key_space), o);
+    }
     if (sv_fused) {
       uint64_t *sq = seq_dot.ensure(o_nelem + 1);
       if (bucket_order) {

@@ -870,16 +870,6 @@ __global__ void __launch_bounds__(256)
   if (src_mx) acc.commit(src_mx, src_cnt);  // (src_mx is uniform)
 }
 
-// packed dots back to u64 after the per-key sort
-__global__ void k_unpack_dots(uint32_t n, const uint32_t *__restrict__ pd, int sb,
-                              uint64_t *__restrict__ out) {
-  const uint32_t m = (1u << sb) - 1;
-  GRID_STRIDE(j, n) {
-    const uint32_t x = pd[j];
-    out[j] = (uint64_t(x >> sb) << 56) | (x & m);
-  }
-}
-
 __global__ void k_copy_dot(uint32_t V, const uint64_t *__restrict__ dot, uint64_t *__restrict__ out) {
   GRID_STRIDE(v, V) out[v] = dot[v];
 }
@@ -1293,10 +1283,9 @@ void GraphCore::build_per_key(const GraphInput &in, GraphOutput &out) {
         k_elem_fill_dots<<<grid_for(nexec, B), B, 0, stream>>>(nexec, in.k, ord, in.key32, in.dot, pk,
                                                                ek, pa, in.src_mx, in.src_cnt);
       }
-      uint32_t *po = nullptr;
-      sort_pairs<uint32_t, uint32_t>(ek, pa, k2, pb, ek, pa, ne, in.key_bits, sort_ws, stream, &ko,
-                                     &po);
-      k_unpack_dots<<<grid_for(ne, B), B, 0, stream>>>(ne, po, in.dot_sb, ed);
+      // the last pass writes the u64 dots into ed (pk_da)
+      sort_pairs_unpack_dots(ek, pa, k2, pb, ek, pa, ne, in.key_bits, in.dot_sb, ed, sort_ws, stream,
+                             &ko);
       dout = ed;
     } else {
       if (fill_from_groups) {

@@ -31,5 +31,14 @@ void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va,
                 K *kb, VT *vb, size_t n, int key_bits, SortWorkspace &ws,
                 hipStream_t s, K **kout, VT **vout);
 
+// sort_pairs of (key, packed 32-bit dot src << sb | seq) whose last pass
+// writes the values widened to u64 dots (src << 56 | seq) into dout (no
+// separate unpacking pass over the sorted values); *kout: the sorted keys
+// (ka or kb).  dout must not alias the value buffers.
+void sort_pairs_unpack_dots(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *ka,
+                            uint32_t *va, uint32_t *kb, uint32_t *vb, size_t n, int key_bits,
+                            int sb, uint64_t *dout, SortWorkspace &ws, hipStream_t s,
+                            uint32_t **kout);
+
 
 }  // namespace fh

@@ -74,6 +74,59 @@ void sort_pairs(const K *keys_in, const VT *vals_in, K *ka, VT *va, K *kb, VT *v
 #undef FH_SORT_RUN
 }
 
+namespace {
+template <int DB>
+void unpack_passes(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *ka, uint32_t *va,
+                   uint32_t *kb, uint32_t *vb, size_t n, int passes, int db, int sb,
+                   uint64_t *dout, SortWorkspace &ws, hipStream_t s, uint32_t **kout) {
+  using Src = ArraySrc<uint32_t, uint32_t, false>;
+  const uint32_t tiles = uint32_t((n + kTile - 1) / kTile);
+  const uint32_t groups = (tiles + kGroup - 1) / kGroup;
+  ws.prepare(tiles, passes, s);
+  const uint32_t R = 1u << db;
+  uint32_t *counts = ws.meta.get();
+  uint32_t *gsum = counts + size_t(tiles) * R;
+  uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
+  const uint32_t *ki = keys_in, *vi = vals_in;
+  for (int p = 0; p + 1 < passes; p++) {
+    // never write a pass over its own input
+    const bool to_b = ki == ka || vi == va;
+    uint32_t *kn = to_b ? kb : ka, *vn = to_b ? vb : va;
+    sort_pass<uint32_t, uint32_t, DB, Src>(Src{ki, vi}, kn, StoreVal<uint32_t>{vn}, n, db * p,
+                                           tiles, groups, counts, gsum, dbase, s, true);
+    ki = kn;
+    vi = vn;
+  }
+  uint32_t *kn = ki == ka ? kb : ka;
+  sort_pass<uint32_t, uint32_t, DB, Src, StoreUnpackDot>(Src{ki, vi}, kn, StoreUnpackDot{dout, sb},
+                                                         n, db * (passes - 1), tiles, groups,
+                                                         counts, gsum, dbase, s, true);
+  *kout = kn;
+}
+}  // namespace
+
+void sort_pairs_unpack_dots(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *ka,
+                            uint32_t *va, uint32_t *kb, uint32_t *vb, size_t n, int key_bits,
+                            int sb, uint64_t *dout, SortWorkspace &ws, hipStream_t s,
+                            uint32_t **kout) {
+  FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "sort: too many elements (>= 2^30)");
+  FH_CHECK(vals_in != nullptr && sb >= 1 && sb <= 31, FH_EINVAL, "sort: packed dots expected");
+  const int db = sort_digit_bits(key_bits, 4);
+  int passes = (key_bits + db - 1) / db;
+  if (passes < 1) passes = 1;
+  if (db == 8 && passes > 4) passes = 4;
+  if (n == 0) {
+    *kout = ka;
+    return;
+  }
+  if (db == 6)
+    unpack_passes<6>(keys_in, vals_in, ka, va, kb, vb, n, passes, db, sb, dout, ws, s, kout);
+  else if (db == 7)
+    unpack_passes<7>(keys_in, vals_in, ka, va, kb, vb, n, passes, db, sb, dout, ws, s, kout);
+  else
+    unpack_passes<8>(keys_in, vals_in, ka, va, kb, vb, n, passes, db, sb, dout, ws, s, kout);
+}
+
 template void sort_pairs<uint32_t, uint32_t>(const uint32_t *, const uint32_t *, uint32_t *,
                                              uint32_t *, uint32_t *, uint32_t *, size_t, int,
                                              SortWorkspace &, hipStream_t, uint32_t **,

@@ -298,15 +298,32 @@ __device__ __forceinline__ uint32_t block_excl_scan_t(uint32_t v, uint32_t *s_tm
   return pre + x - v;
 }
 
+// Value stores of the scatter: as they are, or (the per-key sequences) a
+// packed 32-bit dot src << sb | seq widened to the u64 dot src << 56 | seq
+template <class VT>
+struct StoreVal {
+  static constexpr int kBytes = sizeof(VT);
+  VT *p;
+  __device__ __forceinline__ void operator()(uint32_t o, VT v) const { p[o] = v; }
+};
+struct StoreUnpackDot {
+  static constexpr int kBytes = 8;
+  uint64_t *p;
+  int sb;
+  __device__ __forceinline__ void operator()(uint32_t o, uint32_t v) const {
+    p[o] = (uint64_t(v >> sb) << 56) | (v & ((1u << sb) - 1));
+  }
+};
+
 // The scatter of one pass over a tile of kTile elements, TH threads of kTile /
 // TH items (512 by default: twice the waves per tile for the same LDS, so a
 // CU holds 24 instead of 12 waves of the u64-value scatter).  Wave
 // w owns the contiguous sub-tile [w·64·IT, (w+1)·64·IT), so (wave, item,
 // lane) order is input order and the scatter stays stable; the tile digit
 // counts (k_up) do not depend on TH.
-template <class K, class VT, int DB, class Src, int TH = kThreads>
+template <class K, class VT, int DB, class Src, int TH = kThreads, class St = StoreVal<VT>>
 __global__ void __launch_bounds__(TH)
-    k_down(Src src, K *__restrict__ kout, VT *__restrict__ vout, uint32_t n, int shift,
+    k_down(Src src, K *__restrict__ kout, St vout, uint32_t n, int shift,
            const uint32_t *__restrict__ counts, const uint32_t *__restrict__ gsum,
            uint32_t gsize, const uint32_t *__restrict__ dbase) {
   // digits per thread in the tile-wide scan: Q = R / TH, or one digit for
@@ -401,7 +418,7 @@ __global__ void __launch_bounds__(TH)
     const uint32_t d = uint32_t((k >> shift) & (R - 1));
     const uint32_t o = s_gb[d] + (j - s_dex[d]);
     kout[o] = k;
-    vout[o] = s_v[j];
+    vout(o, s_v[j]);
   }
 }
 
@@ -420,8 +437,8 @@ struct ArraySrc {
 };
 
 // one LSD pass over DB bits at `shift`, input from `src`
-template <class K, class VT, int DB, class Src>
-void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tiles,
+template <class K, class VT, int DB, class Src, class St = StoreVal<VT>>
+void sort_pass(const Src &src, K *ko, St vo, size_t n, int shift, uint32_t tiles,
                uint32_t groups, uint32_t *counts, uint32_t *gsum, uint32_t *dbase, hipStream_t s,
                bool probe, bool have_counts = false) {
   if (!have_counts)  // (else the producer of the input wrote the tile counts)
@@ -446,15 +463,15 @@ void sort_pass(const Src &src, K *ko, VT *vo, size_t n, int shift, uint32_t tile
       // one probe name per kernel instantiation, as rocprof reports them
       const char *name = sizeof(K) == 8 ? "sort_scatter_u64"
                          : sizeof(VT) == 8 ? "sort_scatter_dots" : "sort_scatter";
-      probed_launch(name, double(n) * 2.0 * (sizeof(K) + sizeof(VT)), kern, dim3(tiles), dim3(th),
-                    s, src, ko, vo, uint32_t(n), shift, (const uint32_t *)counts,
+      probed_launch(name, double(n) * (2.0 * sizeof(K) + sizeof(VT) + St::kBytes), kern, dim3(tiles),
+                    dim3(th), s, src, ko, vo, uint32_t(n), shift, (const uint32_t *)counts,
                     (const uint32_t *)gsum, gsize, (const uint32_t *)dbase);
     }
   };
   if (down_th == 512)
-    down(k_down<K, VT, DB, Src, 512>, 512);
+    down(k_down<K, VT, DB, Src, 512, St>, 512);
   else
-    down(k_down<K, VT, DB, Src, kThreads>, kThreads);
+    down(k_down<K, VT, DB, Src, kThreads, St>, kThreads);
 }
 
 template <class K, class VT, int DB, class Src0>
@@ -470,16 +487,16 @@ void sort_passes(const Src0 &src0, bool probe0, K *ka, VT *va, K *kb, VT *vb, bo
   uint32_t *dbase = gsum + size_t(std::max<uint32_t>(groups, 4)) * R;
   K *ko = alias_a ? kb : ka;
   VT *vo = alias_a ? vb : va;
-  sort_pass<K, VT, DB, Src0>(src0, ko, vo, n, 0, tiles, groups, counts, gsum, dbase, s, probe0,
-                            counts0);
+  sort_pass<K, VT, DB, Src0>(src0, ko, StoreVal<VT>{vo}, n, 0, tiles, groups, counts, gsum, dbase,
+                            s, probe0, counts0);
   const K *ki = ko;
   const VT *vi = vo;
   for (int p = 1; p < passes; p++) {
     K *kn = ko == ka ? kb : ka;
     VT *vn = ko == ka ? vb : va;
-    sort_pass<K, VT, DB, ArraySrc<K, VT, false>>(ArraySrc<K, VT, false>{ki, vi}, kn, vn, n,
-                                                 db * p, tiles, groups, counts, gsum, dbase, s,
-                                                 true);
+    sort_pass<K, VT, DB, ArraySrc<K, VT, false>>(ArraySrc<K, VT, false>{ki, vi}, kn,
+                                                 StoreVal<VT>{vn}, n, db * p, tiles, groups,
+                                                 counts, gsum, dbase, s, true);
     ko = kn;
     vo = vn;
     ki = ko;
