@@ -5,7 +5,7 @@ rocprofv3 --kernel-trace run of bench.py.
 A run spans from its first kernel (--run-start, default k_view_records: the
 command-level KeyDeps pass that opens every C4 run; k_log_keys for the
 chunked path) to its last one
-(--run-end, default k_run_count: the per-key offsets that close it).  A
+(--run-end, default k_key_offsets: the per-key offsets that close it).  A
 copyBuffer dispatch inside a run is in-step: a copy the run itself makes
 (graph_tile's pass-2 core list, H2D; the small read-backs are k_fetch_u32
 kernels, not copies).  One outside every run is staging or read-back: the
@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--run-start", default="k_view_records", help="the kernel that opens a run")
-    ap.add_argument("--run-end", default="k_run_count", help="the kernel that closes a run")
+    ap.add_argument("--run-end", default="k_key_offsets", help="the kernel that closes a run")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
