@@ -449,6 +449,7 @@ __global__ void __launch_bounds__(kThreads)
 void launch_graph_small(const SmallPass &p, hipStream_t s) {
   FH_CHECK(p.V >= 1 && p.V <= uint32_t(kSmallV), FH_EINVARIANT, "graph_small: vertex count");
   k_graph_small<<<1, kThreads, 0, s>>>(p);
+  FH_HIP(hipGetLastError());  // a failed launch, before the host polls for its completion word
 }
 
 }  // namespace fh
