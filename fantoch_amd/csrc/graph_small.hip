@@ -9,9 +9,12 @@
 // E <= kSmallE dependency entries everything happens here, in LDS, in one
 // launch, reading the batch from and writing its results to mapped pinned
 // host memory:
+//  0. the batch's rows appended after the carried prefix (read over PCIe
+//     from the mapped upload block, every load of a thread issued before its
+//     first store), and the executed-clock mirror when it changed;
 //  1. the dot -> vid index: an LDS hash table (duplicate check,
 //     mod.rs:235-240);
-//  2. dependencies resolved once (the global loads): self and executed ones
+//  2. dependencies resolved once, a thread per entry: self and executed ones
 //     ignored (tarjan.rs:131-148), others are vertices or missing (the
 //     vertex is blocked, tarjan.rs:150-170); missing dots listed;
 //  3. blocked closure: a vertex reaching a missing dependency stays pending
