@@ -10,7 +10,9 @@ reports what DESIGN.md §5.2 / §9 quote for the global SCC path:
   4096-position tiles, and how many edges stay between classes (raw, after
   deduplicating each class's targets, as class-to-class edges);
 * edges implied by a two-edge path (droppable without changing reachability
-  or longest paths).
+  or longest paths);
+* how much edge work a frontier version of the coloring's H propagation
+  would do (vertices re-evaluated only when a target's H changed).
 
 Usage: python tools/c5_graph_stats.py [N]   (default 2,000,000; ~15 min, ~20 GB)
 """
@@ -46,6 +48,53 @@ def scc_labels(n, src, dst):
     return connected_components(a, directed=True, connection="strong")[1]
 
 
+def window_classes(n, src, dst, bs=128):
+    """The engine's windows: SCCs of bs-position blocks and of the blocks
+    shifted by bs / 2, united (k_windows' classes)."""
+    def block(off):
+        m = (src + off) // bs == (dst + off) // bs
+        return scc_labels(n, src[m], dst[m])
+    l1, l2 = block(0), block(bs // 2)
+    n1 = l1.max() + 1
+    u = sp.csr_matrix((np.ones(2 * n, np.int8), (np.r_[np.arange(n), np.arange(n)], np.r_[l1, n1 + l2])),
+                      shape=(n, n1 + l2.max() + 1))
+    g = sp.bmat([[None, u], [u.T, None]])
+    return connected_components(g, directed=False)[1][:n]
+
+
+def frontier_sweeps(n, src, dst, cls):
+    """Round 1 of the coloring's H propagation (pull, class maxima, pointer
+    jumping) as synchronous sweeps: per sweep the vertices whose H changed,
+    and the edges a frontier version would touch (those of vertices with a
+    target that changed in the previous sweep)."""
+    e = len(src)
+    mx = np.zeros(cls.max() + 1, np.int64)
+    np.maximum.at(mx, cls, np.arange(n))
+    h = mx[cls]
+    deg = np.bincount(src, minlength=n)
+    changed = np.ones(n, bool)
+    full = front = 0
+    for it in range(1, 64):
+        need = np.zeros(n, bool)
+        need[src[changed[dst]]] = True
+        need |= changed
+        front += int(deg[need].sum())
+        full += e
+        best = h.copy()
+        np.maximum.at(best, src, h[dst])
+        hc = np.zeros(cls.max() + 1, np.int64)
+        np.maximum.at(hc, cls, best)
+        nh = hc[cls]
+        nh = np.maximum(nh, nh[np.minimum(nh, n - 1)])
+        changed = nh != h
+        print(f"  sweep {it}: {int(changed.sum())} vertices changed, frontier edges "
+              f"{int(deg[need].sum())} of {e}")
+        h = nh
+        if not changed.any():
+            break
+    print(f"H propagation edge work: frontier / full = {front / full:.2f}")
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 2_000_000
     t = time.time()
@@ -74,6 +123,7 @@ def main():
     a2.data[:] = 1
     red = a.multiply(a2).nnz
     print(f"distinct edges {a.nnz}, implied by a two-edge path {red} ({red / a.nnz:.1%})")
+    frontier_sweeps(n, src, dst, window_classes(n, src, dst))
 
 
 if __name__ == "__main__":
