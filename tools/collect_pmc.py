@@ -50,7 +50,7 @@ PROBES = {
     "log_keys": r"k_log_keys",
     "tail_engine": r"k_tail_engine<unsigned int>",
     "exec_fill_dots": r"k_exec_fill_dots",
-    "elem_fill_dots": r"k_elem_fill_dots",
+    "vid_fill_dots": r"k_vid_fill_dots",
     "exec_from_groups": r"k_exec_from_groups",
     # global graph path (C3 / C5)
     "kap_relax": r"k_kap_relax",
