@@ -15,7 +15,10 @@ and per-key dot sequences (fh_engine_run).  Between steps fh_engine_rewind
 clears the latest tables and executed clock on the engine stream.
 
 Multi-GPU (`--gpus N`, one process per GPU under torch.distributed.run): the
-stream is key-sharded (owner = key mod N).  With one key per
+stream is key-sharded by a balanced key map: every rank counts the
+stream's commands per key and packs keys largest-first onto the least loaded
+rank (fh_key_owners_balanced; the same map on every rank, max shard = the mean
+on C4 where key mod 8 gave 1.37x).  With one key per
 command every dependency joins two commands of one key, so a shard's graph is
 closed: each rank orders its shard of the same global stream (global dots)
 with no data-path collective; torch.distributed (RCCL) carries only the
@@ -252,7 +255,8 @@ def other_configs(local, steps=3):
                                       n=5), 10_000_000,
                "EPaxos n=5, ConflictPool 100% (key 0 + 16-key pool), 2 keys, replica views"),
         "c4_shard": (Workload.zipf(0.99, 1 << 20, k=1, views=3, window=64, seed=C4_SEED, n=5),
-                     12_500_000, "C4 per-GPU size at 8 GPUs: Zipf 0.99 / 2^20 keys, 1 key"),
+                     12_500_000, "C4's largest key shard at 8 GPUs (balanced key map, global "
+                                 "dots): Zipf 0.99 / 2^20 keys, 1 key"),
         "c5_12m": (Workload.zipf(0.99, 1 << 20, k=4, views=3, window=64,
                                  seed=0xFA170C4000000005, n=5), 12_500_000,
                    "first 12.5M commands of C5's stream, unsharded: Zipf 0.99 / 2^20 keys, "
@@ -260,7 +264,18 @@ def other_configs(local, steps=3):
     }
     out = {}
     for name, (w, n, desc) in cfgs.items():
-        s = w.generate(n, logs=True, times=False)
+        if name == "c4_shard":
+            # the largest shard of the 100M stream over 8 GPUs under the
+            # balanced key map (what rank q of bench.py --gpus 8 orders)
+            from fantoch_amd.workload import key_owners_balanced
+            h = w.key_histogram(100_000_000)
+            owner = key_owners_balanced(h, 8)
+            loads = np.bincount(owner, weights=h.astype(np.float64), minlength=8)
+            q = int(np.argmax(loads))
+            s = w.generate_shard(100_000_000, 8, q, owner=owner)
+            n = s.n
+        else:
+            s = w.generate(n, logs=True, times=False)
         eng = Engine(s.key_space, n=5, device=local)
         eng.stage(s)
         eng.run(sync=True)  # warmup (also picks the graph path's entry)
@@ -410,8 +425,11 @@ def cpu_sharded_worker(arg):
     keys, nsh, sh, sample = arg
     import numpy as np
     from oracle import oracle as O
-    s = c4_workload(keys).generate(sample)
-    mine = np.nonzero(s.keys[:, 0] % np.uint64(nsh) == np.uint64(sh))[0]
+    from fantoch_amd.workload import key_owners_balanced
+    w = c4_workload(keys)
+    s = w.generate(sample)
+    owner = key_owners_balanced(w.key_histogram(sample), nsh)
+    mine = np.nonzero(owner[s.keys[:, 0]] == sh)[0]
     dots, kk = s.dots[mine], s.keys[mine].reshape(-1)
     ko = (np.arange(len(mine) + 1, dtype=np.uint64)).astype(np.uint32)
     fp, ft = s.fq_proc[mine], s.fq_time[mine]
@@ -422,9 +440,9 @@ def cpu_sharded_worker(arg):
 
 
 def cpu_baseline_sharded(keys, sample, procs):
-    """The oracle on `procs` key shards of the same prefix in parallel
-    processes (one key per command: every shard's graph is closed, as on the
-    GPUs): whole-prefix commands / the slowest shard's time."""
+    """The oracle on `procs` key shards of the same prefix (balanced key map,
+    as on the GPUs) in parallel processes (one key per command: every shard's
+    graph is closed): whole-prefix commands / the slowest shard's time."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs) as pool:
@@ -489,10 +507,13 @@ def main():
 
     w = c4_workload(args.keys)
     t_gen = time.perf_counter()
+    owner = None
     if world == 1:
         s = w.generate(args.commands, logs=True, times=False)
     else:
-        s = w.generate_shard(args.commands, world, rank)
+        from fantoch_amd.workload import key_owners_balanced
+        owner = key_owners_balanced(w.key_histogram(args.commands), world)
+        s = w.generate_shard(args.commands, world, rank, owner=owner)
     t_gen = time.perf_counter() - t_gen
     eng = Engine(s.key_space, n=5, device=local)
     eng.stage(s)
@@ -527,6 +548,10 @@ def main():
     cold_ms = eng.run(sync=True)
     eng.close()
 
+    rank_commands = [n_local]
+    if dist is not None:
+        rank_commands = [None] * world
+        dist.all_gather_object(rank_commands, int(n_local))
     d = deps_total / max(1, n_local)
     k, views = 1, 3
     b8d = sec8d_bytes(k, views, d)
@@ -553,7 +578,10 @@ def main():
         "path_roofline": path_roofline(value, k, views, d, world),
         "cold_ms": round(cold_ms, 3),
         "first_ms": round(first_ms, 3) if first_ms is not None else None,
-        "stream": {"commands_this_rank": n_local, "deps_per_cmd": d, "sccs": int(len(scc_sizes)),
+        "stream": {"commands_this_rank": n_local, "commands_per_rank": rank_commands,
+                   "partition": ("balanced key map (fh_key_owners_balanced)" if world > 1
+                                 else "whole stream"),
+                   "deps_per_cmd": d, "sccs": int(len(scc_sizes)),
                    "largest_scc": int(scc_sizes.max()) if len(scc_sizes) else 0,
                    "generate_s": round(t_gen, 2)},
     }
@@ -577,7 +605,7 @@ def main():
             result["cpu_baseline_sharded"] = {
                 "value": vs, "unit": "commands/s", "cores": procs, "kind": "port",
                 "sample": f"the same {sample}-command prefix split into {procs} key shards "
-                          f"(key mod {procs}), one oracle process per shard; slowest shard "
+                          f"(balanced key map), one oracle process per shard; slowest shard "
                           f"{ts:.2f}s"}
     if rank == 0 and world == 1 and not args.no_c5:
         result["c5"] = c5_line(args, local)

@@ -119,12 +119,17 @@ SIGNATURES = {
     "fh_multi_run": (C.c_int, [V, P(C.c_float)]),
     "fh_multi_results": (C.c_int, [V, V, V, S, P(S), V, V, V, V]),
     "fh_multi_shard_size": (C.c_int, [V, S, P(S)]),
+    "fh_multi_owners": (C.c_int, [V, V]),
+    "fh_key_owners_balanced": (C.c_int, [V, S, C.c_uint32, V]),
     "fh_workload_key_space": (C.c_uint64, [P(fh_workload)]),
     "fh_workload_generate": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V, V, V]),
     "fh_workload_generate_logs": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V]),
     "fh_workload_generate_element_logs": (C.c_int, [P(fh_workload), C.c_uint64, S, V, V]),
     "fh_workload_generate_shard": (C.c_int, [P(fh_workload), C.c_uint64, S, C.c_uint32,
                                              C.c_uint32, P(S), V, V, V, V]),
+    "fh_workload_generate_shard_owned": (C.c_int, [P(fh_workload), C.c_uint64, S, V,
+                                                   C.c_uint32, C.c_uint32, P(S), V, V, V, V]),
+    "fh_workload_key_histogram": (C.c_int, [P(fh_workload), C.c_uint64, S, V]),
     "fh_dgraph_create": (C.c_int, [P(fh_config), C.c_uint32, C.c_uint32, P(V)]),
     "fh_dgraph_destroy": (C.c_int, [V]),
     "fh_dgraph_stage": (C.c_int, [V, P(fh_stream_desc), C.c_uint32, V, V, V, V, V, V, V]),

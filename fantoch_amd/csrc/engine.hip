@@ -481,60 +481,61 @@ __global__ void __launch_bounds__(kThreads)
 // One thread per command in (key, command) order, a 1024-command tile staged
 // in LDS with kSrchHalo neighbours on either side, unpacked: key, command and
 // the arrival position at each replica (kNoArr if the replica does not
-// process it).  A scan that leaves the staged span continues on the packed
-// global arrays.  Per view j the predecessor is the key's latest arrival at
-// replica r_j before the command (SequentialKeyDeps::add_cmd,
-// sequential.rs:72-104): scanning back, every r_j-command arriving earlier is
-// a candidate; a command c' with c' + W below the best candidate so far (or
-// below the first candidate under c - W) arrives before it and cannot win,
-// nor can anything further back.  Forward, commands up to c + W may still
-// arrive earlier.  The command is its view's tail (latest_deps becomes it,
-// :88-95) iff no r_j-command of the key arrives later; any beyond c + W does.
-// Writes the fq dependency codes of the command (the chunked path's encoding)
-// and a mask of the views it is the tail of.
+// process it), stored shifted to the top of the word so that arrival
+// differences wrap modulo 2^qb by themselves.  A scan that leaves the staged
+// span continues on the packed global arrays.  Per view j the predecessor is
+// the key's latest arrival at replica r_j before the command
+// (SequentialKeyDeps::add_cmd, sequential.rs:72-104).  Backward, every
+// r_j-command arriving earlier is a candidate; one c' with c' + W below the
+// best candidate so far arrives before it and cannot win, nor can anything
+// further back, so the scan stops once that holds for every view.  Forward,
+// commands up to c + W may still arrive earlier; nothing beyond c + W does.
+//
+// Tails (latest_deps becomes the key's last arrival, :88-95) need no forward
+// search: in the arrival order of one (key, replica) every element but the
+// last is the predecessor of the next one, so an element is the tail iff no
+// element names it.  Each command marks its views' predecessors: in LDS when
+// the predecessor is a core command of the tile, else in `mrem` (one byte of
+// replica bits per sorted position, atomic OR); k_cmd_tails combines both.
+//
+// Codes: with `rec` set (fq <= 3), each command's (command, codes) record is
+// written into the tile's slice of `rec` grouped by command region (c >>
+// kRegShift; offsets per tile in `toff`), and k_code_scatter moves the
+// records region by region, so the scattered code stores of a moment stay in
+// a cache-sized slice of the code array (a random 12-B store per command over
+// the whole array ran at 4.6 ms per 100M commands, confined to 4M-command
+// regions at 1.7 ms: tools/scatter_bench.hip, profiles/r05_scatter_bench.jsonl).
 constexpr int kSrchHalo = 128;
 constexpr int kSrchMaxRep = 8;  // replicas (logs) of the command-level path
 constexpr uint32_t kNoArr = ~0u;
+constexpr uint32_t kRegShift = 22;   // code regions of 4M commands (48 MB of codes)
+constexpr uint32_t kMaxRegions = 32; // n < 2^27
 
-// Per-view scan state.  Each step takes one neighbour (command cc, arrival t
-// at the view's replica or kNoArr) and returns whether the scan goes on; the
-// body is branch-free (bitwise logic, 32-bit arithmetic: c + W < 2^32), since
-// the short-circuit form compiled to a chain of divergent exec-mask branches
-// per neighbour.
+// Per-view scan state; `bc` is the best candidate's command + 1 (0: none),
+// `bp` its sorted position.  Arrivals are shifted left by 32 - qb, so `close`
+// -- the candidate reaches the replica first, when the two commands are
+// within W of each other -- is one wrapping subtraction and one compare
+// (CmdMeta::before).
 struct ViewScan {
-  uint32_t c, tq, W, qm, half;
-  uint32_t bc = kNoCmd, bt = 0, farc = kNoCmd;
-  bool tail = true;
-  // (c1, q1) reaches the replica before (c2, q2) (CmdMeta::before)
-  __device__ __forceinline__ bool before(uint32_t c1, uint32_t q1, uint32_t c2, uint32_t q2) const {
-    const uint32_t d = (q2 - q1) & qm;
-    return (c1 + W < c2) | (!(c2 + W < c1) & (d != 0) & (d <= half));
+  uint32_t c, tq, H;
+  uint32_t bc = 0, bt = 0, bp = 0;
+  __device__ __forceinline__ static bool close(uint32_t d, uint32_t H) { return d - 1u < H; }
+  // backward neighbour: command cc (ccW1 = cc + W + 1, far = cc + W < c),
+  // arrival t at the view's replica, sorted position p
+  __device__ __forceinline__ void back(bool sk, uint32_t cc, uint32_t ccW1, bool far, uint32_t t, uint32_t p) {
+    const bool earlier = sk & (t != kNoArr) & (far | close(tq - t, H));
+    const bool better = earlier & ((bc == 0u) | (!(ccW1 < bc) & close(t - bt, H)));
+    bt = better ? t : bt;
+    bc = better ? cc + 1u : bc;
+    bp = better ? p : bp;
   }
-  __device__ __forceinline__ void take(uint32_t cc, uint32_t t, bool earlier, bool mine) {
-    const bool repl = earlier & ((bc == kNoCmd) | before(bc, bt, cc, t));
-    bt = repl ? t : bt;
-    bc = repl ? cc : bc;
-    tail = tail & !(mine & !earlier);
-  }
-  // backward: false once nothing further back can matter (a command c' with
-  // c' + W below the best candidate, or below the first candidate under
-  // c - W, arrives before it)
-  __device__ __forceinline__ bool back(bool same_key, uint32_t cc, uint32_t t) {
-    const uint32_t lim = max(bc == kNoCmd ? 0u : bc, farc == kNoCmd ? 0u : farc);
-    const bool go = same_key & !((lim != 0u) & (cc + W < lim));
-    const bool mine = go & (t != kNoArr);
-    const bool earlier = mine & before(cc, t, c, tq);
-    take(cc, t, earlier, mine);
-    farc = earlier & (farc == kNoCmd) & (cc + W < c) ? cc : farc;
-    return go;
-  }
-  // forward: false once past c + W with the tail decided
-  __device__ __forceinline__ bool fwd(bool same_key, uint32_t cc, uint32_t t) {
-    const bool go = same_key & !((cc > c + W) & !tail);
-    const bool mine = go & (t != kNoArr);
-    const bool earlier = mine & before(cc, t, c, tq);
-    take(cc, t, earlier, mine);
-    return go;
+  // forward neighbour (c < cc <= c + W)
+  __device__ __forceinline__ void fwd(bool sk, uint32_t cc, uint32_t W, uint32_t t, uint32_t p) {
+    const bool earlier = sk & (t != kNoArr) & close(tq - t, H);
+    const bool better = earlier & ((bc == 0u) | (bc + W <= cc) | close(t - bt, H));
+    bt = better ? t : bt;
+    bc = better ? cc + 1u : bc;
+    bp = better ? p : bp;
   }
 };
 
@@ -542,15 +543,22 @@ template <uint32_t FQ, int TH>
 __global__ void __launch_bounds__(TH)
     k_cmd_search(uint32_t n, CmdMeta cm, uint32_t K, uint32_t np, const uint32_t *__restrict__ kws,
                  const uint64_t *__restrict__ vals, const uint64_t *__restrict__ latest,
-                 uint32_t *__restrict__ code, uint8_t *__restrict__ tailm) {
+                 uint32_t *__restrict__ code, uint4 *__restrict__ rec,
+                 const uint32_t *__restrict__ roff, uint8_t *__restrict__ tailm,
+                 uint32_t *__restrict__ mrem) {
   constexpr int kSpan = TH + 2 * kSrchHalo;
   __shared__ uint32_t s_key[kSpan], s_c[kSpan];
   __shared__ uint32_t s_q[kSpan * kSrchMaxRep];
+  __shared__ uint8_t s_mark[TH * kSrchMaxRep];
+  __shared__ uint32_t s_reg[kMaxRegions];
   const uint32_t tid = threadIdx.x, core = blockIdx.x * TH, i = core + tid;
   const uint32_t lo = core > uint32_t(kSrchHalo) ? core - kSrchHalo : 0u;
   const uint32_t hi = min(n, core + TH + kSrchHalo);
   const uint32_t span = hi - lo;
+  const uint32_t qs = 32u - cm.qb;  // arrival shift
   for (uint32_t x = tid; x < span * np; x += TH) s_q[x] = kNoArr;
+  for (uint32_t x = tid; x < TH * np; x += TH) s_mark[x] = 0;
+  if (tid < kMaxRegions) s_reg[tid] = 0;
   __syncthreads();
   for (uint32_t x = tid; x < span; x += TH) {
     const uint32_t kw = kws[lo + x];
@@ -559,127 +567,189 @@ __global__ void __launch_bounds__(TH)
     s_key[x] = kw & cm.kmask;
     s_c[x] = uint32_t(v & cm.cmask);
 #pragma unroll
-    for (uint32_t j = 0; j < FQ; j++) s_q[x * np + cm.rep(m, j)] = cm.arr(m, j);
+    for (uint32_t j = 0; j < FQ; j++) s_q[x * np + cm.rep(m, j)] = cm.arr(m, j) << qs;
   }
   __syncthreads();
-  if (i >= n) return;
+  const bool act = i < n;
   const uint32_t me = i - lo;
-  const uint32_t key = s_key[me], c = s_c[me];
-  const uint64_t m0 = cm.meta(kws[i], vals[i]);
-  // all views in one pass over the neighbours (shared key and command
-  // loads); each view's scan stops on its own
+  const uint32_t W = cm.W, H = uint32_t(cm.qmask >> 1) << qs;
+  uint32_t key = 0, c = 0;
   ViewScan vs[FQ];
   uint32_t rr[FQ];
-  bool on[FQ];
-#pragma unroll
-  for (uint32_t j = 0; j < FQ; j++) {
-    rr[j] = cm.rep(m0, j);
-    vs[j].c = c;
-    vs[j].W = cm.W;
-    vs[j].qm = uint32_t(cm.qmask);
-    vs[j].half = uint32_t(cm.qmask >> 1);
-    vs[j].tq = cm.arr(m0, j);
-    on[j] = true;
-  }
-  // backward: the staged span, then global memory (a neighbour outside the
-  // span is unpacked from the packed arrays)
-  bool go = true;
-  for (uint32_t x = me; go && x > 0;) {
-    x--;
-    const bool sk = s_key[x] == key;
-    const uint32_t cc = s_c[x];
-    go = false;
+  if (act) {
+    key = s_key[me];
+    c = s_c[me];
+    const uint64_t m0 = cm.meta(kws[i], vals[i]);
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) {
-      on[j] = vs[j].back(sk & on[j], cc, s_q[x * np + rr[j]]);
-      go |= on[j];
+      rr[j] = cm.rep(m0, j);
+      vs[j].c = c;
+      vs[j].H = H;
+      vs[j].tq = cm.arr(m0, j) << qs;
     }
-  }
-  for (uint32_t ip = lo; go && ip-- > 0;) {
-    const uint32_t kw = kws[ip];
-    const uint64_t v = vals[ip];
-    const uint64_t m = cm.meta(kw, v);
-    const bool sk = (kw & cm.kmask) == key;
-    const uint32_t cc = uint32_t(v & cm.cmask);
-    go = false;
+    // backward: the staged span, then global memory (a neighbour outside the
+    // span is unpacked from the packed arrays); every view's state moves on
+    // each neighbour, and the scan ends when no view can still improve
+    bool go = true;
+    for (uint32_t x = me; go && x > 0;) {
+      x--;
+      const bool sk = s_key[x] == key;
+      const uint32_t cc = s_c[x], ccW1 = cc + W + 1u;
+      const bool far = cc + W < c;
+      uint32_t lim = ~0u;
+#pragma unroll
+      for (uint32_t j = 0; j < FQ; j++) {
+        vs[j].back(sk, cc, ccW1, far, s_q[x * np + rr[j]], lo + x);
+        lim = min(lim, vs[j].bc);
+      }
+      go = sk & !(ccW1 < lim);
+    }
+    for (uint32_t ip = lo; go && ip-- > 0;) {
+      const uint32_t kw = kws[ip];
+      const uint64_t v = vals[ip];
+      const uint64_t m = cm.meta(kw, v);
+      const bool sk = (kw & cm.kmask) == key;
+      const uint32_t cc = uint32_t(v & cm.cmask), ccW1 = cc + W + 1u;
+      const bool far = cc + W < c;
+      uint32_t lim = ~0u;
+#pragma unroll
+      for (uint32_t j = 0; j < FQ; j++) {
+        uint32_t t = kNoArr;
+        if (cm.find(m, rr[j], &t)) t <<= qs;
+        vs[j].back(sk, cc, ccW1, far, t, ip);
+        lim = min(lim, vs[j].bc);
+      }
+      go = sk & !(ccW1 < lim);
+    }
+    // forward, up to c + W
+    go = true;
+    for (uint32_t x = me + 1; go && x < span; x++) {
+      const uint32_t cc = s_c[x];
+      const bool sk = (s_key[x] == key) & (cc <= c + W);
+#pragma unroll
+      for (uint32_t j = 0; j < FQ; j++) vs[j].fwd(sk, cc, W, s_q[x * np + rr[j]], lo + x);
+      go = sk;
+    }
+    for (uint32_t ip = hi; go && ip < n; ip++) {
+      const uint32_t kw = kws[ip];
+      const uint64_t v = vals[ip];
+      const uint64_t m = cm.meta(kw, v);
+      const uint32_t cc = uint32_t(v & cm.cmask);
+      const bool sk = ((kw & cm.kmask) == key) & (cc <= c + W);
+#pragma unroll
+      for (uint32_t j = 0; j < FQ; j++) {
+        uint32_t t = kNoArr;
+        if (cm.find(m, rr[j], &t)) t <<= qs;
+        vs[j].fwd(sk, cc, W, t, ip);
+      }
+      go = sk;
+    }
+    // mark each view's predecessor: it is not the tail of that replica
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) {
-      uint32_t t = kNoArr;
-      cm.find(m, rr[j], &t);
-      on[j] = vs[j].back(sk & on[j], cc, t);
-      go |= on[j];
+      if (vs[j].bc == 0u) continue;
+      const uint32_t p = vs[j].bp;
+      if (p >= core && p < core + uint32_t(TH)) {
+        s_mark[(p - core) * np + rr[j]] = 1;
+      } else {
+        atomicOr(&mrem[p >> 2], (1u << rr[j]) << ((p & 3u) * 8u));
+      }
     }
   }
-  // forward
-  go = true;
-#pragma unroll
-  for (uint32_t j = 0; j < FQ; j++) on[j] = true;
-  for (uint32_t x = me + 1; go && x < span; x++) {
-    const bool sk = s_key[x] == key;
-    const uint32_t cc = s_c[x];
-    go = false;
-#pragma unroll
-    for (uint32_t j = 0; j < FQ; j++) {
-      on[j] = vs[j].fwd(sk & on[j], cc, s_q[x * np + rr[j]]);
-      go |= on[j];
-    }
-  }
-  for (uint32_t ip = hi; go && ip < n; ip++) {
-    const uint32_t kw = kws[ip];
-    const uint64_t v = vals[ip];
-    const uint64_t m = cm.meta(kw, v);
-    const bool sk = (kw & cm.kmask) == key;
-    const uint32_t cc = uint32_t(v & cm.cmask);
-    go = false;
-#pragma unroll
-    for (uint32_t j = 0; j < FQ; j++) {
-      uint32_t t = kNoArr;
-      cm.find(m, rr[j], &t);
-      on[j] = vs[j].fwd(sk & on[j], cc, t);
-      go |= on[j];
-    }
-  }
+  __syncthreads();
   uint32_t cds[FQ];
-  uint32_t msk = 0;
+  uint32_t reg = 0, rank = 0;
+  if (act) {
+    uint32_t msk = 0;
 #pragma unroll
-  for (uint32_t j = 0; j < FQ; j++) {
-    if (vs[j].bc != kNoCmd) {
-      cds[j] = vs[j].bc + 1;
-    } else {
-      const uint64_t xl = latest[uint64_t(rr[j] + 1) * K + key];
-      cds[j] = xl ? (0x80000000u | uint32_t(xl - kLogFlag)) : 0u;
+    for (uint32_t j = 0; j < FQ; j++) {
+      if (vs[j].bc != 0u) {
+        cds[j] = vs[j].bc;  // in-batch: vid + 1
+      } else {
+        const uint64_t xl = latest[uint64_t(rr[j] + 1) * K + key];
+        cds[j] = xl ? (0x80000000u | uint32_t(xl - kLogFlag)) : 0u;
+      }
+      msk |= s_mark[tid * np + rr[j]] ? 0u : 1u << j;
     }
-    msk |= vs[j].tail ? 1u << j : 0u;
-  }
-  // the views' codes leave in one store per command (tried: 16-B aligned
-  // stores and non-temporal stores, both flat; round 3)
-  uint32_t *o = code + size_t(c) * FQ;
-  if constexpr (FQ == 3) {
-    *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(o) =
-        HIP_vector_type<uint32_t, 3>(cds[0], cds[1], cds[2]);
-  } else if constexpr (FQ == 4) {
-    *reinterpret_cast<uint4 *>(o) = make_uint4(cds[0], cds[1], cds[2], cds[3]);
-  } else {
+    tailm[i] = uint8_t(msk);
+    if (rec) {
+      reg = c >> kRegShift;
+      rank = atomicAdd(&s_reg[reg], 1u);
+    } else {
+      uint32_t *o = code + size_t(c) * FQ;
+      if constexpr (FQ == 4) {
+        *reinterpret_cast<uint4 *>(o) = make_uint4(cds[0], cds[1], cds[2], cds[3]);
+      } else {
 #pragma unroll
-    for (uint32_t j = 0; j < FQ; j++) o[j] = cds[j];
+        for (uint32_t j = 0; j < FQ; j++) o[j] = cds[j];
+      }
+    }
   }
-  tailm[i] = uint8_t(msk);
+  if (!rec) return;  // uniform over the grid
+  if (act) {
+    // roff[r * tiles + t]: the first record of tile t in region r
+    // (k_region_count + scan), so each region's records are contiguous
+    uint4 o = make_uint4(c, 0u, 0u, 0u);
+    if constexpr (FQ >= 1) o.y = cds[0];
+    if constexpr (FQ >= 2) o.z = cds[1];
+    if constexpr (FQ >= 3) o.w = cds[2];
+    rec[roff[size_t(reg) * gridDim.x + blockIdx.x] + rank] = o;
+  }
 }
 
-// the tails become the replicas' latest entries (after every head's read)
+// Commands per (region, search tile) from the sorted values, region-major
+// (counts[r * tiles + t]) so that one exclusive scan gives every tile its
+// first record in its region's contiguous slice.
+__global__ void __launch_bounds__(1024)
+    k_region_count(uint32_t n, uint64_t cmask, uint32_t nreg, const uint64_t *__restrict__ vals,
+                   uint32_t *__restrict__ counts) {
+  __shared__ uint32_t s_h[kMaxRegions];
+  const uint32_t tid = threadIdx.x, i = blockIdx.x * 1024 + tid;
+  if (tid < kMaxRegions) s_h[tid] = 0;
+  __syncthreads();
+  if (i < n) atomicAdd(&s_h[uint32_t(vals[i] & cmask) >> kRegShift], 1u);
+  __syncthreads();
+  if (tid < nreg) counts[size_t(tid) * gridDim.x + blockIdx.x] = s_h[tid];
+}
+
+// The (command, codes) records, region-major -> their command slots of the
+// code array (fq <= 3).  Blocks run in order, so the stores of a moment land
+// in one or two regions' slices of `code` (a few tens of MB: cache-resident).
+template <uint32_t FQ>
+__global__ void __launch_bounds__(256)
+    k_code_scatter(uint32_t n, const uint4 *__restrict__ rec, uint32_t *__restrict__ code) {
+  GRID_STRIDE(i, n) {
+    const uint4 o = rec[i];
+    uint32_t *d = code + size_t(o.x) * FQ;
+    if constexpr (FQ == 3) {
+      *reinterpret_cast<HIP_vector_type<uint32_t, 3> *>(d) = HIP_vector_type<uint32_t, 3>(o.y, o.z, o.w);
+    } else {
+      d[0] = o.y;
+      if constexpr (FQ >= 2) d[1] = o.z;
+    }
+  }
+}
+
+// the tails become the replicas' latest entries (after every head's read):
+// view j of a sorted command is its replica's tail iff neither the tile
+// (tailm) nor another tile (mrem) marked it as some element's predecessor
 __global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *__restrict__ kws,
                             const uint64_t *__restrict__ vals, const uint8_t *__restrict__ tailm,
-                            uint64_t *__restrict__ latest, uint64_t log_base) {
+                            const uint8_t *__restrict__ mrem, uint64_t *__restrict__ latest,
+                            uint64_t log_base) {
   GRID_STRIDE(i, n) {
     const uint32_t msk = tailm[i];
     if (!msk) continue;
+    const uint32_t rm = mrem[i];
     const uint32_t kw = kws[i];
     const uint64_t v = vals[i];
     const uint64_t m = cm.meta(kw, v);
     const uint32_t key = kw & cm.kmask, c = uint32_t(v & cm.cmask);
-    for (uint32_t j = 0; j < cm.fq; j++)
-      if (msk & (1u << j))
-        latest[uint64_t(cm.rep(m, j) + 1) * K + key] = kLogFlag | (log_base + c);
+    for (uint32_t j = 0; j < cm.fq; j++) {
+      const uint32_t r = cm.rep(m, j);
+      if ((msk & (1u << j)) && !(rm & (1u << r)))
+        latest[uint64_t(r + 1) * K + key] = kLogFlag | (log_base + c);
+    }
   }
 }
 
@@ -1240,10 +1310,10 @@ __global__ void k_identity_labels(uint32_t n, const uint64_t *__restrict__ dot,
   }
 }
 
-// Per-key element counts of a key-grouped sequence (every key's elements
-// contiguous): a run's head records its start, its tail the count.  One
-// write per distinct key -- an atomic histogram serialises on Zipf-hot keys
-// (key 0 of C4 holds 6.5% of the stream: 4 ms of same-address atomics).
+// 32-bit packed dots: src << sb | seq.  Order-preserving (dots order by
+// (src, seq), id.rs) when every sequence is below 2^sb and src fits the
+// 32 - sb bits above it; the host picks sb (pb = src bits + sb <= 32) before
+// taking this form, else the dots stay u64.
 __global__ void k_pack_dots(uint32_t n, const uint64_t *__restrict__ dot, int sb,
                             uint32_t *__restrict__ out) {
   GRID_STRIDE(i, n) {
@@ -1359,6 +1429,14 @@ struct EngineDevice {
   DBuf<uint32_t> tail_defer;  // k_bucket_codes: deferred (segment, command) per workgroup
   DBuf<uint32_t> vrec;        // command-level views path: replica | arrival per element
   DBuf<uint8_t> tailm;        // command-level views path: tail views per sorted command
+  DBuf<uint32_t> mrem;        // command-level views path: predecessor marks across tiles
+  DBuf<uint4> crec;           // command-level views path: (command, codes) by tile and region
+  DBuf<uint32_t> ctoff;       // command-level views path: records per (region, tile), offsets
+  // FH_CODE_REGIONS=0 (measurement): codes stored straight at the command slot
+  const bool region_off = [] {
+    const char *e = getenv("FH_CODE_REGIONS");
+    return e && *e == '0';
+  }();
   DBuf<uint64_t> cv64a, cv64b;  // command-level views path: packed sort values
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
   // per batch: (seq bits, packed bits) of its dots, src << sb | seq (0: wider
@@ -1986,17 +2064,34 @@ struct EngineDevice {
     sort_pairs_counted<uint32_t, uint64_t>(kwa, va, sk32b.ensure(n + 1), cv64b.ensure(n + 1), n,
                                            key_bits, sort_ws, stream, &ks, &vs, db);
     uint8_t *tm = tailm.ensure(n + 1);
+    // predecessor marks from other tiles (k_cmd_search, k_cmd_tails)
+    const size_t mwords = (size_t(n) + 3) / 4;
+    uint32_t *mr = mrem.ensure(mwords);
+    FH_HIP(hipMemsetAsync(mr, 0, mwords * sizeof(uint32_t), stream));
     // reads the sorted key words and values (12 B, neighbours from LDS) and
-    // the heads' latest entries, writes fq codes and the tail mask.  1024
-    // threads (tried 256 / 512: flat)
+    // the heads' latest entries, writes fq codes (through region records when
+    // fq <= 3) and the tail mask.  1024 threads (tried 256 / 512: flat)
     uint32_t *codes = dep32.ensure(size_t(M) + 1);
-    const double sb = double(n) * (12.0 + fq * 4.0 + 1.0);
+    const uint32_t stiles = (n + kSrchThreads - 1) / kSrchThreads;
+    const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> kRegShift) + 1;
+    FH_CHECK(nreg <= kMaxRegions, FH_EINVARIANT, "command regions");
+    uint4 *rec4 = nullptr;
+    uint32_t *roff = nullptr;
+    if (fq <= 3 && !region_off) {
+      rec4 = crec.ensure(size_t(n) + 1);
+      const size_t nc = size_t(stiles) * nreg;
+      uint32_t *cnt = ctoff.ensure(2 * nc + 2);
+      roff = cnt + nc + 1;
+      k_region_count<<<dim3(stiles), dim3(1024), 0, stream>>>(n, cm.cmask, nreg, vs, cnt);
+      exclusive_scan_u32(cnt, roff, nc, scan_ws, stream);
+    }
+    const double sb = double(n) * (12.0 + (rec4 ? 16.0 : fq * 4.0) + 1.0);
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
     auto go = [&](auto kern) {
-      probed_launch("cmd_search", sb, kern, dim3((n + kSrchThreads - 1) / kSrchThreads),
-                    dim3(kSrchThreads), stream, n, cm, K, np, (const uint32_t *)ks,
-                    (const uint64_t *)vs, lat, codes, tm);
+      probed_launch("cmd_search", sb, kern, dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np,
+                    (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, rec4,
+                    (const uint32_t *)roff, tm, mr);
     };
     switch (fq) {
       case 1: go(k_cmd_search<1, kSrchThreads>); break;
@@ -2004,7 +2099,19 @@ struct EngineDevice {
       case 3: go(k_cmd_search<3, kSrchThreads>); break;
       default: go(k_cmd_search<4, kSrchThreads>); break;
     }
+    if (rec4) {
+      auto sc = [&](auto kern) {
+        probed_launch("code_scatter", double(n) * (16.0 + 4.0 * fq), kern,
+                      dim3((n + 255) / 256), dim3(256), stream, n, (const uint4 *)rec4, codes);
+      };
+      switch (fq) {
+        case 1: sc(k_code_scatter<1>); break;
+        case 2: sc(k_code_scatter<2>); break;
+        default: sc(k_code_scatter<3>); break;
+      }
+    }
     k_cmd_tails<<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks, vs, tm,
+                                                  reinterpret_cast<const uint8_t *>(mr),
                                                   views_latest(), bbase);
   }
 
@@ -2299,6 +2406,9 @@ EngineDevice *engine_new(const fh_config &cfg) { return new EngineDevice(cfg); }
 void engine_free(EngineDevice *e) { delete e; }
 void engine_stage_subset(EngineDevice *e, const fh_stream_desc &d, const uint64_t *dot,
                          const uint64_t *key, const uint64_t *off, const uint32_t *ent) {
+  // the range codes are log references relative to a command log that starts
+  // at 0 (k_gather_codes): a re-stage starts a fresh log and fresh tables
+  e->reset();
   e->stage_logs(d, 1, dot, key, off, ent, true);
 }
 const uint32_t *engine_run_codes(EngineDevice *e, float *ms) {

@@ -388,8 +388,11 @@ struct GraphDevice {
     if (clk) {
       clock.exceptions(exc_sorted);
       d_exc.ensure(exc_sorted.size() + 1);
-      exc_version = clock.version;
     }
+    // the device mirror is current only once the append that writes it is
+    // enqueued (a throw before then leaves exc_version stale: re-sent next
+    // pass)
+    const uint64_t clk_version = clock.version;
     // one pinned block, one copy, one append launch (separate pageable
     // copies cost several microseconds each: the floor of a small batch)
     Upload u{};
@@ -445,11 +448,15 @@ struct GraphDevice {
       // k_graph_small appends the rows itself
       small_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, V, KB, DB, ddot_v, dko, dk,
                  ddo, dd, dexc, uint32_t(exc.size()), u, adst);
+      exc_version = clk_version;
       return;
     }
-    if (n || clk)
+    if (n || clk) {
       k_append<<<grid_for(std::max({u.n ? u.n + 1 : 0u, u.nk, u.nd, u.nf + u.ne}), B), B, 0,
                  stream>>>(u, adst);
+      FH_HIP(hipGetLastError());
+    }
+    exc_version = clk_version;
     // dot -> vid index
     uint64_t *sd = nullptr;
     uint32_t *sv = nullptr;
@@ -625,7 +632,9 @@ struct GraphDevice {
     sp.nddot = nddot;
     static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
     sp.stamps = debug ? 1 : 0;
-    sp.seq = ++small_seq;
+    // 0 is the value the host stores before the launch: never a sequence
+    if (++small_seq == 0) small_seq = 1;
+    sp.seq = small_seq;
     volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h_small) + 31;
     *done = 0;
     const auto t_launch = std::chrono::steady_clock::now();

@@ -1,7 +1,9 @@
 // multi.cpp -- fh_multi_*: the fused engine over several GPUs of one node
 // from one process (SURVEY §8b "fh_multi_create / fh_multi_run", §8e).
 //
-// Key-shard partition: owner(key) = key mod G (G = engines).  With one key
+// Key-shard partition: owner(key) from fh_key_owners_balanced over the
+// staged stream's per-key command counts (G = engines; key mod G left the
+// largest of 8 shards at 1.37x the mean under Zipf 0.99).  With one key
 // per command every dependency joins two commands of one key (each
 // replica's KeyDeps chains a key's commands, keys/sequential.rs:72-104), so
 // a shard's dependency graph is closed: the shards order independently and
@@ -29,6 +31,7 @@ struct fh_multi {
   std::vector<int> devices;
   std::vector<fh_engine *> eng;
   std::vector<std::vector<uint32_t>> cmds;  // per shard: global command indices
+  std::vector<uint32_t> owner;              // key -> shard of the last staging
   fh_stream_desc desc{};
   size_t n = 0;
   bool staged = false, ran = false;
@@ -123,11 +126,18 @@ fh_status fh_multi_stage_logs(fh_multi *h, const fh_stream_desc *desc, const uin
     FH_CHECK(log_off[r + 1] >= log_off[r], FH_EINVAL, "logs: offsets");
   for (uint64_t q = 0; q < log_off[np]; q++)
     FH_CHECK(log_cmd[q] < n, FH_EINVAL, "logs: command index >= n");
+  const size_t K = h->cfg.key_space;
+  std::vector<uint64_t> hist(K, 0);
+  for (size_t i = 0; i < n; i++) {
+    FH_CHECK(key_id[i] < K, FH_EINVAL, "key id >= key_space");
+    hist[key_id[i]]++;
+  }
+  std::vector<uint32_t> owner(K);
+  check_status(fh_key_owners_balanced(hist.data(), K, uint32_t(G), owner.data()));
   std::vector<uint32_t> shard_of(n), local(n);
   std::vector<std::vector<uint32_t>> cmds(G);
   for (size_t i = 0; i < n; i++) {
-    FH_CHECK(key_id[i] < h->cfg.key_space, FH_EINVAL, "key id >= key_space");
-    const uint32_t g = uint32_t(key_id[i] % G);
+    const uint32_t g = owner[key_id[i]];
     shard_of[i] = g;
     local[i] = uint32_t(cmds[g].size());
     cmds[g].push_back(uint32_t(i));
@@ -152,6 +162,7 @@ fh_status fh_multi_stage_logs(fh_multi *h, const fh_stream_desc *desc, const uin
                                       lc.data()));
   });
   h->cmds.swap(cmds);
+  h->owner.swap(owner);
   h->desc = *desc;
   h->n = n;
   h->staged = true;
@@ -234,17 +245,17 @@ fh_status fh_multi_results(fh_multi *h, uint32_t *dep_off, uint64_t *dep_dot, si
     if (scc_label) scc_label[i] = r[g].lab[j];
     if (exec_rank) exec_rank[i] = base[g] + r[g].rank[j];
   }
-  // per-key sequences: key k's comes from its owner, shard k mod G
+  // per-key sequences: key k's comes from its owner
   if (key_off || key_seq) {
     std::vector<uint32_t> ko(K + 1, 0);
     for (size_t k = 0; k < K; k++) {
-      const R &x = r[k % G];
+      const R &x = r[h->owner[k]];
       ko[k + 1] = ko[k] + (x.koff[k + 1] - x.koff[k]);
     }
     if (key_off) std::memcpy(key_off, ko.data(), (K + 1) * sizeof(uint32_t));
     if (key_seq)
       for (size_t k = 0; k < K; k++) {
-        const R &x = r[k % G];
+        const R &x = r[h->owner[k]];
         std::copy(x.seq.begin() + x.koff[k], x.seq.begin() + x.koff[k + 1], key_seq + ko[k]);
       }
   }
@@ -255,6 +266,37 @@ fh_status fh_multi_shard_size(fh_multi *h, size_t shard, size_t *n) {
   FH_API_BEGIN
   FH_CHECK(h && n && shard < h->eng.size(), FH_EINVAL, "bad argument");
   *n = h->cmds.size() > shard ? h->cmds[shard].size() : 0;
+  FH_API_END
+}
+
+fh_status fh_multi_owners(fh_multi *h, uint32_t *owner) {
+  FH_API_BEGIN
+  FH_CHECK(h && owner && h->staged, FH_EINVAL, "bad argument");
+  std::copy(h->owner.begin(), h->owner.end(), owner);
+  FH_API_END
+}
+
+fh_status fh_key_owners_balanced(const uint64_t *hist, size_t key_space, uint32_t nshards,
+                                 uint32_t *owner) {
+  FH_API_BEGIN
+  FH_CHECK(hist && owner && nshards >= 1 && key_space >= 1, FH_EINVAL, "bad argument");
+  std::vector<uint32_t> ord(key_space);
+  for (size_t x = 0; x < key_space; x++) ord[x] = uint32_t(x);
+  std::stable_sort(ord.begin(), ord.end(),
+                   [&](uint32_t a, uint32_t b) { return hist[a] > hist[b]; });
+  // min-heap of (load, shard)
+  using E = std::pair<uint64_t, uint32_t>;
+  std::vector<E> heap;
+  for (uint32_t g = 0; g < nshards; g++) heap.push_back({0, g});
+  auto gt = [](const E &a, const E &b) { return a > b; };
+  std::make_heap(heap.begin(), heap.end(), gt);
+  for (uint32_t x : ord) {
+    std::pop_heap(heap.begin(), heap.end(), gt);
+    E &e = heap.back();
+    owner[x] = e.second;
+    e.first += hist[x];
+    std::push_heap(heap.begin(), heap.end(), gt);
+  }
   FH_API_END
 }
 

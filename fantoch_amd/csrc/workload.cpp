@@ -333,10 +333,50 @@ std::vector<std::vector<uint64_t>> seq_bases(const fh_workload &w, const Alias *
 
 extern "C" {
 
+fh_status fh_workload_key_histogram(const fh_workload *w, uint64_t first, size_t count,
+                                    uint64_t *hist) {
+  FH_API_BEGIN
+  FH_CHECK(w && hist, FH_EINVAL, "null argument");
+  fh::validate(*w);
+  const uint64_t K = fh::key_space_of(*w);
+  FH_CHECK(K >= 1 && K < (uint64_t(1) << 32), FH_EINVAL, "workload: key space");
+  const fh::Alias *za = w->kind == 0 ? &fh::zipf_alias(w->zipf_s, w->key_count) : nullptr;
+  const uint32_t k = w->keys_per_cmd;
+  const std::vector<size_t> bounds = fh::chunk_bounds(count);
+  const size_t T = bounds.size() - 1;
+  // per-thread 32-bit counts (a chunk holds < 2^32 commands), summed once
+  std::vector<std::vector<uint32_t>> part(T, std::vector<uint32_t>(K, 0));
+  std::vector<std::thread> ts;
+  for (size_t t = 0; t < T; t++)
+    ts.emplace_back([&, t] {
+      std::vector<uint64_t> ks(k);
+      for (size_t c = bounds[t]; c < bounds[t + 1]; c++) {
+        fh::gen_range(*w, za, first + c, 0, 1, nullptr, ks.data(), nullptr, nullptr, nullptr);
+        part[t][ks[0]]++;
+      }
+    });
+  for (auto &t : ts) t.join();
+  for (uint64_t x = 0; x < K; x++) {
+    uint64_t s = 0;
+    for (size_t t = 0; t < T; t++) s += part[t][x];
+    hist[x] = s;
+  }
+  FH_API_END
+}
+
 fh_status fh_workload_generate_shard(const fh_workload *w, uint64_t first, size_t count,
                                      uint32_t nshards, uint32_t shard, size_t *n_out,
                                      uint64_t *dot, uint64_t *key_id, uint64_t *log_off,
                                      uint32_t *log_cmd) {
+  return fh_workload_generate_shard_owned(w, first, count, nullptr, nshards, shard, n_out, dot,
+                                          key_id, log_off, log_cmd);
+}
+
+fh_status fh_workload_generate_shard_owned(const fh_workload *w, uint64_t first, size_t count,
+                                           const uint32_t *owner, uint32_t nshards,
+                                           uint32_t shard, size_t *n_out, uint64_t *dot,
+                                           uint64_t *key_id, uint64_t *log_off,
+                                           uint32_t *log_cmd) {
   FH_API_BEGIN
   FH_CHECK(w && n_out, FH_EINVAL, "null argument");
   fh::validate(*w);
@@ -354,7 +394,7 @@ fh_status fh_workload_generate_shard(const fh_workload *w, uint64_t first, size_
     size_t m = 0;
     for (size_t c = lo; c < hi; c++) {
       fh::gen_range(*w, za, first + c, 0, 1, nullptr, ks.data(), nullptr, nullptr, nullptr);
-      const bool mine = ks[0] % nshards == shard;
+      const bool mine = (owner ? owner[ks[0]] : uint32_t(ks[0] % nshards)) == shard;
       keep[c] = mine ? 1u : ~0u;
       m += mine;
     }
@@ -469,6 +509,8 @@ fh_status fh_workload_generate_element_logs(const fh_workload *w, uint64_t first
   const uint32_t nlog = n * S, per = k * V;
   FH_CHECK(uint64_t(count) * per < (uint64_t(1) << 31), FH_EINVAL,
            "workload: element positions must be < 2^31");
+  // the arrival sort below keeps each element's delay (< window) in a byte
+  FH_CHECK(w->window <= 256, FH_EINVAL, "workload: element logs need window <= 256");
   const fh::Alias *za = w->kind == 0 ? &fh::zipf_alias(w->zipf_s, w->key_count) : nullptr;
   const std::vector<size_t> bounds = fh::chunk_bounds(count);
   const size_t T = bounds.size() - 1;

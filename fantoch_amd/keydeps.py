@@ -6,7 +6,8 @@ Mirrors fantoch_ps/src/protocol/common/graph/deps/keys/mod.rs:37-63:
     add_cmd(dot, &cmd, past) -> HashSet<Dep>   -> add_cmd(dot, cmd, past)
     add_noop(dot) -> HashSet<Dep>              -> add_noop(dot)
     cmd_deps(&cmd) / noop_deps() (test-only)   -> cmd_deps(cmd) / noop_deps()
-    parallel() -> bool                         -> parallel()  (False, like SequentialKeyDeps)
+    parallel() -> bool                         -> parallel()  (SequentialKeyDeps: False;
+                                                  LockedKeyDeps, read_write=True: True)
 
 plus the batched form the engine is built for, add_batch(), which computes a
 whole arrival-ordered batch of add_cmd/add_noop calls in one device pass.
@@ -14,11 +15,20 @@ whole arrival-ordered batch of add_cmd/add_noop calls in one device pass.
 Results are sets of packed dots.  `Dependency.shards` (keys/mod.rs:18-35) is a
 function of the dependency's dot (the shard set of that command), so dot-set
 equality is the parity contract; `dependencies()` rebuilds
-full Dependency values from the shard sets the instance has seen.
+full Dependency values from the shard sets of the dots the device state can
+still return (the latest dot of each key slot and the latest noop, as the Rust
+crate's HipKeyDeps keeps them, fantoch_hip/src/keydeps.rs), so the bookkeeping
+is bounded by the keys like the reference's latest table
+(keys/sequential.rs:7-12, locked.rs:10-15).
+
+Like LockedKeyDeps (keys/locked.rs:17-22, `Clone` shares the state), one
+instance may be used from several threads: every call holds the instance's
+lock, so concurrent workers serialise on the device handle.
 """
 from __future__ import annotations
 
 import ctypes as C
+import threading
 from dataclasses import dataclass
 from typing import FrozenSet, Iterable, Optional
 
@@ -76,7 +86,13 @@ class HipKeyDeps:
         L.check(self._lib.fh_keydeps_create(shard_id, C.byref(self.cfg), C.byref(h)))
         self._h = h
         self.keys = KeyInterner(key_space) if intern else None
-        self._shards = {}
+        self._lock = threading.RLock()
+        # Dependency.shards of the dots a slot still holds: dot -> [shards,
+        # slots holding it]; (key id, read slot) -> its latest dot; the
+        # latest noop (fantoch_hip/src/keydeps.rs State)
+        self._live = {}
+        self._slots = {}
+        self._noop = None
 
     def close(self):
         if getattr(self, "_h", None):
@@ -85,52 +101,87 @@ class HipKeyDeps:
 
     __del__ = close
 
-    @staticmethod
-    def parallel() -> bool:
-        return False  # SequentialKeyDeps::parallel (sequential.rs:60-62)
+    def parallel(self) -> bool:
+        # SequentialKeyDeps::parallel is false (sequential.rs:60-62),
+        # LockedKeyDeps::parallel true (locked.rs:70-72): the Rust crate's
+        # HipKeyDeps / HipLockedKeyDeps (fantoch_hip/src/keydeps.rs)
+        return self.read_write
 
     # -- helpers ---------------------------------------------------------
     def _key_ids(self, cmd):
         keys = cmd.keys(self.shard_id) if hasattr(cmd, "keys") else cmd
         return self.keys.many(keys) if self.keys is not None else [int(k) for k in keys]
 
-    def _note_shards(self, dot, cmd):
-        if hasattr(cmd, "shards"):
-            self._shards[dot] = frozenset(cmd.shards())
+    def _hold(self, dot, shards):
+        e = self._live.get(dot)
+        if e is None:
+            self._live[dot] = [shards, 1]
+        else:
+            e[1] += 1
+
+    def _release(self, dot):
+        e = self._live.get(dot)
+        if e is not None:
+            e[1] -= 1
+            if e[1] == 0:
+                del self._live[dot]
 
     def dependencies(self, dots) -> set:
-        return {Dependency(d, self._shards.get(d)) for d in dots}
+        """Dots -> Dependency values, shards from the live slots (None when no
+        slot holds the dot any more, or for a noop)."""
+        with self._lock:
+            return {Dependency(d, self._live[d][0] if d in self._live else None) for d in dots}
 
     # -- KeyDeps ---------------------------------------------------------
     def add_cmd(self, dot: int, cmd, past: Optional[Iterable[int]] = None) -> set:
-        self._note_shards(dot, cmd)
         past_l = None if past is None else [p.dot if isinstance(p, Dependency) else int(p)
                                             for p in past]
-        ro = [bool(getattr(cmd, "read_only", False))] if self.read_write else None
-        off, deps = self.add_batch([dot], [self._key_ids(cmd)], None,
-                                   None if past_l is None else [past_l], read_only=ro)
-        return set(int(x) for x in deps[off[0]:off[1]])
+        read_only = bool(getattr(cmd, "read_only", False))
+        ro = [read_only] if self.read_write else None
+        with self._lock:
+            kid = self._key_ids(cmd)
+            off, deps = self.add_batch([dot], [kid], None,
+                                       None if past_l is None else [past_l], read_only=ro)
+            # the command becomes its keys' latest (the read slot for a
+            # read-only command under LockedKeyDeps, locked.rs:100-117)
+            shards = frozenset(cmd.shards()) if hasattr(cmd, "shards") else None
+            slot_ro = self.read_write and read_only
+            for k in kid:
+                self._hold(dot, shards)
+                old = self._slots.get((k, slot_ro))
+                self._slots[(k, slot_ro)] = dot
+                if old is not None:
+                    self._release(old)
+            return set(int(x) for x in deps[off[0]:off[1]])
 
     def add_noop(self, dot: int) -> set:
-        off, deps = self.add_batch([dot], [[]], [True], None,
-                                   read_only=[False] if self.read_write else None)
-        return set(int(x) for x in deps[off[0]:off[1]])
+        with self._lock:
+            off, deps = self.add_batch([dot], [[]], [True], None,
+                                       read_only=[False] if self.read_write else None)
+            # the latest noop (sequential.rs:66-70); keys' slots are unchanged
+            self._hold(dot, None)
+            old, self._noop = self._noop, dot
+            if old is not None:
+                self._release(old)
+            return set(int(x) for x in deps[off[0]:off[1]])
 
     def cmd_deps(self, cmd) -> set:
-        k = np.asarray(self._key_ids(cmd), dtype=np.uint64)
-        cap = 2 * len(k) + 1
-        out = np.zeros(cap, dtype=np.uint64)
-        n = C.c_size_t(0)
-        L.check(self._lib.fh_keydeps_cmd_deps(self._h, len(k), L.ptr(k), L.ptr(out), cap,
-                                              C.byref(n)))
-        return set(int(x) for x in out[:n.value])
+        with self._lock:
+            k = np.asarray(self._key_ids(cmd), dtype=np.uint64)
+            cap = 2 * len(k) + 1
+            out = np.zeros(cap, dtype=np.uint64)
+            n = C.c_size_t(0)
+            L.check(self._lib.fh_keydeps_cmd_deps(self._h, len(k), L.ptr(k), L.ptr(out), cap,
+                                                  C.byref(n)))
+            return set(int(x) for x in out[:n.value])
 
     def noop_deps(self) -> set:
-        n = C.c_size_t(0)
-        L.check(self._lib.fh_keydeps_noop_deps(self._h, None, 0, C.byref(n)))
-        out = np.zeros(max(1, n.value), dtype=np.uint64)
-        L.check(self._lib.fh_keydeps_noop_deps(self._h, L.ptr(out), len(out), C.byref(n)))
-        return set(int(x) for x in out[:n.value])
+        with self._lock:
+            n = C.c_size_t(0)
+            L.check(self._lib.fh_keydeps_noop_deps(self._h, None, 0, C.byref(n)))
+            out = np.zeros(max(1, n.value), dtype=np.uint64)
+            L.check(self._lib.fh_keydeps_noop_deps(self._h, L.ptr(out), len(out), C.byref(n)))
+            return set(int(x) for x in out[:n.value])
 
     # -- batched form ------------------------------------------------------
     def add_batch(self, dots, keys, is_noop=None, past=None, read_only=None):
@@ -140,6 +191,10 @@ class HipKeyDeps:
         read_only: optional bools -- LockedKeyDeps' read/write rules
         (fh_keydeps_add_batch_rw).  Returns (dep_off[n+1], dep_dots) as numpy
         arrays."""
+        with self._lock:
+            return self._add_batch(dots, keys, is_noop, past, read_only)
+
+    def _add_batch(self, dots, keys, is_noop, past, read_only):
         n = len(dots)
         dot_a = np.ascontiguousarray(dots, dtype=np.uint64)
         if isinstance(keys, tuple):

@@ -1,6 +1,7 @@
 """MultiEngine -- the fused engine over several GPUs from one process
-(fh_multi_*): one engine per device over key shards (owner = key mod ndev);
-see include/fantoch_hip.h."""
+(fh_multi_*): one engine per device over key shards (owner from
+fh_key_owners_balanced over the staged stream's key counts); see
+include/fantoch_hip.h."""
 from __future__ import annotations
 
 import ctypes as C
@@ -59,6 +60,12 @@ class MultiEngine:
             L.check(self._lib.fh_multi_shard_size(self._h, g, C.byref(n)))
             out.append(n.value)
         return out
+
+    def owners(self) -> np.ndarray:
+        """The key -> shard map of the last staging."""
+        o = np.zeros(self.key_space, dtype=np.uint32)
+        L.check(self._lib.fh_multi_owners(self._h, L.ptr(o)))
+        return o
 
     def results(self):
         n = self.n

@@ -143,16 +143,30 @@ class Workload:
                                                       L.ptr(s.log_cmd)))
         return s
 
+    def key_histogram(self, count: int, first: int = 0) -> np.ndarray:
+        """u64[key_space]: commands of [first, first + count) per first key
+        (fh_workload_key_histogram)."""
+        lib = L.load()
+        w = self._c()
+        h = np.zeros(self.key_space(), dtype=np.uint64)
+        L.check(lib.fh_workload_key_histogram(C.byref(w), first, count, L.ptr(h)))
+        return h
+
     def generate_shard(self, count: int, nshards: int, shard: int, first: int = 0,
-                       logs: bool = True) -> Stream:
-        """Key shard `shard` of `nshards` (owner of the first key = key %
-        nshards) of commands [first, first + count), global dots, with the
-        replicas' logs restricted to it (fh_workload_generate_shard)."""
+                       logs: bool = True, owner: np.ndarray = None) -> Stream:
+        """Key shard `shard` of `nshards` of commands [first, first + count):
+        the commands whose first key k0 has owner[k0] == shard (`owner` from
+        key_owners_balanced; None = k0 % nshards), global dots, with the
+        replicas' logs restricted to it (fh_workload_generate_shard_owned)."""
         lib = L.load()
         w = self._c()
         n = C.c_size_t(0)
-        L.check(lib.fh_workload_generate_shard(C.byref(w), first, count, nshards, shard,
-                                               C.byref(n), None, None, None, None))
+        if owner is not None:
+            owner = np.ascontiguousarray(owner, dtype=np.uint32)
+            assert len(owner) == self.key_space()
+        L.check(lib.fh_workload_generate_shard_owned(C.byref(w), first, count, L.ptr(owner),
+                                                     nshards, shard, C.byref(n), None, None,
+                                                     None, None))
         m = n.value
         dots = np.zeros(m, dtype=np.uint64)
         keys = np.zeros((m, self.keys_per_cmd), dtype=np.uint64)
@@ -160,10 +174,20 @@ class Workload:
         if self.views and logs:
             lo = np.zeros(self.n + 1, dtype=np.uint64)
             lc = np.zeros(max(1, m * self.views), dtype=np.uint32)
-        L.check(lib.fh_workload_generate_shard(C.byref(w), first, count, nshards, shard,
-                                               C.byref(n), L.ptr(dots), L.ptr(keys), L.ptr(lo),
-                                               L.ptr(lc)))
+        L.check(lib.fh_workload_generate_shard_owned(C.byref(w), first, count, L.ptr(owner),
+                                                     nshards, shard, C.byref(n), L.ptr(dots),
+                                                     L.ptr(keys), L.ptr(lo), L.ptr(lc)))
         s = Stream(dots, keys, None, None, self.key_space(), views_n=self.views)
         if lo is not None:
             s.log_off, s.log_cmd = lo, lc[:m * self.views]
         return s
+
+
+def key_owners_balanced(hist: np.ndarray, nshards: int) -> np.ndarray:
+    """u32[key_space] key -> shard map balancing the per-key command counts
+    `hist` over `nshards` (fh_key_owners_balanced: greedy largest-first
+    packing; deterministic, so every rank computes the same map)."""
+    hist = np.ascontiguousarray(hist, dtype=np.uint64)
+    owner = np.zeros(len(hist), dtype=np.uint32)
+    L.check(L.load().fh_key_owners_balanced(L.ptr(hist), len(hist), nshards, L.ptr(owner)))
+    return owner

@@ -22,6 +22,12 @@ CONFIGS = {
     "c4shard": dict(desc="C4 key shard 0 of 8 of a 20M-command stream (global dots)",
                     total=20_000_000, nshards=8, shard=0,
                     workload=lambda: Workload.zipf(0.99, 1 << 20, k=1, seed=SEED + 4, **KW)),
+    # the same stream's shard 0 of 8 under the balanced key map the multi-GPU
+    # bench uses (fh_key_owners_balanced over the stream's key counts)
+    "c4shard_bal": dict(desc="C4 balanced key shard 0 of 8 of a 20M-command stream (global dots; "
+                             "owner = fh_key_owners_balanced over the stream's key counts)",
+                        total=20_000_000, nshards=8, shard=0, balanced=True,
+                        workload=lambda: Workload.zipf(0.99, 1 << 20, k=1, seed=SEED + 4, **KW)),
     "c3": dict(desc="C3 EPaxos ConflictPool 100% (key 0 + 16-key pool), 2 keys: deps at 10M, "
                     "everything on the first 50k", n=10_000_000, prefix=50_000,
                workload=lambda: Workload.conflict_pool(100, 16, k=2, seed=SEED + 3, **KW)),

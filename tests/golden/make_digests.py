@@ -19,6 +19,8 @@ Configurations (seeds as tools/bench_configs.py):
   c4        the headline stream: Zipf 0.99 over 2^20 keys, 1 key, 100M commands
             (full size, bench.py's stream)
   c4shard   key shard 0 of 8 of a 20M-command C4 stream (global dots)
+  c4shard_bal  the same stream's shard 0 of 8 under the balanced key map
+            (fh_key_owners_balanced over its key counts; bench.py --gpus N)
   c3        EPaxos ConflictPool 100% (key 0 + 16-key pool), 2 keys: deps at the
             full 10M, everything on the first 50k (the incremental Tarjan is
             quadratic on its one stream-wide SCC)
@@ -92,9 +94,14 @@ def main():
         w = c["workload"]()
         t0 = time.time()
         entry = {"desc": c["desc"]}
-        if name == "c4shard":
+        if name.startswith("c4shard"):
             full = w.generate(c["total"])
-            mine = np.nonzero(full.keys[:, 0] % c["nshards"] == c["shard"])[0]
+            if c.get("balanced"):
+                from fantoch_amd.workload import key_owners_balanced
+                owner = key_owners_balanced(w.key_histogram(c["total"]), c["nshards"])
+                mine = np.nonzero(owner[full.keys[:, 0]] == c["shard"])[0]
+            else:
+                mine = np.nonzero(full.keys[:, 0] % c["nshards"] == c["shard"])[0]
             from fantoch_amd.workload import Stream
             s = Stream(full.dots[mine], full.keys[mine], full.fq_proc[mine], full.fq_time[mine],
                        full.key_space)

@@ -30,7 +30,7 @@ def make_stream(n, seed, keys, k=4, shards=8):
     return w.generate(n, logs=True)
 
 
-def _worker(rank, world, port, n, seed, keys, q):
+def _worker(rank, world, port, n, seed, keys, q, pre=None):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -41,6 +41,13 @@ def _worker(rank, world, port, n, seed, keys, q):
     from fantoch_amd.dgraph import DistPartial
     s = make_stream(n, seed, keys)
     p = DistPartial(rank, world, s.key_space, device=0)
+    if pre is not None:
+        # another stream staged and run on the same handle first: the second
+        # stage must start a fresh command log (log references in
+        # the range codes are relative to a log that starts at 0)
+        p0 = make_stream(pre[0], pre[1], keys)
+        p.stage(p0)
+        p.run()
     p.stage(s)
     for _ in range(2):  # a second run on the same staged stream (rewind inside)
         p.run()
@@ -54,11 +61,11 @@ def _worker(rank, world, port, n, seed, keys, q):
     dist.destroy_process_group()
 
 
-def run_ranks(world, n, seed, keys):
+def run_ranks(world, n, seed, keys, pre=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, keys, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, keys, q, pre))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -69,14 +76,17 @@ def run_ranks(world, n, seed, keys):
     return parts
 
 
-@pytest.mark.parametrize("world,n,seed,keys", [(1, 6000, 71, 4096), (2, 8000, 72, 4096),
-                                               (4, 8000, 73, 1 << 20), (2, 12_000, 74, 1 << 16)])
-def test_dgraph_hip_ranks_match_oracle(world, n, seed, keys):
+@pytest.mark.parametrize("world,n,seed,keys,pre", [(1, 6000, 71, 4096, None),
+                                                   (2, 8000, 72, 4096, None),
+                                                   (4, 8000, 73, 1 << 20, None),
+                                                   (2, 12_000, 74, 1 << 16, None),
+                                                   (2, 7000, 75, 4096, (9000, 76))])
+def test_dgraph_hip_ranks_match_oracle(world, n, seed, keys, pre):
     sys.path.insert(0, HERE)
     from fantoch_amd.dgraph import assemble
     from fullsize import shard_union
     from oracle import oracle as O
-    parts = run_ranks(world, n, seed, keys)
+    parts = run_ranks(world, n, seed, keys, pre)
     s = make_stream(n, seed, keys)
     got = assemble(parts, s.n, s.key_space)
     off, deps = shard_union(s)

@@ -81,3 +81,51 @@ def test_engine_rejects_key_out_of_space():
     eng = Engine(s.key_space // 2, n=5)
     with pytest.raises(L.FhError):
         eng.stage(s)
+
+
+EMPTY_OVER_BACKLOG = """
+import sys
+sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
+import torch; torch.zeros(1, device="cuda")
+from conftest import D
+from fantoch_amd.executor import GraphExecutionInfo, HipGraphExecutor
+ex = HipGraphExecutor(1, 0, 5, 1, key_space=16)
+# a backlog: a chain of 40 commands on key 3 waiting on (5, 1), plus a 2-cycle
+# waiting on (5, 2); each pass carries them
+miss1, miss2 = D((5, 1)), D((5, 2))
+chain = [D((1, i)) for i in range(1, 41)]
+for i, d in enumerate(chain):
+    ex.handle(GraphExecutionInfo.add(d, [3], [miss1] if i == 0 else [chain[i - 1]]))
+a, b = D((2, 1)), D((3, 1))
+ex.handle_batch([GraphExecutionInfo.add(a, [4], [b, miss2]), GraphExecutionInfo.add(b, [4], [a])])
+assert ex.pending() == 42, ex.pending()
+for _ in range(5):  # empty batches over the carried set (r04i: k_append)
+    ex.handle_batch([])
+    assert ex.pending() == 42, ex.pending()
+    assert sorted(ex.missing()) == sorted([miss1, miss2]), ex.missing()
+ex.handle(GraphExecutionInfo.add(miss1, [3], []))
+assert ex.pending() == 2
+ex.handle_batch([])
+ex.handle(GraphExecutionInfo.add(miss2, [4], []))
+assert ex.pending() == 0
+assert ex.monitor()[3] == [miss1] + chain
+assert ex.monitor()[4] == [miss2, a, b]
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_executor_empty_batches_over_carried_backlog(small):
+    """Empty batches while vertices are carried pending (the round-4 fault:
+    k_append rewrote the carried set's end offsets on an empty batch), through
+    the one-launch small pass (default) and the general pass
+    (FH_GRAPH_SMALL=0, read once per process: a child); then the missing deps
+    arrive and everything executes in order."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = EMPTY_OVER_BACKLOG.format(root=os.path.dirname(here), tests=here)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                       timeout=200, env=dict(os.environ, FH_GRAPH_SMALL=small))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

@@ -349,6 +349,7 @@ print("ok")
 
 @pytest.mark.parametrize("env", [
     {},
+    {"FH_CODE_REGIONS": "0"},
     {"FH_VIEW_CMD": "0"},
     {"FH_VIEW_CMD": "0", "FH_PLACE_SLACK": "0"},
 ])
@@ -407,3 +408,20 @@ def test_views_mixed_tile_bounds_match_oracle(window, seed):
         assert np.array_equal(r["dep_off"], dep_off) and np.array_equal(r["deps"], deps)
         assert dict(zip(s.dots.tolist(), r["scc_label"].tolist())) == want_label
         assert np.array_equal(r["key_off"], kso) and np.array_equal(r["key_seq"], ks)
+
+
+@pytest.mark.parametrize("views,nproc,n,keys", [(1, 1, 30_000, 1 << 12), (2, 3, 30_000, 1 << 12),
+                                                (4, 5, 30_000, 1 << 12),
+                                                (3, 5, 4_500_000, 1 << 20)])
+def test_views_command_level_quorum_sizes(views, nproc, n, keys):
+    """The command-level KeyDeps path (k_cmd_search) at every fast-quorum size
+    it takes (1-3: codes through region records and k_code_scatter; 4: direct
+    stores), with the tails found from predecessor marks (in-tile and across
+    tiles); the 4.5M-command case spans two 4M-command code regions.  Each
+    fast quorum intersects every other (views > nproc / 2), as Atlas/EPaxos
+    require: with disjoint quorums two commands on one key need not be
+    connected, and the reference's per-key order then follows its hash-set
+    iteration (oracle.c check_pending)."""
+    s = Workload.zipf(0.99, keys, k=1, views=views, window=64, seed=40 + views,
+                      n=nproc).generate(n)
+    check_engine(s, nproc=nproc)

@@ -1,6 +1,8 @@
 """The C4 multi-GPU path on CPU: world_size-2 gloo processes each order their
-key shard of a replica-view stream with global dots (owner = key mod world,
-what bench.py --gpus N does with fh_workload_generate_shard), through the
+key shard of a replica-view stream with global dots (owner = the balanced key
+map, fh_key_owners_balanced over the stream's key counts, computed by every
+rank independently -- what bench.py --gpus N does with
+fh_workload_generate_shard_owned), through the
 oracle -- no GPU here -- and all-gather.  Rank 0 checks that the shards
 compose to the unsharded stream's outputs: the same committed deps, SCC
 labels and per-key sequences.  With one key per command every dependency
@@ -38,15 +40,20 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from fantoch_amd.workload import Stream, Workload
+    from fantoch_amd.workload import Stream, Workload, key_owners_balanced
     w = Workload.zipf(0.99, KEYS, k=1, views=3, window=64, seed=SEED, n=5)
     full = w.generate(TOTAL)
-    mine = np.nonzero(full.keys[:, 0] % world == rank)[0]
+    owner = key_owners_balanced(w.key_histogram(TOTAL), world)
+    mine = np.nonzero(owner[full.keys[:, 0]] == rank)[0]
     s = Stream(full.dots[mine], full.keys[mine], full.fq_proc[mine], full.fq_time[mine],
                full.key_space)
     # the shard generator (what bench.py stages) holds exactly these commands
-    g = w.generate_shard(TOTAL, world, rank)
+    g = w.generate_shard(TOTAL, world, rank, owner=owner)
     assert np.array_equal(g.dots, s.dots) and np.array_equal(g.keys, s.keys)
+    # balanced: each rank within 5% of the mean (key mod 2 is not, on Zipf)
+    sizes = [None] * world
+    dist.all_gather_object(sizes, int(s.n))
+    assert max(sizes) <= 1.05 * TOTAL / world, sizes
     off, deps, lab, kso, ks = _oracle(s)
     deps_of = {int(s.dots[i]): deps[off[i]:off[i + 1]].tolist() for i in range(s.n)}
     seqs = {int(k): ks[kso[k]:kso[k + 1]].tolist() for k in np.nonzero(np.diff(kso))[0]}

@@ -72,6 +72,21 @@ PROBES = {
 CALIB_BYTES = 1 << 30
 
 
+def read_durations(d):
+    """-> {kernel name: [per-dispatch duration in s]} from the counter CSVs'
+    timestamps (ns)."""
+    per = defaultdict(dict)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f, newline="") as fh:
+            for row in csv.DictReader(fh):
+                try:
+                    t = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9
+                except (KeyError, ValueError):
+                    continue
+                per[row["Kernel_Name"]][(f, row.get("Dispatch_Id"))] = t
+    return {k: list(v.values()) for k, v in per.items()}
+
+
 def read_counters(d, counter):
     """-> {kernel name: [per-dispatch value]} for `counter` under dir `d`."""
     per = defaultdict(lambda: defaultdict(float))
@@ -94,14 +109,17 @@ def calib(root):
                                ("write", "calib_write", "WRITE_SIZE")):
         rows = read_counters(os.path.join(root, sub), counter)
         for name, vals in rows.items():
-            m = re.search(r"calib_(read|write)<(.*)>\s*\(", name)
-            if not m or m.group(1) != kind:
+            m = re.search(r"calib_(read|write|gather|scatter)<(.*)>\s*\(", name)
+            if not m:
+                continue
+            k = m.group(1)
+            if (k in ("read", "gather")) != (kind == "read"):
                 continue
             t = m.group(2)
             w = 16 if "4u" in t else 8 if "2u" in t else 4
             vals = sorted(vals)
             med = vals[len(vals) // 2] * 1024.0
-            out[f"{kind}{w}"] = med / CALIB_BYTES
+            out[f"{k}{w}"] = med / CALIB_BYTES
     return out
 
 
@@ -121,9 +139,16 @@ def main():
         with open(a.out) as fh:
             res = {k: v for k, v in json.load(fh).items() if not k.startswith("_")}
     res.update({"_calibration": {"counter_bytes_over_true_bytes": cal,
-                            "note": "1 GiB streams per access width; raw engine counters are "
-                                    "divided by read4 / write4"},
-           "_command": a.command})
+                            "note": "1 GiB per access width: read/write = coalesced streams, "
+                                    "gather/scatter = one access per lane to a random line of "
+                                    "the same buffer (counter bytes per algorithmic byte); raw "
+                                    "engine counters are divided by read4 / write4"},
+                "_units": "fabric bytes: FETCH_SIZE / WRITE_SIZE count the L2's memory-side "
+                          "requests (Infinity-Cache hits included, MI355X_MICROARCH.md §HBM), "
+                          "corrected by the stream factors; for gather-bound kernels they "
+                          "are fabric traffic, not HBM bytes",
+                "_command": a.command})
+    dur = read_durations(os.path.join(a.root, "fetch"))
     for probe, pat in PROBES.items():
         fv = [v for k, vs in fetch.items() if pat in k for v in vs]
         wv = [v for k, vs in write.items() if pat in k for v in vs]
@@ -131,10 +156,19 @@ def main():
             continue
         fr = sum(fv) / len(fv) * 1024.0
         wr = sum(wv) / len(wv) * 1024.0
-        res[probe] = {"hbm_bytes_per_launch": fr / rf + wr / wf,
-                      "fetch_bytes_raw": fr, "write_bytes_raw": wr,
-                      "read_bytes_corrected": fr / rf, "write_bytes_corrected": wr / wf,
-                      "launches": [len(fv), len(wv)]}
+        tv = [t for k, ts in dur.items() if pat in k for t in ts]
+        e = {"hbm_bytes_per_launch": fr / rf + wr / wf,
+             "fetch_bytes_raw": fr, "write_bytes_raw": wr,
+             "read_bytes_corrected": fr / rf, "write_bytes_corrected": wr / wf,
+             "launches": [len(fv), len(wv)]}
+        if tv and sum(tv) > 0:
+            t = sum(tv) / len(tv)
+            e["avg_launch_s"] = t
+            e["fabric_TBs"] = e["hbm_bytes_per_launch"] / t / 1e12
+            # above the ~6.3 TB/s a copy achieves, the bytes cannot all be HBM
+            # traffic: Infinity-Cache hits are in them
+            e["exceeds_hbm_achievable"] = e["fabric_TBs"] > 6.3
+        res[probe] = e
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as fh:
         json.dump(res, fh, indent=1)

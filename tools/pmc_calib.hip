@@ -47,6 +47,41 @@ __global__ void __launch_bounds__(256) calib_write(T *__restrict__ a, size_t n) 
   }
 }
 
+// Random gathers and scatters (the engine's union, fill and code stores):
+// element i reads / writes slot perm(i) of the same 1 GiB buffer, a
+// bijection that puts every lane of a wave on a different line, so each
+// access costs a line from HBM while the algorithmic bytes stay sizeof(T) per
+// element.  The counters divided by kBytes give the gather / scatter factors
+// (bytes counted per algorithmic byte) that make a gather kernel's FETCH_SIZE
+// comparable with its byte count.
+__device__ __forceinline__ size_t calib_perm(size_t i, size_t n) {
+  return size_t((uint64_t(i) * 0x9E3779B1ull + 12345ull) % n);
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) calib_gather(const T *__restrict__ a, size_t n,
+                                                    uint32_t *__restrict__ sink) {
+  uint32_t acc = 0;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += size_t(gridDim.x) * 256) {
+    const T v = a[calib_perm(i, n)];
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(&v);
+#pragma unroll
+    for (unsigned j = 0; j < sizeof(T) / 4; j++) acc ^= w[j];
+  }
+  if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) calib_scatter(T *__restrict__ a, size_t n) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += size_t(gridDim.x) * 256) {
+    T v;
+    uint32_t *w = reinterpret_cast<uint32_t *>(&v);
+#pragma unroll
+    for (unsigned j = 0; j < sizeof(T) / 4; j++) w[j] = uint32_t(i) + j;
+    a[calib_perm(i, n)] = v;
+  }
+}
+
 int main() {
   void *buf = nullptr;
   uint32_t *sink = nullptr;
@@ -66,6 +101,14 @@ int main() {
     calib_write<uint2><<<grid, 256>>>((uint2 *)buf, kBytes / 8);
     CK(hipDeviceSynchronize());
     calib_write<uint4><<<grid, 256>>>((uint4 *)buf, kBytes / 16);
+    CK(hipDeviceSynchronize());
+    calib_gather<uint32_t><<<grid, 256>>>((const uint32_t *)buf, kBytes / 4, sink);
+    CK(hipDeviceSynchronize());
+    calib_gather<uint2><<<grid, 256>>>((const uint2 *)buf, kBytes / 8, sink);
+    CK(hipDeviceSynchronize());
+    calib_scatter<uint32_t><<<grid, 256>>>((uint32_t *)buf, kBytes / 4);
+    CK(hipDeviceSynchronize());
+    calib_scatter<uint2><<<grid, 256>>>((uint2 *)buf, kBytes / 8);
     CK(hipDeviceSynchronize());
   }
   CK(hipFree(buf));
