@@ -452,6 +452,23 @@ struct CmdMeta {
   }
 };
 
+// Sorted command values: the u64 (command | meta) alone, or (key-order
+// path) with the command's packed 32-bit dot beside it (V3, 12 B), so the
+// search and the graph read each command's dot in key order without a
+// gather.
+struct V3 {
+  uint32_t x, y, z;  // u64 value (lo, hi), packed dot
+  V3() = default;
+  __host__ __device__ V3(int) : x(0), y(0), z(0) {}
+};
+__device__ __forceinline__ uint64_t vload(const uint64_t *v, uint32_t i) { return v[i]; }
+__device__ __forceinline__ uint64_t vload(const V3 *v, uint32_t i) {
+  const V3 t = v[i];
+  return uint64_t(t.x) | (uint64_t(t.y) << 32);
+}
+__device__ __forceinline__ uint32_t vdot32(const uint64_t *, uint32_t) { return 0u; }
+__device__ __forceinline__ uint32_t vdot32(const V3 *v, uint32_t i) { return v[i].z; }
+
 // One workgroup per sort tile: packs each command's key, index and view
 // records (k_view_records) into the sort input, and writes the tile's digit
 // counts for the sort's first pass (sort_pairs_counted).
@@ -471,6 +488,36 @@ __global__ void __launch_bounds__(kThreads)
       m |= ((uint64_t(r >> kRecT) << cm.qb) | (r & cm.qmask)) << (j * cm.vb);
     }
     val[x] = uint64_t(x) | (m << cm.cb);
+    kw[x] = key | uint32_t((m >> (64 - cm.cb)) << cm.kb);
+    atomicAdd(&s_h[key & dmask], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
+}
+
+// k_cmd_pack with the command's packed dot beside the value (key-order path)
+__global__ void __launch_bounds__(kThreads)
+    k_cmd_pack3(uint32_t n, CmdMeta cm, const uint32_t *__restrict__ key32,
+                const uint32_t *__restrict__ rec, const uint32_t *__restrict__ dot32,
+                uint32_t *__restrict__ kw, V3 *__restrict__ val, uint32_t *__restrict__ counts,
+                uint32_t dmask) {
+  __shared__ uint32_t s_h[256];
+  s_h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(n, base + uint32_t(kTile));
+  for (uint32_t x = base + threadIdx.x; x < end; x += kThreads) {
+    const uint32_t key = key32[x];
+    uint64_t m = 0;
+    for (uint32_t j = 0; j < cm.fq; j++) {
+      const uint32_t r = rec[size_t(x) * cm.fq + j];
+      m |= ((uint64_t(r >> kRecT) << cm.qb) | (r & cm.qmask)) << (j * cm.vb);
+    }
+    const uint64_t v = uint64_t(x) | (m << cm.cb);
+    V3 o;
+    o.x = uint32_t(v);
+    o.y = uint32_t(v >> 32);
+    o.z = dot32[x];
+    val[x] = o;
     kw[x] = key | uint32_t((m >> (64 - cm.cb)) << cm.kb);
     atomicAdd(&s_h[key & dmask], 1u);
   }
@@ -539,16 +586,23 @@ struct ViewScan {
   }
 };
 
-template <uint32_t FQ, int TH>
+// KO (key-order path, VS = V3): every code that names an in-batch command
+// names it by its sorted position (pcode[i·FQ + j] = position + 1: the key-
+// order graph's edges), the region records carry the predecessors' packed
+// dots instead of their commands (the union then needs no gather), and the
+// command's own packed dot goes to pd32[i].
+template <uint32_t FQ, int TH, class VS, bool KO>
 __global__ void __launch_bounds__(TH)
     k_cmd_search(uint32_t n, CmdMeta cm, uint32_t K, uint32_t np, const uint32_t *__restrict__ kws,
-                 const uint64_t *__restrict__ vals, const uint64_t *__restrict__ latest,
+                 const VS *__restrict__ vals, const uint64_t *__restrict__ latest,
                  uint32_t *__restrict__ code, uint4 *__restrict__ rec,
                  const uint32_t *__restrict__ roff, uint8_t *__restrict__ tailm,
-                 uint32_t *__restrict__ mrem) {
+                 uint32_t *__restrict__ mrem, uint32_t *__restrict__ pcode,
+                 uint32_t *__restrict__ pd32) {
   constexpr int kSpan = TH + 2 * kSrchHalo;
   __shared__ uint32_t s_key[kSpan], s_c[kSpan];
   __shared__ uint32_t s_q[kSpan * kSrchMaxRep];
+  __shared__ uint32_t s_d[KO ? kSpan : 1];
   __shared__ uint8_t s_mark[TH * kSrchMaxRep];
   __shared__ uint32_t s_reg[kMaxRegions];
   const uint32_t tid = threadIdx.x, core = blockIdx.x * TH, i = core + tid;
@@ -562,10 +616,11 @@ __global__ void __launch_bounds__(TH)
   __syncthreads();
   for (uint32_t x = tid; x < span; x += TH) {
     const uint32_t kw = kws[lo + x];
-    const uint64_t v = vals[lo + x];
+    const uint64_t v = vload(vals, lo + x);
     const uint64_t m = cm.meta(kw, v);
     s_key[x] = kw & cm.kmask;
     s_c[x] = uint32_t(v & cm.cmask);
+    if constexpr (KO) s_d[x] = vdot32(vals, lo + x);
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) s_q[x * np + cm.rep(m, j)] = cm.arr(m, j) << qs;
   }
@@ -579,7 +634,7 @@ __global__ void __launch_bounds__(TH)
   if (act) {
     key = s_key[me];
     c = s_c[me];
-    const uint64_t m0 = cm.meta(kws[i], vals[i]);
+    const uint64_t m0 = cm.meta(kws[i], vload(vals, i));
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) {
       rr[j] = cm.rep(m0, j);
@@ -590,23 +645,44 @@ __global__ void __launch_bounds__(TH)
     // backward: the staged span, then global memory (a neighbour outside the
     // span is unpacked from the packed arrays); every view's state moves on
     // each neighbour, and the scan ends when no view can still improve
+    // Neighbours go in batches of kBk (forward kFw): the batch's LDS loads
+    // are issued together and waited for once.  Steps past the scan's end
+    // change nothing (further back a different key, or commands that cannot
+    // beat any view's best), so a batch runs whole and `go` after its last
+    // step says whether to continue.
+    constexpr uint32_t kBk = 4, kFw = 2;
     bool go = true;
-    for (uint32_t x = me; go && x > 0;) {
-      x--;
-      const bool sk = s_key[x] == key;
-      const uint32_t cc = s_c[x], ccW1 = cc + W + 1u;
-      const bool far = cc + W < c;
-      uint32_t lim = ~0u;
+    uint32_t x = me;
+    while (go && x > 0) {
+      uint32_t bk[kBk], bcc[kBk], bq[kBk][FQ];
 #pragma unroll
-      for (uint32_t j = 0; j < FQ; j++) {
-        vs[j].back(sk, cc, ccW1, far, s_q[x * np + rr[j]], lo + x);
-        lim = min(lim, vs[j].bc);
+      for (uint32_t u = 0; u < kBk; u++) {
+        const uint32_t y = x > u ? x - 1 - u : 0u;
+        bk[u] = x > u ? s_key[y] : ~key;
+        bcc[u] = s_c[y];
+#pragma unroll
+        for (uint32_t j = 0; j < FQ; j++) bq[u][j] = s_q[y * np + rr[j]];
       }
-      go = sk & !(ccW1 < lim);
+#pragma unroll
+      for (uint32_t u = 0; u < kBk; u++) {
+        const bool sk = bk[u] == key;
+        const uint32_t cc = bcc[u], ccW1 = cc + W + 1u;
+        const bool far = cc + W < c;
+        uint32_t lim = ~0u;
+#pragma unroll
+        for (uint32_t j = 0; j < FQ; j++) {
+          vs[j].back(sk, cc, ccW1, far, bq[u][j], lo + x - 1 - u);
+          lim = min(lim, vs[j].bc);
+        }
+        if (x > u) go = sk & !(ccW1 < lim);  // (a step below the span keeps it)
+      }
+      x = x > kBk ? x - kBk : 0u;
     }
+    // a batch that ran off the span's start with the scan still going
+    // continues on global memory below the span
     for (uint32_t ip = lo; go && ip-- > 0;) {
       const uint32_t kw = kws[ip];
-      const uint64_t v = vals[ip];
+      const uint64_t v = vload(vals, ip);
       const uint64_t m = cm.meta(kw, v);
       const bool sk = (kw & cm.kmask) == key;
       const uint32_t cc = uint32_t(v & cm.cmask), ccW1 = cc + W + 1u;
@@ -623,16 +699,30 @@ __global__ void __launch_bounds__(TH)
     }
     // forward, up to c + W
     go = true;
-    for (uint32_t x = me + 1; go && x < span; x++) {
-      const uint32_t cc = s_c[x];
-      const bool sk = (s_key[x] == key) & (cc <= c + W);
+    x = me + 1;
+    while (go && x < span) {
+      uint32_t fk[kFw], fcc[kFw], fq2[kFw][FQ];
 #pragma unroll
-      for (uint32_t j = 0; j < FQ; j++) vs[j].fwd(sk, cc, W, s_q[x * np + rr[j]], lo + x);
-      go = sk;
+      for (uint32_t u = 0; u < kFw; u++) {
+        const uint32_t y = x + u < span ? x + u : me;
+        fk[u] = x + u < span ? s_key[y] : ~key;
+        fcc[u] = s_c[y];
+#pragma unroll
+        for (uint32_t j = 0; j < FQ; j++) fq2[u][j] = s_q[y * np + rr[j]];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kFw; u++) {
+        const uint32_t cc = fcc[u];
+        const bool sk = (fk[u] == key) & (cc <= c + W);
+#pragma unroll
+        for (uint32_t j = 0; j < FQ; j++) vs[j].fwd(sk, cc, W, fq2[u][j], lo + x + u);
+        if (x + u < span) go = sk;  // (a step past the span keeps it)
+      }
+      x += kFw;
     }
     for (uint32_t ip = hi; go && ip < n; ip++) {
       const uint32_t kw = kws[ip];
-      const uint64_t v = vals[ip];
+      const uint64_t v = vload(vals, ip);
       const uint64_t m = cm.meta(kw, v);
       const uint32_t cc = uint32_t(v & cm.cmask);
       const bool sk = ((kw & cm.kmask) == key) & (cc <= c + W);
@@ -664,14 +754,23 @@ __global__ void __launch_bounds__(TH)
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) {
       if (vs[j].bc != 0u) {
-        cds[j] = vs[j].bc;  // in-batch: vid + 1
+        if constexpr (KO) {
+          // the predecessor's packed dot (staged, or beyond the span)
+          const uint32_t p = vs[j].bp;
+          cds[j] = p >= lo && p < hi ? s_d[p - lo] : vdot32(vals, p);
+          pcode[size_t(i) * FQ + j] = p + 1u;
+        } else {
+          cds[j] = vs[j].bc;  // in-batch: vid + 1
+        }
       } else {
         const uint64_t xl = latest[uint64_t(rr[j] + 1) * K + key];
         cds[j] = xl ? (0x80000000u | uint32_t(xl - kLogFlag)) : 0u;
+        if constexpr (KO) pcode[size_t(i) * FQ + j] = cds[j];
       }
       msk |= s_mark[tid * np + rr[j]] ? 0u : 1u << j;
     }
     tailm[i] = uint8_t(msk);
+    if constexpr (KO) pd32[i] = s_d[me];
     if (rec) {
       reg = c >> kRegShift;
       rank = atomicAdd(&s_reg[reg], 1u);
@@ -700,14 +799,15 @@ __global__ void __launch_bounds__(TH)
 // Commands per (region, search tile) from the sorted values, region-major
 // (counts[r * tiles + t]) so that one exclusive scan gives every tile its
 // first record in its region's contiguous slice.
+template <class VS>
 __global__ void __launch_bounds__(1024)
-    k_region_count(uint32_t n, uint64_t cmask, uint32_t nreg, const uint64_t *__restrict__ vals,
+    k_region_count(uint32_t n, uint64_t cmask, uint32_t nreg, const VS *__restrict__ vals,
                    uint32_t *__restrict__ counts) {
   __shared__ uint32_t s_h[kMaxRegions];
   const uint32_t tid = threadIdx.x, i = blockIdx.x * 1024 + tid;
   if (tid < kMaxRegions) s_h[tid] = 0;
   __syncthreads();
-  if (i < n) atomicAdd(&s_h[uint32_t(vals[i] & cmask) >> kRegShift], 1u);
+  if (i < n) atomicAdd(&s_h[uint32_t(vload(vals, i) & cmask) >> kRegShift], 1u);
   __syncthreads();
   if (tid < nreg) counts[size_t(tid) * gridDim.x + blockIdx.x] = s_h[tid];
 }
@@ -733,8 +833,9 @@ __global__ void __launch_bounds__(256)
 // the tails become the replicas' latest entries (after every head's read):
 // view j of a sorted command is its replica's tail iff neither the tile
 // (tailm) nor another tile (mrem) marked it as some element's predecessor
+template <class VS>
 __global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *__restrict__ kws,
-                            const uint64_t *__restrict__ vals, const uint8_t *__restrict__ tailm,
+                            const VS *__restrict__ vals, const uint8_t *__restrict__ tailm,
                             const uint8_t *__restrict__ mrem, uint64_t *__restrict__ latest,
                             uint64_t log_base) {
   GRID_STRIDE(i, n) {
@@ -742,13 +843,170 @@ __global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *
     if (!msk) continue;
     const uint32_t rm = mrem[i];
     const uint32_t kw = kws[i];
-    const uint64_t v = vals[i];
+    const uint64_t v = vload(vals, i);
     const uint64_t m = cm.meta(kw, v);
     const uint32_t key = kw & cm.kmask, c = uint32_t(v & cm.cmask);
     for (uint32_t j = 0; j < cm.fq; j++) {
       const uint32_t r = cm.rep(m, j);
       if ((msk & (1u << j)) && !(rm & (1u << r)))
         latest[uint64_t(r + 1) * K + key] = kLogFlag | (log_base + c);
+    }
+  }
+}
+
+// ---- the key-order path (one key per command, fast quorums of 2-3, dots
+// packable in 31 bits; EngineDevice::cmd_views_keyorder).  Every dependency
+// joins two commands of one key, so the graph is a disjoint union of per-key
+// graphs and the (key, command) sort order is as good a vertex order as the
+// arrival order: ready times, SCCs, depths and ties map monotonically
+// between the two inside a key.  Ordered by key, every edge spans a handful
+// of positions (C4: <= 20, maximum excess H(v) - v 65 against 728 in
+// arrival order at 5M commands, tools/keyorder_stats.py), so the tile
+// kernel runs with no certificate failures, its per-key execution order is
+// the per-key sequence itself (groups never straddle keys), and only the
+// per-command outputs travel back to command order.
+
+// The committed deps of each command in command order from its fq entries
+// (k_code_scatter of the key-order records): 0 none, 0x80000000 | x the log
+// reference of an earlier batch's latest entry, else a packed in-batch dot.
+// Dots are unique per command, so the count is the number of distinct
+// nonzero entries (a log reference never equals a packed dot: top bit).
+template <uint32_t FQ>
+__global__ void k_row_count(uint32_t n, const uint32_t *__restrict__ ent, uint32_t *__restrict__ cnt) {
+  GRID_STRIDE(i, n) {
+    uint32_t e[FQ];
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) e[j] = ent[size_t(i) * FQ + j];
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) {
+      bool dup = e[j] == 0u;
+#pragma unroll
+      for (uint32_t q = 0; q < j; q++) dup |= e[q] == e[j];
+      c += dup ? 0u : 1u;
+    }
+    cnt[i] = c;
+  }
+}
+
+// (An external dot equal to an in-batch one -- a dot of the batch repeating
+// an earlier batch's -- shortens the row below its count: err, as the
+// general union reports it.)
+template <uint32_t FQ>
+__global__ void k_row_union(uint32_t n, const uint32_t *__restrict__ ent,
+                            const uint64_t *__restrict__ dlog, int sb,
+                            const uint32_t *__restrict__ off, uint64_t *__restrict__ dep,
+                            uint32_t *__restrict__ err) {
+  GRID_STRIDE(i, n) {
+    uint64_t r[FQ];
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) {
+      const uint32_t e = ent[size_t(i) * FQ + j];
+      r[j] = e == 0u ? ~0ull
+             : (e & 0x80000000u) ? dlog[e & 0x7FFFFFFFu]
+                                 : (uint64_t(e >> sb) << 56) | (e & ((1u << sb) - 1));
+    }
+    // sort the FQ (<= 3) dots, then write the unique ones
+#pragma unroll
+    for (uint32_t a = 0; a < FQ; a++)
+#pragma unroll
+      for (uint32_t b2 = a + 1; b2 < FQ; b2++) {
+        const uint64_t x = r[a], y = r[b2];
+        r[a] = x < y ? x : y;
+        r[b2] = x < y ? y : x;
+      }
+    uint64_t *d = dep + off[i];
+    const uint32_t cap = off[i + 1] - off[i];
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++)
+      if (r[j] != ~0ull && (j == 0 || r[j] != r[j - 1])) {
+        if (m < cap) d[m] = r[j];
+        m++;
+      }
+    if (m != cap) atomicOr(err, 1u);
+  }
+}
+
+// Per key-order position p after the tile kernel (H = ready time, rank in
+// its group, group size at the root, labels; all in key order):
+//  * the per-key sequence: p runs at gstart[H] + rank of the key-order
+//    execution order, which is the key's sequence position (groups lie in
+//    one key, keys ascend);
+//  * the executed clock (per source: max sequence, count);
+//  * for command order: vertices of a multi-member ready group hand (H in
+//    command order, rank, label) to their command (flag bit + record), and
+//    every raised vertex (H > p) adds itself to the straddle counts
+//    (+1 at c + 1, -1 at c(H) + 1): the vertices before position t whose
+//    group runs at or after t, so that a group rooted at t starts at
+//    t - straddle(t) in the command-order execution.
+__global__ void __launch_bounds__(256)
+    k_ko_epilogue(uint32_t n, const V3 *__restrict__ vals, uint64_t cmask,
+                  const uint32_t *__restrict__ pd32, int sb, const uint32_t *__restrict__ th,
+                  const uint32_t *__restrict__ trank, const uint32_t *__restrict__ tcnt,
+                  const uint32_t *__restrict__ gstart, const uint64_t *__restrict__ label,
+                  uint64_t *__restrict__ seq, uint32_t *__restrict__ flag,
+                  uint4 *__restrict__ hl, uint32_t *__restrict__ diff,
+                  unsigned long long *__restrict__ smx, unsigned int *__restrict__ scnt) {
+  __shared__ unsigned long long s_mx[256];
+  __shared__ unsigned int s_cnt[256];
+  SrcAcc acc;
+  acc.init(s_mx, s_cnt);
+  __syncthreads();
+  GRID_STRIDE(p, n) {
+    const uint32_t h = th[p], rk = trank[p];
+    const uint32_t d = pd32[p];
+    const uint64_t dot = (uint64_t(d >> sb) << 56) | (d & ((1u << sb) - 1));
+    seq[gstart[h] + rk] = dot;
+    acc.add(dot);
+    if (h != p || tcnt[p] > 1u) {
+      const uint32_t c = uint32_t(vload(vals, p) & cmask);
+      const uint32_t hc = h == p ? c : uint32_t(vload(vals, h) & cmask);
+      const uint64_t lab = label[p];
+      atomicOr(&flag[c >> 5], 1u << (c & 31));
+      hl[c] = make_uint4(hc, rk, uint32_t(lab), uint32_t(lab >> 32));
+      if (h != p) {
+        atomicAdd(&diff[c + 1], 1u);
+        atomicAdd(&diff[hc + 1], ~0u);
+      }
+    }
+  }
+  acc.commit(smx, scnt);
+}
+
+// Command order: exec_rank[c] = start(t) + rank with t the group's ready
+// time in command order and start(t) = t - straddle(t) (ss = exclusive scan
+// of the straddle counts: straddle(t) = ss[t + 1]); a vertex outside a
+// multi-member group is its group's root with rank 0 and its own label.
+__global__ void k_ko_final(uint32_t n, const uint32_t *__restrict__ flag,
+                           const uint4 *__restrict__ hl, const uint32_t *__restrict__ ss,
+                           const uint64_t *__restrict__ dot, uint64_t *__restrict__ label,
+                           uint32_t *__restrict__ rank) {
+  GRID_STRIDE(c, n) {
+    if ((flag[c >> 5] >> (c & 31)) & 1u) {
+      const uint4 r = hl[c];
+      rank[c] = r.x - ss[r.x + 1] + r.y;
+      label[c] = uint64_t(r.z) | (uint64_t(r.w) << 32);
+    } else {
+      rank[c] = c - ss[c + 1];
+      label[c] = dot[c];
+    }
+  }
+}
+
+// Certificate failure on the key-order graph: its codes back to command
+// order with command-index references (the general path's encoding), then
+// the general union + graph run as for any batch.
+template <uint32_t FQ>
+__global__ void k_pcode_to_vid(uint32_t n, const V3 *__restrict__ vals, uint64_t cmask,
+                               const uint32_t *__restrict__ pcode, uint32_t *__restrict__ code) {
+  GRID_STRIDE(p, n) {
+    const uint32_t c = uint32_t(vload(vals, p) & cmask);
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) {
+      const uint32_t e = pcode[size_t(p) * FQ + j];
+      code[size_t(c) * FQ + j] =
+          (e == 0u || (e & 0x80000000u)) ? e : uint32_t(vload(vals, e - 1u) & cmask) + 1u;
     }
   }
 }
@@ -1326,12 +1584,12 @@ __global__ void k_pack_dots(uint32_t n, const uint64_t *__restrict__ dot, int sb
 // elements whose key is below k (lower bound), for k in [0, K] -- one launch
 // instead of a histogram (run starts, run counts) and its scan
 __global__ void k_key_offsets(uint32_t m, const uint32_t *__restrict__ keys, uint32_t K,
-                              uint32_t *__restrict__ o) {
+                              uint32_t *__restrict__ o, uint32_t kmask = ~0u) {
   GRID_STRIDE(k, K + 1) {
     uint32_t lo = 0, hi = m;
     while (lo < hi) {
       const uint32_t mid = lo + ((hi - lo) >> 1);
-      if (keys[mid] < k)
+      if ((keys[mid] & kmask) < k)
         lo = mid + 1;
       else
         hi = mid;
@@ -1432,6 +1690,19 @@ struct EngineDevice {
   DBuf<uint32_t> mrem;        // command-level views path: predecessor marks across tiles
   DBuf<uint4> crec;           // command-level views path: (command, codes) by tile and region
   DBuf<uint32_t> ctoff;       // command-level views path: records per (region, tile), offsets
+  // key-order path (cmd_views_keyorder)
+  bool ko_done = false;       // this run's outputs came from the key-order path
+  DBuf<V3> kv3a, kv3b;        // sort values with packed dots
+  DBuf<uint32_t> kpcode;      // [n·fq] codes by sorted position (graph edges)
+  DBuf<uint32_t> kpd32;       // [n] packed dot by sorted position
+  DBuf<uint32_t> kflag;       // [n/32] multi-member ready group, by command
+  DBuf<uint4> khl;            // [n] (H, rank, label) of those, by command
+  DBuf<uint32_t> kdiff, kss;  // straddle counts and their scan
+  // FH_KEYORDER=0 (measurement, tests): the command-order graph path
+  const bool keyorder_off = [] {
+    const char *e = getenv("FH_KEYORDER");
+    return e && *e == '0';
+  }();
   // FH_CODE_REGIONS=0 (measurement): codes stored straight at the command slot
   const bool region_off = [] {
     const char *e = getenv("FH_CODE_REGIONS");
@@ -1818,6 +2089,7 @@ struct EngineDevice {
     const size_t b = cursor++;
     last = b;
     last_deps_only = deps_only;
+    ko_done = false;
     const uint64_t bbase = stage_base + b * n;  // log position of this batch
     const uint64_t *bdot = dot.get() + bbase;
     const uint32_t *bkey = key32.get() + b * size_t(n) * k;
@@ -1911,8 +2183,12 @@ struct EngineDevice {
       sorted_keys32 = ks;
     } else if (CmdMeta cm; cmd_meta(b, k, fq, n, &cm)) {
       sv_fused = false;
-      cmd_views(b, n, fq, M, bkey, bbase, cm);
-      mark("keydeps_views");
+      if (keyorder_ok(b, fq)) {
+        ko_done = cmd_views_keyorder(b, n, fq, bkey, bdot, bbase, cm);
+      } else {
+        cmd_views(b, n, fq, M, bkey, bbase, cm);
+        mark("keydeps_views");
+      }
     } else {
       sv_fused = false;
       // every replica's KeyDeps over its arrival log, in chunks: chunk c
@@ -1990,8 +2266,10 @@ struct EngineDevice {
       if (profile) collect_times();
       return;
     }
-    if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bdot, bbase);
-    materialize(n, S, bdot);
+    if (!ko_done) {
+      if (!sv_fused) run_general(n, k, fq, S, M, views, bkey, bdot, bbase);
+      materialize(n, S, bdot);
+    }
     if (ms || profile) FH_HIP(hipEventRecord(ev1, stream));
     if (ms) {
       FH_HIP(hipEventSynchronize(ev1));
@@ -2033,6 +2311,169 @@ struct EngineDevice {
     m.qmask = (uint64_t(1) << m.qb) - 1;
     if (uint64_t(3) * m.W + 1 >= (uint64_t(1) << (m.qb - 1))) return false;
     *cm = m;
+    return true;
+  }
+
+  // The key-order path applies to command-level batches with fast quorums of
+  // 2 or 3 whose dots pack into 31 bits (the records' top bit marks a log
+  // reference).
+  bool keyorder_ok(size_t b, uint32_t fq) const {
+    return !keyorder_off && (fq == 2 || fq == 3) && b < h_dpack.size() &&
+           h_dpack[b].second > 0 && h_dpack[b].second <= 31 && dot32.get() != nullptr;
+  }
+
+  // One batch through the key-order path (kernels above k_row_count): the
+  // commands sorted by key once, carrying their packed dots; KeyDeps,
+  // union entries, graph edges, the tile kernel and the per-key sequence in
+  // key order; the committed deps, labels and execution ranks in command
+  // order.  Returns false (after leaving command-order codes in dep32) if the
+  // tile certificate fails, so the general path takes the batch.
+  bool cmd_views_keyorder(size_t b, uint32_t n, uint32_t fq, const uint32_t *bkey,
+                          const uint64_t *bdot, uint64_t bbase, const CmdMeta &cm) {
+    const uint32_t np = desc.nproc;
+    const int sb = h_dpack[b].first;
+    LogOffs lo{};
+    const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
+    for (uint32_t r = 0; r <= np; r++) lo.off[r] = bl[r];
+    const uint32_t *bent = lent.get() + b * size_t(n) * fq;
+    const uint32_t M = n * fq;
+    uint32_t *rec = vrec.ensure(M + 1);
+    const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * rec_slack(kRecWin)) / fq);
+    const uint32_t G = std::max<uint32_t>(1, (n + per - 1) / per);
+    probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records<kRecWin>, dim3(G),
+                  dim3(1024), stream, n, fq, np, G, lo, bent, rec);
+    const uint32_t tiles = (n + kTile - 1) / kTile;
+    sort_ws.prepare(tiles, 1, stream);
+    const int db = sort_digit_bits(key_bits, 4);
+    uint32_t *kwa = sk32a.ensure(n + 1);
+    V3 *va = kv3a.ensure(n + 1);
+    probed_launch("cmd_pack", double(n) * (4.0 + 4.0 * fq + 4.0 + 4.0 + 12.0), k_cmd_pack3,
+                  dim3(tiles), dim3(kThreads), stream, n, cm, bkey, (const uint32_t *)rec,
+                  (const uint32_t *)(dot32.get() + b * size_t(n)), kwa, va,
+                  sort_ws.meta.get(), (1u << db) - 1);
+    uint32_t *ks = nullptr;
+    V3 *vs = nullptr;
+    sort_pairs_counted<uint32_t, V3>(kwa, va, sk32b.ensure(n + 1), kv3b.ensure(n + 1), n,
+                                     key_bits, sort_ws, stream, &ks, &vs, db);
+    uint8_t *tm = tailm.ensure(n + 1);
+    const size_t mwords = (size_t(n) + 3) / 4;
+    uint32_t *mr = mrem.ensure(mwords);
+    FH_HIP(hipMemsetAsync(mr, 0, mwords * sizeof(uint32_t), stream));
+    const uint32_t stiles = (n + kSrchThreads - 1) / kSrchThreads;
+    const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> kRegShift) + 1;
+    FH_CHECK(nreg <= kMaxRegions, FH_EINVARIANT, "command regions");
+    uint4 *rec4 = crec.ensure(size_t(n) + 1);
+    const size_t nc = size_t(stiles) * nreg;
+    uint32_t *cnt = ctoff.ensure(2 * nc + 2);
+    uint32_t *roff = cnt + nc + 1;
+    k_region_count<V3><<<dim3(stiles), dim3(1024), 0, stream>>>(n, cm.cmask, nreg, vs, cnt);
+    exclusive_scan_u32(cnt, roff, nc, scan_ws, stream);
+    uint32_t *pcode = kpcode.ensure(size_t(n) * fq + 1);
+    uint32_t *pd32 = kpd32.ensure(n + 1);
+    uint32_t *codes = dep32.ensure(size_t(M) + 1);
+    const uint32_t K = uint32_t(key_space);
+    const uint64_t *lat = views_latest();
+    auto go = [&](auto kern) {
+      probed_launch("cmd_search", double(n) * (16.0 + 16.0 + 4.0 * fq + 4.0 + 1.0), kern,
+                    dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np, (const uint32_t *)ks,
+                    (const V3 *)vs, lat, codes, rec4, (const uint32_t *)roff, tm, mr, pcode,
+                    pd32);
+    };
+    if (fq == 2)
+      go(k_cmd_search<2, kSrchThreads, V3, true>);
+    else
+      go(k_cmd_search<3, kSrchThreads, V3, true>);
+    // the records' entries to their commands (region by region)
+    if (fq == 2)
+      probed_launch("code_scatter", double(n) * (16.0 + 8.0), k_code_scatter<2>,
+                    dim3((n + 255) / 256), dim3(256), stream, n, (const uint4 *)rec4, codes);
+    else
+      probed_launch("code_scatter", double(n) * (16.0 + 12.0), k_code_scatter<3>,
+                    dim3((n + 255) / 256), dim3(256), stream, n, (const uint4 *)rec4, codes);
+    k_cmd_tails<V3><<<grid_for(n, B), B, 0, stream>>>(n, cm, K, ks, vs, tm,
+                                                     reinterpret_cast<const uint8_t *>(mr),
+                                                     views_latest(), bbase);
+    mark("keydeps_views");
+    // committed deps (QuorumDeps union, deps/quorum.rs:28-98) from the dot
+    // entries: no gathers
+    uint32_t *dcnt = dep_cnt.ensure(n + 1);
+    uint32_t *doff = o_dep_off.ensure(n + 1);
+    uint64_t *ddot = o_dep.ensure(M + 1);
+    // the union's error word (results() checks it)
+    FH_HIP(hipMemsetAsync(scal.get(), 0, 2 * sizeof(uint32_t), stream));
+    if (fq == 2)
+      k_row_count<2><<<grid_for(n, B), B, 0, stream>>>(n, codes, dcnt);
+    else
+      k_row_count<3><<<grid_for(n, B), B, 0, stream>>>(n, codes, dcnt);
+    exclusive_scan_u32(dcnt, doff, n, scan_ws, stream);
+    mark("keydeps_count");
+    if (fq == 2)
+      probed_launch("row_union", double(n) * (8.0 + 4.0 + 16.0), k_row_union<2>,
+                    dim3(grid_for(n, B)), dim3(B), stream, n, (const uint32_t *)codes,
+                    (const uint64_t *)dot.get(), sb, (const uint32_t *)doff, ddot,
+                    scal.get() + 1);
+    else
+      probed_launch("row_union", double(n) * (12.0 + 4.0 + 16.0), k_row_union<3>,
+                    dim3(grid_for(n, B)), dim3(B), stream, n, (const uint32_t *)codes,
+                    (const uint64_t *)dot.get(), sb, (const uint32_t *)doff, ddot,
+                    scal.get() + 1);
+    deps_direct = true;
+    mark("keydeps_union");
+    if (deps_only) return true;
+    // the key-order graph on the tile path
+    GraphInput gin;
+    gin.V = n;
+    gin.stride = fq;
+    gin.dst = pcode;
+    gin.dst_codes = true;
+    gin.dot32 = pd32;
+    gin.dot32_sb = sb;
+    gin.k = 1;
+    gin.key_bits = key_bits;
+    gin.want_per_key = false;
+    gin.tiles_only = true;
+    graph.run(gin, gout);
+    if (gout.nexec == 0) {
+      // certificate failure: command-order codes for the general path
+      if (fq == 2)
+        k_pcode_to_vid<2><<<grid_for(n, B), B, 0, stream>>>(n, vs, cm.cmask, pcode, codes);
+      else
+        k_pcode_to_vid<3><<<grid_for(n, B), B, 0, stream>>>(n, vs, cm.cmask, pcode, codes);
+      return false;
+    }
+    // key-order epilogue: per-key sequences, executed clock, command-order
+    // records of multi-member groups and the straddle counts
+    uint64_t *sq = seq_dot.ensure(n + 1);
+    const uint32_t fw = (n + 31) / 32;
+    uint32_t *flag = kflag.ensure(fw + 1);
+    FH_HIP(hipMemsetAsync(flag, 0, size_t(fw) * sizeof(uint32_t), stream));
+    uint32_t *diff = kdiff.ensure(n + 2);
+    FH_HIP(hipMemsetAsync(diff, 0, size_t(n + 1) * sizeof(uint32_t), stream));
+    uint4 *hl = khl.ensure(n + 1);
+    unsigned long long *stt = srcstats.ensure(4 * 256);
+    FH_HIP(hipMemsetAsync(stt + 256, 0, 512 * sizeof(unsigned long long), stream));
+    probed_launch("ko_epilogue", double(n) * (4.0 * 5 + 8.0 + 8.0), k_ko_epilogue,
+                  dim3(grid_for(n, 256, 4096)), dim3(256), stream, n, (const V3 *)vs, cm.cmask,
+                  (const uint32_t *)pd32, sb, graph.tile_h(), graph.tile_rank(),
+                  graph.tile_count(), graph.tile_start(), (const uint64_t *)gout.scc_label, sq,
+                  flag, hl, diff, stt + 256, reinterpret_cast<unsigned int *>(stt + 512));
+    k_frontier_update<<<1, 256, 0, stream>>>(stt + 256, reinterpret_cast<unsigned int *>(stt + 512),
+                                             frontier.get(), excount_ptr());
+    uint32_t *ss = kss.ensure(n + 2);
+    exclusive_scan_u32(diff, ss, n + 1, scan_ws, stream);
+    mark("ko_epilogue");
+    uint64_t *lb = lab.ensure(n + 1);
+    uint32_t *rk = rank_tmp.ensure(n + 1);
+    probed_launch("ko_final", double(n) * (4.0 + 8.0 + 8.0 + 4.0), k_ko_final,
+                  dim3(grid_for(n, B)), dim3(B), stream, n, (const uint32_t *)flag,
+                  (const uint4 *)hl, (const uint32_t *)ss, bdot, lb, rk);
+    o_label = lb;
+    o_rank = rk;
+    o_seq = sq;
+    o_nelem = n;
+    k_key_offsets<<<grid_for(uint32_t(key_space) + 1, B), B, 0, stream>>>(
+        n, ks, uint32_t(key_space), key_offs.ensure(key_space + 2), cm.kmask);
+    mark("out_per_key");
     return true;
   }
 
@@ -2082,7 +2523,7 @@ struct EngineDevice {
       const size_t nc = size_t(stiles) * nreg;
       uint32_t *cnt = ctoff.ensure(2 * nc + 2);
       roff = cnt + nc + 1;
-      k_region_count<<<dim3(stiles), dim3(1024), 0, stream>>>(n, cm.cmask, nreg, vs, cnt);
+      k_region_count<uint64_t><<<dim3(stiles), dim3(1024), 0, stream>>>(n, cm.cmask, nreg, vs, cnt);
       exclusive_scan_u32(cnt, roff, nc, scan_ws, stream);
     }
     const double sb = double(n) * (12.0 + (rec4 ? 16.0 : fq * 4.0) + 1.0);
@@ -2091,13 +2532,13 @@ struct EngineDevice {
     auto go = [&](auto kern) {
       probed_launch("cmd_search", sb, kern, dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np,
                     (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, rec4,
-                    (const uint32_t *)roff, tm, mr);
+                    (const uint32_t *)roff, tm, mr, (uint32_t *)nullptr, (uint32_t *)nullptr);
     };
     switch (fq) {
-      case 1: go(k_cmd_search<1, kSrchThreads>); break;
-      case 2: go(k_cmd_search<2, kSrchThreads>); break;
-      case 3: go(k_cmd_search<3, kSrchThreads>); break;
-      default: go(k_cmd_search<4, kSrchThreads>); break;
+      case 1: go(k_cmd_search<1, kSrchThreads, uint64_t, false>); break;
+      case 2: go(k_cmd_search<2, kSrchThreads, uint64_t, false>); break;
+      case 3: go(k_cmd_search<3, kSrchThreads, uint64_t, false>); break;
+      default: go(k_cmd_search<4, kSrchThreads, uint64_t, false>); break;
     }
     if (rec4) {
       auto sc = [&](auto kern) {
@@ -2110,7 +2551,7 @@ struct EngineDevice {
         default: sc(k_code_scatter<3>); break;
       }
     }
-    k_cmd_tails<<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks, vs, tm,
+    k_cmd_tails<uint64_t><<<grid_for(n, B), B, 0, stream>>>(n, cm, uint32_t(key_space), ks, vs, tm,
                                                   reinterpret_cast<const uint8_t *>(mr),
                                                   views_latest(), bbase);
   }

@@ -69,6 +69,17 @@ struct GraphInput {
   // by a pass that reads every dot anyway (GraphOutput::src_stats_done)
   unsigned long long *src_mx = nullptr;   // [256]
   unsigned int *src_cnt = nullptr;        // [256]
+  // the engine's key-order graph (engine.hip, cmd_views_keyorder): edge
+  // slots are codes (0 none, 0x80000000 | x external, else target + 1), the
+  // dots packed 32-bit (dot32, src << dot32_sb | seq; `dot` unused), and
+  // only the tile path runs: on a certificate failure run() returns with
+  // out.nexec == 0 and the caller takes another route.  On success the
+  // tiles' outputs are read through tile_h / tile_rank / tile_count /
+  // tile_start and out.scc_label.
+  bool dst_codes = false;
+  const uint32_t *dot32 = nullptr;
+  int dot32_sb = 0;
+  bool tiles_only = false;
 };
 
 struct GraphOutput {
@@ -133,6 +144,13 @@ struct GraphCore {
   std::vector<std::pair<const char *, hipEvent_t>> *marks = nullptr;
 
   void run(const GraphInput &in, GraphOutput &out);
+  // tile outputs of the last run (valid after a tiles_only run succeeded):
+  // ready time H, rank in the ready group, group size at the root (0
+  // elsewhere), first execution position of each group
+  const uint32_t *tile_h() const { return t_h.get(); }
+  const uint32_t *tile_rank() const { return t_rank.get(); }
+  const uint32_t *tile_count() const { return t_cnt.get(); }
+  const uint32_t *tile_start() const { return t_start.get(); }
 
   // back to a fresh engine's first guesses (fh_engine_forget_tuning)
   void forget_tuning() {

@@ -1374,9 +1374,13 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   if (!in.no_forward_hint && !in.global_only && tiles_eligible(in)) {
     if (run_tiles(in, out)) {  // (labels come from the tiles)
       dbg_tile_ok++;
-      build_per_key(in, out);
+      if (!in.tiles_only) build_per_key(in, out);
       return;
     }
+  }
+  if (in.tiles_only) {  // the caller takes another route
+    out.nexec = 0;
+    return;
   }
   pending_closure(in, out);
   // trivial: nothing pending and every edge points to an earlier arrival ->

@@ -145,6 +145,17 @@ struct TileOut {
   unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
   int r0;      // certified reach bound R0 (L = 2·R0)
   int core;    // core vertices per tile T (T + 2L <= kTileC, T <= kMaxCore·1024)
+  // the engine's key-order graph (GraphInput::dst_codes / dot32): edge slots
+  // are codes (0 none, 0x80000000 | x external, else target + 1) and the
+  // dots are packed src << dot_sb | seq
+  bool codes = false;
+  const uint32_t *dot32 = nullptr;
+  int dot_sb = 0;
+  __device__ __forceinline__ uint64_t vdot(const uint64_t *dot, uint32_t v) const {
+    if (!dot32) return dot[v];
+    const uint32_t d = dot32[v];
+    return (uint64_t(d >> dot_sb) << 56) | (d & ((1u << dot_sb) - 1));
+  }
 };
 
 namespace {
@@ -193,7 +204,7 @@ __global__ void __launch_bounds__(kTileThreads)
 #pragma unroll
   for (int j = 0; j < kMaxCore; j++) {
     const int x = ca + tid + j * kTileThreads;
-    pdot[j] = x < cb ? dot[lo + x] : 0ull;
+    pdot[j] = x < cb ? out.vdot(dot, lo + x) : 0ull;
   }
 
   // 1. context edges; certificate part 2: forward spans of core vertices
@@ -202,7 +213,8 @@ __global__ void __launch_bounds__(kTileThreads)
     const uint32_t v = lo + x;
 #pragma unroll
     for (int s = 0; s < S; s++) {
-      const uint32_t u = dst[size_t(v) * S + s];
+      const uint32_t raw = dst[size_t(v) * S + s];
+      const uint32_t u = out.codes ? ((raw - 1u) < 0x7FFFFFFFu ? raw - 1u : v) : raw;
       uint16_t l = kNone;
       if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
       if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
@@ -509,7 +521,7 @@ __global__ void __launch_bounds__(kTileThreads)
   if (lds_dots)
     for (uint32_t i = tid; i < nraised; i += kTileThreads) {
       const uint16_t y = gmem[i];
-      gdot[i] = dot[lo + y];
+      gdot[i] = out.vdot(dot, lo + y);
       gkey[i] = (uint32_t(W1[sR[y]]) << 16) | sR[y];
     }
   __syncthreads();
@@ -532,7 +544,7 @@ __global__ void __launch_bounds__(kTileThreads)
         const uint32_t dy = W1[sR[y]], my = sR[y];
         if (dy != dx) return dy < dx;
         if (my != mx) return my < mx;
-        return dot[lo + y] < dotx;
+        return out.vdot(dot, lo + y) < dotx;
       };
       if (t != uint32_t(x)) rk += cmp(t);
       if (lds_dots) {
@@ -569,7 +581,7 @@ __global__ void __launch_bounds__(kTileThreads)
         }
 #pragma unroll
         for (int u = 0; u < 8; u++)
-          dy[u] = st[u] != 0 ? 0ull : lds_dots ? gdot[j + u] : dot[lo + ys[u]];
+          dy[u] = st[u] != 0 ? 0ull : lds_dots ? gdot[j + u] : out.vdot(dot, lo + ys[u]);
 #pragma unroll
         for (int u = 0; u < 8; u++) {
           rk += st[u] < 0 || (st[u] == 0 && dy[u] < dotx);
@@ -579,7 +591,7 @@ __global__ void __launch_bounds__(kTileThreads)
       // the root t is in x's SCC iff it shares the SCC slot (cmp(t) above
       // compared it; its dot was not kept)
       if (t != uint32_t(x) && sR[t] == mx) {
-        const uint64_t dt = dot[lo + t];
+        const uint64_t dt = out.vdot(dot, lo + t);
         if (lab == 0 || dt < lab) lab = dt;
       }
       gmax = max(gmax, cnt + 1);
@@ -728,6 +740,9 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.redo = nullptr;
   to.cores = nullptr;
   to.failf = nullptr;
+  to.codes = in.dst_codes;
+  to.dot32 = in.dot32;
+  to.dot_sb = in.dot32_sb;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   to.prof = nullptr;
   if (debug) {
@@ -794,6 +809,17 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   // execution order: groups in ready-time order, ranks inside a group
   uint32_t *gs = t_start.ensure(V + 1);
   exclusive_scan_u32(t_cnt.get(), gs, V, scan_ws, stream);
+  if (in.tiles_only) {
+    // the caller takes (H, rank in group, group starts, labels) as they are
+    out.exec_rank = nullptr;
+    out.exec_order = nullptr;
+    out.nexec = V;
+    out.npending = 0;
+    out.rep = nullptr;
+    out.scc_label = tmp64c.get();
+    mark("exec_order");
+    return true;
+  }
   uint32_t *er = tmp32d.ensure(V + 1);
   // the per-key pass of dots takes each vertex's rank from its group and
   // writes (key, dot) at it directly (build_per_key): no order array

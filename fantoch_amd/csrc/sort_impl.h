@@ -462,7 +462,8 @@ void sort_pass(const Src &src, K *ko, St vo, size_t n, int shift, uint32_t tiles
       // pair once
       // one probe name per kernel instantiation, as rocprof reports them
       const char *name = sizeof(K) == 8 ? "sort_scatter_u64"
-                         : sizeof(VT) == 8 ? "sort_scatter_dots" : "sort_scatter";
+                         : sizeof(VT) == 8 ? "sort_scatter_dots"
+                         : sizeof(VT) == 12 ? "sort_scatter_v3" : "sort_scatter";
       probed_launch(name, double(n) * (2.0 * sizeof(K) + sizeof(VT) + St::kBytes), kern, dim3(tiles),
                     dim3(th), s, src, ko, vo, uint32_t(n), shift, (const uint32_t *)counts,
                     (const uint32_t *)gsum, gsize, (const uint32_t *)dbase);

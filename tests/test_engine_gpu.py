@@ -349,7 +349,8 @@ print("ok")
 
 @pytest.mark.parametrize("env", [
     {},
-    {"FH_CODE_REGIONS": "0"},
+    {"FH_KEYORDER": "0"},
+    {"FH_KEYORDER": "0", "FH_CODE_REGIONS": "0"},
     {"FH_VIEW_CMD": "0"},
     {"FH_VIEW_CMD": "0", "FH_PLACE_SLACK": "0"},
 ])
