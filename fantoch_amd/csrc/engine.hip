@@ -645,41 +645,23 @@ __global__ void __launch_bounds__(TH)
     // backward: the staged span, then global memory (a neighbour outside the
     // span is unpacked from the packed arrays); every view's state moves on
     // each neighbour, and the scan ends when no view can still improve
-    // Neighbours go in batches of kBk (forward kFw): the batch's LDS loads
-    // are issued together and waited for once.  Steps past the scan's end
-    // change nothing (further back a different key, or commands that cannot
-    // beat any view's best), so a batch runs whole and `go` after its last
-    // step says whether to continue.
-    constexpr uint32_t kBk = 4, kFw = 2;
+    // (tried: batches of 4 neighbours with the batch's LDS loads issued
+    // together: 4.15 against 3.2 ms at C4, the extra steps cost more VALU
+    // than the waits they hid)
     bool go = true;
-    uint32_t x = me;
-    while (go && x > 0) {
-      uint32_t bk[kBk], bcc[kBk], bq[kBk][FQ];
+    for (uint32_t x = me; go && x > 0;) {
+      x--;
+      const bool sk = s_key[x] == key;
+      const uint32_t cc = s_c[x], ccW1 = cc + W + 1u;
+      const bool far = cc + W < c;
+      uint32_t lim = ~0u;
 #pragma unroll
-      for (uint32_t u = 0; u < kBk; u++) {
-        const uint32_t y = x > u ? x - 1 - u : 0u;
-        bk[u] = x > u ? s_key[y] : ~key;
-        bcc[u] = s_c[y];
-#pragma unroll
-        for (uint32_t j = 0; j < FQ; j++) bq[u][j] = s_q[y * np + rr[j]];
+      for (uint32_t j = 0; j < FQ; j++) {
+        vs[j].back(sk, cc, ccW1, far, s_q[x * np + rr[j]], lo + x);
+        lim = min(lim, vs[j].bc);
       }
-#pragma unroll
-      for (uint32_t u = 0; u < kBk; u++) {
-        const bool sk = bk[u] == key;
-        const uint32_t cc = bcc[u], ccW1 = cc + W + 1u;
-        const bool far = cc + W < c;
-        uint32_t lim = ~0u;
-#pragma unroll
-        for (uint32_t j = 0; j < FQ; j++) {
-          vs[j].back(sk, cc, ccW1, far, bq[u][j], lo + x - 1 - u);
-          lim = min(lim, vs[j].bc);
-        }
-        if (x > u) go = sk & !(ccW1 < lim);  // (a step below the span keeps it)
-      }
-      x = x > kBk ? x - kBk : 0u;
+      go = sk & !(ccW1 < lim);
     }
-    // a batch that ran off the span's start with the scan still going
-    // continues on global memory below the span
     for (uint32_t ip = lo; go && ip-- > 0;) {
       const uint32_t kw = kws[ip];
       const uint64_t v = vload(vals, ip);
@@ -699,26 +681,12 @@ __global__ void __launch_bounds__(TH)
     }
     // forward, up to c + W
     go = true;
-    x = me + 1;
-    while (go && x < span) {
-      uint32_t fk[kFw], fcc[kFw], fq2[kFw][FQ];
+    for (uint32_t x = me + 1; go && x < span; x++) {
+      const uint32_t cc = s_c[x];
+      const bool sk = (s_key[x] == key) & (cc <= c + W);
 #pragma unroll
-      for (uint32_t u = 0; u < kFw; u++) {
-        const uint32_t y = x + u < span ? x + u : me;
-        fk[u] = x + u < span ? s_key[y] : ~key;
-        fcc[u] = s_c[y];
-#pragma unroll
-        for (uint32_t j = 0; j < FQ; j++) fq2[u][j] = s_q[y * np + rr[j]];
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kFw; u++) {
-        const uint32_t cc = fcc[u];
-        const bool sk = (fk[u] == key) & (cc <= c + W);
-#pragma unroll
-        for (uint32_t j = 0; j < FQ; j++) vs[j].fwd(sk, cc, W, fq2[u][j], lo + x + u);
-        if (x + u < span) go = sk;  // (a step past the span keeps it)
-      }
-      x += kFw;
+      for (uint32_t j = 0; j < FQ; j++) vs[j].fwd(sk, cc, W, s_q[x * np + rr[j]], lo + x);
+      go = sk;
     }
     for (uint32_t ip = hi; go && ip < n; ip++) {
       const uint32_t kw = kws[ip];
@@ -803,13 +771,20 @@ template <class VS>
 __global__ void __launch_bounds__(1024)
     k_region_count(uint32_t n, uint64_t cmask, uint32_t nreg, const VS *__restrict__ vals,
                    uint32_t *__restrict__ counts) {
-  __shared__ uint32_t s_h[kMaxRegions];
-  const uint32_t tid = threadIdx.x, i = blockIdx.x * 1024 + tid;
-  if (tid < kMaxRegions) s_h[tid] = 0;
+  // per-wave counters: a wave's 64 lanes meet on ~24 regions, not the
+  // block's 1024 on the same 24
+  __shared__ uint32_t s_h[16][kMaxRegions];
+  const uint32_t tid = threadIdx.x, i = blockIdx.x * 1024 + tid, w = tid >> 6;
+  if (tid < 16 * kMaxRegions) (&s_h[0][0])[tid] = 0;
   __syncthreads();
-  if (i < n) atomicAdd(&s_h[uint32_t(vload(vals, i) & cmask) >> kRegShift], 1u);
+  if (i < n) atomicAdd(&s_h[w][uint32_t(vload(vals, i) & cmask) >> kRegShift], 1u);
   __syncthreads();
-  if (tid < nreg) counts[size_t(tid) * gridDim.x + blockIdx.x] = s_h[tid];
+  if (tid < nreg) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) t += s_h[q][tid];
+    counts[size_t(tid) * gridDim.x + blockIdx.x] = t;
+  }
 }
 
 // The (command, codes) records, region-major -> their command slots of the
@@ -934,19 +909,21 @@ __global__ void k_row_union(uint32_t n, const uint32_t *__restrict__ ent,
 //    execution order, which is the key's sequence position (groups lie in
 //    one key, keys ascend);
 //  * the executed clock (per source: max sequence, count);
-//  * for command order: vertices of a multi-member ready group hand (H in
-//    command order, rank, label) to their command (flag bit + record), and
-//    every raised vertex (H > p) adds itself to the straddle counts
-//    (+1 at c + 1, -1 at c(H) + 1): the vertices before position t whose
-//    group runs at or after t, so that a group rooted at t starts at
-//    t - straddle(t) in the command-order execution.
+//  * for command order, the straddle counts: straddle(t) = the vertices
+//    before position t whose group runs at or after t, so that a group
+//    rooted at t starts at t - straddle(t) in the command-order execution.
+//    A member u of a group rooted at t is raised (H(u) = t > u) iff u != t,
+//    so the difference array takes +1 at c(u) + 1 from each raised u and
+//    -(size - 1) at c(t) + 1 from each multi-member root: plain stores, no
+//    two on one slot (c(u) = c(t) means u = t), and d[c + 1] != 0 exactly
+//    for the vertices of multi-member groups, which also hand (H in command
+//    order, rank, label) to their command.
 __global__ void __launch_bounds__(256)
     k_ko_epilogue(uint32_t n, const V3 *__restrict__ vals, uint64_t cmask,
                   const uint32_t *__restrict__ pd32, int sb, const uint32_t *__restrict__ th,
                   const uint32_t *__restrict__ trank, const uint32_t *__restrict__ tcnt,
                   const uint32_t *__restrict__ gstart, const uint64_t *__restrict__ label,
-                  uint64_t *__restrict__ seq, uint32_t *__restrict__ flag,
-                  uint4 *__restrict__ hl, uint32_t *__restrict__ diff,
+                  uint64_t *__restrict__ seq, uint4 *__restrict__ hl, uint32_t *__restrict__ diff,
                   unsigned long long *__restrict__ smx, unsigned int *__restrict__ scnt) {
   __shared__ unsigned long long s_mx[256];
   __shared__ unsigned int s_cnt[256];
@@ -959,16 +936,13 @@ __global__ void __launch_bounds__(256)
     const uint64_t dot = (uint64_t(d >> sb) << 56) | (d & ((1u << sb) - 1));
     seq[gstart[h] + rk] = dot;
     acc.add(dot);
-    if (h != p || tcnt[p] > 1u) {
+    const uint32_t gc = h == p ? tcnt[p] : 0u;
+    if (h != p || gc > 1u) {
       const uint32_t c = uint32_t(vload(vals, p) & cmask);
       const uint32_t hc = h == p ? c : uint32_t(vload(vals, h) & cmask);
       const uint64_t lab = label[p];
-      atomicOr(&flag[c >> 5], 1u << (c & 31));
       hl[c] = make_uint4(hc, rk, uint32_t(lab), uint32_t(lab >> 32));
-      if (h != p) {
-        atomicAdd(&diff[c + 1], 1u);
-        atomicAdd(&diff[hc + 1], ~0u);
-      }
+      diff[c + 1] = h != p ? 1u : 0u - (gc - 1u);
     }
   }
   acc.commit(smx, scnt);
@@ -976,14 +950,15 @@ __global__ void __launch_bounds__(256)
 
 // Command order: exec_rank[c] = start(t) + rank with t the group's ready
 // time in command order and start(t) = t - straddle(t) (ss = exclusive scan
-// of the straddle counts: straddle(t) = ss[t + 1]); a vertex outside a
-// multi-member group is its group's root with rank 0 and its own label.
-__global__ void k_ko_final(uint32_t n, const uint32_t *__restrict__ flag,
+// of the difference array: straddle(t) = ss[t + 1]); a vertex outside a
+// multi-member group (d[c + 1] == 0) is its group's root with rank 0 and
+// its own label.
+__global__ void k_ko_final(uint32_t n, const uint32_t *__restrict__ diff,
                            const uint4 *__restrict__ hl, const uint32_t *__restrict__ ss,
                            const uint64_t *__restrict__ dot, uint64_t *__restrict__ label,
                            uint32_t *__restrict__ rank) {
   GRID_STRIDE(c, n) {
-    if ((flag[c >> 5] >> (c & 31)) & 1u) {
+    if (diff[c + 1] != 0u) {
       const uint4 r = hl[c];
       rank[c] = r.x - ss[r.x + 1] + r.y;
       label[c] = uint64_t(r.z) | (uint64_t(r.w) << 32);
@@ -1695,7 +1670,6 @@ struct EngineDevice {
   DBuf<V3> kv3a, kv3b;        // sort values with packed dots
   DBuf<uint32_t> kpcode;      // [n·fq] codes by sorted position (graph edges)
   DBuf<uint32_t> kpd32;       // [n] packed dot by sorted position
-  DBuf<uint32_t> kflag;       // [n/32] multi-member ready group, by command
   DBuf<uint4> khl;            // [n] (H, rank, label) of those, by command
   DBuf<uint32_t> kdiff, kss;  // straddle counts and their scan
   // FH_KEYORDER=0 (measurement, tests): the command-order graph path
@@ -2432,6 +2406,9 @@ struct EngineDevice {
     gin.key_bits = key_bits;
     gin.want_per_key = false;
     gin.tiles_only = true;
+    // (tried: the tile kernel at 5120-vertex contexts, two workgroups per
+    // CU, R0 = 256, T = 4096: 4.45 against 3.2 ms per C4 step -- twice the
+    // tiles and their barrier-bound fixed phases)
     graph.run(gin, gout);
     if (gout.nexec == 0) {
       // certificate failure: command-order codes for the general path
@@ -2444,9 +2421,6 @@ struct EngineDevice {
     // key-order epilogue: per-key sequences, executed clock, command-order
     // records of multi-member groups and the straddle counts
     uint64_t *sq = seq_dot.ensure(n + 1);
-    const uint32_t fw = (n + 31) / 32;
-    uint32_t *flag = kflag.ensure(fw + 1);
-    FH_HIP(hipMemsetAsync(flag, 0, size_t(fw) * sizeof(uint32_t), stream));
     uint32_t *diff = kdiff.ensure(n + 2);
     FH_HIP(hipMemsetAsync(diff, 0, size_t(n + 1) * sizeof(uint32_t), stream));
     uint4 *hl = khl.ensure(n + 1);
@@ -2456,7 +2430,7 @@ struct EngineDevice {
                   dim3(grid_for(n, 256, 4096)), dim3(256), stream, n, (const V3 *)vs, cm.cmask,
                   (const uint32_t *)pd32, sb, graph.tile_h(), graph.tile_rank(),
                   graph.tile_count(), graph.tile_start(), (const uint64_t *)gout.scc_label, sq,
-                  flag, hl, diff, stt + 256, reinterpret_cast<unsigned int *>(stt + 512));
+                  hl, diff, stt + 256, reinterpret_cast<unsigned int *>(stt + 512));
     k_frontier_update<<<1, 256, 0, stream>>>(stt + 256, reinterpret_cast<unsigned int *>(stt + 512),
                                              frontier.get(), excount_ptr());
     uint32_t *ss = kss.ensure(n + 2);
@@ -2465,7 +2439,7 @@ struct EngineDevice {
     uint64_t *lb = lab.ensure(n + 1);
     uint32_t *rk = rank_tmp.ensure(n + 1);
     probed_launch("ko_final", double(n) * (4.0 + 8.0 + 8.0 + 4.0), k_ko_final,
-                  dim3(grid_for(n, B)), dim3(B), stream, n, (const uint32_t *)flag,
+                  dim3(grid_for(n, B)), dim3(B), stream, n, (const uint32_t *)diff,
                   (const uint4 *)hl, (const uint32_t *)ss, bdot, lb, rk);
     o_label = lb;
     o_rank = rk;
