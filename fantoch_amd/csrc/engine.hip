@@ -903,70 +903,40 @@ __global__ void k_row_union(uint32_t n, const uint32_t *__restrict__ ent,
   }
 }
 
-// Per key-order position p after the tile kernel (H = ready time, rank in
-// its group, group size at the root, labels; all in key order):
-//  * the per-key sequence: p runs at gstart[H] + rank of the key-order
-//    execution order, which is the key's sequence position (groups lie in
-//    one key, keys ascend);
-//  * the executed clock (per source: max sequence, count);
-//  * for command order, the straddle counts: straddle(t) = the vertices
-//    before position t whose group runs at or after t, so that a group
-//    rooted at t starts at t - straddle(t) in the command-order execution.
-//    A member u of a group rooted at t is raised (H(u) = t > u) iff u != t,
-//    so the difference array takes +1 at c(u) + 1 from each raised u and
-//    -(size - 1) at c(t) + 1 from each multi-member root: plain stores, no
-//    two on one slot (c(u) = c(t) means u = t), and d[c + 1] != 0 exactly
-//    for the vertices of multi-member groups, which also hand (H in command
-//    order, rank, label) to their command.
-__global__ void __launch_bounds__(256)
-    k_ko_epilogue(uint32_t n, const V3 *__restrict__ vals, uint64_t cmask,
-                  const uint32_t *__restrict__ pd32, int sb, const uint32_t *__restrict__ th,
-                  const uint32_t *__restrict__ trank, const uint32_t *__restrict__ tcnt,
-                  const uint32_t *__restrict__ gstart, const uint64_t *__restrict__ label,
-                  uint64_t *__restrict__ seq, uint4 *__restrict__ hl, uint32_t *__restrict__ diff,
-                  unsigned long long *__restrict__ smx, unsigned int *__restrict__ scnt) {
-  __shared__ unsigned long long s_mx[256];
-  __shared__ unsigned int s_cnt[256];
-  SrcAcc acc;
-  acc.init(s_mx, s_cnt);
-  __syncthreads();
-  GRID_STRIDE(p, n) {
-    const uint32_t h = th[p], rk = trank[p];
-    const uint32_t d = pd32[p];
-    const uint64_t dot = (uint64_t(d >> sb) << 56) | (d & ((1u << sb) - 1));
-    seq[gstart[h] + rk] = dot;
-    acc.add(dot);
-    const uint32_t gc = h == p ? tcnt[p] : 0u;
-    if (h != p || gc > 1u) {
-      const uint32_t c = uint32_t(vload(vals, p) & cmask);
-      const uint32_t hc = h == p ? c : uint32_t(vload(vals, h) & cmask);
-      const uint64_t lab = label[p];
-      hl[c] = make_uint4(hc, rk, uint32_t(lab), uint32_t(lab >> 32));
-      diff[c + 1] = h != p ? 1u : 0u - (gc - 1u);
-    }
-  }
-  acc.commit(smx, scnt);
-}
-
 // Command order: exec_rank[c] = start(t) + rank with t the group's ready
 // time in command order and start(t) = t - straddle(t) (ss = exclusive scan
 // of the difference array: straddle(t) = ss[t + 1]); a vertex outside a
 // multi-member group (d[c + 1] == 0) is its group's root with rank 0 and
 // its own label.
-__global__ void k_ko_final(uint32_t n, const uint32_t *__restrict__ diff,
-                           const uint4 *__restrict__ hl, const uint32_t *__restrict__ ss,
-                           const uint64_t *__restrict__ dot, uint64_t *__restrict__ label,
-                           uint32_t *__restrict__ rank) {
+// The straddle difference array (graph_tile.hip, key-order outputs): +1 at
+// c(u) + 1 from each raised member u of a ready group (H(u) > u), -(size -
+// 1) at c(t) + 1 from each multi-member root t -- no slot written twice,
+// d[c + 1] != 0 exactly for the vertices of multi-member groups -- so that
+// straddle(t) = vertices before t whose group runs at or after t.  Also the
+// executed clock over the batch's dots (per source: max sequence, count).
+__global__ void __launch_bounds__(256)
+    k_ko_final(uint32_t n, const uint32_t *__restrict__ diff, const uint4 *__restrict__ hl,
+               const uint32_t *__restrict__ ss, const uint64_t *__restrict__ dot,
+               uint64_t *__restrict__ label, uint32_t *__restrict__ rank,
+               unsigned long long *__restrict__ smx, unsigned int *__restrict__ scnt) {
+  __shared__ unsigned long long s_mx[256];
+  __shared__ unsigned int s_cnt[256];
+  SrcAcc acc;
+  acc.init(s_mx, s_cnt);
+  __syncthreads();
   GRID_STRIDE(c, n) {
+    const uint64_t dc = dot[c];
+    acc.add(dc);
     if (diff[c + 1] != 0u) {
       const uint4 r = hl[c];
       rank[c] = r.x - ss[r.x + 1] + r.y;
       label[c] = uint64_t(r.z) | (uint64_t(r.w) << 32);
     } else {
       rank[c] = c - ss[c + 1];
-      label[c] = dot[c];
+      label[c] = dc;
     }
   }
+  acc.commit(smx, scnt);
 }
 
 // Certificate failure on the key-order graph: its codes back to command
@@ -2406,6 +2376,17 @@ struct EngineDevice {
     gin.key_bits = key_bits;
     gin.want_per_key = false;
     gin.tiles_only = true;
+    // the tiles write the per-key sequence and the command-order records
+    uint64_t *sq = seq_dot.ensure(n + 1);
+    uint32_t *diff = kdiff.ensure(n + 2);
+    FH_HIP(hipMemsetAsync(diff, 0, size_t(n + 1) * sizeof(uint32_t), stream));
+    uint4 *hl = khl.ensure(n + 1);
+    gin.ko_seq = sq;
+    gin.ko_hl = hl;
+    gin.ko_diff = diff;
+    gin.ko_cmd = reinterpret_cast<const uint32_t *>(vs);
+    gin.ko_cstride = 3;
+    gin.ko_cmask = uint32_t(cm.cmask);
     // (tried: the tile kernel at 5120-vertex contexts, two workgroups per
     // CU, R0 = 256, T = 4096: 4.45 against 3.2 ms per C4 step -- twice the
     // tiles and their barrier-bound fixed phases)
@@ -2418,29 +2399,19 @@ struct EngineDevice {
         k_pcode_to_vid<3><<<grid_for(n, B), B, 0, stream>>>(n, vs, cm.cmask, pcode, codes);
       return false;
     }
-    // key-order epilogue: per-key sequences, executed clock, command-order
-    // records of multi-member groups and the straddle counts
-    uint64_t *sq = seq_dot.ensure(n + 1);
-    uint32_t *diff = kdiff.ensure(n + 2);
-    FH_HIP(hipMemsetAsync(diff, 0, size_t(n + 1) * sizeof(uint32_t), stream));
-    uint4 *hl = khl.ensure(n + 1);
     unsigned long long *stt = srcstats.ensure(4 * 256);
     FH_HIP(hipMemsetAsync(stt + 256, 0, 512 * sizeof(unsigned long long), stream));
-    probed_launch("ko_epilogue", double(n) * (4.0 * 5 + 8.0 + 8.0), k_ko_epilogue,
-                  dim3(grid_for(n, 256, 4096)), dim3(256), stream, n, (const V3 *)vs, cm.cmask,
-                  (const uint32_t *)pd32, sb, graph.tile_h(), graph.tile_rank(),
-                  graph.tile_count(), graph.tile_start(), (const uint64_t *)gout.scc_label, sq,
-                  hl, diff, stt + 256, reinterpret_cast<unsigned int *>(stt + 512));
-    k_frontier_update<<<1, 256, 0, stream>>>(stt + 256, reinterpret_cast<unsigned int *>(stt + 512),
-                                             frontier.get(), excount_ptr());
     uint32_t *ss = kss.ensure(n + 2);
     exclusive_scan_u32(diff, ss, n + 1, scan_ws, stream);
-    mark("ko_epilogue");
+    mark("ko_straddle");
     uint64_t *lb = lab.ensure(n + 1);
     uint32_t *rk = rank_tmp.ensure(n + 1);
     probed_launch("ko_final", double(n) * (4.0 + 8.0 + 8.0 + 4.0), k_ko_final,
-                  dim3(grid_for(n, B)), dim3(B), stream, n, (const uint32_t *)diff,
-                  (const uint4 *)hl, (const uint32_t *)ss, bdot, lb, rk);
+                  dim3(grid_for(n, 256, 8192)), dim3(256), stream, n, (const uint32_t *)diff,
+                  (const uint4 *)hl, (const uint32_t *)ss, bdot, lb, rk, stt + 256,
+                  reinterpret_cast<unsigned int *>(stt + 512));
+    k_frontier_update<<<1, 256, 0, stream>>>(stt + 256, reinterpret_cast<unsigned int *>(stt + 512),
+                                             frontier.get(), excount_ptr());
     o_label = lb;
     o_rank = rk;
     o_seq = sq;

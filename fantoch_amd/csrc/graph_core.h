@@ -80,6 +80,14 @@ struct GraphInput {
   const uint32_t *dot32 = nullptr;
   int dot32_sb = 0;
   bool tiles_only = false;
+  // tiles_only with the key-order outputs written by the tiles themselves
+  // (TileOut::ko_*, graph_tile.hip): per-key sequence, command-order
+  // records and straddle differences of multi-member groups
+  uint64_t *ko_seq = nullptr;
+  uint4 *ko_hl = nullptr;
+  uint32_t *ko_diff = nullptr;
+  const uint32_t *ko_cmd = nullptr;
+  uint32_t ko_cstride = 0, ko_cmask = 0;
 };
 
 struct GraphOutput {

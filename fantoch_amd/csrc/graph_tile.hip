@@ -151,6 +151,17 @@ struct TileOut {
   bool codes = false;
   const uint32_t *dot32 = nullptr;
   int dot_sb = 0;
+  // key-order outputs (GraphInput::ko_seq; the engine's key-order path):
+  // each core vertex writes its dot at its key-order execution position
+  // (the per-key sequence), and a vertex of a multi-member ready group its
+  // command-order record and straddle difference (engine.hip k_ko_final);
+  // label / hgrp / grank / gcount are then not written.  cmd: the sorted
+  // values (command index in the low word, stride cstride words).
+  uint64_t *ko_seq = nullptr;
+  uint4 *ko_hl = nullptr;
+  uint32_t *ko_diff = nullptr;
+  const uint32_t *ko_cmd = nullptr;
+  uint32_t ko_cstride = 0, ko_cmask = 0;
   __device__ __forceinline__ uint64_t vdot(const uint64_t *dot, uint32_t v) const {
     if (!dot32) return dot[v];
     const uint32_t d = dot32[v];
@@ -201,10 +212,13 @@ __global__ void __launch_bounds__(kTileThreads)
   // the core vertices' own dots, loaded now and used by the last phase (its
   // labels and dot tie-breaks): the loads complete behind the LDS phases
   uint64_t pdot[kMaxCore];
+  uint32_t pcmd[kMaxCore];
 #pragma unroll
   for (int j = 0; j < kMaxCore; j++) {
     const int x = ca + tid + j * kTileThreads;
     pdot[j] = x < cb ? out.vdot(dot, lo + x) : 0ull;
+    pcmd[j] = out.ko_seq && x < cb ? out.ko_cmd[size_t(lo + x) * out.ko_cstride] & out.ko_cmask
+                                   : 0u;
   }
 
   // 1. context edges; certificate part 2: forward spans of core vertices
@@ -515,6 +529,32 @@ __global__ void __launch_bounds__(kTileThreads)
   // for every vertex of a large SCC
   // With them each member's order key (depth << 16 | SCC slot), so the rank
   // loop reads two independent arrays instead of a gmem -> sR -> W1 chain.
+  // key order: rp[j] = raised context vertices below the root t of core
+  // vertex j's group (W2 is still the ascending raised list); with b0 =
+  // gend[t - 1] = raised vertices whose group root is below t, rp - b0 =
+  // straddle(t) = vertices u < t with H(u) >= t (all within R0 below t, in
+  // the context, with exact H: the certificate), so t's group starts at
+  // lo + t - straddle(t) in the key-order execution.
+  uint32_t rpv[kMaxCore];
+  if (out.ko_seq) {
+#pragma unroll
+    for (int j = 0; j < kMaxCore; j++) {
+      const int x = ca + tid + j * kTileThreads;
+      uint32_t l0 = 0, h0 = nraised;
+      if (x < cb) {
+        const uint16_t t = sH[x];
+        while (l0 < h0) {
+          const uint32_t mid = (l0 + h0) >> 1;
+          if (W2[mid] < t)
+            l0 = mid + 1;
+          else
+            h0 = mid;
+        }
+      }
+      rpv[j] = l0;
+    }
+    __syncthreads();  // W2 becomes gdot below
+  }
   uint64_t *gdot = reinterpret_cast<uint64_t *>(W2);
   uint32_t *gkey = S == 3 ? reinterpret_cast<uint32_t *>(&eL[S - 1][0]) : gkey_s;
   const bool lds_dots = nraised <= uint32_t(kTileC / 4);
@@ -596,7 +636,20 @@ __global__ void __launch_bounds__(kTileThreads)
       }
       gmax = max(gmax, cnt + 1);
     }
-    out.label[v] = (lab == 0 || dotx < lab) ? dotx : lab;
+    const uint64_t label = (lab == 0 || dotx < lab) ? dotx : lab;
+    if (out.ko_seq) {
+      const uint32_t b0 = t ? uint32_t(gend[t - 1]) : 0u;
+      out.ko_seq[lo + t - rpv[j] + b0 + rk] = dotx;
+      if (t != uint32_t(x) || cnt > 0) {
+        const uint32_t c = pcmd[j];
+        const uint32_t ct = t == uint32_t(x) ? c : out.ko_cmd[size_t(lo + t) * out.ko_cstride] &
+                                                      out.ko_cmask;
+        out.ko_hl[c] = make_uint4(ct, rk, uint32_t(label), uint32_t(label >> 32));
+        out.ko_diff[c + 1] = t != uint32_t(x) ? 1u : 0u - cnt;
+      }
+      continue;
+    }
+    out.label[v] = label;
     if (out.rep) out.rep[v] = lo + sR[x];
     out.hgrp[v] = lo + t;
     out.grank[v] = rk;
@@ -743,6 +796,12 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.codes = in.dst_codes;
   to.dot32 = in.dot32;
   to.dot_sb = in.dot32_sb;
+  to.ko_seq = in.ko_seq;
+  to.ko_hl = in.ko_hl;
+  to.ko_diff = in.ko_diff;
+  to.ko_cmd = in.ko_cmd;
+  to.ko_cstride = in.ko_cstride;
+  to.ko_cmask = in.ko_cmask;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
   to.prof = nullptr;
   if (debug) {
@@ -805,6 +864,15 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   if (!ok) {
     dbg_tile_fail++;
     return false;
+  }
+  if (in.ko_seq) {  // the tiles wrote the caller's outputs themselves
+    out.exec_rank = nullptr;
+    out.exec_order = nullptr;
+    out.nexec = V;
+    out.npending = 0;
+    out.rep = nullptr;
+    out.scc_label = nullptr;
+    return true;
   }
   // execution order: groups in ready-time order, ranks inside a group
   uint32_t *gs = t_start.ensure(V + 1);
