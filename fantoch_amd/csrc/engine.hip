@@ -586,9 +586,11 @@ struct ViewScan {
   }
 };
 
-// KO (key-order path, VS = V3): every code that names an in-batch command
-// names it by its sorted position (pcode[i·FQ + j] = position + 1: the key-
-// order graph's edges), the region records carry the predecessors' packed
+// KO (key-order path, VS = V3): the key-order graph's edges are each
+// command's in-batch predecessors as signed 8-bit distances in sorted
+// position (pe8[i], byte j: i - position, 0 = none; key-order edges span a
+// handful of positions, C4 <= 20), with -128 escaping to the full position +
+// 1 in pcode[i·FQ + j]; the region records carry the predecessors' packed
 // dots instead of their commands (the union then needs no gather), and the
 // command's own packed dot goes to pd32[i].
 template <uint32_t FQ, int TH, class VS, bool KO>
@@ -598,7 +600,7 @@ __global__ void __launch_bounds__(TH)
                  uint32_t *__restrict__ code, uint4 *__restrict__ rec,
                  const uint32_t *__restrict__ roff, uint8_t *__restrict__ tailm,
                  uint32_t *__restrict__ mrem, uint32_t *__restrict__ pcode,
-                 uint32_t *__restrict__ pd32) {
+                 uint32_t *__restrict__ pd32, uint32_t *__restrict__ pe8) {
   constexpr int kSpan = TH + 2 * kSrchHalo;
   __shared__ uint32_t s_key[kSpan], s_c[kSpan];
   __shared__ uint32_t s_q[kSpan * kSrchMaxRep];
@@ -718,7 +720,7 @@ __global__ void __launch_bounds__(TH)
   uint32_t cds[FQ];
   uint32_t reg = 0, rank = 0;
   if (act) {
-    uint32_t msk = 0;
+    uint32_t msk = 0, e8 = 0;
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) {
       if (vs[j].bc != 0u) {
@@ -726,19 +728,27 @@ __global__ void __launch_bounds__(TH)
           // the predecessor's packed dot (staged, or beyond the span)
           const uint32_t p = vs[j].bp;
           cds[j] = p >= lo && p < hi ? s_d[p - lo] : vdot32(vals, p);
-          pcode[size_t(i) * FQ + j] = p + 1u;
+          const int d = int(i) - int(p);
+          if (d >= -127 && d <= 127) {
+            e8 |= (uint32_t(d) & 0xFFu) << (8 * j);
+          } else {
+            e8 |= 0x80u << (8 * j);
+            pcode[size_t(i) * FQ + j] = p + 1u;
+          }
         } else {
           cds[j] = vs[j].bc;  // in-batch: vid + 1
         }
       } else {
         const uint64_t xl = latest[uint64_t(rr[j] + 1) * K + key];
         cds[j] = xl ? (0x80000000u | uint32_t(xl - kLogFlag)) : 0u;
-        if constexpr (KO) pcode[size_t(i) * FQ + j] = cds[j];
       }
       msk |= s_mark[tid * np + rr[j]] ? 0u : 1u << j;
     }
     tailm[i] = uint8_t(msk);
-    if constexpr (KO) pd32[i] = s_d[me];
+    if constexpr (KO) {
+      pd32[i] = s_d[me];
+      pe8[i] = e8;
+    }
     if (rec) {
       reg = c >> kRegShift;
       rank = atomicAdd(&s_reg[reg], 1u);
@@ -939,19 +949,24 @@ __global__ void __launch_bounds__(256)
   acc.commit(smx, scnt);
 }
 
-// Certificate failure on the key-order graph: its codes back to command
-// order with command-index references (the general path's encoding), then
-// the general union + graph run as for any batch.
+// Certificate failure on the key-order graph: its in-batch edges back to
+// command order as command-index references (the general path's encoding)
+// over the command-order entries (which hold packed dots there; external
+// and empty entries stay), then the general union + graph run as for any
+// batch.
 template <uint32_t FQ>
 __global__ void k_pcode_to_vid(uint32_t n, const V3 *__restrict__ vals, uint64_t cmask,
-                               const uint32_t *__restrict__ pcode, uint32_t *__restrict__ code) {
+                               const uint32_t *__restrict__ pe8, const uint32_t *__restrict__ pcode,
+                               uint32_t *__restrict__ code) {
   GRID_STRIDE(p, n) {
     const uint32_t c = uint32_t(vload(vals, p) & cmask);
+    const uint32_t e8 = pe8[p];
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) {
-      const uint32_t e = pcode[size_t(p) * FQ + j];
-      code[size_t(c) * FQ + j] =
-          (e == 0u || (e & 0x80000000u)) ? e : uint32_t(vload(vals, e - 1u) & cmask) + 1u;
+      const int d = int(int8_t(uint8_t(e8 >> (8 * j))));
+      if (d == 0) continue;
+      const uint32_t q = d == -128 ? pcode[size_t(p) * FQ + j] - 1u : uint32_t(int(p) - d);
+      code[size_t(c) * FQ + j] = uint32_t(vload(vals, q) & cmask) + 1u;
     }
   }
 }
@@ -1638,7 +1653,8 @@ struct EngineDevice {
   // key-order path (cmd_views_keyorder)
   bool ko_done = false;       // this run's outputs came from the key-order path
   DBuf<V3> kv3a, kv3b;        // sort values with packed dots
-  DBuf<uint32_t> kpcode;      // [n·fq] codes by sorted position (graph edges)
+  DBuf<uint32_t> kpcode;      // [n·fq] escaped edge targets (position + 1)
+  DBuf<uint32_t> kpe8;        // [n] key-order edges as 8-bit distances
   DBuf<uint32_t> kpd32;       // [n] packed dot by sorted position
   DBuf<uint4> khl;            // [n] (H, rank, label) of those, by command
   DBuf<uint32_t> kdiff, kss;  // straddle counts and their scan
@@ -1663,6 +1679,23 @@ struct EngineDevice {
   DBuf<unsigned long long> srcstats;
   SortWorkspace sort_ws;
   ScanWorkspace scan_ws;
+  // key-order path: the command-order half of a batch (code scatter, tails,
+  // union) runs on `side` beside the tile kernel on `stream`; FH_KO_SIDE=0
+  // (measurement) keeps it on `stream`
+  const bool side_off = [] {
+    const char *e = getenv("FH_KO_SIDE");
+    return e && *e == '0';
+  }();
+  // Workgroups of the side kernels (FH_KO_SIDE_GRID, measurement; 0: one per
+  // 256 items): two 256-thread workgroups per CU.  The tile kernel holds one
+  // 16-wave workgroup per CU (its LDS), so 8 side waves leave room for the
+  // next tile's workgroup as soon as one retires.  C4, ms per step: 2 per CU
+  // 15.6, 1.5 per CU 16.9, 2.5 16.7, 3 16.1, 4 17.7, uncapped 16.8, no side
+  // stream 17.2 (profiles/r05_side_sweep.txt).
+  unsigned side_grid = 0;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  ScanWorkspace scan_ws2;
   GraphCore graph;
   GraphOutput gout;
   Probe probe;
@@ -1698,9 +1731,23 @@ struct EngineDevice {
     }
     device = pick_device(&cfg, 0);
     FH_HIP(hipSetDevice(device));
-    FH_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    {
+      // the engine's stream first: the side stream's kernels fill in
+      int least = 0, greatest = 0;
+      FH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      FH_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, greatest));
+      FH_HIP(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, least));
+    }
     FH_HIP(hipEventCreate(&ev0));
     FH_HIP(hipEventCreate(&ev1));
+    {
+      int cus = 0;
+      FH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+      const char *e = getenv("FH_KO_SIDE_GRID");
+      side_grid = e ? unsigned(atoi(e)) : 2u * unsigned(std::max(cus, 1));
+    }
+    FH_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    FH_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
 
     graph.stream = stream;
     graph.marks = &marks;
@@ -1715,6 +1762,10 @@ struct EngineDevice {
     clear_marks();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    if (side) (void)hipStreamSynchronize(side);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -2314,6 +2365,7 @@ struct EngineDevice {
     exclusive_scan_u32(cnt, roff, nc, scan_ws, stream);
     uint32_t *pcode = kpcode.ensure(size_t(n) * fq + 1);
     uint32_t *pd32 = kpd32.ensure(n + 1);
+    uint32_t *pe8 = kpe8.ensure(n + 1);
     uint32_t *codes = dep32.ensure(size_t(M) + 1);
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
@@ -2321,55 +2373,76 @@ struct EngineDevice {
       probed_launch("cmd_search", double(n) * (16.0 + 16.0 + 4.0 * fq + 4.0 + 1.0), kern,
                     dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np, (const uint32_t *)ks,
                     (const V3 *)vs, lat, codes, rec4, (const uint32_t *)roff, tm, mr, pcode,
-                    pd32);
+                    pd32, pe8);
     };
     if (fq == 2)
       go(k_cmd_search<2, kSrchThreads, V3, true>);
     else
       go(k_cmd_search<3, kSrchThreads, V3, true>);
-    // the records' entries to their commands (region by region)
-    if (fq == 2)
-      probed_launch("code_scatter", double(n) * (16.0 + 8.0), k_code_scatter<2>,
-                    dim3((n + 255) / 256), dim3(256), stream, n, (const uint4 *)rec4, codes);
-    else
-      probed_launch("code_scatter", double(n) * (16.0 + 12.0), k_code_scatter<3>,
-                    dim3((n + 255) / 256), dim3(256), stream, n, (const uint4 *)rec4, codes);
-    k_cmd_tails<V3><<<grid_for(n, B), B, 0, stream>>>(n, cm, K, ks, vs, tm,
-                                                     reinterpret_cast<const uint8_t *>(mr),
-                                                     views_latest(), bbase);
     mark("keydeps_views");
+    // The command-order half -- the records' entries to their commands
+    // (region by region), the tails, the committed deps -- needs nothing the
+    // graph computes, and the graph needs none of it: it runs on the side
+    // stream while the tile kernel (latency bound, one workgroup per CU)
+    // runs here.
+    hipStream_t cs = side_off ? stream : side;
+    ScanWorkspace &cws = side_off ? scan_ws : scan_ws2;
+    if (!side_off) {
+      FH_HIP(hipEventRecord(ev_fork, stream));
+      FH_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+    }
+    auto join = [&] {
+      if (side_off) return;
+      FH_HIP(hipEventRecord(ev_join, side));
+      FH_HIP(hipStreamWaitEvent(stream, ev_join, 0));
+    };
+    const unsigned sg = side_off || side_grid == 0 ? ~0u : side_grid;
+    const dim3 gs(grid_for(n, B, std::min(sg, 1u << 30)));
+    const dim3 gs8(grid_for(n, B, std::min(sg, 8192u)));
+    if (fq == 2)
+      probed_launch("code_scatter", double(n) * (16.0 + 8.0), k_code_scatter<2>, gs, dim3(B), cs,
+                    n, (const uint4 *)rec4, codes);
+    else
+      probed_launch("code_scatter", double(n) * (16.0 + 12.0), k_code_scatter<3>, gs, dim3(B), cs,
+                    n, (const uint4 *)rec4, codes);
+    k_cmd_tails<V3><<<gs8, B, 0, cs>>>(n, cm, K, ks, vs, tm,
+                                                 reinterpret_cast<const uint8_t *>(mr),
+                                                 views_latest(), bbase);
     // committed deps (QuorumDeps union, deps/quorum.rs:28-98) from the dot
     // entries: no gathers
     uint32_t *dcnt = dep_cnt.ensure(n + 1);
     uint32_t *doff = o_dep_off.ensure(n + 1);
     uint64_t *ddot = o_dep.ensure(M + 1);
     // the union's error word (results() checks it)
-    FH_HIP(hipMemsetAsync(scal.get(), 0, 2 * sizeof(uint32_t), stream));
+    FH_HIP(hipMemsetAsync(scal.get(), 0, 2 * sizeof(uint32_t), cs));
     if (fq == 2)
-      k_row_count<2><<<grid_for(n, B), B, 0, stream>>>(n, codes, dcnt);
+      k_row_count<2><<<gs8, B, 0, cs>>>(n, codes, dcnt);
     else
-      k_row_count<3><<<grid_for(n, B), B, 0, stream>>>(n, codes, dcnt);
-    exclusive_scan_u32(dcnt, doff, n, scan_ws, stream);
-    mark("keydeps_count");
+      k_row_count<3><<<gs8, B, 0, cs>>>(n, codes, dcnt);
+    exclusive_scan_u32(dcnt, doff, n, cws, cs);
     if (fq == 2)
-      probed_launch("row_union", double(n) * (8.0 + 4.0 + 16.0), k_row_union<2>,
-                    dim3(grid_for(n, B)), dim3(B), stream, n, (const uint32_t *)codes,
+      probed_launch("row_union", double(n) * (8.0 + 4.0 + 16.0), k_row_union<2>, gs8, dim3(B), cs,
+                    n, (const uint32_t *)codes,
                     (const uint64_t *)dot.get(), sb, (const uint32_t *)doff, ddot,
                     scal.get() + 1);
     else
-      probed_launch("row_union", double(n) * (12.0 + 4.0 + 16.0), k_row_union<3>,
-                    dim3(grid_for(n, B)), dim3(B), stream, n, (const uint32_t *)codes,
+      probed_launch("row_union", double(n) * (12.0 + 4.0 + 16.0), k_row_union<3>, gs8, dim3(B), cs,
+                    n, (const uint32_t *)codes,
                     (const uint64_t *)dot.get(), sb, (const uint32_t *)doff, ddot,
                     scal.get() + 1);
     deps_direct = true;
-    mark("keydeps_union");
-    if (deps_only) return true;
+    if (deps_only) {
+      join();
+      mark("keydeps_union");
+      return true;
+    }
     // the key-order graph on the tile path
     GraphInput gin;
     gin.V = n;
     gin.stride = fq;
-    gin.dst = pcode;
+    gin.dst = pe8;
     gin.dst_codes = true;
+    gin.dst_esc = pcode;
     gin.dot32 = pd32;
     gin.dot32_sb = sb;
     gin.k = 1;
@@ -2393,10 +2466,11 @@ struct EngineDevice {
     graph.run(gin, gout);
     if (gout.nexec == 0) {
       // certificate failure: command-order codes for the general path
+      join();
       if (fq == 2)
-        k_pcode_to_vid<2><<<grid_for(n, B), B, 0, stream>>>(n, vs, cm.cmask, pcode, codes);
+        k_pcode_to_vid<2><<<grid_for(n, B), B, 0, stream>>>(n, vs, cm.cmask, pe8, pcode, codes);
       else
-        k_pcode_to_vid<3><<<grid_for(n, B), B, 0, stream>>>(n, vs, cm.cmask, pcode, codes);
+        k_pcode_to_vid<3><<<grid_for(n, B), B, 0, stream>>>(n, vs, cm.cmask, pe8, pcode, codes);
       return false;
     }
     unsigned long long *stt = srcstats.ensure(4 * 256);
@@ -2419,6 +2493,8 @@ struct EngineDevice {
     k_key_offsets<<<grid_for(uint32_t(key_space) + 1, B), B, 0, stream>>>(
         n, ks, uint32_t(key_space), key_offs.ensure(key_space + 2), cm.kmask);
     mark("out_per_key");
+    join();
+    mark("keydeps_union");
     return true;
   }
 
@@ -2477,7 +2553,8 @@ struct EngineDevice {
     auto go = [&](auto kern) {
       probed_launch("cmd_search", sb, kern, dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np,
                     (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, rec4,
-                    (const uint32_t *)roff, tm, mr, (uint32_t *)nullptr, (uint32_t *)nullptr);
+                    (const uint32_t *)roff, tm, mr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                    (uint32_t *)nullptr);
     };
     switch (fq) {
       case 1: go(k_cmd_search<1, kSrchThreads, uint64_t, false>); break;

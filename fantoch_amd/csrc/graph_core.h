@@ -70,13 +70,16 @@ struct GraphInput {
   unsigned long long *src_mx = nullptr;   // [256]
   unsigned int *src_cnt = nullptr;        // [256]
   // the engine's key-order graph (engine.hip, cmd_views_keyorder): edge
-  // slots are codes (0 none, 0x80000000 | x external, else target + 1), the
+  // slots are 8-bit distances (dst_codes), the
   // dots packed 32-bit (dot32, src << dot32_sb | seq; `dot` unused), and
   // only the tile path runs: on a certificate failure run() returns with
   // out.nexec == 0 and the caller takes another route.  On success the
   // tiles' outputs are read through tile_h / tile_rank / tile_count /
   // tile_start and out.scc_label.
-  bool dst_codes = false;
+  bool dst_codes = false;  // dst = one u32 per vertex of signed 8-bit
+                           // distances (byte s: v - target, 0 none, -128:
+                           // target + 1 in dst_esc[v·stride + s])
+  const uint32_t *dst_esc = nullptr;
   const uint32_t *dot32 = nullptr;
   int dot32_sb = 0;
   bool tiles_only = false;

@@ -145,12 +145,13 @@ struct TileOut {
   unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
   int r0;      // certified reach bound R0 (L = 2·R0)
   int core;    // core vertices per tile T (T + 2L <= kTileC, T <= kMaxCore·1024)
-  // the engine's key-order graph (GraphInput::dst_codes / dot32): edge slots
-  // are codes (0 none, 0x80000000 | x external, else target + 1) and the
-  // dots are packed src << dot_sb | seq
+  // the engine's key-order graph (GraphInput::dst_codes / dot32): edges as
+  // one u32 of 8-bit distances per vertex (GraphInput::dst_codes) and the
+  // dots packed src << dot_sb | seq
   bool codes = false;
   const uint32_t *dot32 = nullptr;
   int dot_sb = 0;
+  const uint32_t *esc = nullptr;  // codes: escaped targets (GraphInput::dst_esc)
   // key-order outputs (GraphInput::ko_seq; the engine's key-order path):
   // each core vertex writes its dot at its key-order execution position
   // (the per-key sequence), and a vertex of a multi-member ready group its
@@ -223,18 +224,42 @@ __global__ void __launch_bounds__(kTileThreads)
 
   // 1. context edges; certificate part 2: forward spans of core vertices
   uint32_t nlong = 0;
-  for (int x = tid; x < C; x += kTileThreads) {
-    const uint32_t v = lo + x;
+  auto put_edge = [&](int x, int s, uint32_t v, uint32_t u) {
+    uint16_t l = kNone;
+    if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
+    if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
+    eL[s][x] = l;
+  };
+  if (out.codes) {
+    // one word per vertex: all of the thread's words in flight at once
+    constexpr int kPI = kTileC / kTileThreads;
+    uint32_t ew[kPI];
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-      const uint32_t raw = dst[size_t(v) * S + s];
-      const uint32_t u = out.codes ? ((raw - 1u) < 0x7FFFFFFFu ? raw - 1u : v) : raw;
-      uint16_t l = kNone;
-      if (u != v && u >= lo && u < hi) l = uint16_t(u - lo);
-      if (x >= ca && x < cb && u > v && u - v >= uint32_t(L - R0)) nlong++;
-      eL[s][x] = l;
+    for (int j = 0; j < kPI; j++) {
+      const int x = tid + j * kTileThreads;
+      ew[j] = x < C ? dst[lo + x] : 0u;
     }
-    sH[x] = uint16_t(x);
+#pragma unroll
+    for (int j = 0; j < kPI; j++) {
+      const int x = tid + j * kTileThreads;
+      if (x >= C) break;
+      const uint32_t v = lo + x;
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const int d = int(int8_t(uint8_t(ew[j] >> (8 * s))));
+        const uint32_t u =
+            d == 0 ? v : d == -128 ? out.esc[size_t(v) * S + s] - 1u : uint32_t(int(v) - d);
+        put_edge(x, s, v, u);
+      }
+      sH[x] = uint16_t(x);
+    }
+  } else {
+    for (int x = tid; x < C; x += kTileThreads) {
+      const uint32_t v = lo + x;
+#pragma unroll
+      for (int s = 0; s < S; s++) put_edge(x, s, v, dst[size_t(v) * S + s]);
+      sH[x] = uint16_t(x);
+    }
   }
   __syncthreads();
   phase(0);
@@ -794,6 +819,7 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.cores = nullptr;
   to.failf = nullptr;
   to.codes = in.dst_codes;
+  to.esc = in.dst_esc;
   to.dot32 = in.dot32;
   to.dot_sb = in.dot32_sb;
   to.ko_seq = in.ko_seq;

@@ -349,6 +349,7 @@ print("ok")
 
 @pytest.mark.parametrize("env", [
     {},
+    {"FH_KO_SIDE": "0"},
     {"FH_KEYORDER": "0"},
     {"FH_KEYORDER": "0", "FH_CODE_REGIONS": "0"},
     {"FH_VIEW_CMD": "0"},
