@@ -525,6 +525,41 @@ __global__ void __launch_bounds__(kThreads)
   if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
 }
 
+// The key-order path's sort input, produced inside the sort's first scatter
+// (sort_pairs_counted_src): element x's key word and V3 value as k_cmd_pack3
+// writes them, computed from the command's key, view records and packed dot
+// as the scatter loads the element (the packed arrays are never written:
+// 2 x 16 B per command less traffic).  k_key_counts writes the tile digit
+// counts of that first pass.
+struct PackSrc {
+  CmdMeta cm;
+  const uint32_t *key32, *rec, *dot32;
+  __device__ __forceinline__ void get(uint32_t x, uint32_t &kw, V3 &o) const {
+    const uint32_t key = key32[x];
+    uint64_t m = 0;
+    for (uint32_t j = 0; j < cm.fq; j++) {
+      const uint32_t r = rec[size_t(x) * cm.fq + j];
+      m |= ((uint64_t(r >> kRecT) << cm.qb) | (r & cm.qmask)) << (j * cm.vb);
+    }
+    const uint64_t v = uint64_t(x) | (m << cm.cb);
+    o.x = uint32_t(v);
+    o.y = uint32_t(v >> 32);
+    o.z = dot32[x];
+    kw = key | uint32_t((m >> (64 - cm.cb)) << cm.kb);
+  }
+};
+__global__ void __launch_bounds__(kThreads)
+    k_key_counts(uint32_t n, const uint32_t *__restrict__ key32, uint32_t *__restrict__ counts,
+                 uint32_t dmask) {
+  __shared__ uint32_t s_h[256];
+  s_h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(n, base + uint32_t(kTile));
+  for (uint32_t x = base + threadIdx.x; x < end; x += kThreads) atomicAdd(&s_h[key32[x] & dmask], 1u);
+  __syncthreads();
+  if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
+}
+
 // One thread per command in (key, command) order, a 1024-command tile staged
 // in LDS with kSrchHalo neighbours on either side, unpacked: key, command and
 // the arrival position at each replica (kNoArr if the replica does not
@@ -1693,6 +1728,12 @@ struct EngineDevice {
   // 15.6, 1.5 per CU 16.9, 2.5 16.7, 3 16.1, 4 17.7, uncapped 16.8, no side
   // stream 17.2 (profiles/r05_side_sweep.txt).
   unsigned side_grid = 0;
+  // key-order path: the sort input produced inside the first scatter
+  // (PackSrc); FH_KO_PACK=0 (measurement) writes it with k_cmd_pack3 first
+  const bool pack_fused = [] {
+    const char *e = getenv("FH_KO_PACK");
+    return !(e && *e == '0');
+  }();
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   ScanWorkspace scan_ws2;
@@ -2342,14 +2383,23 @@ struct EngineDevice {
     const int db = sort_digit_bits(key_bits, 4);
     uint32_t *kwa = sk32a.ensure(n + 1);
     V3 *va = kv3a.ensure(n + 1);
-    probed_launch("cmd_pack", double(n) * (4.0 + 4.0 * fq + 4.0 + 4.0 + 12.0), k_cmd_pack3,
-                  dim3(tiles), dim3(kThreads), stream, n, cm, bkey, (const uint32_t *)rec,
-                  (const uint32_t *)(dot32.get() + b * size_t(n)), kwa, va,
-                  sort_ws.meta.get(), (1u << db) - 1);
     uint32_t *ks = nullptr;
     V3 *vs = nullptr;
-    sort_pairs_counted<uint32_t, V3>(kwa, va, sk32b.ensure(n + 1), kv3b.ensure(n + 1), n,
-                                     key_bits, sort_ws, stream, &ks, &vs, db);
+    if (pack_fused) {
+      k_key_counts<<<dim3(tiles), dim3(kThreads), 0, stream>>>(n, bkey, sort_ws.meta.get(),
+                                                               (1u << db) - 1);
+      const PackSrc src{cm, bkey, rec, dot32.get() + b * size_t(n)};
+      sort_pairs_counted_src<uint32_t, V3, PackSrc>(src, kwa, va, sk32b.ensure(n + 1),
+                                                    kv3b.ensure(n + 1), n, key_bits, sort_ws,
+                                                    stream, &ks, &vs, db);
+    } else {
+      probed_launch("cmd_pack", double(n) * (4.0 + 4.0 * fq + 4.0 + 4.0 + 12.0), k_cmd_pack3,
+                    dim3(tiles), dim3(kThreads), stream, n, cm, bkey, (const uint32_t *)rec,
+                    (const uint32_t *)(dot32.get() + b * size_t(n)), kwa, va,
+                    sort_ws.meta.get(), (1u << db) - 1);
+      sort_pairs_counted<uint32_t, V3>(kwa, va, sk32b.ensure(n + 1), kv3b.ensure(n + 1), n,
+                                       key_bits, sort_ws, stream, &ks, &vs, db);
+    }
     uint8_t *tm = tailm.ensure(n + 1);
     const size_t mwords = (size_t(n) + 3) / 4;
     uint32_t *mr = mrem.ensure(mwords);

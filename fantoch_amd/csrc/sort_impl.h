@@ -562,5 +562,29 @@ void sort_pairs_counted(K *ka, VT *va, K *kb, VT *vb, size_t n, int key_bits, So
                                vout, true);
 }
 
+// sort_pairs_counted with pass 0 reading `src` (whose tile digit counts the
+// caller wrote, as for sort_pairs_counted): the producer of the sort input is
+// folded into the first scatter; result in (ka, va) or (kb, vb).
+template <class K, class VT, class Src>
+void sort_pairs_counted_src(const Src &src, K *ka, VT *va, K *kb, VT *vb, size_t n, int key_bits,
+                            SortWorkspace &ws, hipStream_t s, K **kout, VT **vout, int db) {
+  FH_CHECK(n < (size_t(1) << 30), FH_EINVAL, "sort: too many elements (>= 2^30)");
+  const int passes = std::max(1, (key_bits + db - 1) / db);
+  if (n == 0) {
+    *kout = ka;
+    *vout = va;
+    return;
+  }
+  if (db == 6)
+    sort_passes<K, VT, 6, Src>(src, true, ka, va, kb, vb, false, n, passes, 6, ws, s, kout, vout,
+                               true);
+  else if (db == 7)
+    sort_passes<K, VT, 7, Src>(src, true, ka, va, kb, vb, false, n, passes, 7, ws, s, kout, vout,
+                               true);
+  else
+    sort_passes<K, VT, 8, Src>(src, true, ka, va, kb, vb, false, n, passes, 8, ws, s, kout, vout,
+                               true);
+}
+
 }  // namespace
 }  // namespace fh
