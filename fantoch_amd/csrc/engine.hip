@@ -1734,6 +1734,11 @@ struct EngineDevice {
     const char *e = getenv("FH_KO_PACK");
     return !(e && *e == '0');
   }();
+  // FH_TILE_PRIO=0 (measurement): the tile kernel's waves at normal priority
+  const bool tile_prio = [] {
+    const char *e = getenv("FH_TILE_PRIO");
+    return !(e && *e == '0');
+  }();
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   ScanWorkspace scan_ws2;
@@ -2493,6 +2498,7 @@ struct EngineDevice {
     gin.dst = pe8;
     gin.dst_codes = true;
     gin.dst_esc = pcode;
+    gin.tile_prio = !side_off && tile_prio;
     gin.dot32 = pd32;
     gin.dot32_sb = sb;
     gin.k = 1;

@@ -80,6 +80,7 @@ struct GraphInput {
                            // distances (byte s: v - target, 0 none, -128:
                            // target + 1 in dst_esc[v·stride + s])
   const uint32_t *dst_esc = nullptr;
+  bool tile_prio = false;  // tile kernel waves at raised issue priority
   const uint32_t *dot32 = nullptr;
   int dot32_sb = 0;
   bool tiles_only = false;

@@ -152,6 +152,7 @@ struct TileOut {
   const uint32_t *dot32 = nullptr;
   int dot_sb = 0;
   const uint32_t *esc = nullptr;  // codes: escaped targets (GraphInput::dst_esc)
+  bool prio = false;              // raise the waves' issue priority
   // key-order outputs (GraphInput::ko_seq; the engine's key-order path):
   // each core vertex writes its dot at its key-order execution position
   // (the per-key sequence), and a vertex of a multi-member ready group its
@@ -194,6 +195,9 @@ __global__ void __launch_bounds__(kTileThreads)
   __shared__ uint32_t s_fail, s_maxex, s_over, s_long;
 
   const int tid = threadIdx.x;
+  // issue priority over co-resident waves (the engine's key-order path runs
+  // its command-order kernels on a side stream beside this one)
+  if (out.prio) __builtin_amdgcn_s_setprio(3);
   uint64_t t_last = wall_clock64();
   auto phase = [&](int i) {  // after a barrier: thread 0 accounts the phase
     if (out.prof && tid == 0) {
@@ -820,6 +824,7 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.failf = nullptr;
   to.codes = in.dst_codes;
   to.esc = in.dst_esc;
+  to.prio = in.tile_prio;
   to.dot32 = in.dot32;
   to.dot_sb = in.dot32_sb;
   to.ko_seq = in.ko_seq;
