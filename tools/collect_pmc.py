@@ -37,6 +37,15 @@ PROBES = {
     "sort_scatter": r"k_down<unsigned int, unsigned int,",
     "sort_scatter_dots": r"k_down<unsigned int, unsigned long,",
     "sort_scatter_u64": r"k_down<unsigned long, unsigned int,",
+    # the key-order path (round 5): V3 values, pass 0 reading through PackSrc
+    "sort_scatter_v3": r"k_down<unsigned int, fh::(anonymous namespace)::V3, 7, fh::(anonymous namespace)::ArraySrc",
+    "sort_scatter_v3_pack": r"k_down<unsigned int, fh::(anonymous namespace)::V3, 7, fh::(anonymous namespace)::PackSrc",
+    "code_scatter": r"k_code_scatter<",
+    "region_count": r"k_region_count<",
+    "row_count": r"k_row_count<",
+    "row_union": r"k_row_union<",
+    "ko_final": r"k_ko_final",
+    "key_counts": r"k_key_counts",
     "sort_up": r"k_up<",
     "graph_tile": r"k_graph_tile<",
     "prev_bucket": r"k_bucket_codes",
