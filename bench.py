@@ -406,7 +406,10 @@ def c5_dist_line(args, rank, world, local, group):
             "ms_per_step": round(el / steps * 1e3, 3), "commands_per_s": v, "scaling": "strong",
             "parallelism": f"KeyDeps by key shard x{world}; union + SCC by stream range x{world}",
             "backend": dist.get_backend(group), "generate_s": round(t_gen, 2),
-            "stage_s": round(t_stage, 2), "rank0_stage_ms": stage_ms}
+            "stage_s": round(t_stage, 2), "rank0_stage_ms": stage_ms,
+            # the graph every rank solves in step 4 (replicated work)
+            "condensed_graph": {"super_vertices": int(p.condensed[0]),
+                                "edges": int(p.condensed[1])}}
 
 
 def streaming_line():

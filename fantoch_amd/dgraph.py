@@ -11,8 +11,9 @@ Per step (DistPartial.run):
      MShardCommit, atlas.rs:559-639), cuts the cross-range edges and runs
      the local SCCs; vertices reaching a cross-range edge are contracted.
   3. all-to-all of cross-range queries and the owners' answers.
-  4. all-gather of every rank's part of the condensed graph; every rank
-     solves it (SCCs, ready times, depths of the escaping vertices).
+  4. all-gather of every rank's part of the condensed graph (vertices and
+     edges in one exchange); every rank solves it (SCCs, ready times,
+     depths of the escaping vertices).
   5. all-to-all of the (key, order) elements to the keys' owners, sorted
      there into the per-key execution sequences.
 The reference reaches other shards' vertices one request / reply at a time
@@ -205,19 +206,32 @@ class Exchange:
                                     group=self.group)
         return self._back(out, x)
 
-    def gather(self, x):
-        src = self._comm(x)
-        n = self.torch.tensor([len(src)], dtype=self.torch.int64, device=src.device)
+    def gather(self, *xs):
+        """all-gather of several 1-D tensors of one dtype in one exchange:
+        one all-gather of the sizes (read back once) and one of the
+        concatenated parts -> every rank's parts, concatenated per tensor."""
+        srcs = [self._comm(x) for x in xs]
+        dev = srcs[0].device
+        n = self.torch.tensor([len(t) for t in srcs], dtype=self.torch.int64, device=dev)
         sizes = [self.torch.zeros_like(n) for _ in range(self.world)]
         self.dist.all_gather(sizes, n, group=self.group)
-        sizes = [int(v.item()) for v in sizes]
-        mx = max(1, max(sizes))
-        buf = self.torch.zeros(mx, dtype=src.dtype, device=src.device)
-        buf[:len(src)] = src
+        sizes = self.torch.stack(sizes).cpu().tolist()  # [rank][tensor]
+        mx = max(1, max(sum(r) for r in sizes))
+        buf = self.torch.zeros(mx, dtype=srcs[0].dtype, device=dev)
+        o = 0
+        for t in srcs:
+            buf[o:o + len(t)] = t
+            o += len(t)
         bufs = [self.torch.zeros_like(buf) for _ in range(self.world)]
         self.dist.all_gather(bufs, buf, group=self.group)
-        out = self.torch.cat([b[:m] for b, m in zip(bufs, sizes)])
-        return self._back(out, x)
+        outs = []
+        for i, x in enumerate(xs):
+            parts = []
+            for b, r in zip(bufs, sizes):
+                o = sum(r[:i])
+                parts.append(b[o:o + r[i]])
+            outs.append(self._back(self.torch.cat(parts), x))
+        return outs[0] if len(xs) == 1 else outs
 
 
 class DistPartial:
@@ -251,8 +265,9 @@ class DistPartial:
         ans = st.answer(incoming)
         answers = ex.a2a(ans, qin, qc)
         verts, edges = st.condense(answers)
-        vg = ex.gather(verts)
-        eg = ex.gather(edges)
+        vg, eg = ex.gather(verts, edges)
+        # the condensed graph every rank solves (super vertices, edges)
+        self.condensed = (len(vg) // 2, len(eg))
         ec, elems = st.solve(vg, eg)
         ein = ex.counts(ec)
         mine = ex.a2a(elems, 2 * ec, 2 * ein)
