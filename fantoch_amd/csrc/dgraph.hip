@@ -248,11 +248,13 @@ __global__ void k_ckeys_super(uint32_t nv, const uint64_t *__restrict__ verts,
     sid[i] = uint32_t(verts[2 * size_t(i)] >> 32);
   }
 }
+// (non-marker edges get `fill`, above every key: the sort then needs only
+// the keys' bits, not 64)
 __global__ void k_ckeys_marker(uint32_t ne, const uint64_t *__restrict__ edges,
-                               uint64_t *__restrict__ keys) {
+                               uint64_t *__restrict__ keys, uint64_t fill) {
   GRID_STRIDE(i, ne) {
     const uint32_t t = uint32_t(edges[i]);
-    keys[i] = (t & kMarker) ? ((uint64_t(t & ~kMarker) << 1) | 1u) : ~0ull;
+    keys[i] = (t & kMarker) ? ((uint64_t(t & ~kMarker) << 1) | 1u) : fill;
   }
 }
 // super vertex i (in sid order) -> its condensed vid
@@ -272,7 +274,7 @@ __global__ void k_sid_vid(uint32_t nv, const uint64_t *__restrict__ verts,
 __global__ void k_fill_u64(uint32_t n, uint64_t *p, uint64_t v) { GRID_STRIDE(i, n) p[i] = v; }
 __global__ void k_cedges(uint32_t ne, const uint64_t *__restrict__ edges,
                          const uint32_t *__restrict__ sids, const uint32_t *__restrict__ vid,
-                         uint32_t nv, const uint64_t *__restrict__ ck, uint32_t ncv,
+                         uint32_t nv, const uint64_t *__restrict__ ck, uint32_t ncv, int cb,
                          uint64_t *__restrict__ out) {
   GRID_STRIDE(i, ne) {
     const uint64_t e = edges[i];
@@ -280,14 +282,16 @@ __global__ void k_cedges(uint32_t ne, const uint64_t *__restrict__ edges,
     const uint32_t t = uint32_t(e);
     const uint32_t d = (t & kMarker) ? lower_bound_dev(ck, ncv, (uint64_t(t & ~kMarker) << 1) | 1u)
                                      : vid[lower_bound_dev(sids, nv, t)];
-    out[i] = (uint64_t(s) << 32) | d;
+    out[i] = (uint64_t(s) << cb) | d;
   }
 }
-__global__ void k_csr_counts(uint32_t ne, const uint64_t *__restrict__ e, uint32_t *__restrict__ cnt) {
-  GRID_STRIDE(i, ne) atomicAdd(&cnt[uint32_t(e[i] >> 32)], 1u);
+__global__ void k_csr_counts(uint32_t ne, const uint64_t *__restrict__ e, int cb,
+                             uint32_t *__restrict__ cnt) {
+  GRID_STRIDE(i, ne) atomicAdd(&cnt[uint32_t(e[i] >> cb)], 1u);
 }
-__global__ void k_csr_dst(uint32_t ne, const uint64_t *__restrict__ e, uint32_t *__restrict__ dst) {
-  GRID_STRIDE(i, ne) dst[i] = uint32_t(e[i]);
+__global__ void k_csr_dst(uint32_t ne, const uint64_t *__restrict__ e, int cb,
+                          uint32_t *__restrict__ dst) {
+  GRID_STRIDE(i, ne) dst[i] = uint32_t(e[i] & ((uint64_t(1) << cb) - 1));
 }
 
 // ---- expansion and per-key elements ----------------------------------------
@@ -696,15 +700,18 @@ struct DistGraph {
     uint64_t *kk = ck.ensure(size_t(nv) + ne + 1);
     uint32_t *sid = csid.ensure(nv + 1);
     if (nv) k_ckeys_super<<<grid_for(nv, B), B, 0, stream>>>(nv, vg, kk, sid);
-    if (ne) k_ckeys_marker<<<grid_for(ne, B), B, 0, stream>>>(ne, eg, kk + nv);
+    // keys: positions (< n) << 1 | marker bit, the filler above them all
+    const int kbits = bits_for(uint64_t(n) + 1) + 2;
+    const uint64_t fill = (uint64_t(1) << kbits) - 1;
+    if (ne) k_ckeys_marker<<<grid_for(ne, B), B, 0, stream>>>(ne, eg, kk + nv, fill);
     uint64_t *cks = nullptr;
-    uint32_t ncv = sort_unique_u64(ck, ck2, nv + ne, 64, &cks);
-    // drop the ~0 filler (non-marker edges) at the end
+    uint32_t ncv = sort_unique_u64(ck, ck2, nv + ne, kbits, &cks);
+    // drop the filler (non-marker edges) at the end
     if (ncv) {
       uint64_t last = 0;
       FH_HIP(hipMemcpyAsync(&last, cks + ncv - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
       sync();
-      if (last == ~0ull) ncv--;
+      if (last == fill) ncv--;
     }
     // super vertices by sid -> condensed vid; their labels as the vertex dots
     uint32_t *idx = cidx.ensure(nv + 1), *vid = cvid.ensure(nv + 1);
@@ -723,15 +730,17 @@ struct DistGraph {
     }
     // edges -> (src vid, dst vid), sorted unique -> CSR
     uint64_t *ed = ce.ensure(ne + 1);
-    if (ne) k_cedges<<<grid_for(ne, B), B, 0, stream>>>(ne, eg, sids, vid, nv, cks, ncv, ed);
+    // edges (src vid << cb | dst vid): 2·cb key bits
+    const int cb = bits_for(uint64_t(ncv) + 1);
+    if (ne) k_cedges<<<grid_for(ne, B), B, 0, stream>>>(ne, eg, sids, vid, nv, cks, ncv, cb, ed);
     uint64_t *eds = nullptr;
-    const uint32_t nce = sort_unique_u64(ce, ce2, ne, 64, &eds);
+    const uint32_t nce = sort_unique_u64(ce, ce2, ne, 2 * cb, &eds);
     uint32_t *cc = ccnt.ensure(ncv + 1), *co = coffs.ensure(ncv + 1);
     FH_HIP(hipMemsetAsync(cc, 0, size_t(ncv + 1) * sizeof(uint32_t), stream));
-    if (nce) k_csr_counts<<<grid_for(nce, B), B, 0, stream>>>(nce, eds, cc);
+    if (nce) k_csr_counts<<<grid_for(nce, B), B, 0, stream>>>(nce, eds, cb, cc);
     exclusive_scan_u32(cc, co, ncv, scan_ws, stream);
     uint32_t *cdst_ = cdst2.ensure(nce + 1);
-    if (nce) k_csr_dst<<<grid_for(nce, B), B, 0, stream>>>(nce, eds, cdst_);
+    if (nce) k_csr_dst<<<grid_for(nce, B), B, 0, stream>>>(nce, eds, cb, cdst_);
     GraphInput gin;
     gin.V = ncv;
     gin.off = co;

@@ -581,9 +581,9 @@ __global__ void __launch_bounds__(kThreads)
 // replica bits per sorted position, atomic OR); k_cmd_tails combines both.
 //
 // Codes: with `rec` set (fq <= 3), each command's (command, codes) record is
-// written into the tile's slice of `rec` grouped by command region (c >>
-// kRegShift; offsets per tile in `toff`), and k_code_scatter moves the
-// records region by region, so the scattered code stores of a moment stay in
+// written into its command region's slice of `rec` (c >> kRegShift; the
+// tile's run of each region claimed from the region's cursor `rcur`), and
+// k_code_scatter moves the records region by region, so the scattered code stores of a moment stay in
 // a cache-sized slice of the code array (a random 12-B store per command over
 // the whole array ran at 4.6 ms per 100M commands, confined to 4M-command
 // regions at 1.7 ms: tools/scatter_bench.hip, profiles/r05_scatter_bench.jsonl).
@@ -633,7 +633,7 @@ __global__ void __launch_bounds__(TH)
     k_cmd_search(uint32_t n, CmdMeta cm, uint32_t K, uint32_t np, const uint32_t *__restrict__ kws,
                  const VS *__restrict__ vals, const uint64_t *__restrict__ latest,
                  uint32_t *__restrict__ code, uint4 *__restrict__ rec,
-                 const uint32_t *__restrict__ roff, uint8_t *__restrict__ tailm,
+                 uint32_t *__restrict__ rcur, uint8_t *__restrict__ tailm,
                  uint32_t *__restrict__ mrem, uint32_t *__restrict__ pcode,
                  uint32_t *__restrict__ pd32, uint32_t *__restrict__ pe8) {
   constexpr int kSpan = TH + 2 * kSrchHalo;
@@ -641,7 +641,7 @@ __global__ void __launch_bounds__(TH)
   __shared__ uint32_t s_q[kSpan * kSrchMaxRep];
   __shared__ uint32_t s_d[KO ? kSpan : 1];
   __shared__ uint8_t s_mark[TH * kSrchMaxRep];
-  __shared__ uint32_t s_reg[kMaxRegions];
+  __shared__ uint32_t s_reg[kMaxRegions], s_rb[kMaxRegions];
   const uint32_t tid = threadIdx.x, core = blockIdx.x * TH, i = core + tid;
   const uint32_t lo = core > uint32_t(kSrchHalo) ? core - kSrchHalo : 0u;
   const uint32_t hi = min(n, core + TH + kSrchHalo);
@@ -661,7 +661,19 @@ __global__ void __launch_bounds__(TH)
 #pragma unroll
     for (uint32_t j = 0; j < FQ; j++) s_q[x * np + cm.rep(m, j)] = cm.arr(m, j) << qs;
   }
+  // the command's slot among the tile's records of its region (rec mode)
+  uint32_t reg = 0, rank = 0;
+  if (rec && i < n) {
+    reg = uint32_t(vload(vals, i) & cm.cmask) >> kRegShift;
+    rank = atomicAdd(&s_reg[reg], 1u);
+  }
   __syncthreads();
+  // Region r's records fill rec[r << kRegShift, ...) exactly (a region holds
+  // 2^kRegShift commands), in any order: the tile claims its run of each
+  // region from the region's cursor, one atomic per (tile, region), issued
+  // now and read after the scans' barrier
+  if (rec && tid < uint32_t(kMaxRegions) && s_reg[tid])
+    s_rb[tid] = (tid << kRegShift) + atomicAdd(&rcur[tid], s_reg[tid]);
   const bool act = i < n;
   const uint32_t me = i - lo;
   const uint32_t W = cm.W, H = uint32_t(cm.qmask >> 1) << qs;
@@ -753,7 +765,6 @@ __global__ void __launch_bounds__(TH)
   }
   __syncthreads();
   uint32_t cds[FQ];
-  uint32_t reg = 0, rank = 0;
   if (act) {
     uint32_t msk = 0, e8 = 0;
 #pragma unroll
@@ -784,10 +795,7 @@ __global__ void __launch_bounds__(TH)
       pd32[i] = s_d[me];
       pe8[i] = e8;
     }
-    if (rec) {
-      reg = c >> kRegShift;
-      rank = atomicAdd(&s_reg[reg], 1u);
-    } else {
+    if (!rec) {
       uint32_t *o = code + size_t(c) * FQ;
       if constexpr (FQ == 4) {
         *reinterpret_cast<uint4 *>(o) = make_uint4(cds[0], cds[1], cds[2], cds[3]);
@@ -799,36 +807,11 @@ __global__ void __launch_bounds__(TH)
   }
   if (!rec) return;  // uniform over the grid
   if (act) {
-    // roff[r * tiles + t]: the first record of tile t in region r
-    // (k_region_count + scan), so each region's records are contiguous
     uint4 o = make_uint4(c, 0u, 0u, 0u);
     if constexpr (FQ >= 1) o.y = cds[0];
     if constexpr (FQ >= 2) o.z = cds[1];
     if constexpr (FQ >= 3) o.w = cds[2];
-    rec[roff[size_t(reg) * gridDim.x + blockIdx.x] + rank] = o;
-  }
-}
-
-// Commands per (region, search tile) from the sorted values, region-major
-// (counts[r * tiles + t]) so that one exclusive scan gives every tile its
-// first record in its region's contiguous slice.
-template <class VS>
-__global__ void __launch_bounds__(1024)
-    k_region_count(uint32_t n, uint64_t cmask, uint32_t nreg, const VS *__restrict__ vals,
-                   uint32_t *__restrict__ counts) {
-  // per-wave counters: a wave's 64 lanes meet on ~24 regions, not the
-  // block's 1024 on the same 24
-  __shared__ uint32_t s_h[16][kMaxRegions];
-  const uint32_t tid = threadIdx.x, i = blockIdx.x * 1024 + tid, w = tid >> 6;
-  if (tid < 16 * kMaxRegions) (&s_h[0][0])[tid] = 0;
-  __syncthreads();
-  if (i < n) atomicAdd(&s_h[w][uint32_t(vload(vals, i) & cmask) >> kRegShift], 1u);
-  __syncthreads();
-  if (tid < nreg) {
-    uint32_t t = 0;
-#pragma unroll
-    for (int q = 0; q < 16; q++) t += s_h[q][tid];
-    counts[size_t(tid) * gridDim.x + blockIdx.x] = t;
+    rec[s_rb[reg] + rank] = o;
   }
 }
 
@@ -1684,7 +1667,7 @@ struct EngineDevice {
   DBuf<uint8_t> tailm;        // command-level views path: tail views per sorted command
   DBuf<uint32_t> mrem;        // command-level views path: predecessor marks across tiles
   DBuf<uint4> crec;           // command-level views path: (command, codes) by tile and region
-  DBuf<uint32_t> ctoff;       // command-level views path: records per (region, tile), offsets
+  DBuf<uint32_t> ctoff;       // command-level views path: region cursors
   // key-order path (cmd_views_keyorder)
   bool ko_done = false;       // this run's outputs came from the key-order path
   DBuf<V3> kv3a, kv3b;        // sort values with packed dots
@@ -2413,11 +2396,8 @@ struct EngineDevice {
     const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> kRegShift) + 1;
     FH_CHECK(nreg <= kMaxRegions, FH_EINVARIANT, "command regions");
     uint4 *rec4 = crec.ensure(size_t(n) + 1);
-    const size_t nc = size_t(stiles) * nreg;
-    uint32_t *cnt = ctoff.ensure(2 * nc + 2);
-    uint32_t *roff = cnt + nc + 1;
-    k_region_count<V3><<<dim3(stiles), dim3(1024), 0, stream>>>(n, cm.cmask, nreg, vs, cnt);
-    exclusive_scan_u32(cnt, roff, nc, scan_ws, stream);
+    uint32_t *rcur = ctoff.ensure(kMaxRegions);
+    FH_HIP(hipMemsetAsync(rcur, 0, kMaxRegions * sizeof(uint32_t), stream));
     uint32_t *pcode = kpcode.ensure(size_t(n) * fq + 1);
     uint32_t *pd32 = kpd32.ensure(n + 1);
     uint32_t *pe8 = kpe8.ensure(n + 1);
@@ -2427,8 +2407,7 @@ struct EngineDevice {
     auto go = [&](auto kern) {
       probed_launch("cmd_search", double(n) * (16.0 + 16.0 + 4.0 * fq + 4.0 + 1.0), kern,
                     dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np, (const uint32_t *)ks,
-                    (const V3 *)vs, lat, codes, rec4, (const uint32_t *)roff, tm, mr, pcode,
-                    pd32, pe8);
+                    (const V3 *)vs, lat, codes, rec4, rcur, tm, mr, pcode, pd32, pe8);
     };
     if (fq == 2)
       go(k_cmd_search<2, kSrchThreads, V3, true>);
@@ -2594,23 +2573,19 @@ struct EngineDevice {
     const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> kRegShift) + 1;
     FH_CHECK(nreg <= kMaxRegions, FH_EINVARIANT, "command regions");
     uint4 *rec4 = nullptr;
-    uint32_t *roff = nullptr;
+    uint32_t *rcur = nullptr;
     if (fq <= 3 && !region_off) {
       rec4 = crec.ensure(size_t(n) + 1);
-      const size_t nc = size_t(stiles) * nreg;
-      uint32_t *cnt = ctoff.ensure(2 * nc + 2);
-      roff = cnt + nc + 1;
-      k_region_count<uint64_t><<<dim3(stiles), dim3(1024), 0, stream>>>(n, cm.cmask, nreg, vs, cnt);
-      exclusive_scan_u32(cnt, roff, nc, scan_ws, stream);
+      rcur = ctoff.ensure(kMaxRegions);
+      FH_HIP(hipMemsetAsync(rcur, 0, kMaxRegions * sizeof(uint32_t), stream));
     }
     const double sb = double(n) * (12.0 + (rec4 ? 16.0 : fq * 4.0) + 1.0);
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
     auto go = [&](auto kern) {
       probed_launch("cmd_search", sb, kern, dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np,
-                    (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, rec4,
-                    (const uint32_t *)roff, tm, mr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                    (uint32_t *)nullptr);
+                    (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, rec4, rcur, tm, mr,
+                    (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr);
     };
     switch (fq) {
       case 1: go(k_cmd_search<1, kSrchThreads, uint64_t, false>); break;

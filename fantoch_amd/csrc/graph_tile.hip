@@ -51,7 +51,7 @@ namespace {
 constexpr int kTileThreads = 1024;
 constexpr int kTileC = 10240;  // max context vertices (LDS: 15 B per vertex)
 constexpr uint16_t kNone = 0xFFFF;
-constexpr int kMaxCore = 8;     // core vertices per thread (T <= 8192)
+constexpr int kMaxCore = 10;    // core vertices per thread (T <= 10240)
 constexpr uint32_t kMixR1 = 512;  // pass-1 reach bound of the mixed tiling
 
 // R0 rounded up to a multiple of 64 (at least 256)
@@ -702,6 +702,16 @@ __global__ void k_exec_from_groups(uint32_t V, const uint32_t *__restrict__ hgrp
 
 }  // namespace
 
+// the core cap (FH_TILE_CORE, measurement; default kMaxCore · kTileThreads)
+static int tile_core_cap() {
+  static const int cap = [] {
+    const char *e = getenv("FH_TILE_CORE");
+    const int c = e ? atoi(e) : kMaxCore * kTileThreads;
+    return std::max(1024, std::min(c, kMaxCore * kTileThreads));
+  }();
+  return cap;
+}
+
 static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint64_t *dot,
                          const TileOut &to, hipStream_t stream, uint32_t ncores = 0,
                          bool count_bytes = true) {
@@ -777,7 +787,7 @@ bool GraphCore::tiles_mixed(const GraphInput &in, TileOut &to, uint32_t r2, uint
     if (hf[t])
       for (int d = -1; d <= 1; d++)
         if (int64_t(t) + d >= 0 && int64_t(t) + d < int64_t(tiles1)) redo[t + d] = 1;
-  const uint32_t t2 = uint32_t(std::min(kTileC - 4 * int(r2), kMaxCore * kTileThreads));
+  const uint32_t t2 = uint32_t(std::min(kTileC - 4 * int(r2), tile_core_cap()));
   std::vector<uint32_t> cores;
   for (uint32_t t = 0; t < tiles1;) {
     if (!redo[t]) {
@@ -861,7 +871,7 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   }
   for (int attempt = 0; attempt < 4 && !ok; attempt++) {
     to.r0 = int(r0);
-    to.core = std::min(kTileC - 4 * int(r0), kMaxCore * kTileThreads);
+    to.core = std::min(kTileC - 4 * int(r0), tile_core_cap());
     FH_HIP(hipMemsetAsync(stat, 0, 7 * sizeof(uint32_t), stream));
     if (to.prof) FH_HIP(hipMemsetAsync(to.prof, 0, 8 * sizeof(unsigned long long), stream));
     launch_tiles(V, in.stride, in.dst, in.dot, to, stream);
