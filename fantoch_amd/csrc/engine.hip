@@ -495,41 +495,12 @@ __global__ void __launch_bounds__(kThreads)
   if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
 }
 
-// k_cmd_pack with the command's packed dot beside the value (key-order path)
-__global__ void __launch_bounds__(kThreads)
-    k_cmd_pack3(uint32_t n, CmdMeta cm, const uint32_t *__restrict__ key32,
-                const uint32_t *__restrict__ rec, const uint32_t *__restrict__ dot32,
-                uint32_t *__restrict__ kw, V3 *__restrict__ val, uint32_t *__restrict__ counts,
-                uint32_t dmask) {
-  __shared__ uint32_t s_h[256];
-  s_h[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(n, base + uint32_t(kTile));
-  for (uint32_t x = base + threadIdx.x; x < end; x += kThreads) {
-    const uint32_t key = key32[x];
-    uint64_t m = 0;
-    for (uint32_t j = 0; j < cm.fq; j++) {
-      const uint32_t r = rec[size_t(x) * cm.fq + j];
-      m |= ((uint64_t(r >> kRecT) << cm.qb) | (r & cm.qmask)) << (j * cm.vb);
-    }
-    const uint64_t v = uint64_t(x) | (m << cm.cb);
-    V3 o;
-    o.x = uint32_t(v);
-    o.y = uint32_t(v >> 32);
-    o.z = dot32[x];
-    val[x] = o;
-    kw[x] = key | uint32_t((m >> (64 - cm.cb)) << cm.kb);
-    atomicAdd(&s_h[key & dmask], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x <= dmask) counts[size_t(blockIdx.x) * (dmask + 1) + threadIdx.x] = s_h[threadIdx.x];
-}
-
 // The key-order path's sort input, produced inside the sort's first scatter
-// (sort_pairs_counted_src): element x's key word and V3 value as k_cmd_pack3
-// writes them, computed from the command's key, view records and packed dot
-// as the scatter loads the element (the packed arrays are never written:
-// 2 x 16 B per command less traffic).  k_key_counts writes the tile digit
+// (sort_pairs_counted_src): element x's key word (as k_cmd_pack packs it)
+// and V3 value (k_cmd_pack's u64 and the command's packed dot), computed from
+// the command's key, view records and packed dot as the scatter loads the
+// element (the packed arrays are never written: 2 x 16 B per command less
+// traffic).  k_key_counts writes the tile digit
 // counts of that first pass.
 struct PackSrc {
   CmdMeta cm;
@@ -1704,24 +1675,12 @@ struct EngineDevice {
     const char *e = getenv("FH_KO_SIDE");
     return e && *e == '0';
   }();
-  // Workgroups of the side kernels (FH_KO_SIDE_GRID, measurement; 0: one per
-  // 256 items): two 256-thread workgroups per CU.  The tile kernel holds one
-  // 16-wave workgroup per CU (its LDS), so 8 side waves leave room for the
-  // next tile's workgroup as soon as one retires.  C4, ms per step: 2 per CU
-  // 15.6, 1.5 per CU 16.9, 2.5 16.7, 3 16.1, 4 17.7, uncapped 16.8, no side
-  // stream 17.2 (profiles/r05_side_sweep.txt).
+  // Workgroups of the side kernels: two 256-thread workgroups per CU.  The
+  // tile kernel holds one 16-wave workgroup per CU (its LDS), so 8 side waves
+  // leave room for the next tile's workgroup as soon as one retires.  C4, ms
+  // per step: 2 per CU 15.6, 1.5 per CU 16.9, 2.5 16.7, 3 16.1, 4 17.7,
+  // uncapped 16.8, no side stream 17.2 (profiles/r05_side_sweep.txt).
   unsigned side_grid = 0;
-  // key-order path: the sort input produced inside the first scatter
-  // (PackSrc); FH_KO_PACK=0 (measurement) writes it with k_cmd_pack3 first
-  const bool pack_fused = [] {
-    const char *e = getenv("FH_KO_PACK");
-    return !(e && *e == '0');
-  }();
-  // FH_TILE_PRIO=0 (measurement): the tile kernel's waves at normal priority
-  const bool tile_prio = [] {
-    const char *e = getenv("FH_TILE_PRIO");
-    return !(e && *e == '0');
-  }();
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   ScanWorkspace scan_ws2;
@@ -1772,8 +1731,7 @@ struct EngineDevice {
     {
       int cus = 0;
       FH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-      const char *e = getenv("FH_KO_SIDE_GRID");
-      side_grid = e ? unsigned(atoi(e)) : 2u * unsigned(std::max(cus, 1));
+      side_grid = 2u * unsigned(std::max(cus, 1));
     }
     FH_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     FH_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
@@ -2373,21 +2331,14 @@ struct EngineDevice {
     V3 *va = kv3a.ensure(n + 1);
     uint32_t *ks = nullptr;
     V3 *vs = nullptr;
-    if (pack_fused) {
-      k_key_counts<<<dim3(tiles), dim3(kThreads), 0, stream>>>(n, bkey, sort_ws.meta.get(),
-                                                               (1u << db) - 1);
-      const PackSrc src{cm, bkey, rec, dot32.get() + b * size_t(n)};
-      sort_pairs_counted_src<uint32_t, V3, PackSrc>(src, kwa, va, sk32b.ensure(n + 1),
-                                                    kv3b.ensure(n + 1), n, key_bits, sort_ws,
-                                                    stream, &ks, &vs, db);
-    } else {
-      probed_launch("cmd_pack", double(n) * (4.0 + 4.0 * fq + 4.0 + 4.0 + 12.0), k_cmd_pack3,
-                    dim3(tiles), dim3(kThreads), stream, n, cm, bkey, (const uint32_t *)rec,
-                    (const uint32_t *)(dot32.get() + b * size_t(n)), kwa, va,
-                    sort_ws.meta.get(), (1u << db) - 1);
-      sort_pairs_counted<uint32_t, V3>(kwa, va, sk32b.ensure(n + 1), kv3b.ensure(n + 1), n,
-                                       key_bits, sort_ws, stream, &ks, &vs, db);
-    }
+    // (k_cmd_pack3 writing the packed arrays, then the sort: 724 + 864 against
+    // 1226 us per C4 step for the first pass producing its own input, r05r)
+    k_key_counts<<<dim3(tiles), dim3(kThreads), 0, stream>>>(n, bkey, sort_ws.meta.get(),
+                                                             (1u << db) - 1);
+    const PackSrc src{cm, bkey, rec, dot32.get() + b * size_t(n)};
+    sort_pairs_counted_src<uint32_t, V3, PackSrc>(src, kwa, va, sk32b.ensure(n + 1),
+                                                  kv3b.ensure(n + 1), n, key_bits, sort_ws,
+                                                  stream, &ks, &vs, db);
     uint8_t *tm = tailm.ensure(n + 1);
     const size_t mwords = (size_t(n) + 3) / 4;
     uint32_t *mr = mrem.ensure(mwords);
@@ -2430,7 +2381,7 @@ struct EngineDevice {
       FH_HIP(hipEventRecord(ev_join, side));
       FH_HIP(hipStreamWaitEvent(stream, ev_join, 0));
     };
-    const unsigned sg = side_off || side_grid == 0 ? ~0u : side_grid;
+    const unsigned sg = side_off ? ~0u : side_grid;
     const dim3 gs(grid_for(n, B, std::min(sg, 1u << 30)));
     const dim3 gs8(grid_for(n, B, std::min(sg, 8192u)));
     if (fq == 2)
@@ -2477,7 +2428,8 @@ struct EngineDevice {
     gin.dst = pe8;
     gin.dst_codes = true;
     gin.dst_esc = pcode;
-    gin.tile_prio = !side_off && tile_prio;
+    // (C4: 14.91 against 14.94 ms at normal priority, r05u)
+    gin.tile_prio = !side_off;
     gin.dot32 = pd32;
     gin.dot32_sb = sb;
     gin.k = 1;
