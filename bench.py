@@ -99,6 +99,9 @@ def parse():
     ap.add_argument("--c5-backend", default="",
                     help="N > 1: exchange backend of the C5 leg (default: the process group's, "
                          "RCCL; gloo for a dry run of N ranks sharing one GPU)")
+    ap.add_argument("--c5-solo", action="store_true",
+                    help="dry runs: the C5 condense / solve stages one rank at a time, so their "
+                         "stage times are those of an unshared GPU (not a throughput run)")
     ap.add_argument("--no-cpu-sharded", action="store_true",
                     help="skip the key-sharded multi-process CPU baseline")
     return ap.parse_args()
@@ -358,6 +361,18 @@ def c5_line(args, local):
     return r
 
 
+def condensed_degrees(eg):
+    """Out-degree profile of the condensed graph's edge records (src << 32 |
+    target), for the solo measurement runs; {} otherwise."""
+    if eg is None or len(eg) == 0:
+        return {}
+    e = eg.cpu().numpy() if hasattr(eg, "cpu") else np.asarray(eg)
+    _, deg = np.unique((e.astype(np.uint64) >> np.uint64(32)), return_counts=True)
+    deg = np.sort(deg)[::-1]
+    return {"max_out_degree": int(deg[0]), "top8_out_degrees": [int(x) for x in deg[:8]],
+            "sources": int(len(deg))}
+
+
 def c5_dist_line(args, rank, world, local, group):
     """C5 across GPUs: fantoch_amd.dgraph.DistPartial -- KeyDeps by key shard
     (shard h on rank h % N), the per-command union and local SCCs by stream-
@@ -372,7 +387,8 @@ def c5_dist_line(args, rank, world, local, group):
     t_gen = time.perf_counter()
     s = c5_workload().generate(n, logs=True, times=False)
     t_gen = time.perf_counter() - t_gen
-    p = DistPartial(rank, world, s.key_space, group=group, device=local)
+    p = DistPartial(rank, world, s.key_space, group=group, device=local,
+                    solo=args.c5_solo)
     t_stage = time.perf_counter()
     p.stage(s)
     t_stage = time.perf_counter() - t_stage
@@ -409,7 +425,9 @@ def c5_dist_line(args, rank, world, local, group):
             "stage_s": round(t_stage, 2), "rank0_stage_ms": stage_ms,
             # the graph every rank solves in step 4 (replicated work)
             "condensed_graph": {"super_vertices": int(p.condensed[0]),
-                                "edges": int(p.condensed[1])}}
+                                "edges": int(p.condensed[1]),
+                                **condensed_degrees(p.condensed_eg)},
+            "solo_stages": bool(args.c5_solo)}
 
 
 def streaming_line():

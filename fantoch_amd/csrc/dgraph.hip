@@ -213,6 +213,28 @@ __global__ void k_cross_records(uint32_t m, uint32_t a, const uint32_t *__restri
   }
 }
 
+// The condensed edge records of this rank, sorted (src << 32 | target, a
+// marker target carrying kMarker | H): keep the first of each run of equal
+// records, and of a source's marker targets only the largest H.  Markers are
+// sinks keyed by ready time (a settled vertex never reaches an escaping
+// one), so a super vertex's ready time takes only their maximum, and its
+// depth counts only successors of its own ready group, which among markers
+// is at most the one with the largest H: the dropped edges change no output.
+// (A super vertex standing for a large local SCC otherwise carries one edge
+// per distinct settled ready time it reaches, which one thread of the solve
+// walks on every propagation launch.)
+__global__ void k_cond_flags(uint32_t m, const uint64_t *__restrict__ x, uint32_t *__restrict__ fl) {
+  GRID_STRIDE(i, m) {
+    const uint64_t v = x[i];
+    bool keep;
+    if (uint32_t(v) & kMarker)
+      keep = i + 1 == m || (x[i + 1] >> 32) != (v >> 32);
+    else
+      keep = i == 0 || x[i - 1] != v;
+    fl[i] = keep ? 1u : 0u;
+  }
+}
+
 // sorted u64 / u32 arrays: keep the first of each run
 template <class T>
 __global__ void k_first_flags(uint32_t m, const T *__restrict__ x, uint32_t *__restrict__ fl) {
@@ -272,6 +294,57 @@ __global__ void k_sid_vid(uint32_t nv, const uint64_t *__restrict__ verts,
   }
 }
 __global__ void k_fill_u64(uint32_t n, uint64_t *p, uint64_t v) { GRID_STRIDE(i, n) p[i] = v; }
+
+// ---- hub split of the condensed graph ---------------------------------------
+// A super vertex standing for a large local SCC can carry tens of thousands of
+// distinct out-edges (C5 at 8 ranges: up to 22.7K), which one thread of the
+// global path walks on every propagation launch.  Each such vertex x becomes
+// a group of ids base(x) .. base(x) + nax(x) holding kHubDeg of its edges each,
+// x itself last (the group's maximum id, so the class maximum -- the ready
+// time -- stays x), the others auxiliary with the largest dot (no label);
+// GraphInput::rep0 makes every group one class from the start, and the global
+// path works on classes: ready times, depths and the coloring see the
+// group's edges as x's.
+constexpr uint32_t kHubDeg = 256;  // FH_DGRAPH_HUB (a test switch) overrides
+__global__ void k_hub_aux(uint32_t ncv, uint32_t D, const uint32_t *__restrict__ cnt,
+                          uint32_t *__restrict__ nax) {
+  GRID_STRIDE(x, ncv) {
+    const uint32_t d = cnt[x];
+    nax[x] = d > D ? (d - 1) / D : 0u;
+  }
+}
+__global__ void k_hub_layout(uint32_t ncv, uint32_t D, const uint32_t *__restrict__ cnt,
+                             const uint32_t *__restrict__ nax, const uint32_t *__restrict__ aoff,
+                             const uint64_t *__restrict__ cd, const uint64_t *__restrict__ ck,
+                             uint32_t *__restrict__ cnt2, uint64_t *__restrict__ cd2,
+                             uint64_t *__restrict__ ck2, uint32_t *__restrict__ rep0,
+                             uint32_t *__restrict__ vmap) {
+  GRID_STRIDE(x, ncv) {
+    const uint32_t b = x + aoff[x], na = nax[x], d = cnt[x];
+    for (uint32_t j = 0; j <= na; j++) {
+      cnt2[b + j] = min(D, d - j * D);
+      cd2[b + j] = j == na ? cd[x] : ~0ull;
+      ck2[b + j] = ck[x];
+      rep0[b + j] = b;
+    }
+    vmap[x] = b + na;
+  }
+}
+// edges (sorted by source: co[x] = x's first) -> the split CSR, targets mapped
+__global__ void k_hub_edges(uint32_t nce, uint32_t D, const uint64_t *__restrict__ eds, int cb,
+                            const uint32_t *__restrict__ co, const uint32_t *__restrict__ aoff,
+                            const uint32_t *__restrict__ off2, const uint32_t *__restrict__ vmap,
+                            uint32_t *__restrict__ dst2) {
+  GRID_STRIDE(e, nce) {
+    const uint32_t x = uint32_t(eds[e] >> cb);
+    const uint32_t d = uint32_t(eds[e] & ((uint64_t(1) << cb) - 1));
+    const uint32_t k = e - co[x];
+    dst2[off2[x + aoff[x] + k / D] + k % D] = vmap[d];
+  }
+}
+__global__ void k_map_u32(uint32_t n, uint32_t *__restrict__ x, const uint32_t *__restrict__ m) {
+  GRID_STRIDE(i, n) x[i] = m[x[i]];
+}
 __global__ void k_cedges(uint32_t ne, const uint64_t *__restrict__ edges,
                          const uint32_t *__restrict__ sids, const uint32_t *__restrict__ vid,
                          uint32_t nv, const uint64_t *__restrict__ ck, uint32_t ncv, int cb,
@@ -421,6 +494,12 @@ struct DistGraph {
   // condensed solve
   DBuf<uint64_t> ck, ck2, ce, ce2, cdot;
   DBuf<uint32_t> csid, cvid, cidx, cidx2, coffs, cdst2, ccnt;
+  DBuf<uint32_t> hub_nax, hub_aoff, hub_cnt, hub_off, hub_rep0, hub_vmap, hub_dst;
+  const uint32_t hub_deg = [] {
+    const char *e = getenv("FH_DGRAPH_HUB");
+    return e && atoi(e) > 0 ? uint32_t(atoi(e)) : kHubDeg;
+  }();
+  DBuf<uint64_t> hub_dot, hub_ck;
   // elements
   std::vector<uint64_t> el_cnt;
   DBuf<uint32_t> el_cursor, el_base;
@@ -476,7 +555,7 @@ struct DistGraph {
   // sorted-unique of m u64 keys in place in (x, spare) -> returns the count;
   // *res = the buffer holding the result
   uint32_t sort_unique_u64(DBuf<uint64_t> &x, DBuf<uint64_t> &spare, uint32_t m, int bits,
-                           uint64_t **res) {
+                           uint64_t **res, bool cond_records = false) {
     if (m == 0) {
       *res = x.get();
       return 0;
@@ -489,7 +568,10 @@ struct DistGraph {
                                    stream, &ks, &vs);
     uint64_t *other = ks == x.get() ? spare.get() : x.get();
     uint32_t *fl = tmp_c.ensure(m + 1), *ps = tmp_d.ensure(m + 1);
-    k_first_flags<uint64_t><<<grid_for(m, B), B, 0, stream>>>(m, ks, fl);
+    if (cond_records)
+      k_cond_flags<<<grid_for(m, B), B, 0, stream>>>(m, ks, fl);
+    else
+      k_first_flags<uint64_t><<<grid_for(m, B), B, 0, stream>>>(m, ks, fl);
     const uint32_t u = scan_total(fl, ps, m);
     k_compact_by<uint64_t><<<grid_for(m, B), B, 0, stream>>>(m, ks, fl, ps, other);
     *res = other;
@@ -668,7 +750,7 @@ struct DistGraph {
       k_cross_records<<<grid_for(ncross_e, B), B, 0, stream>>>(ncross_e, a, csrc.get(), cdst.get(),
                                                                 lrep, queries.get(), nq, ans,
                                                                 ra + nl);
-    nrec = sort_unique_u64(rec_a, rec_b, tot, 64, &cond_edges);
+    nrec = sort_unique_u64(rec_a, rec_b, tot, 64, &cond_edges, true);
     // super vertices
     uint32_t *m = mx.ensure(V + 1);
     FH_HIP(hipMemsetAsync(m, 0, size_t(V) * sizeof(uint32_t), stream));
@@ -741,11 +823,39 @@ struct DistGraph {
     exclusive_scan_u32(cc, co, ncv, scan_ws, stream);
     uint32_t *cdst_ = cdst2.ensure(nce + 1);
     if (nce) k_csr_dst<<<grid_for(nce, B), B, 0, stream>>>(nce, eds, cb, cdst_);
+    // hub split (k_hub_aux above)
+    uint32_t V2 = ncv;
+    const uint32_t *off_g = co, *dst_g = cdst_, *rep0 = nullptr;
+    const uint64_t *dot_g = cd, *ck_g = cks;
+    if (nce && ncv) {
+      uint32_t *nax = hub_nax.ensure(ncv + 1), *aoff = hub_aoff.ensure(ncv + 1);
+      k_hub_aux<<<grid_for(ncv, B), B, 0, stream>>>(ncv, hub_deg, cc, nax);
+      const uint32_t na = scan_total(nax, aoff, ncv);
+      if (na) {
+        V2 = ncv + na;
+        uint32_t *cnt2 = hub_cnt.ensure(V2 + 1), *off2 = hub_off.ensure(V2 + 1);
+        uint32_t *r0 = hub_rep0.ensure(V2 + 1), *vm = hub_vmap.ensure(ncv + 1);
+        uint64_t *cd2 = hub_dot.ensure(V2 + 1), *ck2 = hub_ck.ensure(V2 + 1);
+        k_hub_layout<<<grid_for(ncv, B), B, 0, stream>>>(ncv, hub_deg, cc, nax, aoff, cd, cks, cnt2,
+                                                         cd2, ck2, r0, vm);
+        exclusive_scan_u32(cnt2, off2, V2, scan_ws, stream);
+        uint32_t *dst2 = hub_dst.ensure(nce + 1);
+        k_hub_edges<<<grid_for(nce, B), B, 0, stream>>>(nce, hub_deg, eds, cb, co, aoff, off2, vm,
+                                                         dst2);
+        if (nv) k_map_u32<<<grid_for(nv, B), B, 0, stream>>>(nv, vid, vm);
+        off_g = off2;
+        dst_g = dst2;
+        dot_g = cd2;
+        ck_g = ck2;
+        rep0 = r0;
+      }
+    }
     GraphInput gin;
-    gin.V = ncv;
-    gin.off = co;
-    gin.dst = cdst_;
-    gin.dot = cd;
+    gin.V = V2;
+    gin.off = off_g;
+    gin.dst = dst_g;
+    gin.dot = dot_g;
+    gin.rep0 = rep0;
     gin.global_only = true;
     gin.want_orders = false;
     gin.want_per_key = false;
@@ -758,7 +868,7 @@ struct DistGraph {
     uint32_t *err = scal.get() + 3;
     FH_HIP(hipMemsetAsync(err, 0, sizeof(uint32_t), stream));
     k_expand<<<grid_for(V, B), B, 0, stream>>>(V, a, lrep, esc.get(), lkap, llab, sids, vid, nv,
-                                               cout_.rep, cout_.kap, cout_.scc_label, cks,
+                                               cout_.rep, cout_.kap, cout_.scc_label, ck_g,
                                                okey.ensure(V + 1), label.ensure(V + 1), err);
     // elements by the key's owner: counts, then placement
     const ElemPack ep{k, hb, shards, world, seqb};

@@ -45,6 +45,10 @@ struct GraphInput {
   const uint32_t *dst = nullptr;     // [E] dependency vids (v itself = padding)
   const uint8_t *blocked0 = nullptr; // [V] or null: has a missing dependency
   const uint64_t *dot = nullptr;     // [V]
+  // [V] or null: an initial partition, each vertex's class root (the class's
+  // minimum vid); the global path treats its classes as strongly connected
+  // (dgraph's split hub vertices)
+  const uint32_t *rep0 = nullptr;
   // keys: fixed k per vertex (key_off == null) or CSR
   uint32_t k = 0;
   const uint32_t *key_off = nullptr; // [V+1] or null
@@ -175,6 +179,7 @@ struct GraphCore {
   uint32_t read_scalar(int i);
   void pending_closure(const GraphInput &in, GraphOutput &out);
   uint64_t count_forward(const GraphInput &in);
+  void init_rep(const GraphInput &in);
   void find_sccs(const GraphInput &in);
   void refresh_edge_rep(const GraphInput &in);
   bool order_kappa(const GraphInput &in, uint32_t max_iters, uint32_t &iters,

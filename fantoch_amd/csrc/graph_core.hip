@@ -984,9 +984,17 @@ uint64_t GraphCore::count_forward(const GraphInput &in) {
   return h;
 }
 
+void GraphCore::init_rep(const GraphInput &in) {
+  if (in.rep0)
+    FH_HIP(hipMemcpyAsync(rep.get(), in.rep0, size_t(in.V) * sizeof(uint32_t),
+                          hipMemcpyDeviceToDevice, stream));
+  else
+    k_iota<<<grid_for(in.V, B), B, 0, stream>>>(in.V, rep.get());
+}
+
 void GraphCore::find_sccs(const GraphInput &in) {
   const uint32_t V = in.V;
-  k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
+  init_rep(in);
   const uint32_t nwin = (V + 63) / 64;
   k_windows<<<(nwin + 3) / 4, 256, 0, stream>>>(V, in.off, in.stride, in.dst, blocked.get(), rep.get(), nwin,
                                                 int(in.blocked0 != nullptr));
@@ -1407,7 +1415,7 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   } else {
     nfwd = count_forward(in);
   }
-  if (nfwd == 0 && !any_blocked && in.sorted_keys && in.sorted_vid && in.want_orders) {
+  if (nfwd == 0 && !any_blocked && !in.rep0 && in.sorted_keys && in.sorted_vid && in.want_orders) {
     // every SCC is a singleton and the execution order is the arrival order:
     // nothing to materialise (rep[v] = v, label = own dot, rank = v)
     out.trivial = true;
@@ -1424,7 +1432,7 @@ void GraphCore::run(const GraphInput &in, GraphOutput &out) {
   if (nfwd) {
     find_sccs(in);
   } else {
-    k_iota<<<grid_for(V, B), B, 0, stream>>>(V, rep.get());
+    init_rep(in);
   }
   uint32_t iters = 0, iters1 = 0;
   hseed_ok = false;

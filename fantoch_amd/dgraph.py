@@ -238,8 +238,12 @@ class DistPartial:
     """One rank of the multi-GPU partial-replication pipeline."""
 
     def __init__(self, rank: int, world: int, key_space: int, group=None, device: int = 0,
-                 backend=None, n: int = 5):
+                 backend=None, n: int = 5, solo: bool = False):
+        """solo (measurement, for N ranks sharing one GPU): the condense and
+        solve stages run one rank at a time between barriers, so their stage
+        times are those of a GPU of their own."""
         self.rank, self.world = rank, world
+        self.solo = solo
         self.stages = backend if backend is not None else HipStages(rank, world, key_space, device, n)
         dev = None
         if isinstance(self.stages, HipStages):
@@ -264,15 +268,26 @@ class DistPartial:
         incoming = ex.a2a(q, qc, qin)
         ans = st.answer(incoming)
         answers = ex.a2a(ans, qin, qc)
-        verts, edges = st.condense(answers)
+        verts, edges = self._solo(lambda: st.condense(answers))
         vg, eg = ex.gather(verts, edges)
         # the condensed graph every rank solves (super vertices, edges)
         self.condensed = (len(vg) // 2, len(eg))
-        ec, elems = st.solve(vg, eg)
+        self.condensed_eg = eg if self.solo else None  # (measurement runs)
+        ec, elems = self._solo(lambda: st.solve(vg, eg))
         ein = ex.counts(ec)
         mine = ex.a2a(elems, 2 * ec, 2 * ein)
         st.per_key(mine)
         return time.perf_counter() - t0
+
+    def _solo(self, fn):
+        if not self.solo:
+            return fn()
+        out = None
+        for q in range(self.world):
+            if q == self.rank:
+                out = fn()
+            self.ex.dist.barrier(group=self.ex.group)
+        return out
 
     def results(self):
         """(first command, committed deps + SCC labels of the range, per-key

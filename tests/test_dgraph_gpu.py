@@ -30,8 +30,10 @@ def make_stream(n, seed, keys, k=4, shards=8):
     return w.generate(n, logs=True)
 
 
-def _worker(rank, world, port, n, seed, keys, q, pre=None):
+def _worker(rank, world, port, n, seed, keys, q, pre=None, hub=None):
     sys.path.insert(0, ROOT)
+    if hub is not None:  # split condensed vertices above `hub` out-edges
+        os.environ["FH_DGRAPH_HUB"] = hub
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -61,11 +63,11 @@ def _worker(rank, world, port, n, seed, keys, q, pre=None):
     dist.destroy_process_group()
 
 
-def run_ranks(world, n, seed, keys, pre=None):
+def run_ranks(world, n, seed, keys, pre=None, hub=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, keys, q, pre))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, keys, q, pre, hub))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -76,17 +78,21 @@ def run_ranks(world, n, seed, keys, pre=None):
     return parts
 
 
-@pytest.mark.parametrize("world,n,seed,keys,pre", [(1, 6000, 71, 4096, None),
-                                                   (2, 8000, 72, 4096, None),
-                                                   (4, 8000, 73, 1 << 20, None),
-                                                   (2, 12_000, 74, 1 << 16, None),
-                                                   (2, 7000, 75, 4096, (9000, 76))])
-def test_dgraph_hip_ranks_match_oracle(world, n, seed, keys, pre):
+# hub: the condensed graph's vertices split above 2 / 3 out-edges (the default
+# 256 is not reached at these sizes; C5 at 8 ranges reaches 22.7K)
+@pytest.mark.parametrize("world,n,seed,keys,pre,hub", [(1, 6000, 71, 4096, None, None),
+                                                       (2, 8000, 72, 4096, None, None),
+                                                       (4, 8000, 73, 1 << 20, None, None),
+                                                       (2, 12_000, 74, 1 << 16, None, None),
+                                                       (2, 7000, 75, 4096, (9000, 76), None),
+                                                       (2, 8000, 72, 4096, None, "2"),
+                                                       (4, 8000, 73, 1 << 20, None, "3")])
+def test_dgraph_hip_ranks_match_oracle(world, n, seed, keys, pre, hub):
     sys.path.insert(0, HERE)
     from fantoch_amd.dgraph import assemble
     from fullsize import shard_union
     from oracle import oracle as O
-    parts = run_ranks(world, n, seed, keys, pre)
+    parts = run_ranks(world, n, seed, keys, pre, hub)
     s = make_stream(n, seed, keys)
     got = assemble(parts, s.n, s.key_space)
     off, deps = shard_union(s)

@@ -15,7 +15,7 @@ for n in ${NS:-2 4}; do
   timeout -k 10 ${LIMIT:-500} python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
     --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --one-gpu --c5-backend gloo \
     --steps 3 --warmup 1 --no-cpu-baseline --no-configs --no-secondary --no-streaming --no-phases \
-    --c5-steps 1 > $OUT/dry_${TAG}_n$n.json 2> $OUT/dry_${TAG}_n$n.err || { tail -30 $OUT/dry_${TAG}_n$n.err; exit 1; }
+    --c5-steps 1 $DRY_ARGS > $OUT/dry_${TAG}_n$n.json 2> $OUT/dry_${TAG}_n$n.err || { tail -30 $OUT/dry_${TAG}_n$n.err; exit 1; }
   python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);c=d['c5'];print(c['ms_per_step'],c['condensed_graph'],c['rank0_stage_ms'])" $OUT/dry_${TAG}_n$n.json
   port=$((port+1))
 done
