@@ -595,6 +595,23 @@ __global__ void __launch_bounds__(kTileThreads)
     }
   __syncthreads();
   phase(5);
+  // the root's command (key-order outputs) for every core vertex of the
+  // thread first, the loads all in flight together (inside the loop each was
+  // a serialised round trip per vertex; phase 6: 50 -> 20 us per tile with
+  // the root's dot prefetched too, but that took the kernel to 125 VGPRs, and
+  // 4 waves x 128 registers fill each SIMD's file: the side stream's kernels
+  // could no longer run beside the tile workgroup, C4 14.5 -> 16.4 ms.  With
+  // the command alone: 105 VGPRs, C4 14.52 against 14.55 ms, r05ai)
+  uint32_t rcv[kMaxCore];
+#pragma unroll
+  for (int j = 0; j < kMaxCore; j++) {
+    const int x = ca + tid + j * kTileThreads;
+    rcv[j] = pcmd[j];
+    if (out.ko_seq && x < cb) {
+      const uint16_t t = sH[x];
+      if (t != uint32_t(x)) rcv[j] = out.ko_cmd[size_t(lo + t) * out.ko_cstride] & out.ko_cmask;
+    }
+  }
   uint32_t gmax = 0;
 #pragma unroll
   for (int j = 0; j < kMaxCore; j++) {
@@ -671,8 +688,7 @@ __global__ void __launch_bounds__(kTileThreads)
       out.ko_seq[lo + t - rpv[j] + b0 + rk] = dotx;
       if (t != uint32_t(x) || cnt > 0) {
         const uint32_t c = pcmd[j];
-        const uint32_t ct = t == uint32_t(x) ? c : out.ko_cmd[size_t(lo + t) * out.ko_cstride] &
-                                                      out.ko_cmask;
+        const uint32_t ct = rcv[j];
         out.ko_hl[c] = make_uint4(ct, rk, uint32_t(label), uint32_t(label >> 32));
         out.ko_diff[c + 1] = t != uint32_t(x) ? 1u : 0u - cnt;
       }
