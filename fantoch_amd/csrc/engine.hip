@@ -386,13 +386,25 @@ __global__ void __launch_bounds__(1024)
   for (uint32_t r = 0; r < np; r++) {
     const uint64_t len = lo.off[r + 1] - lo.off[r];
     const uint32_t q0 = lo.off[r] + uint32_t(len * w / G), q1 = lo.off[r] + uint32_t(len * (w + 1) / G);
-    for (uint32_t q = q0 + threadIdx.x; q < q1; q += 1024) {
-      const uint32_t e = ent[q], v = (r << kRecT) | (q - lo.off[r]);
-      const uint64_t rel = uint64_t(e) - e0;
-      if (e >= e0 && rel < WIN)
-        s_v[rel] = v;
-      else
-        rec[e] = v;
+    // four entries per thread per trip, their loads issued together
+    for (uint32_t qb = q0; qb < q1; qb += 4 * 1024) {
+      uint32_t ev[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t q = qb + u * 1024 + threadIdx.x;
+        ev[u] = q < q1 ? ent[q] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t q = qb + u * 1024 + threadIdx.x;
+        if (q >= q1) break;
+        const uint32_t e = ev[u], v = (r << kRecT) | (q - lo.off[r]);
+        const uint64_t rel = uint64_t(e) - e0;
+        if (e >= e0 && rel < WIN)
+          s_v[rel] = v;
+        else
+          rec[e] = v;
+      }
     }
   }
   __syncthreads();
