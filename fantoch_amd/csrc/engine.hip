@@ -824,18 +824,28 @@ __global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *
                             const VS *__restrict__ vals, const uint8_t *__restrict__ tailm,
                             const uint8_t *__restrict__ mrem, uint64_t *__restrict__ latest,
                             uint64_t log_base) {
-  GRID_STRIDE(i, n) {
-    const uint32_t msk = tailm[i];
-    if (!msk) continue;
-    const uint32_t rm = mrem[i];
-    const uint32_t kw = kws[i];
-    const uint64_t v = vload(vals, i);
-    const uint64_t m = cm.meta(kw, v);
-    const uint32_t key = kw & cm.kmask, c = uint32_t(v & cm.cmask);
-    for (uint32_t j = 0; j < cm.fq; j++) {
-      const uint32_t r = cm.rep(m, j);
-      if ((msk & (1u << j)) && !(rm & (1u << r)))
-        latest[uint64_t(r + 1) * K + key] = kLogFlag | (log_base + c);
+  // four commands' tail masks per load (the buffer is padded to a word):
+  // most are zero, and the side stream runs this with few waves per CU, so
+  // each thread's loop is bound by its loads' latency
+  const uint32_t nw = (n + 3) / 4;
+  GRID_STRIDE(w, nw) {
+    uint32_t msk4 = reinterpret_cast<const uint32_t *>(tailm)[w];
+    while (msk4) {
+      const uint32_t b = uint32_t(__builtin_ctz(msk4)) >> 3;
+      const uint32_t i = 4 * w + b;
+      const uint32_t msk = (msk4 >> (8 * b)) & 0xFFu;
+      msk4 &= ~(0xFFu << (8 * b));
+      if (i >= n) break;
+      const uint32_t rm = mrem[i];
+      const uint32_t kw = kws[i];
+      const uint64_t v = vload(vals, i);
+      const uint64_t m = cm.meta(kw, v);
+      const uint32_t key = kw & cm.kmask, c = uint32_t(v & cm.cmask);
+      for (uint32_t j = 0; j < cm.fq; j++) {
+        const uint32_t r = cm.rep(m, j);
+        if ((msk & (1u << j)) && !(rm & (1u << r)))
+          latest[uint64_t(r + 1) * K + key] = kLogFlag | (log_base + c);
+      }
     }
   }
 }
@@ -2351,7 +2361,7 @@ struct EngineDevice {
     sort_pairs_counted_src<uint32_t, V3, PackSrc>(src, kwa, va, sk32b.ensure(n + 1),
                                                   kv3b.ensure(n + 1), n, key_bits, sort_ws,
                                                   stream, &ks, &vs, db);
-    uint8_t *tm = tailm.ensure(n + 1);
+    uint8_t *tm = tailm.ensure(n + 4);  // (k_cmd_tails reads it by words)
     const size_t mwords = (size_t(n) + 3) / 4;
     uint32_t *mr = mrem.ensure(mwords);
     FH_HIP(hipMemsetAsync(mr, 0, mwords * sizeof(uint32_t), stream));
@@ -2524,7 +2534,7 @@ struct EngineDevice {
     uint64_t *vs = nullptr;
     sort_pairs_counted<uint32_t, uint64_t>(kwa, va, sk32b.ensure(n + 1), cv64b.ensure(n + 1), n,
                                            key_bits, sort_ws, stream, &ks, &vs, db);
-    uint8_t *tm = tailm.ensure(n + 1);
+    uint8_t *tm = tailm.ensure(n + 4);  // (k_cmd_tails reads it by words)
     // predecessor marks from other tiles (k_cmd_search, k_cmd_tails)
     const size_t mwords = (size_t(n) + 3) / 4;
     uint32_t *mr = mrem.ensure(mwords);
