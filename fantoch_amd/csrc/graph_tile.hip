@@ -55,7 +55,11 @@ constexpr int kMaxCore = 10;    // core vertices per thread (T <= 10240)
 constexpr uint32_t kMixR1 = 512;  // pass-1 reach bound of the mixed tiling
 
 // R0 rounded up to a multiple of 64 (at least 256)
-static uint32_t round_r0(uint32_t x) { return std::max<uint32_t>(256, (x + 63) & ~63u); }
+// (floor: 256, or 128 for the key-order graph, whose edges span a handful of
+// positions: C4 excess 102 -> R0 128, T 9728 instead of 9216)
+static uint32_t round_r0(uint32_t x, uint32_t floor = 256) {
+  return std::max<uint32_t>(floor, (x + 63) & ~63u);
+}
 
 // exclusive scan of one value per thread over the 1024-thread block
 __device__ __forceinline__ uint32_t tile_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
@@ -898,7 +902,8 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   }
   // next run: this run's excess with a small margin (a failure there only
   // costs one retry)
-  tile_r0 = ok ? std::min<uint32_t>(2048, round_r0(st[1] + st[1] / 32 + 16)) : 1536;
+  tile_r0 = ok ? std::min<uint32_t>(2048, round_r0(st[1] + st[1] / 32 + 16, in.tiles_only ? 128u : 256u))
+                : 1536;
   if (debug && ok) {
     unsigned long long pr[8];
     FH_HIP(hipMemcpyAsync(pr, to.prof, sizeof(pr), hipMemcpyDeviceToHost, stream));
