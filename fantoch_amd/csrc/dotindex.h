@@ -91,6 +91,10 @@ struct AEClock {
   // add for a list of dots (one executor pass's executed dots): bits first,
   // then each touched process's frontier advances once, by whole runs
   void add_all(const uint64_t *dots, size_t n) {
+    if (n > kBulk) {
+      add_bulk(dots, n);
+      return;
+    }
     bool changed = false;
     uint64_t touched[4] = {0, 0, 0, 0};
     for (size_t i = 0; i < n; i++) {
@@ -114,6 +118,103 @@ struct AEClock {
     }
     for (uint32_t g = 0; g < 4; g++)
       for (uint64_t m = touched[g]; m; m &= m - 1) advance(g * 64 + uint32_t(__builtin_ctzll(m)));
+    if (changed) version++;
+  }
+  // add_all for a large pass (a 1M-command batch spans ~200K sequence numbers
+  // per process, most of them beyond the ring while the frontier has not
+  // moved yet: the hash set took ~55 ns per dot, 55 ms per pass).  Per
+  // process, a dense bitmap over (frontier, the batch's largest sequence]:
+  // the batch's dots and the old exceptions in that range are set there, the
+  // frontier advances over the leading ones, and the remaining bits go back
+  // to the ring (or the hash set beyond it).  O(n + span / 64).
+  static constexpr size_t kBulk = size_t(1) << 14;
+  static constexpr uint64_t kMaxSpan = uint64_t(1) << 28;  // bits per process
+  void add_bulk(const uint64_t *dots, size_t n) {
+    uint64_t hi[256] = {0};
+    for (size_t i = 0; i < n; i++) {
+      const uint32_t s = uint32_t(dots[i] >> 56);
+      const uint64_t q = dots[i] & 0x00FFFFFFFFFFFFFFull;
+      if (q > frontier[s] && q > hi[s]) hi[s] = q;
+    }
+    bool dense[256] = {false};
+    for (uint32_t s = 0; s < 256; s++)
+      if (hi[s] && hi[s] - frontier[s] <= kMaxSpan) {
+        dense[s] = true;
+        bulk[s].assign((hi[s] - frontier[s] + 63) / 64, 0);
+      }
+    bool changed = false;
+    for (size_t i = 0; i < n; i++) {
+      const uint32_t s = uint32_t(dots[i] >> 56);
+      const uint64_t q = dots[i] & 0x00FFFFFFFFFFFFFFull;
+      if (q <= frontier[s]) continue;
+      if (!dense[s]) {
+        changed |= add(dots[i]);
+        continue;
+      }
+      const uint64_t b = q - frontier[s] - 1;
+      bulk[s][b >> 6] |= uint64_t(1) << (b & 63);
+    }
+    for (uint32_t s = 0; s < 256; s++) {
+      if (!dense[s]) continue;
+      std::vector<uint64_t> &bm = bulk[s];
+      const uint64_t f = frontier[s], h = hi[s];
+      uint64_t batch_bits = 0, overlap = 0;
+      for (uint64_t w : bm) batch_bits += uint64_t(__builtin_popcountll(w));
+      // the old exceptions in (f, h] join the bitmap
+      if (nbits[s]) {
+        uint64_t *w = ring[s].get();
+        for (uint64_t x = 0; x < kWin / 64; x++)
+          for (uint64_t m = w[x]; m; m &= m - 1) {
+            const uint64_t i = x * 64 + uint64_t(__builtin_ctzll(m));
+            const uint64_t q = f + 1 + ((i - (f + 1)) & (kWin - 1));
+            if (q > h) continue;
+            const uint64_t b = q - f - 1;
+            overlap += (bm[b >> 6] >> (b & 63)) & 1;
+            bm[b >> 6] |= uint64_t(1) << (b & 63);
+            w[x] &= ~(uint64_t(1) << (i & 63));
+            nbits[s]--;
+          }
+      }
+      if (!far.empty())
+        for (auto it = far.begin(); it != far.end();) {
+          const uint64_t q = *it & 0x00FFFFFFFFFFFFFFull;
+          if ((*it >> 56) == s && q <= h) {
+            const uint64_t b = q - f - 1;
+            overlap += (bm[b >> 6] >> (b & 63)) & 1;
+            bm[b >> 6] |= uint64_t(1) << (b & 63);
+            it = far.erase(it);
+          } else {
+            ++it;
+          }
+        }
+      changed |= batch_bits > overlap;
+      // the frontier over the leading ones
+      uint64_t lead = 0, x = 0;
+      while (x < bm.size() && bm[x] == ~uint64_t(0)) {
+        lead += 64;
+        x++;
+      }
+      if (x < bm.size()) lead += uint64_t(__builtin_ctzll(~bm[x]));
+      lead = std::min(lead, h - f);
+      const uint64_t fn = f + lead;
+      // the rest back to the ring (slot q mod kWin, valid for q - fn <= kWin)
+      // or the hash set
+      for (uint64_t y = lead >> 6; y < bm.size(); y++)
+        for (uint64_t m = bm[y]; m; m &= m - 1) {
+          const uint64_t b = y * 64 + uint64_t(__builtin_ctzll(m));
+          if (b < lead) continue;
+          const uint64_t q = f + 1 + b;
+          if (q - fn <= kWin) {
+            words(s)[(q % kWin) >> 6] |= uint64_t(1) << (q & 63);
+            nbits[s]++;
+          } else {
+            far.insert(make_dot(s, q));
+          }
+        }
+      frontier[s] = fn;
+      advance(s);
+      bm.clear();
+    }
     if (changed) version++;
   }
   // Raise s's frontier to seq (>= the current one): exceptions at or below it
@@ -162,6 +263,7 @@ struct AEClock {
   std::unique_ptr<uint64_t[]> ring[256];
   uint32_t nbits[256] = {0};
   std::unordered_set<uint64_t> far;
+  std::vector<uint64_t> bulk[256];  // add_bulk's per-process bitmaps
   uint64_t *words(uint32_t s) {
     if (!ring[s]) ring[s].reset(new uint64_t[kWin / 64]());
     return ring[s].get();

@@ -94,13 +94,17 @@ __global__ void k_append(Upload u, AppendDst a) {
 }
 
 // executed vertices in execution order: their dots and SCC labels
+// (ocar: per executed vertex, carried from an earlier pass -- vid below the
+// carried prefix P -- so the host looks up pending metadata only for those)
 __global__ void k_gather_exec(uint32_t m, const uint32_t *__restrict__ order,
                               const uint64_t *__restrict__ dot, const uint64_t *__restrict__ label,
-                              uint64_t *__restrict__ odot, uint64_t *__restrict__ olab) {
+                              uint32_t P, uint64_t *__restrict__ odot, uint64_t *__restrict__ olab,
+                              uint8_t *__restrict__ ocar) {
   GRID_STRIDE(j, m) {
     const uint32_t v = order[j];
     odot[j] = dot[v];
     olab[j] = label[v];
+    ocar[j] = v < P ? 1 : 0;
   }
 }
 
@@ -232,6 +236,7 @@ struct GraphDevice {
   uint64_t passes = 0, skipped = 0;
   // device buffers
   DBuf<uint64_t> d_sd, d_sd2, d_frontier, d_exc, d_xdot, d_xlab, d_miss;
+  DBuf<uint8_t> d_xcar;
   uint8_t *h_up = nullptr;      // the batch's upload block: mapped pinned host memory
   uint8_t *h_up_dev = nullptr;  // its device address (k_append reads it)
   size_t h_up_cap = 0;
@@ -451,6 +456,7 @@ struct GraphDevice {
       exc_version = clk_version;
       return;
     }
+    const auto t_up = std::chrono::steady_clock::now();
     if (n || clk) {
       k_append<<<grid_for(std::max({u.n ? u.n + 1 : 0u, u.nk, u.nd, u.nf + u.ne}), B), B, 0,
                  stream>>>(u, adst);
@@ -498,7 +504,9 @@ struct GraphDevice {
     gin.key_bits = key_bits;
     gin.want_per_key = false;  // the executor's monitor is fed from the drain order
     GraphOutput out;
+    const auto t_run0 = std::chrono::steady_clock::now();
     core.run(gin, out);
+    const auto t_run1 = std::chrono::steady_clock::now();
     // which batch vertices stay pending: only those get host metadata (a
     // batch vertex executed in this pass needs none: its execution delay is 0)
     std::vector<uint8_t> bflag(n);
@@ -507,10 +515,13 @@ struct GraphDevice {
     // executed vertices to the host: dots and labels in execution order
     const uint32_t nexec = out.nexec;
     std::vector<uint64_t> xdot(nexec), xlab(nexec);
+    std::vector<uint8_t> xcar(nexec);
     if (nexec) {
       uint64_t *xd = d_xdot.ensure(nexec), *xl = d_xlab.ensure(nexec);
+      uint8_t *xc = d_xcar.ensure(nexec);
       k_gather_exec<<<grid_for(nexec, B), B, 0, stream>>>(nexec, out.exec_order, ddot_v,
-                                                           out.scc_label, xd, xl);
+                                                           out.scc_label, uint32_t(P), xd, xl, xc);
+      FH_HIP(hipMemcpyAsync(xcar.data(), xc, nexec, hipMemcpyDeviceToHost, stream));
       FH_HIP(hipMemcpyAsync(xdot.data(), xd, nexec * sizeof(uint64_t), hipMemcpyDeviceToHost,
                             stream));
       FH_HIP(hipMemcpyAsync(xlab.data(), xl, nexec * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -571,7 +582,19 @@ struct GraphDevice {
     W.P = W.KP = W.DP = 0;
     cur = 1 - cur;
     FH_HIP(hipStreamSynchronize(stream));
-    finish_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, xdot, xlab, bflag, mlist, P2);
+    const auto t_res = std::chrono::steady_clock::now();
+    finish_pass(n, dot, dep_off, dep_dot, cmd_shards, dep_shards, xdot, xlab, bflag, mlist, P2,
+                xcar.data());
+    static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
+    if (debug) {
+      const auto t_end = std::chrono::steady_clock::now();
+      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      fprintf(stderr,
+              "fh graph pass (us): n=%zu V=%zu upload %.0f index %.0f run %.0f results %.0f "
+              "host %.0f\n",
+              n, V, us(t_enter, t_up), us(t_up, t_run0), us(t_run0, t_run1), us(t_run1, t_res),
+              us(t_res, t_end));
+    }
   }
 
   // A small graph's pass (graph_small.hip): one launch, one read-back.
@@ -701,8 +724,9 @@ struct GraphDevice {
                    const std::vector<uint64_t> &xdot, const std::vector<uint64_t> &xlab,
                    const std::vector<uint8_t> &bflag, std::vector<uint64_t> &mlist, uint32_t P2,
                    const uint8_t *xcar = nullptr) {
-    // xcar (the small pass): per executed vertex, carried or not -- only the
-    // carried ones have host metadata to look up
+    // xcar: per executed vertex, carried or not -- only the carried ones have
+    // host metadata to look up (a hash lookup per executed vertex cost ~60
+    // ns: most of a 1M-command batch's host time)
     const size_t nexec = xdot.size();
     // every drained dot is a carried vertex or one of this batch's executed
     // vertices (the reference panics otherwise): the batch part is checked by
