@@ -520,8 +520,17 @@ struct PackSrc {
   __device__ __forceinline__ void get(uint32_t x, uint32_t &kw, V3 &o) const {
     const uint32_t key = key32[x];
     uint64_t m = 0;
+    uint32_t rr[3];
+    if (cm.fq == 3) {  // the command's three records in one 12-B load
+      const auto t = *reinterpret_cast<const HIP_vector_type<uint32_t, 3> *>(rec + size_t(x) * 3);
+      rr[0] = t.x;
+      rr[1] = t.y;
+      rr[2] = t.z;
+    } else {
+      for (uint32_t j = 0; j < cm.fq; j++) rr[j] = rec[size_t(x) * cm.fq + j];
+    }
     for (uint32_t j = 0; j < cm.fq; j++) {
-      const uint32_t r = rec[size_t(x) * cm.fq + j];
+      const uint32_t r = rr[j];
       m |= ((uint64_t(r >> kRecT) << cm.qb) | (r & cm.qmask)) << (j * cm.vb);
     }
     const uint64_t v = uint64_t(x) | (m << cm.cb);
