@@ -427,3 +427,29 @@ def test_views_command_level_quorum_sizes(views, nproc, n, keys):
     s = Workload.zipf(0.99, keys, k=1, views=views, window=64, seed=40 + views,
                       n=nproc).generate(n)
     check_engine(s, nproc=nproc)
+
+
+@pytest.mark.parametrize("window,keys,seed", [(1024, 16, 21), (2048, 64, 22), (300, 8, 23),
+                                             (1024, 256, 24), (600, 1024, 25)])
+def test_keyorder_long_edges(window, keys, seed):
+    """Hot keys under a wide reorder window: key-order edges far longer than
+    the 8-bit distances the search writes (the -128 escapes to full
+    positions), and tile reach bounds well above the key-order floor; the
+    batch is ordered by the key-order path, or handed to the command-order
+    path if the tile certificate fails -- either way equal to the oracle."""
+    s = Workload.zipf(1.2, keys, k=1, views=3, window=window, seed=seed).generate(40_000,
+                                                                                  logs=True)
+    eng = Engine(s.key_space, n=5)
+    eng.stage(s)
+    for _ in range(2):  # a second run on the learned reach bound
+        eng.rewind()
+        eng.run()
+        r = eng.results()
+        off, deps = O.views_run(0, 5, s.dots, s.key_off(), s.keys.reshape(-1), s.fq_proc,
+                                s.fq_time)
+        ex, lab, kso, ks = O.graph_run(s.dots, s.key_off(), s.keys.reshape(-1), off, deps,
+                                       s.key_space)
+        assert np.array_equal(r["dep_off"], off) and np.array_equal(r["deps"], deps)
+        assert dict(zip(s.dots.tolist(), r["scc_label"].tolist())) == dict(
+            zip(ex.tolist(), lab.tolist()))
+        assert np.array_equal(r["key_off"], kso) and np.array_equal(r["key_seq"], ks)
