@@ -2447,6 +2447,11 @@ struct EngineDevice {
                     (const uint64_t *)dot.get(), sb, (const uint32_t *)doff, ddot,
                     scal.get() + 1);
     deps_direct = true;
+    // per-key offsets: a lower bound per key over the sorted keys (they
+    // need nothing else; the side stream has slack beside the tile kernel)
+    if (!deps_only)
+      k_key_offsets<<<grid_for(uint32_t(key_space) + 1, B), B, 0, cs>>>(
+          n, ks, uint32_t(key_space), key_offs.ensure(key_space + 2), cm.kmask);
     if (deps_only) {
       join();
       mark("keydeps_union");
@@ -2508,8 +2513,6 @@ struct EngineDevice {
     o_rank = rk;
     o_seq = sq;
     o_nelem = n;
-    k_key_offsets<<<grid_for(uint32_t(key_space) + 1, B), B, 0, stream>>>(
-        n, ks, uint32_t(key_space), key_offs.ensure(key_space + 2), cm.kmask);
     mark("out_per_key");
     join();
     mark("keydeps_union");
