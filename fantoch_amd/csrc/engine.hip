@@ -2386,6 +2386,12 @@ struct EngineDevice {
     uint32_t *codes = dep32.ensure(size_t(M) + 1);
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
+    // the straddle differences the tile kernel writes, cleared here: after
+    // the search the engine stream's next launch must be the tile kernel
+    // itself, or the side stream's kernels start first and take the CUs (a
+    // 66-us kernel in between cost 2 ms)
+    if (!deps_only)
+      FH_HIP(hipMemsetAsync(kdiff.ensure(n + 2), 0, size_t(n + 1) * sizeof(uint32_t), stream));
     auto go = [&](auto kern) {
       probed_launch("cmd_search", double(n) * (16.0 + 16.0 + 4.0 * fq + 4.0 + 1.0), kern,
                     dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np, (const uint32_t *)ks,
@@ -2474,8 +2480,7 @@ struct EngineDevice {
     gin.tiles_only = true;
     // the tiles write the per-key sequence and the command-order records
     uint64_t *sq = seq_dot.ensure(n + 1);
-    uint32_t *diff = kdiff.ensure(n + 2);
-    FH_HIP(hipMemsetAsync(diff, 0, size_t(n + 1) * sizeof(uint32_t), stream));
+    uint32_t *diff = kdiff.ensure(n + 2);  // (cleared before the search)
     uint4 *hl = khl.ensure(n + 1);
     gin.ko_seq = sq;
     gin.ko_hl = hl;
