@@ -378,33 +378,52 @@ __global__ void __launch_bounds__(1024)
     k_view_records(uint32_t n, uint32_t fq, uint32_t np, uint32_t G, LogOffs lo,
                    const uint32_t *__restrict__ ent, uint32_t *__restrict__ rec) {
   __shared__ uint32_t s_v[WIN];
+  __shared__ uint32_t s_pre[kMaxLogs + 1], s_q0[kMaxLogs], s_ql[kMaxLogs];
   const uint32_t w = blockIdx.x;
   for (uint32_t p = threadIdx.x; p < WIN; p += 1024) s_v[p] = kRecNone;
   const uint64_t c0 = uint64_t(n) * w / G;
   const uint64_t e0 = c0 * fq > rec_slack(WIN) ? c0 * fq - rec_slack(WIN) : 0;
+  // the slice's entries of all logs as one run (log r's part from s_pre[r]:
+  // entry f is ent[s_q0[r] + f], position s_ql[r] + f of log r), sixteen per
+  // thread with their loads issued together (tried: log by log, four loads
+  // per trip: 836 us per C4 launch)
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t r = 0; r < np; r++) {
+      const uint64_t len = lo.off[r + 1] - lo.off[r];
+      const uint32_t q0 = lo.off[r] + uint32_t(len * w / G), q1 = lo.off[r] + uint32_t(len * (w + 1) / G);
+      s_pre[r] = t;
+      s_q0[r] = q0 - t;
+      s_ql[r] = q0 - lo.off[r] - t;
+      t += q1 - q0;
+    }
+    s_pre[np] = t;
+  }
   __syncthreads();
-  for (uint32_t r = 0; r < np; r++) {
-    const uint64_t len = lo.off[r + 1] - lo.off[r];
-    const uint32_t q0 = lo.off[r] + uint32_t(len * w / G), q1 = lo.off[r] + uint32_t(len * (w + 1) / G);
-    // four entries per thread per trip, their loads issued together
-    for (uint32_t qb = q0; qb < q1; qb += 4 * 1024) {
-      uint32_t ev[4];
+  const uint32_t tot = s_pre[np];
+  constexpr int kU = 16;
+  for (uint32_t fb = 0; fb < tot; fb += kU * 1024) {
+    uint32_t ev[kU], vv[kU];
+    uint32_t r = 0;
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t q = qb + u * 1024 + threadIdx.x;
-        ev[u] = q < q1 ? ent[q] : 0u;
+    for (int u = 0; u < kU; u++) {
+      const uint32_t f = fb + u * 1024 + threadIdx.x;
+      ev[u] = kRecNone;
+      if (f < tot) {
+        while (f >= s_pre[r + 1]) r++;
+        ev[u] = ent[s_q0[r] + f];
+        vv[u] = (r << kRecT) | (s_ql[r] + f);
       }
+    }
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t q = qb + u * 1024 + threadIdx.x;
-        if (q >= q1) break;
-        const uint32_t e = ev[u], v = (r << kRecT) | (q - lo.off[r]);
-        const uint64_t rel = uint64_t(e) - e0;
-        if (e >= e0 && rel < WIN)
-          s_v[rel] = v;
-        else
-          rec[e] = v;
-      }
+    for (int u = 0; u < kU; u++) {
+      const uint32_t e = ev[u];
+      if (e == kRecNone) continue;
+      const uint64_t rel = uint64_t(e) - e0;
+      if (e >= e0 && rel < WIN)
+        s_v[rel] = vv[u];
+      else
+        rec[e] = vv[u];
     }
   }
   __syncthreads();
