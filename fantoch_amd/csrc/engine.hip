@@ -973,16 +973,42 @@ __global__ void __launch_bounds__(256)
   SrcAcc acc;
   acc.init(s_mx, s_cnt);
   __syncthreads();
-  GRID_STRIDE(c, n) {
-    const uint64_t dc = dot[c];
-    acc.add(dc);
-    if (diff[c + 1] != 0u) {
-      const uint4 r = hl[c];
-      rank[c] = r.x - ss[r.x + 1] + r.y;
-      label[c] = uint64_t(r.z) | (uint64_t(r.w) << 32);
-    } else {
-      rank[c] = c - ss[c + 1];
-      label[c] = dc;
+  // four commands per thread per trip, each dependent level's loads issued
+  // together (diff / dot / ss, then hl, then the root's ss)
+  constexpr int kU = 4;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t c0 = blockIdx.x * blockDim.x + threadIdx.x; c0 < n; c0 += kU * stride) {
+    uint64_t dc[kU];
+    uint32_t df[kU], sc[kU], sr[kU];
+    uint4 r[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const uint32_t c = c0 + u * stride;
+      df[u] = 0u;
+      if (c < n) {
+        dc[u] = dot[c];
+        df[u] = diff[c + 1];
+        sc[u] = ss[c + 1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (df[u]) r[u] = hl[c0 + u * stride];
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (df[u]) sr[u] = ss[r[u].x + 1];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const uint32_t c = c0 + u * stride;
+      if (c >= n) break;
+      acc.add(dc[u]);
+      if (df[u]) {
+        rank[c] = r[u].x - sr[u] + r[u].y;
+        label[c] = uint64_t(r[u].z) | (uint64_t(r[u].w) << 32);
+      } else {
+        rank[c] = c - sc[u];
+        label[c] = dc[u];
+      }
     }
   }
   acc.commit(smx, scnt);
