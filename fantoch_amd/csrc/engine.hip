@@ -353,6 +353,7 @@ __global__ void __launch_bounds__(1024)
 // Batches whose logs exceed kCmdMaxW take the chunked path.
 constexpr uint32_t kCmdMaxW = 4096;
 constexpr int kSrchThreads = 1024;
+constexpr int kKoSrchThreads = 512;  // the key-order path (cmd_views_keyorder)
 constexpr uint32_t kRecT = 27;  // rec = replica << 27 | arrival position
 constexpr uint32_t kNoCmd = ~0u;
 
@@ -2416,7 +2417,12 @@ struct EngineDevice {
     const size_t mwords = (size_t(n) + 3) / 4;
     uint32_t *mr = mrem.ensure(mwords);
     FH_HIP(hipMemsetAsync(mr, 0, mwords * sizeof(uint32_t), stream));
-    const uint32_t stiles = (n + kSrchThreads - 1) / kSrchThreads;
+    // 512-command tiles: four workgroups per CU (38 KB of LDS each) against two
+    // at 1024, so one tile's staging and barriers overlap three others' scans
+    // (C4, ms per step: 1024 13.39 / 13.70, 512 12.41 / 12.43, 256 13.82 /
+    // 14.08, r05th / r05th2)
+    const uint32_t sth = kKoSrchThreads;
+    const uint32_t stiles = (n + sth - 1) / sth;
     const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> kRegShift) + 1;
     FH_CHECK(nreg <= kMaxRegions, FH_EINVARIANT, "command regions");
     uint4 *rec4 = crec.ensure(size_t(n) + 1);
@@ -2436,13 +2442,13 @@ struct EngineDevice {
       FH_HIP(hipMemsetAsync(kdiff.ensure(n + 2), 0, size_t(n + 1) * sizeof(uint32_t), stream));
     auto go = [&](auto kern) {
       probed_launch("cmd_search", double(n) * (16.0 + 16.0 + 4.0 * fq + 4.0 + 1.0), kern,
-                    dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np, (const uint32_t *)ks,
+                    dim3(stiles), dim3(sth), stream, n, cm, K, np, (const uint32_t *)ks,
                     (const V3 *)vs, lat, codes, rec4, rcur, tm, mr, pcode, pd32, pe8);
     };
     if (fq == 2)
-      go(k_cmd_search<2, kSrchThreads, V3, true>);
+      go(k_cmd_search<2, kKoSrchThreads, V3, true>);
     else
-      go(k_cmd_search<3, kSrchThreads, V3, true>);
+      go(k_cmd_search<3, kKoSrchThreads, V3, true>);
     mark("keydeps_views");
     // The command-order half -- the records' entries to their commands
     // (region by region), the tails, the committed deps -- needs nothing the
