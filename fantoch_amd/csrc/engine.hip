@@ -2420,7 +2420,8 @@ struct EngineDevice {
     // 512-command tiles: four workgroups per CU (38 KB of LDS each) against two
     // at 1024, so one tile's staging and barriers overlap three others' scans
     // (C4, ms per step: 1024 13.39 / 13.70, 512 12.41 / 12.43, 256 13.82 /
-    // 14.08, r05th / r05th2)
+    // 14.08, r05th / r05th2; halos of 64 or 32 instead of 128: no different,
+    // r05ha)
     const uint32_t sth = kKoSrchThreads;
     const uint32_t stiles = (n + sth - 1) / sth;
     const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> kRegShift) + 1;
