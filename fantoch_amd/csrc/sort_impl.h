@@ -452,7 +452,9 @@ void sort_pass(const Src &src, K *ko, St vo, size_t n, int shift, uint32_t tiles
     scan_b<DB>(gsum, groups, dbase, s);
   }
   // the 512-thread scatter (k_down).  Measured on C4, u64 values: 613 -> 592
-  // us per 100M-element pass against 256 threads
+  // us per 100M-element pass against 256 threads.  (Tried for the key-order
+  // path's 12-B values: 1024 threads, 32 waves per CU instead of 16 -- KeyDeps
+  // views 6.07 against 6.09 ms, no different, r05st.)
   constexpr int down_th = 512;
   auto down = [&](auto kern, int th) {
     if (!probe) {
