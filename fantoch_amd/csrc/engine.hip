@@ -2396,19 +2396,31 @@ struct EngineDevice {
     uint32_t *rec = vrec.ensure(M + 1);
     const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * rec_slack(kRecWin)) / fq);
     const uint32_t G = std::max<uint32_t>(1, (n + per - 1) / per);
-    probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records<kRecWin>, dim3(G),
-                  dim3(1024), stream, n, fq, np, G, lo, bent, rec);
     const uint32_t tiles = (n + kTile - 1) / kTile;
     sort_ws.prepare(tiles, 1, stream);
     const int db = sort_digit_bits(key_bits, 4);
+    if (!side_off && !side) FH_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    // the pass-0 tile counts need only the keys: on the side stream beside
+    // the view records
+    // (k_cmd_pack3 writing the packed arrays, then the sort: 724 + 864 against
+    // 1226 us per C4 step for the first pass producing its own input, r05r)
+    hipStream_t ks0 = side_off ? stream : side;
+    if (!side_off) {
+      FH_HIP(hipEventRecord(ev_fork, stream));
+      FH_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+    }
+    k_key_counts<<<dim3(tiles), dim3(kThreads), 0, ks0>>>(n, bkey, sort_ws.meta.get(),
+                                                          (1u << db) - 1);
+    probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records<kRecWin>, dim3(G),
+                  dim3(1024), stream, n, fq, np, G, lo, bent, rec);
+    if (!side_off) {
+      FH_HIP(hipEventRecord(ev_join, side));
+      FH_HIP(hipStreamWaitEvent(stream, ev_join, 0));
+    }
     uint32_t *kwa = sk32a.ensure(n + 1);
     V3 *va = kv3a.ensure(n + 1);
     uint32_t *ks = nullptr;
     V3 *vs = nullptr;
-    // (k_cmd_pack3 writing the packed arrays, then the sort: 724 + 864 against
-    // 1226 us per C4 step for the first pass producing its own input, r05r)
-    k_key_counts<<<dim3(tiles), dim3(kThreads), 0, stream>>>(n, bkey, sort_ws.meta.get(),
-                                                             (1u << db) - 1);
     const PackSrc src{cm, bkey, rec, dot32.get() + b * size_t(n)};
     sort_pairs_counted_src<uint32_t, V3, PackSrc>(src, kwa, va, sk32b.ensure(n + 1),
                                                   kv3b.ensure(n + 1), n, key_bits, sort_ws,
@@ -2456,7 +2468,6 @@ struct EngineDevice {
     // graph computes, and the graph needs none of it: it runs on the side
     // stream while the tile kernel (latency bound, one workgroup per CU)
     // runs here.
-    if (!side_off && !side) FH_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     hipStream_t cs = side_off ? stream : side;
     ScanWorkspace &cws = side_off ? scan_ws : scan_ws2;
     if (!side_off) {
