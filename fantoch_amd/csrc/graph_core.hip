@@ -250,19 +250,37 @@ __global__ void __launch_bounds__(256)
   const uint32_t base = win * 64;
   uint64_t r[2][2] = {{0, 0}, {0, 0}};
   bool fwd = false;
+  auto edge = [&](int h, uint32_t v, uint32_t u) {
+    if (u >= base && u < base + 128 && u != v && !(any_blocked && blocked[u])) {
+      const uint32_t bit = u - base;
+      r[h][bit >> 6] |= uint64_t(1) << (bit & 63);
+      fwd |= u > v;
+    }
+  };
+  // each row's first kPre edges loaded up front, all in flight together,
+  // the rest (rows longer than kPre) one at a time after them (one load at
+  // a time throughout: 18.4 ms per C5 launch)
+  constexpr int kPre = 12;
+  uint32_t eb[2], ee[2], q[2][kPre];
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const uint32_t v = base + h * 64 + lane;
-    if (v < V && !(any_blocked && blocked[v])) {
-      for (uint32_t e = EB(v); e < EE(v); e++) {
-        const uint32_t u = dst[e];
-        if (u >= base && u < base + 128 && u != v && !(any_blocked && blocked[u])) {
-          const uint32_t bit = u - base;
-          r[h][bit >> 6] |= uint64_t(1) << (bit & 63);
-          fwd |= u > v;
-        }
-      }
-    }
+    const bool ok = v < V && !(any_blocked && blocked[v]);
+    eb[h] = ok ? EB(v) : 0u;
+    ee[h] = ok ? EE(v) : 0u;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t v = base + h * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < kPre; i++) q[h][i] = eb[h] + i < ee[h] ? dst[eb[h] + i] : v;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t v = base + h * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < kPre; i++) edge(h, v, q[h][i]);
+    for (uint32_t e = eb[h] + kPre; e < ee[h]; e++) edge(h, v, dst[e]);
   }
   if (!__any(fwd)) return;  // no forward edge inside: no local cycle
   // pivots 0..63 live in rows r[0][*] of lane k, pivots 64..127 in r[1][*];
