@@ -2433,7 +2433,8 @@ struct EngineDevice {
     // at 1024, so one tile's staging and barriers overlap three others' scans
     // (C4, ms per step: 1024 13.39 / 13.70, 512 12.41 / 12.43, 256 13.82 /
     // 14.08, r05th / r05th2; halos of 64 or 32 instead of 128: no different,
-    // r05ha)
+    // r05ha; tiles contiguous per XCD, so a tile's halo sits in the L2 its
+    // predecessor staged it through: 13.84 against 12.94, r05xc)
     const uint32_t sth = kKoSrchThreads;
     const uint32_t stiles = (n + sth - 1) / sth;
     const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> kRegShift) + 1;
