@@ -975,7 +975,8 @@ __global__ void __launch_bounds__(256)
   acc.init(s_mx, s_cnt);
   __syncthreads();
   // four commands per thread per trip, each dependent level's loads issued
-  // together (diff / dot / ss, then hl, then the root's ss)
+  // together (diff / dot / ss, then hl, then the root's ss; two per trip,
+  // 8 waves per SIMD instead of 5: 832-887 against 821-831 us, r05ku)
   constexpr int kU = 4;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t c0 = blockIdx.x * blockDim.x + threadIdx.x; c0 < n; c0 += kU * stride) {
