@@ -85,6 +85,8 @@ SIGNATURES = {
     "fh_graph_take_metrics": (C.c_int, [V, V, S, V, S, P(S), P(S)]),
     "fh_graph_passes": (C.c_int, [V, P(C.c_uint64), P(C.c_uint64)]),
     "fh_graph_missing": (C.c_int, [V, V, S, P(S)]),
+    "fh_graph_inject_small_delay": (C.c_int, [V, C.c_uint32, C.c_uint32]),
+    "fh_selftest_poll_deadline": (C.c_int, [C.c_uint32]),
     "fh_graph_add_batch_sharded": (C.c_int, [V, S, V, V, V, V, V, V, V]),
     "fh_graph_requests": (C.c_int, [V, V, V, S, P(S)]),
     "fh_graph_handle_requests": (C.c_int, [V, C.c_uint64, S, V]),

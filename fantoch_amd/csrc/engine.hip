@@ -1730,11 +1730,6 @@ struct EngineDevice {
     const char *e = getenv("FH_KEYORDER");
     return e && *e == '0';
   }();
-  // FH_CODE_REGIONS=0 (measurement): codes stored straight at the command slot
-  const bool region_off = [] {
-    const char *e = getenv("FH_CODE_REGIONS");
-    return e && *e == '0';
-  }();
   DBuf<uint64_t> cv64a, cv64b;  // command-level views path: packed sort values
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
   // per batch: (seq bits, packed bits) of its dots, src << sb | seq (0: wider
@@ -1864,6 +1859,10 @@ struct EngineDevice {
                             kKeyBucketClockWords * sizeof(unsigned long long), stream));
     }
     FH_HIP(hipStreamSynchronize(stream));
+    // the key-order path's side stream: joined back into `stream` on every
+    // normal exit, but a run that threw between its fork and its join may
+    // have left side kernels running on the buffers the next stage reuses
+    if (side) FH_HIP(hipStreamSynchronize(side));
     kb_next_part = ~size_t(0);
   }
   KeyBucketClock kb_clock(size_t batch) {
@@ -2136,6 +2135,12 @@ struct EngineDevice {
   void run(float *ms) {
     FH_CHECK(staged && cursor < nbatches, FH_EINVAL, "no staged batch left to run");
     FH_HIP(hipSetDevice(device));
+    if (side) {
+      // a run that threw between the side stream's fork and join left no
+      // join behind: this run's kernels wait for whatever still runs there
+      FH_HIP(hipEventRecord(ev_join, side));
+      FH_HIP(hipStreamWaitEvent(stream, ev_join, 0));
+    }
     clear_marks();
     graph.profile = profile;
     const uint32_t n = uint32_t(desc.n), k = desc.keys_per_cmd;
@@ -2628,7 +2633,7 @@ struct EngineDevice {
     FH_CHECK(nreg <= kMaxRegions, FH_EINVARIANT, "command regions");
     uint4 *rec4 = nullptr;
     uint32_t *rcur = nullptr;
-    if (fq <= 3 && !region_off) {
+    if (fq <= 3) {
       rec4 = crec.ensure(size_t(n) + 1);
       rcur = ctoff.ensure(kMaxRegions);
       FH_HIP(hipMemsetAsync(rcur, 0, kMaxRegions * sizeof(uint32_t), stream));

@@ -266,12 +266,12 @@ struct GraphDevice {
   }
   ~GraphDevice() {
     (void)hipSetDevice(device);
+    // the stream first: a pass that missed its deadline may still write the
+    // mapped blocks
+    if (stream) (void)hipStreamSynchronize(stream);
     if (h_small) (void)hipHostFree(h_small);
     if (h_up) (void)hipHostFree(h_up);
-    if (stream) {
-      (void)hipStreamSynchronize(stream);
-      (void)hipStreamDestroy(stream);
-    }
+    if (stream) (void)hipStreamDestroy(stream);
   }
 
   // PendingIndex::index (index.rs:171-205) as called by index_pending
@@ -658,19 +658,20 @@ struct GraphDevice {
     // 0 is the value the host stores before the launch: never a sequence
     if (++small_seq == 0) small_seq = 1;
     sp.seq = small_seq;
+    sp.delay_us = small_delay_us;
     volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(h_small) + 31;
     *done = 0;
     const auto t_launch = std::chrono::steady_clock::now();
     launch_graph_small(sp, stream);  // writes the mapped block: no read-back copy
     // the kernel's last store is the completion word (polled: ~4 us sooner
     // than a stream synchronize at a batch of one); the stream is queried now
-    // and then so that a failed launch cannot spin forever
-    for (uint32_t i = 1; *done != sp.seq; i++) {
-      if ((i & 1023) != 0) continue;
-      const hipError_t st = hipStreamQuery(stream);
-      if (st == hipErrorNotReady) continue;
-      FH_HIP(st);
-      FH_CHECK(*done == sp.seq, FH_EINVARIANT, "graph_small: pass ended without its completion word");
+    // and then so that a failed launch cannot spin forever, and a pass that
+    // has not finished by the deadline fails the call instead of hanging it
+    try {
+      poll_completion(done, sp.seq, [&] { return hipStreamQuery(stream); }, small_deadline_ms);
+    } catch (...) {
+      broken = true;
+      throw;
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     const auto t_sync = std::chrono::steady_clock::now();
@@ -716,6 +717,12 @@ struct GraphDevice {
   std::chrono::steady_clock::time_point t_enter;  // add_batch entry (FH_GRAPH_DEBUG timings)
   uint32_t small_seq = 0;
   uint64_t passes_small = 0;
+  // a small pass missed its deadline: its kernel may still be writing the
+  // vertex sets, so every later call fails (FH_EHIP) until the handle is
+  // destroyed (fh_graph_inject_small_delay sets both knobs in tests)
+  bool broken = false;
+  double small_deadline_ms = 30000.0;
+  uint32_t small_delay_us = 0;
 
   // The host side of a pass: the drained vertices, executed clock, metrics,
   // the survivors' pending metadata and the missing dependencies.
@@ -877,6 +884,7 @@ fh_status fh_graph_add_batch(fh_graph *h, size_t n, const uint64_t *dot, const u
                              const uint64_t *dep_dot) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   h->dev.add_batch(n, dot, key_off, key_id, dep_off, dep_dot);
   FH_API_END
 }
@@ -887,6 +895,7 @@ fh_status fh_graph_add_batch_sharded(fh_graph *h, size_t n, const uint64_t *dot,
                                      const uint64_t *cmd_shards, const uint64_t *dep_shards) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   FH_CHECK(h->dev.shard_id < 64, FH_EINVAL, "shard sets are 64-bit masks: shard_id must be < 64");
   h->dev.add_batch(n, dot, key_off, key_id, dep_off, dep_dot, cmd_shards, dep_shards);
   FH_API_END
@@ -896,6 +905,7 @@ fh_status fh_graph_requests(fh_graph *h, uint64_t *dot, uint64_t *shard, size_t 
                             size_t *len) {
   FH_API_BEGIN
   FH_CHECK(h && len, FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   auto &r = h->dev.out_requests;
   *len = r.size();
   if (r.empty()) return FH_OK;
@@ -914,6 +924,7 @@ fh_status fh_graph_handle_requests(fh_graph *h, uint64_t from_shard, size_t n,
                                    const uint64_t *dots) {
   FH_API_BEGIN
   FH_CHECK(h && (n == 0 || dots), FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   h->dev.process_requests(from_shard, dots, n);
   FH_API_END
 }
@@ -921,6 +932,7 @@ fh_status fh_graph_handle_requests(fh_graph *h, uint64_t from_shard, size_t n,
 fh_status fh_graph_cleanup(fh_graph *h) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   h->dev.retry_buffered();
   FH_API_END
 }
@@ -931,6 +943,7 @@ fh_status fh_graph_request_replies(fh_graph *h, size_t cap, uint64_t *to_shard, 
                                    size_t *n_replies, size_t *n_deps) {
   FH_API_BEGIN
   FH_CHECK(h && n_replies && n_deps, FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   auto &rs = h->dev.replies;
   size_t nd = 0;
   for (const auto &r : rs) nd += r.deps.size();
@@ -962,6 +975,7 @@ fh_status fh_graph_drain(fh_graph *h, uint64_t *exec_dot, uint64_t *scc_label, s
                          size_t *len) {
   FH_API_BEGIN
   FH_CHECK(h && len, FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   *len = h->dev.drain(exec_dot, scc_label, exec_dot || scc_label ? cap : 0);
   FH_API_END
 }
@@ -969,6 +983,7 @@ fh_status fh_graph_drain(fh_graph *h, uint64_t *exec_dot, uint64_t *scc_label, s
 fh_status fh_graph_mark_executed(fh_graph *h, size_t n, const uint64_t *dot) {
   FH_API_BEGIN
   FH_CHECK(h && (n == 0 || dot), FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   for (size_t i = 0; i < n; i++) h->dev.clock_changed |= h->dev.clock.add(dot[i]);
   FH_API_END
 }
@@ -978,6 +993,7 @@ fh_status fh_graph_mark_executed(fh_graph *h, size_t n, const uint64_t *dot) {
 fh_status fh_graph_set_executed_frontier(fh_graph *h, uint32_t source, uint64_t seq) {
   FH_API_BEGIN
   FH_CHECK(h && source < 256, FH_EINVAL, "bad argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   auto &c = h->dev.clock;
   FH_CHECK(seq >= c.frontier[source], FH_EINVAL,
            "set_executed_frontier: the executed frontier cannot move backwards");
@@ -990,6 +1006,7 @@ fh_status fh_graph_set_executed_frontier(fh_graph *h, uint32_t source, uint64_t 
 fh_status fh_graph_set_time(fh_graph *h, uint64_t now_ms) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   h->dev.now_ms = now_ms;
   FH_API_END
 }
@@ -999,6 +1016,7 @@ fh_status fh_graph_monitor_pending(fh_graph *h, uint64_t threshold_ms, uint64_t 
                                    size_t *len) {
   FH_API_BEGIN
   FH_CHECK(h && len, FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   std::vector<std::pair<uint64_t, uint64_t>> old;
   std::vector<uint64_t> nm;
   h->dev.monitor_pending(threshold_ms, old, nm);
@@ -1016,6 +1034,7 @@ fh_status fh_graph_take_metrics(fh_graph *h, uint64_t *chain_size, size_t chain_
                                 size_t *n_delay) {
   FH_API_BEGIN
   FH_CHECK(h && n_chain && n_delay, FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   auto &d = h->dev;
   *n_chain = d.m_chain.size();
   *n_delay = d.m_delay.size();
@@ -1032,14 +1051,33 @@ fh_status fh_graph_take_metrics(fh_graph *h, uint64_t *chain_size, size_t chain_
 fh_status fh_graph_passes(fh_graph *h, uint64_t *passes, uint64_t *skipped) {
   FH_API_BEGIN
   FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   if (passes) *passes = h->dev.passes;
   if (skipped) *skipped = h->dev.skipped;
+  FH_API_END
+}
+
+fh_status fh_graph_inject_small_delay(fh_graph *h, uint32_t delay_us, uint32_t deadline_ms) {
+  FH_API_BEGIN
+  FH_CHECK(h, FH_EINVAL, "null handle");
+  FH_CHECK(delay_us <= 10u * 1000 * 1000, FH_EINVAL, "delay_us <= 10 s");
+  h->dev.small_delay_us = delay_us;
+  if (deadline_ms) h->dev.small_deadline_ms = double(deadline_ms);
+  FH_API_END
+}
+
+fh_status fh_selftest_poll_deadline(uint32_t deadline_ms) {
+  FH_API_BEGIN
+  FH_CHECK(deadline_ms >= 1 && deadline_ms <= 60000, FH_EINVAL, "deadline_ms in [1, 60000]");
+  volatile uint32_t word = 0;
+  fh::poll_completion(&word, 1u, [] { return hipErrorNotReady; }, double(deadline_ms));
   FH_API_END
 }
 
 fh_status fh_graph_pending(fh_graph *h, size_t *count) {
   FH_API_BEGIN
   FH_CHECK(h && count, FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   *count = h->dev.pend.size();
   FH_API_END
 }
@@ -1047,6 +1085,7 @@ fh_status fh_graph_pending(fh_graph *h, size_t *count) {
 fh_status fh_graph_missing(fh_graph *h, uint64_t *dots, size_t cap, size_t *len) {
   FH_API_BEGIN
   FH_CHECK(h && len, FH_EINVAL, "null argument");
+  FH_CHECK(!h->dev.broken, FH_EHIP, "graph: an earlier small pass missed its deadline");
   const auto &m = h->dev.missing_now;
   *len = m.size();
   for (size_t i = 0; i < m.size() && i < cap && dots; i++) dots[i] = m[i];

@@ -103,6 +103,13 @@ __global__ void __launch_bounds__(kThreads)
     }
   };
   stamp(0);
+  if (p.delay_us) {  // fault injection: a pass that takes delay_us longer
+    if (threadIdx.x == 0) {
+      const uint64_t t0 = wall_clock64(), t1 = t0 + uint64_t(p.delay_us) * 100;  // 100 MHz
+      while (wall_clock64() < t1) __builtin_amdgcn_s_sleep(127);
+    }
+    __syncthreads();
+  }
   // the batch's rows after the carried prefix, and the clock mirror
   // (k_append's job on the general path); the pass below reads them back
   // from global memory after the barrier

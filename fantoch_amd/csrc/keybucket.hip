@@ -15,30 +15,6 @@
 
 #include "keybucket.h"
 
-#ifdef FH_KB_STAMPS
-// diagnostic builds (tools/kbbench.cpp): per-workgroup {start, end, work}
-// and phase ends in s_memrealtime ticks (100 MHz); never in the library
-__device__ unsigned long long *g_kb_stamps[2];
-__device__ unsigned long long *g_kb_phase[2];  // [wg][8]
-#define FH_STAMP_BEGIN() const unsigned long long fh_t0 = __builtin_amdgcn_s_memrealtime()
-#define FH_STAMP_END(k, work)                                                \
-  do {                                                                       \
-    if (threadIdx.x == 0 && g_kb_stamps[k]) {                                \
-      g_kb_stamps[k][3 * fh_bid] = fh_t0;                                \
-      g_kb_stamps[k][3 * fh_bid + 1] = __builtin_amdgcn_s_memrealtime(); \
-      g_kb_stamps[k][3 * fh_bid + 2] = (work);                           \
-    }                                                                        \
-  } while (0)
-#define FH_PHASE(k, i)                                                        \
-  do {                                                                        \
-    if (threadIdx.x == 0 && g_kb_phase[k])                                    \
-      g_kb_phase[k][8 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define FH_STAMP_BEGIN() (void)0
-#define FH_STAMP_END(k, work) (void)0
-#define FH_PHASE(k, i) (void)0
-#endif
 
 namespace fh {
 namespace {
@@ -61,9 +37,7 @@ constexpr int kHot = 16;                  // hot-key buckets (after the B regula
 constexpr int kCand = 64;                 // hot-key candidates per schedule refresh
 // hot table words: [kHot] mapped keys, [1] candidate count, [kCand][2] (count, key)
 constexpr int kHotWords = kHot + 1 + 2 * kCand;
-#ifndef FH_MATCH_BLOCK
-#define FH_MATCH_BLOCK 4                  // items whose ballot matches are interleaved
-#endif
+constexpr int kMatchBlock = 4;           // items whose ballot matches are interleaved
 
 // Peer masks of N independent items at once: peers[i] = lanes whose BITS-bit
 // value d[i] equals this lane's (valid lanes only).  The bits loop is
@@ -203,9 +177,6 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
                                                const uint32_t *__restrict__ hot,
                                                uint32_t *__restrict__ hot_snap,
                                                unsigned char *smem) {
-  const uint32_t fh_bid = bid;
-  (void)fh_bid;
-  FH_STAMP_BEGIN();
   using L = PartSmem<BB>;
   constexpr int BMAX = L::BMAX;
   constexpr int RB = (BMAX + kThreads - 1) / kThreads;  // buckets per thread in the scan
@@ -241,7 +212,6 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
     d[i] = tl.dot[i];
   }
   __syncthreads();
-  FH_PHASE(0, 0);
   const uint64_t lt = (uint64_t(1) << lane) - 1;
   const uint32_t smask = (1u << hb) - 1;
   // matches first (independent across items), then the ordered LDS counts
@@ -258,18 +228,15 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
   match_n<kItems>(mb, bkt, vld, peers);
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
-#ifndef FH_ABL_NOCLOCK  // diagnostic builds only: partition without the clock
     if (vld[i]) {
       atomicMax(&s_mx[d[i] >> 56], (unsigned long long)(d[i] & 0x00FFFFFFFFFFFFFFull));
       atomicAdd(&s_nc[d[i] >> 56], 1u);
     }
-#endif
     const uint32_t b0 = vld[i] ? s_wh[w][bkt[i]] : 0u;
     if (vld[i] && (peers[i] & lt) == 0) s_wh[w][bkt[i]] = b0 + uint32_t(__popcll(peers[i]));
     rank[i] = b0 + uint32_t(__popcll(peers[i] & lt));
   }
   __syncthreads();
-  FH_PHASE(0, 1);
   // per-bucket tile counts -> per-wave exclusive offsets and bucket starts
   uint32_t loc[RB];
   uint32_t sum = 0;
@@ -304,12 +271,10 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
     pre += loc[r];
   }
   __syncthreads();
-  FH_PHASE(0, 2);
 #pragma unroll
   for (int i = 0; i < kItems; i++)
     if (vld[i]) s_out[s_dex[bkt[i]] + s_wh[w][bkt[i]] + rank[i]] = pk[i];
   __syncthreads();
-  FH_PHASE(0, 3);
   if (tile_n == uint32_t(kTile)) {
     uint4 *dst = reinterpret_cast<uint4 *>(part + base);
     const uint4 *src = reinterpret_cast<const uint4 *>(s_out);
@@ -323,7 +288,6 @@ __device__ __forceinline__ void partition_tile(uint32_t bid, uint32_t n, int bb,
     atomicMax(&shard[tid], s_mx[tid]);
     atomicAdd(&shard[256 + tid], (unsigned long long)s_nc[tid]);
   }
-  FH_STAMP_END(0, tile_n);
 }
 
 // ---------------------------------------------------------------- order
@@ -410,21 +374,19 @@ __device__ __forceinline__ void rank_items(const uint32_t (&xe)[IT], uint32_t c,
 template <int IT, int NBITS>
 __device__ __forceinline__ void slot_sort_pass(const uint32_t (&xe)[IT], uint32_t *dst, uint32_t c,
                                                int vb, int shift, uint32_t (*s_h)[1 << kDigit],
-                                               uint32_t *s_db, bool zeroed, bool stamp) {
+                                               uint32_t *s_db, bool zeroed) {
   constexpr int nbits = NBITS;
   constexpr int ND = 1 << kDigit;
-  constexpr int HALF = IT < FH_MATCH_BLOCK ? IT : IT % FH_MATCH_BLOCK == 0 ? FH_MATCH_BLOCK : IT % 3 == 0 ? 3 : 2;
+  constexpr int HALF = IT < kMatchBlock ? IT : IT % kMatchBlock == 0 ? kMatchBlock : IT % 3 == 0 ? 3 : 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (!zeroed) {
     for (int i = tid; i < kOWaves * ND; i += kOThreads) (&s_h[0][0])[i] = 0;
     __syncthreads();
   }
-  if (stamp) FH_PHASE(1, 4);
   uint32_t rk[IT];
   const uint32_t dm = (1u << nbits) - 1;
   rank_items<IT, HALF, 0, NBITS>(xe, c, vb, shift, s_h, rk);
   __syncthreads();
-  if (stamp) FH_PHASE(1, 5);
   if (w == 0) {
     // digit totals over waves (lane = digit), then the digit bases
     uint32_t cw[kOWaves];
@@ -445,7 +407,6 @@ __device__ __forceinline__ void slot_sort_pass(const uint32_t (&xe)[IT], uint32_
     s_db[lane] = x - tot;
   }
   __syncthreads();
-  if (stamp) FH_PHASE(1, 6);
 #pragma unroll
   for (int i = 0; i < IT; i++) {
     const uint32_t q = uint32_t(w) * 64 * IT + uint32_t(i) * 64 + lane;
@@ -463,13 +424,13 @@ template <int IT>
 __device__ __forceinline__ void slot_sort_pass_n(const uint32_t (&xe)[IT], uint32_t *dst,
                                                  uint32_t c, int vb, int shift, int nbits,
                                                  uint32_t (*s_h)[1 << kDigit], uint32_t *s_db,
-                                                 bool zeroed, bool stamp) {
+                                                 bool zeroed) {
   switch (nbits) {
 #define FH_PASS_CASE(K) \
-  case K: slot_sort_pass<IT, K>(xe, dst, c, vb, shift, s_h, s_db, zeroed, stamp); break;
+  case K: slot_sort_pass<IT, K>(xe, dst, c, vb, shift, s_h, s_db, zeroed); break;
     FH_PASS_CASE(1) FH_PASS_CASE(2) FH_PASS_CASE(3) FH_PASS_CASE(4) FH_PASS_CASE(5)
 #undef FH_PASS_CASE
-    default: slot_sort_pass<IT, 6>(xe, dst, c, vb, shift, s_h, s_db, zeroed, stamp); break;
+    default: slot_sort_pass<IT, 6>(xe, dst, c, vb, shift, s_h, s_db, zeroed); break;
   }
 }
 
@@ -493,17 +454,17 @@ __device__ __forceinline__ const uint32_t *sort_chunk(const uint32_t (&xe)[IT], 
     return a;
   }
   if (hb <= kDigit) {
-    slot_sort_pass_n<IT>(xe, b, c, vb, 0, hb, s_h0, s_db, zeroed, true);
+    slot_sort_pass_n<IT>(xe, b, c, vb, 0, hb, s_h0, s_db, zeroed);
     return b;
   }
-  slot_sort_pass<IT, kDigit>(xe, b, c, vb, 0, s_h0, s_db, zeroed, true);
+  slot_sort_pass<IT, kDigit>(xe, b, c, vb, 0, s_h0, s_db, zeroed);
   uint32_t x2[IT];
 #pragma unroll
   for (int i = 0; i < IT; i++) {
     const uint32_t q = w * 64 * IT + uint32_t(i) * 64 + lane;
     x2[i] = q < c ? b[q] : 0u;
   }
-  slot_sort_pass_n<IT>(x2, a, c, vb, kDigit, hb - kDigit, s_h1, s_db, zeroed, false);
+  slot_sort_pass_n<IT>(x2, a, c, vb, kDigit, hb - kDigit, s_h1, s_db, zeroed);
   return a;
 }
 
@@ -545,21 +506,8 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
   const uint32_t tid = threadIdx.x;
   const uint32_t vmask = (1u << vb) - 1;
   uint32_t xe[IT];
-#ifdef FH_ABL_NOGATHER  // diagnostic builds only: contiguous loads instead
-  for (int i = 0; i < IT; i++) {
-    const uint32_t q = (threadIdx.x >> 6) * 64 * IT + uint32_t(i) * 64 + (threadIdx.x & 63);
-    xe[i] = q < Nb ? part[q] : 0u;
-  }
-#else
   gather_items<IT>(part, s_rs, s_src, tiles, 0, Nb, xe);
-#endif
-  FH_PHASE(1, 1);
-#ifdef FH_ABL_NOSORT  // diagnostic builds only: timing without the sort
-  const uint32_t *S = sort_chunk<IT>(xe, s_a, s_b, Nb, vb, 0, s_h0, s_h1, s_db, true);
-#else
   const uint32_t *S = sort_chunk<IT>(xe, s_a, s_b, Nb, vb, hb, s_h0, s_h1, s_db, true);
-#endif
-  FH_PHASE(1, 2);
   if (staged) {
     for (uint32_t j = tid; j < Nb; j += kOThreads) {
       const uint32_t e = S[j], slot = e >> vb, vid = e & vmask;
@@ -574,7 +522,6 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
         note_hot(S, j, slot, vb, mk, hot_min, cand);
       }
     }
-    FH_PHASE(1, 3);
     return;
   }
   for (uint32_t j = tid; j < Nb; j += kOThreads) {
@@ -587,7 +534,6 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
     dep_sorted[pos] = head ? latest[mk] : uint64_t(S[j - 1] & vmask) + 1;
   }
   __syncthreads();  // every head has read latest
-  FH_PHASE(1, 3);
   for (uint32_t j = tid; j < Nb; j += kOThreads) {
     const uint32_t e = S[j], slot = e >> vb;
     if (j + 1 == Nb || (S[j + 1] >> vb) != slot) {
@@ -673,9 +619,6 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
                                              const uint32_t *__restrict__ hot_snap,
                                              uint32_t hot_min, uint32_t *__restrict__ cand,
                                              unsigned char *smem) {
-  const uint32_t fh_bid = b;
-  (void)fh_bid;
-  FH_STAMP_BEGIN();
   constexpr int HMAX = 1 << kSlotBits;
   constexpr int ND = 1 << kDigit;
   uint32_t *s_a = reinterpret_cast<uint32_t *>(smem + OrderSmem::a);
@@ -720,11 +663,7 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
   // is loaded now and staged in LDS before the sort, when it is not much
   // larger than an average bucket; the loads overlap the scan and gather.
   constexpr int LR = (1 << kSlotBits) / kOThreads;
-#ifdef FH_ABL_NOSTAGE  // diagnostic builds only
-  const bool staged = false;
-#else
   const bool staged = !hot && H <= 2u * ((uint32_t(tiles) * uint32_t(kTile)) >> bb);
-#endif
   uint64_t lv[LR];
   if (staged) {
 #pragma unroll
@@ -744,7 +683,6 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
   }
   if (tid == 0) s_rs[tiles] = Nb;
   if (Nb == 0) {  // uniform
-    FH_STAMP_END(1, 0);
     return;
   }
   if (staged) {
@@ -755,12 +693,10 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
     }
   }
   __syncthreads();
-  FH_PHASE(1, 0);
 
   if (hot) {
     order_hot(Nb, gbase, hot_snap[b - B], vb, kinv, kmask, tiles, part, log_base, latest, sk, sv,
               dep_sorted, s_a, s_rs, s_src);
-    FH_STAMP_END(1, Nb);
     return;
   }
   if (Nb <= uint32_t(kChunk)) {
@@ -772,7 +708,6 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
     else if (Nb <= 6144) FH_ORDER_SINGLE(6);
     else FH_ORDER_SINGLE(8);
 #undef FH_ORDER_SINGLE
-    FH_STAMP_END(1, Nb);
     return;
   }
 
@@ -866,7 +801,6 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
       }
     }
   }
-  FH_STAMP_END(1, Nb);
 }
 
 // Arguments of the two roles (kernel arguments by value).

@@ -93,6 +93,11 @@ class HipKeyDeps:
         self._live = {}
         self._slots = {}
         self._noop = None
+        # the shards of the deps the last add_cmd / add_noop returned, taken
+        # before that call released the slots it replaced (the returned deps
+        # are exactly the dots it displaced: fantoch_hip/src/keydeps.rs builds
+        # its Dependency values before set_slot for the same reason)
+        self._returned = {}
 
     def close(self):
         if getattr(self, "_h", None):
@@ -126,11 +131,23 @@ class HipKeyDeps:
             if e[1] == 0:
                 del self._live[dot]
 
+    def _shards_of(self, d):
+        e = self._live.get(d)
+        if e is not None:
+            return e[0]
+        return self._returned.get(d)
+
     def dependencies(self, dots) -> set:
-        """Dots -> Dependency values, shards from the live slots (None when no
-        slot holds the dot any more, or for a noop)."""
+        """Dots -> Dependency values, shards from the live slots or from the
+        last add_cmd / add_noop's returned deps (None when neither holds the
+        dot any more, or for a noop)."""
         with self._lock:
-            return {Dependency(d, self._live[d][0] if d in self._live else None) for d in dots}
+            return {Dependency(d, self._shards_of(d)) for d in dots}
+
+    def _snapshot(self, deps) -> set:
+        out = set(int(x) for x in deps)
+        self._returned = {d: self._live[d][0] for d in out if d in self._live}
+        return out
 
     # -- KeyDeps ---------------------------------------------------------
     def add_cmd(self, dot: int, cmd, past: Optional[Iterable[int]] = None) -> set:
@@ -146,24 +163,26 @@ class HipKeyDeps:
             # read-only command under LockedKeyDeps, locked.rs:100-117)
             shards = frozenset(cmd.shards()) if hasattr(cmd, "shards") else None
             slot_ro = self.read_write and read_only
+            result = self._snapshot(deps[off[0]:off[1]])
             for k in kid:
                 self._hold(dot, shards)
                 old = self._slots.get((k, slot_ro))
                 self._slots[(k, slot_ro)] = dot
                 if old is not None:
                     self._release(old)
-            return set(int(x) for x in deps[off[0]:off[1]])
+            return result
 
     def add_noop(self, dot: int) -> set:
         with self._lock:
             off, deps = self.add_batch([dot], [[]], [True], None,
                                        read_only=[False] if self.read_write else None)
             # the latest noop (sequential.rs:66-70); keys' slots are unchanged
+            result = self._snapshot(deps[off[0]:off[1]])
             self._hold(dot, None)
             old, self._noop = self._noop, dot
             if old is not None:
                 self._release(old)
-            return set(int(x) for x in deps[off[0]:off[1]])
+            return result
 
     def cmd_deps(self, cmd) -> set:
         with self._lock:

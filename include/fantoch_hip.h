@@ -227,6 +227,18 @@ fh_status fh_graph_pending(fh_graph *h, size_t *count);
  * indexed; the dots PendingIndex waits on, index.rs:171-205). */
 fh_status fh_graph_missing(fh_graph *h, uint64_t *dots, size_t cap,
                            size_t *len);
+/* Fault injection and a self-test of the small pass's completion wait
+ * (tests only; no reference counterpart: the reference's executor cannot
+ * hang on a device).  fh_graph_inject_small_delay makes every later small
+ * pass (graph_small.hip) wait delay_us on the device before it starts, and
+ * sets the host's completion deadline to deadline_ms (0 keeps the default,
+ * 30,000): a pass that misses it returns FH_EHIP with fh_last_error() set,
+ * and the handle then refuses every call but fh_graph_destroy (which waits
+ * for the kernel).  fh_selftest_poll_deadline runs the same host wait
+ * against a stream that never completes (no GPU needed) and returns the
+ * status it raised: FH_EHIP. */
+fh_status fh_graph_inject_small_delay(fh_graph *h, uint32_t delay_us, uint32_t deadline_ms);
+fh_status fh_selftest_poll_deadline(uint32_t deadline_ms);
 
 /* ---- Partial replication: requests and replies between shards ----------
  * (graph/mod.rs:139-157, 168-179, 279-408; index.rs:145-211;

@@ -70,3 +70,18 @@ def test_zipf_is_skewed_like_the_zipf_crate():
     H = np.sum(np.arange(1, K + 1, dtype=np.float64) ** -sexp)
     p0 = c[u == 0][0] / len(s.keys)
     assert abs(p0 - 1 / H) < 0.01
+
+
+def test_small_pass_wait_has_a_deadline():
+    """graph_small's host wait (graph_small.h poll_completion) against a
+    stream that never completes: FH_EHIP with fh_last_error set after the
+    deadline, instead of spinning (no GPU involved)."""
+    import time
+    lib = L.load()
+    t0 = time.perf_counter()
+    st = lib.fh_selftest_poll_deadline(50)
+    dt = time.perf_counter() - t0
+    assert st == L.FH_EHIP
+    assert b"did not complete within 50 ms" in lib.fh_last_error()
+    assert 0.04 < dt < 5.0
+    assert lib.fh_selftest_poll_deadline(0) == L.FH_EINVAL

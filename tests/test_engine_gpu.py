@@ -351,7 +351,6 @@ print("ok")
     {},
     {"FH_KO_SIDE": "0"},
     {"FH_KEYORDER": "0"},
-    {"FH_KEYORDER": "0", "FH_CODE_REGIONS": "0"},
     {"FH_VIEW_CMD": "0"},
     {"FH_VIEW_CMD": "0", "FH_PLACE_SLACK": "0"},
 ])

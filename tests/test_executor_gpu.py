@@ -380,3 +380,32 @@ print(json.dumps(out))
     # the 2-key stream at batch 1 crosses 1024 pending while below 2048
     pend = res[0][3][2]
     assert any(1024 < x < 2047 for x in pend), max(pend)
+
+
+def test_small_pass_deadline_returns_ehip():
+    """A small pass (graph_small.hip) that does not finish by the host's
+    deadline fails the call with FH_EHIP and fh_last_error set instead of
+    spinning (graph_small.h poll_completion).  Fault injection: the kernel
+    waits 300 ms before it starts, the deadline is 20 ms.  The handle then
+    refuses further calls; destroying it waits for the kernel."""
+    from fantoch_amd import _lib as L
+    ex = HipGraphExecutor(process_id=1, shard_id=0, n=5, f=1, key_space=64)
+    a = D([1, 1])
+    ex.handle(GraphExecutionInfo.add(a, Command(a, ["x"]), []))
+    assert ex.to_clients() is not None
+    lib = L.load()
+    L.check(lib.fh_graph_inject_small_delay(ex._h, 300_000, 20))
+    b = D([2, 1])
+    with pytest.raises(L.FhError) as e:
+        ex.handle(GraphExecutionInfo.add(b, Command(b, ["x"]), [a]))
+    assert e.value.status == L.FH_EHIP
+    assert "did not complete within 20 ms" in str(e.value)
+    with pytest.raises(L.FhError) as e2:
+        ex.pending()
+    assert e2.value.status == L.FH_EHIP
+    ex.close()
+    # a fresh handle is unaffected
+    ex2 = HipGraphExecutor(process_id=1, shard_id=0, n=5, f=1, key_space=64)
+    ex2.handle(GraphExecutionInfo.add(a, Command(a, ["x"]), []))
+    assert ex2.to_clients() is not None
+    ex2.close()

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from conftest import D, Interner, UD, load_golden
-from fantoch_amd.keydeps import HipKeyDeps
+from fantoch_amd.keydeps import Dependency, HipKeyDeps
 from fantoch_amd.workload import Workload
 from oracle import oracle as O
 
@@ -36,6 +36,35 @@ def test_add_cmd_returns_sequential_deps_and_past_union():
     assert kd.add_cmd(c, ["y"], past) == past | {b}
     assert kd.add_noop(D([5, 1])) == {b, c}
     assert kd.add_cmd(D([5, 2]), ["z"]) == {D([5, 1])}
+
+
+class _Cmd:
+    """keys(shard) / shards() of a command (fantoch/src/command.rs:95-110)."""
+
+    def __init__(self, keys, shards):
+        self._keys, self._shards = keys, shards
+
+    def keys(self, shard_id):
+        return self._keys
+
+    def shards(self):
+        return self._shards
+
+
+def test_returned_deps_keep_their_shards():
+    """add_cmd(B) returns exactly the dot B displaced from x's slot, so the
+    Dependency values of that result still carry A's shards
+    (Dependency::from_cmd, keys/mod.rs:25-30), as the Rust shim builds them
+    before set_slot (fantoch_hip/src/keydeps.rs)."""
+    kd = HipKeyDeps(0, key_space=64)
+    a, b, n = D([1, 1]), D([2, 1]), D([3, 1])
+    assert kd.add_cmd(a, _Cmd(["x"], [0, 2])) == set()
+    deps = kd.add_cmd(b, _Cmd(["x"], [0]))
+    assert deps == {a}
+    assert kd.dependencies(deps) == {Dependency(a, frozenset({0, 2}))}
+    # a noop's deps carry the shards of the key slots it read
+    nd = kd.add_noop(n)
+    assert kd.dependencies(nd) == {Dependency(b, frozenset({0}))}
 
 
 def _oracle_csr(dots, key_off, keys, is_noop=None):
