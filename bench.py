@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=16_000_000,
                     help="C4 commands in the CPU-baseline prefix (~10 s of one host core)")
     ap.add_argument("--probe", default="sort_scatter,sort_scatter_dots,sort_scatter_v3,graph_tile,cmd_search,"
-                    "view_records,cmd_pack,code_scatter,row_union,ko_final,"
+                    "view_records,cmd_pack,code_scatter,row_place,ko_final,"
                     "cmd_union,prev_bucket,place,log_keys",
                     help="kernels whose launches are timed in the probe pass")
     ap.add_argument("--no-phases", action="store_true", help="skip the per-phase profile pass")

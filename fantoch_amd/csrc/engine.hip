@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "engine_internal.h"
+#include "hoststage.h"
 #include "graph_core.h"
 #include "keybucket.h"
 #include "sort_impl.h"
@@ -599,6 +600,7 @@ __global__ void __launch_bounds__(kThreads)
 // a cache-sized slice of the code array (a random 12-B store per command over
 // the whole array ran at 4.6 ms per 100M commands, confined to 4M-command
 // regions at 1.7 ms: tools/scatter_bench.hip, profiles/r05_scatter_bench.jsonl).
+static const int kDiag = getenv("FH_DIAG") ? atoi(getenv("FH_DIAG")) : 0;  // DIAG
 constexpr int kSrchHalo = 128;
 constexpr int kSrchMaxRep = 8;  // replicas (logs) of the command-level path
 constexpr uint32_t kNoArr = ~0u;
@@ -853,27 +855,32 @@ __global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *
                             const VS *__restrict__ vals, const uint8_t *__restrict__ tailm,
                             const uint8_t *__restrict__ mrem, uint64_t *__restrict__ latest,
                             uint64_t log_base) {
-  // four commands' tail masks per load (the buffer is padded to a word):
-  // most are zero, and the side stream runs this with few waves per CU, so
-  // each thread's loop is bound by its loads' latency
-  const uint32_t nw = (n + 3) / 4;
+  // sixteen commands' tail masks per load (the buffer is padded to 16
+  // bytes): most are zero, and the side stream runs this with few waves per
+  // CU, so each thread's loop is bound by its loads' latency
+  const uint32_t nw = (n + 15) / 16;
   GRID_STRIDE(w, nw) {
-    uint32_t msk4 = reinterpret_cast<const uint32_t *>(tailm)[w];
-    while (msk4) {
-      const uint32_t b = uint32_t(__builtin_ctz(msk4)) >> 3;
-      const uint32_t i = 4 * w + b;
-      const uint32_t msk = (msk4 >> (8 * b)) & 0xFFu;
-      msk4 &= ~(0xFFu << (8 * b));
-      if (i >= n) break;
-      const uint32_t rm = mrem[i];
-      const uint32_t kw = kws[i];
-      const uint64_t v = vload(vals, i);
-      const uint64_t m = cm.meta(kw, v);
-      const uint32_t key = kw & cm.kmask, c = uint32_t(v & cm.cmask);
-      for (uint32_t j = 0; j < cm.fq; j++) {
-        const uint32_t r = cm.rep(m, j);
-        if ((msk & (1u << j)) && !(rm & (1u << r)))
-          latest[uint64_t(r + 1) * K + key] = kLogFlag | (log_base + c);
+    const uint4 m16 = reinterpret_cast<const uint4 *>(tailm)[w];
+    const uint32_t mw[4] = {m16.x, m16.y, m16.z, m16.w};
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+      uint32_t msk4 = mw[h];
+      while (msk4) {
+        const uint32_t b = uint32_t(__builtin_ctz(msk4)) >> 3;
+        const uint32_t i = 16 * w + 4 * h + b;
+        const uint32_t msk = (msk4 >> (8 * b)) & 0xFFu;
+        msk4 &= ~(0xFFu << (8 * b));
+        if (i >= n) break;
+        const uint32_t rm = mrem[i];
+        const uint32_t kw = kws[i];
+        const uint64_t v = vload(vals, i);
+        const uint64_t m = cm.meta(kw, v);
+        const uint32_t key = kw & cm.kmask, c = uint32_t(v & cm.cmask);
+        for (uint32_t j = 0; j < cm.fq; j++) {
+          const uint32_t r = cm.rep(m, j);
+          if ((msk & (1u << j)) && !(rm & (1u << r)))
+            latest[uint64_t(r + 1) * K + key] = kLogFlag | (log_base + c);
+        }
       }
     }
   }
@@ -891,65 +898,103 @@ __global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *
 // the per-key sequence itself (groups never straddle keys), and only the
 // per-command outputs travel back to command order.
 
-// The committed deps of each command in command order from its fq entries
-// (k_code_scatter of the key-order records): 0 none, 0x80000000 | x the log
-// reference of an earlier batch's latest entry, else a packed in-batch dot.
-// Dots are unique per command, so the count is the number of distinct
-// nonzero entries (a log reference never equals a packed dot: top bit).
+// The key-order path's committed deps (QuorumDeps union, quorum.rs:28-98)
+// straight from the search's region records: each record's fq entries (0
+// none, 0x80000000 | x an earlier batch's log reference, else an in-batch
+// packed dot) as dots, sorted and deduplicated into the command's row of fq
+// slots, empty slots holding the reserved all-ones dot (stage_logs rejects
+// it as a dot).  One pass: no command-order entry array, count pass or scan
+// (pack_dep_rows builds the ABI's CSR from the rows when results() asks).
+// Records are region-major, so the row stores of a moment stay in one or
+// two regions' slices of `rows`.  An external dot equal to an in-batch one
+// (a dot of the batch repeating an earlier batch's) sets *err, as the
+// general union reports it.
+// 16 bytes at 8-byte alignment (one global_store_dwordx4)
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(8)));
 template <uint32_t FQ>
-__global__ void k_row_count(uint32_t n, const uint32_t *__restrict__ ent, uint32_t *__restrict__ cnt) {
-  GRID_STRIDE(i, n) {
-    uint32_t e[FQ];
+__device__ __forceinline__ void row_place_one(const uint4 o, const uint64_t *__restrict__ dlog,
+                                              int sb, uint64_t *__restrict__ rows,
+                                              uint32_t *__restrict__ err) {
+  const uint32_t e[3] = {o.y, o.z, o.w};
+  uint64_t r[FQ];
+  uint32_t codes = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < FQ; j++) e[j] = ent[size_t(i) * FQ + j];
-    uint32_t c = 0;
+  for (uint32_t j = 0; j < FQ; j++) {
+    bool dup = e[j] == 0u;
 #pragma unroll
-    for (uint32_t j = 0; j < FQ; j++) {
-      bool dup = e[j] == 0u;
+    for (uint32_t q = 0; q < j; q++) dup |= e[q] == e[j];
+    codes += dup ? 0u : 1u;
+    r[j] = e[j] == 0u ? ~0ull
+           : (e[j] & 0x80000000u) ? dlog[e[j] & 0x7FFFFFFFu]
+                                  : (uint64_t(e[j] >> sb) << 56) | (e[j] & ((1u << sb) - 1));
+  }
 #pragma unroll
-      for (uint32_t q = 0; q < j; q++) dup |= e[q] == e[j];
-      c += dup ? 0u : 1u;
+  for (uint32_t a = 0; a < FQ; a++)
+#pragma unroll
+    for (uint32_t b2 = a + 1; b2 < FQ; b2++) {
+      const uint64_t x = r[a], y = r[b2];
+      r[a] = x < y ? x : y;
+      r[b2] = x < y ? y : x;
     }
+  // the unique dots first, then the sentinel
+  uint64_t w[FQ];
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < FQ; j++) w[j] = ~0ull;
+#pragma unroll
+  for (uint32_t j = 0; j < FQ; j++)
+    if (r[j] != ~0ull && (j == 0 || r[j] != r[j - 1])) {
+#pragma unroll
+      for (uint32_t q = 0; q < FQ; q++)
+        if (q == m) w[q] = r[j];
+      m++;
+    }
+  if (m != codes) atomicOr(err, 1u);
+  // the row in as few store instructions as it takes (a scattered store
+  // costs the address unit a line per lane whatever its width, and the
+  // tile kernel beside this one waits on the same unit)
+  uint64_t *d = rows + size_t(o.x) * FQ;
+  if constexpr (FQ == 3) {
+    *reinterpret_cast<u32x4u *>(d) =
+        u32x4u{uint32_t(w[0]), uint32_t(w[0] >> 32), uint32_t(w[1]), uint32_t(w[1] >> 32)};
+    d[2] = w[2];
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < FQ; j++) d[j] = w[j];
+  }
+}
+// One record per thread per trip: eight per trip (loads issued together)
+// doubled it beside the tile kernel, 3.1 -> 7.0 ms, and slowed the tile
+// kernel 5.3 -> 7.5 ms -- more random row stores in flight congest the
+// write path the tile kernel's own stores wait on.
+template <uint32_t FQ>
+__global__ void __launch_bounds__(256)
+    k_row_place(uint32_t n, const uint4 *__restrict__ rec, const uint64_t *__restrict__ dlog,
+                int sb, uint64_t *__restrict__ rows, uint32_t *__restrict__ err, int diag) {
+  if (diag & 2) {  // DIAG: reads only
+    uint32_t acc = 0;
+    GRID_STRIDE(i, n) acc += rec[i].y;
+    if (acc == 0x12345678u) atomicOr(err, 2u);
+    return;
+  }
+  GRID_STRIDE(i, n) row_place_one<FQ>(rec[i], dlog, sb, rows, err);
+}
+
+// Rows -> CSR (results(), outside the run): the length of every row, then
+// (after a scan) each row's dots at its offset.
+__global__ void k_rows_count(uint32_t n, uint32_t fq, const uint64_t *__restrict__ rows,
+                             uint32_t *__restrict__ cnt) {
+  GRID_STRIDE(i, n) {
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < fq; j++) c += rows[size_t(i) * fq + j] != ~0ull;
     cnt[i] = c;
   }
 }
-
-// (An external dot equal to an in-batch one -- a dot of the batch repeating
-// an earlier batch's -- shortens the row below its count: err, as the
-// general union reports it.)
-template <uint32_t FQ>
-__global__ void k_row_union(uint32_t n, const uint32_t *__restrict__ ent,
-                            const uint64_t *__restrict__ dlog, int sb,
-                            const uint32_t *__restrict__ off, uint64_t *__restrict__ dep,
-                            uint32_t *__restrict__ err) {
+__global__ void k_rows_compact(uint32_t n, uint32_t fq, const uint64_t *__restrict__ rows,
+                               const uint32_t *__restrict__ off, uint64_t *__restrict__ dep) {
   GRID_STRIDE(i, n) {
-    uint64_t r[FQ];
-#pragma unroll
-    for (uint32_t j = 0; j < FQ; j++) {
-      const uint32_t e = ent[size_t(i) * FQ + j];
-      r[j] = e == 0u ? ~0ull
-             : (e & 0x80000000u) ? dlog[e & 0x7FFFFFFFu]
-                                 : (uint64_t(e >> sb) << 56) | (e & ((1u << sb) - 1));
-    }
-    // sort the FQ (<= 3) dots, then write the unique ones
-#pragma unroll
-    for (uint32_t a = 0; a < FQ; a++)
-#pragma unroll
-      for (uint32_t b2 = a + 1; b2 < FQ; b2++) {
-        const uint64_t x = r[a], y = r[b2];
-        r[a] = x < y ? x : y;
-        r[b2] = x < y ? y : x;
-      }
-    uint64_t *d = dep + off[i];
-    const uint32_t cap = off[i + 1] - off[i];
-    uint32_t m = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < FQ; j++)
-      if (r[j] != ~0ull && (j == 0 || r[j] != r[j - 1])) {
-        if (m < cap) d[m] = r[j];
-        m++;
-      }
-    if (m != cap) atomicOr(err, 1u);
+    const uint32_t o = off[i], c = off[i + 1] - o;
+    for (uint32_t j = 0; j < c; j++) dep[o + j] = rows[size_t(i) * fq + j];
   }
 }
 
@@ -1512,32 +1557,20 @@ __global__ void __launch_bounds__(256)
 }
 
 // results: single-view sorted deps -> per-command dep dots
-__global__ void k_sv_unpermute(uint32_t M, const uint32_t *__restrict__ vs,
-                               const uint64_t *__restrict__ dep_sorted,
-                               const uint64_t *__restrict__ dot, const uint64_t *__restrict__ dlog,
-                               uint64_t *__restrict__ dep_dot, uint32_t *__restrict__ cnt) {
+// Single view: each command's one dependency slot, from sorted order to its
+// command's row (rows of one slot, the reserved all-ones dot for none:
+// results() packs the rows into the ABI's CSR, so no count, scan or
+// compaction runs in the step).
+__global__ void k_sv_rows(uint32_t M, const uint32_t *__restrict__ vs,
+                          const uint64_t *__restrict__ dep_sorted,
+                          const uint64_t *__restrict__ dot, const uint64_t *__restrict__ dlog,
+                          uint64_t *__restrict__ rows) {
   GRID_STRIDE(j, M) {
     const uint64_t x = dep_sorted[j];
-    const uint32_t c = vs[j];
-    dep_dot[c] = is_log_ref(x) ? dlog[x - kLogFlag]  // an earlier batch
-                 : (x != 0 && (x >> 56) == 0) ? dot[x - 1]  // in-batch index + 1
-                 : x;
-    cnt[c] = x != 0;  // the CSR row length (one slot per command)
-  }
-}
-
-// one slot per command: CSR compaction, and for a trivially ordered batch
-// (singleton SCCs in arrival order) label = own dot, rank = position
-__global__ void k_sv_compact(uint32_t n, const uint64_t *__restrict__ dd,
-                             const uint32_t *__restrict__ off, uint64_t *__restrict__ out,
-                             const uint64_t *__restrict__ dot, uint64_t *__restrict__ lab,
-                             uint32_t *__restrict__ rank) {
-  GRID_STRIDE(i, n) {
-    if (off[i + 1] != off[i]) out[off[i]] = dd[i];
-    if (lab) {
-      lab[i] = dot[i];
-      rank[i] = i;
-    }
+    rows[vs[j]] = x == 0 ? ~0ull
+                  : is_log_ref(x) ? dlog[x - kLogFlag]  // an earlier batch
+                  : (x >> 56) == 0 ? dot[x - 1]         // in-batch index + 1
+                                   : x;
   }
 }
 
@@ -1698,6 +1731,12 @@ struct EngineDevice {
   DBuf<uint32_t> sk32a, sk32b, sva, svb, dep_cnt, dst, sorted_vid, rank_tmp, u32tmp;
   // outputs of the last run (materialised inside run(), copied by results())
   bool deps_direct = false;  // run_general wrote o_dep_off / o_dep (no compaction)
+  // the key-order path wrote each command's committed deps as a row of
+  // deps_rows slots (o_rows); results() packs them into o_dep_off / o_dep
+  // once (rows_packed)
+  uint32_t deps_rows = 0;
+  bool rows_packed = false;
+  DBuf<uint64_t> o_rows;
   bool sv_labels_done = false;  // k_sv_compact wrote the trivial labels / ranks
   DBuf<uint32_t> o_dep_off;
   DBuf<uint64_t> o_dep;
@@ -1731,6 +1770,7 @@ struct EngineDevice {
     return e && *e == '0';
   }();
   DBuf<uint64_t> cv64a, cv64b;  // command-level views path: packed sort values
+  PinnedRing ring;              // staging uploads (hoststage.h)
   std::vector<uint32_t> h_win;  // per batch: the logs' inversion span W (stage_logs)
   // per batch: (seq bits, packed bits) of its dots, src << sb | seq (0: wider
   // than 32 bits), so the per-key sort can move 4-byte dots
@@ -1801,7 +1841,9 @@ struct EngineDevice {
     {
       int cus = 0;
       FH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-      side_grid = 2u * unsigned(std::max(cus, 1));
+      // (measurement, round 6: FH_SIDE_WG workgroups per CU)
+      const char *e = getenv("FH_SIDE_WG");
+      side_grid = unsigned(e ? std::max(1, atoi(e)) : 2) * unsigned(std::max(cus, 1));
     }
     FH_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     FH_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
@@ -1966,6 +2008,85 @@ struct EngineDevice {
     stage_logs(d, nb, h_dot, h_key, off.data(), cmd.data());
   }
 
+  // Command logs of nb batches (stage_logs): validated per batch on
+  // host_threads() threads and uploaded to dl.  Entry q of log r (command c)
+  // is c·fq + j with j = the number of lower logs holding c: each command's
+  // membership mask (bit r, set atomically; a bit set twice is a replica
+  // processing c twice) gives j as a popcount, and every mask must hold
+  // exactly fq bits.  h_win[b] = the logs' inversion span W, max over
+  // entries of (the log's running maximum - c), combined across slices as
+  // max(slice win, earlier slices' maximum - slice minimum).
+  template <class M>
+  void views_entries(size_t nb, size_t n, uint32_t fq, size_t np, const uint64_t *h_off,
+                     const uint32_t *h_cmd, uint32_t *dl) {
+    std::vector<M> mask(n);
+    h_win.assign(nb, 0);
+    struct Seg {
+      uint32_t r, maxc, minc, win;
+    };
+    for (size_t b = 0; b < nb; b++) {
+      if (b)
+        par_for(n, size_t(1) << 22, [&](size_t, size_t l, size_t h) {
+          std::memset(mask.data() + l, 0, (h - l) * sizeof(M));
+        });
+      const uint64_t base = h_off[b * np], cnt = uint64_t(n) * fq;
+      const uint64_t *lb = h_off + b * np;  // this batch's np + 1 log bounds
+      // the log holding global entry q
+      auto log_of = [&](uint64_t q) {
+        return uint32_t(std::upper_bound(lb, lb + np + 1, q) - lb) - 1;
+      };
+      std::vector<std::vector<Seg>> segs(host_threads());
+      par_for(cnt, size_t(1) << 20, [&](size_t part, size_t l, size_t h) {
+        auto &sg = segs[part];
+        uint64_t q = base + l;
+        uint32_t r = log_of(q);
+        while (q < base + h) {
+          while (lb[r + 1] <= q) r++;
+          const uint64_t e = std::min<uint64_t>(base + h, lb[r + 1]);
+          const M bit = M(M(1) << r);
+          Seg g{r, 0, ~0u, 0};
+          uint32_t pmax = 0;
+          for (; q < e; q++) {
+            const uint32_t c = h_cmd[q];
+            FH_CHECK(c < n, FH_EINVAL, "logs: command index >= n");
+            const M old = __atomic_fetch_or(&mask[c], bit, __ATOMIC_RELAXED);
+            FH_CHECK(!(old & bit), FH_EINVAL, "logs: a replica processes a command once");
+            pmax = std::max(pmax, c);
+            g.win = std::max(g.win, pmax - c);
+            g.minc = std::min(g.minc, c);
+          }
+          g.maxc = pmax;
+          sg.push_back(g);
+        }
+      });
+      std::vector<uint32_t> run_max(np, 0);
+      std::vector<bool> started(np, false);
+      uint32_t w = 0;
+      for (auto &sg : segs)
+        for (const Seg &g : sg) {
+          w = std::max(w, g.win);
+          if (started[g.r] && run_max[g.r] > g.minc) w = std::max(w, run_max[g.r] - g.minc);
+          run_max[g.r] = started[g.r] ? std::max(run_max[g.r], g.maxc) : g.maxc;
+          started[g.r] = true;
+        }
+      h_win[b] = w;
+      par_for(n, size_t(1) << 20, [&](size_t, size_t l, size_t h) {
+        for (size_t c = l; c < h; c++)
+          FH_CHECK(uint32_t(__builtin_popcountll(uint64_t(mask[c]))) == fq, FH_EINVAL,
+                   "logs: every command must appear in exactly `views` replica logs");
+      });
+      ring.upload(dl + base, cnt, [&](uint32_t *o, size_t first, size_t k) {
+        uint64_t q = base + first;
+        uint32_t r = log_of(q);
+        for (size_t x = 0; x < k; x++, q++) {
+          while (lb[r + 1] <= q) r++;
+          const uint32_t c = h_cmd[q];
+          o[x] = uint32_t(c * fq + uint32_t(__builtin_popcountll(uint64_t(mask[c]) & ((uint64_t(1) << r) - 1))));
+        }
+      }, stream);
+    }
+  }
+
   // log_off[nb·nproc + 1] (global offsets into log_cmd), log_cmd[] batch-local
   // command indices; every command appears in exactly `views` logs, at most
   // once per log
@@ -1995,82 +2116,67 @@ struct EngineDevice {
     FH_HIP(hipSetDevice(device));
     sync_all();
     const size_t n = d.n, nk = n * d.keys_per_cmd;
-    std::vector<uint32_t> k32(nk * nb);
-    for (size_t e = 0; e < nk * nb; e++) {
-      FH_CHECK(h_key[e] < key_space, FH_EINVAL, "stage: key id >= key_space");
-      k32[e] = uint32_t(h_key[e]);
+    // Validation first, on host_threads() threads (no device state changes
+    // until the whole stream is accepted), then the uploads through pinned
+    // chunks (hoststage.h); round 5 ran these loops on one thread with
+    // pageable copies: 1,037 ms per 100M C4 commands.
+    par_for(nk * nb, size_t(1) << 20, [&](size_t, size_t lo_, size_t hi_) {
+      for (size_t e = lo_; e < hi_; e++)
+        FH_CHECK(h_key[e] < key_space, FH_EINVAL, "stage: key id >= key_space");
+    });
+    // the all-ones dot, (255, 2^56 - 1), is the union's empty-slot sentinel;
+    // per batch the widest source and sequence (the 32-bit packing)
+    std::vector<std::pair<int, int>> dpack(nb, {0, 0});
+    for (size_t b = 0; b < nb; b++) {
+      std::vector<std::pair<uint64_t, uint64_t>> mx(host_threads(), {0, 0});
+      par_for(n, size_t(1) << 20, [&](size_t part, size_t lo_, size_t hi_) {
+        uint64_t ms = 0, mq = 0;
+        for (size_t i = b * n + lo_; i < b * n + hi_; i++) {
+          const uint64_t x = h_dot[i];
+          FH_CHECK(x != ~0ull && (x >> 56) != 0, FH_EINVAL,
+                   "stage: dot (255, 2^56 - 1) is reserved and ProcessId 0 is not a process");
+          ms = std::max<uint64_t>(ms, x >> 56);
+          mq = std::max<uint64_t>(mq, x & 0x00FFFFFFFFFFFFFFull);
+        }
+        mx[part] = {ms, mq};
+      });
+      uint64_t ms = 0, mq = 0;
+      for (auto &m : mx) {
+        ms = std::max(ms, m.first);
+        mq = std::max(mq, m.second);
+      }
+      const int sb = bits_for(mq + 1), pb = sb + bits_for(ms + 1);
+      dpack[b] = pb <= 32 ? std::make_pair(sb, pb) : std::make_pair(0, 0);
     }
-    // the all-ones dot, (255, 2^56 - 1), is the union's empty-slot sentinel
-    for (size_t i = 0; i < n * nb; i++)
-      FH_CHECK(h_dot[i] != ~0ull && (h_dot[i] >> 56) != 0, FH_EINVAL,
-               "stage: dot (255, 2^56 - 1) is reserved and ProcessId 0 is not a process");
-    std::vector<uint32_t> ent, lo;
-    if (d.views && elem) {
-      // element logs: every position (c·fq + j)·k + s of a batch in exactly
-      // one log (a replica may hold several of a command's key slots)
-      const size_t np = d.nproc, per_b = n * fq * d.keys_per_cmd;
-      FH_CHECK(h_off[0] == 0 && (subset ? h_off[np] <= per_b : h_off[nb * np] == per_b * nb),
-               FH_EINVAL, "element logs: every element position must appear in exactly one log");
-      ent.resize(subset ? size_t(h_off[np]) : per_b * nb);
+    const size_t np = d.nproc;
+    std::vector<uint32_t> lo;
+    const size_t per_b = n * fq * d.keys_per_cmd;  // element positions of a batch
+    if (d.views) {
+      FH_CHECK(elem ? (h_off[0] == 0 &&
+                       (subset ? h_off[np] <= per_b : h_off[nb * np] == per_b * nb))
+                    : (h_off[0] == 0 && h_off[nb * np] == n * fq * nb),
+               FH_EINVAL, elem ? "element logs: every element position must appear in exactly one log"
+                               : "logs: every command must appear in exactly `views` replica logs");
+      FH_CHECK(elem || np <= 64, FH_ENOTIMPL, "replica views: nproc <= 64");
       lo.resize(nb * (np + 1));
-      std::vector<uint8_t> seen(per_b);
-      h_win.assign(nb, 0);
       for (size_t b = 0; b < nb; b++) {
-        std::fill(seen.begin(), seen.end(), 0);
         const uint64_t base = h_off[b * np];
-        FH_CHECK(subset || h_off[(b + 1) * np] - base == per_b, FH_EINVAL,
-                 "element logs: a batch's logs must hold n * views * keys_per_cmd entries");
+        if (elem)
+          FH_CHECK(subset || h_off[(b + 1) * np] - base == per_b, FH_EINVAL,
+                   "element logs: a batch's logs must hold n * views * keys_per_cmd entries");
+        else
+          FH_CHECK(h_off[(b + 1) * np] - base == n * fq, FH_EINVAL,
+                   "logs: a batch's logs must hold n * views entries");
         for (size_t r = 0; r < np; r++) {
           lo[b * (np + 1) + r] = uint32_t(h_off[b * np + r] - base);
           FH_CHECK(h_off[b * np + r + 1] >= h_off[b * np + r], FH_EINVAL, "logs: offsets");
-          for (uint64_t q = h_off[b * np + r]; q < h_off[b * np + r + 1]; q++) {
-            const uint32_t p = h_cmd[q];
-            FH_CHECK(p < per_b && !seen[p], FH_EINVAL,
-                     "element logs: every element position must appear in exactly one log");
-            seen[p] = 1;
-            ent[q] = p;
-          }
         }
         lo[b * (np + 1) + np] = uint32_t(h_off[(b + 1) * np] - base);
       }
-    } else if (d.views) {
-      const size_t np = d.nproc;
-      FH_CHECK(h_off[0] == 0 && h_off[nb * np] == n * fq * nb, FH_EINVAL,
-               "logs: every command must appear in exactly `views` replica logs");
-      ent.resize(n * fq * nb);
-      lo.resize(nb * (np + 1));
-      std::vector<uint8_t> seen(n);
-      std::vector<int16_t> last_r(n);
-      h_win.assign(nb, 0);
-      for (size_t b = 0; b < nb; b++) {
-        std::fill(seen.begin(), seen.end(), 0);
-        std::fill(last_r.begin(), last_r.end(), -1);
-        const uint64_t base = h_off[b * np];
-        FH_CHECK(h_off[(b + 1) * np] - base == n * fq, FH_EINVAL,
-                 "logs: a batch's logs must hold n * views entries");
-        for (size_t r = 0; r < np; r++) {
-          lo[b * (np + 1) + r] = uint32_t(h_off[b * np + r] - base);
-          FH_CHECK(h_off[b * np + r + 1] >= h_off[b * np + r], FH_EINVAL, "logs: offsets");
-          uint32_t pmax = 0;  // inversion span of this log (command-level path)
-          for (uint64_t q = h_off[b * np + r]; q < h_off[b * np + r + 1]; q++) {
-            const uint32_t c = h_cmd[q];
-            pmax = std::max(pmax, c);
-            h_win[b] = std::max(h_win[b], pmax - c);
-            FH_CHECK(c < n, FH_EINVAL, "logs: command index >= n");
-            FH_CHECK(last_r[c] != int16_t(r), FH_EINVAL,
-                     "logs: a replica processes a command once");
-            FH_CHECK(seen[c] < fq, FH_EINVAL,
-                     "logs: every command must appear in exactly `views` replica logs");
-            last_r[c] = int16_t(r);
-            ent[q] = uint32_t(c * fq + seen[c]++);
-          }
-        }
-        lo[b * (np + 1) + np] = uint32_t(n * fq);
-        for (size_t c = 0; c < n; c++)
-          FH_CHECK(seen[c] == fq, FH_EINVAL,
-                   "logs: every command must appear in exactly `views` replica logs");
-      }
     }
+    // the device side from here: a stage that fails below leaves nothing staged
+    staged = false;
+    h_dpack = dpack;
     // append the batches' dots to the command log (grown by doubling, old
     // entries kept: earlier batches stay referenced by the latest table)
     const size_t need = log_len + n * nb + 1;
@@ -2086,18 +2192,7 @@ struct EngineDevice {
     FH_CHECK(log_len + n * nb < kLogFlag, FH_ENOTIMPL, "command log exceeds 2^48 commands");
     FH_CHECK(!d.views || log_len + n * nb < (size_t(1) << 31), FH_ENOTIMPL,
              "replica views: command log exceeds 2^31 commands (32-bit dependency codes)");
-    FH_HIP(hipMemcpyAsync(dot.get() + log_len, h_dot, n * nb * sizeof(uint64_t),
-                          hipMemcpyHostToDevice, stream));
-    h_dpack.assign(nb, {0, 0});
-    for (size_t b = 0; b < nb; b++) {
-      uint64_t ms = 0, mq = 0;
-      for (size_t i = b * n; i < (b + 1) * n; i++) {
-        ms = std::max<uint64_t>(ms, h_dot[i] >> 56);
-        mq = std::max<uint64_t>(mq, h_dot[i] & 0x00FFFFFFFFFFFFFFull);
-      }
-      const int sb = bits_for(mq + 1), pb = sb + bits_for(ms + 1);
-      h_dpack[b] = pb <= 32 ? std::make_pair(sb, pb) : std::make_pair(0, 0);
-    }
+    ring.upload_copy(dot.get() + log_len, h_dot, n * nb, stream);
     // the union's gathers read a packed copy of each batch's dots (input
     // layout, built here with the upload)
     {
@@ -2111,18 +2206,47 @@ struct EngineDevice {
                 uint32_t(n), dot.get() + log_len + b * n, h_dpack[b].first, d32 + b * n);
       }
     }
-    stage_base = log_len;
-    log_len += n * nb;
-    FH_HIP(hipMemcpyAsync(key32.ensure(nk * nb + 1), k32.data(), nk * nb * sizeof(uint32_t),
-                          hipMemcpyHostToDevice, stream));
+    ring.upload(key32.ensure(nk * nb + 1), nk * nb, [&](uint32_t *o, size_t first, size_t cnt) {
+      for (size_t e = 0; e < cnt; e++) o[e] = uint32_t(h_key[first + e]);
+    }, stream);
     if (d.views) {
-      FH_HIP(hipMemcpyAsync(lent.ensure(ent.size() + 1), ent.data(), ent.size() * sizeof(uint32_t),
-                            hipMemcpyHostToDevice, stream));
+      uint32_t *dl = lent.ensure(size_t(h_off[subset ? np : nb * np]) + 1);
+      if (elem) {
+        // every position once per batch (a byte per position, set atomically
+        // by the validating threads), then the entries as they are
+        std::vector<uint8_t> seen(per_b);
+        h_win.assign(nb, 0);
+        for (size_t b = 0; b < nb; b++) {
+          const uint64_t base = h_off[b * np], cnt = h_off[subset ? np : (b + 1) * np] - base;
+          if (b)
+            par_for(per_b, size_t(1) << 22, [&](size_t, size_t l, size_t h) {
+              std::memset(seen.data() + l, 0, h - l);
+            });
+          par_for(cnt, size_t(1) << 20, [&](size_t, size_t l, size_t h) {
+            for (uint64_t q = base + l; q < base + h; q++) {
+              const uint32_t pq = h_cmd[q];
+              FH_CHECK(pq < per_b && !__atomic_exchange_n(&seen[pq], uint8_t(1), __ATOMIC_RELAXED),
+                       FH_EINVAL, "element logs: every element position must appear in exactly one log");
+            }
+          });
+          ring.upload_copy(dl + base, h_cmd + base, cnt, stream);
+        }
+      } else if (np <= 8) {
+        views_entries<uint8_t>(nb, n, fq, np, h_off, h_cmd, dl);
+      } else if (np <= 16) {
+        views_entries<uint16_t>(nb, n, fq, np, h_off, h_cmd, dl);
+      } else if (np <= 32) {
+        views_entries<uint32_t>(nb, n, fq, np, h_off, h_cmd, dl);
+      } else {
+        views_entries<uint64_t>(nb, n, fq, np, h_off, h_cmd, dl);
+      }
       h_loff = lo;
       FH_HIP(hipMemcpyAsync(loff.ensure(lo.size() + 1), lo.data(), lo.size() * sizeof(uint32_t),
                             hipMemcpyHostToDevice, stream));
       ensure_latest(d.nproc + 1);
     }
+    stage_base = log_len;
+    log_len += n * nb;
     FH_HIP(hipStreamSynchronize(stream));
     desc = d;
     nbatches = nb;
@@ -2152,6 +2276,8 @@ struct EngineDevice {
     last = b;
     last_deps_only = deps_only;
     ko_done = false;
+    deps_rows = 0;
+    rows_packed = false;
     const uint64_t bbase = stage_base + b * n;  // log position of this batch
     const uint64_t *bdot = dot.get() + bbase;
     const uint32_t *bkey = key32.get() + b * size_t(n) * k;
@@ -2384,7 +2510,7 @@ struct EngineDevice {
            h_dpack[b].second > 0 && h_dpack[b].second <= 31 && dot32.get() != nullptr;
   }
 
-  // One batch through the key-order path (kernels above k_row_count): the
+  // One batch through the key-order path (kernels above k_row_place): the
   // commands sorted by key once, carrying their packed dots; KeyDeps,
   // union entries, graph edges, the tile kernel and the per-key sequence in
   // key order; the committed deps, labels and execution ranks in command
@@ -2431,7 +2557,7 @@ struct EngineDevice {
     sort_pairs_counted_src<uint32_t, V3, PackSrc>(src, kwa, va, sk32b.ensure(n + 1),
                                                   kv3b.ensure(n + 1), n, key_bits, sort_ws,
                                                   stream, &ks, &vs, db);
-    uint8_t *tm = tailm.ensure(n + 4);  // (k_cmd_tails reads it by words)
+    uint8_t *tm = tailm.ensure(n + 16);  // (k_cmd_tails reads it 16 bytes at a time)
     const size_t mwords = (size_t(n) + 3) / 4;
     uint32_t *mr = mrem.ensure(mwords);
     FH_HIP(hipMemsetAsync(mr, 0, mwords * sizeof(uint32_t), stream));
@@ -2489,38 +2615,25 @@ struct EngineDevice {
     const unsigned sg = side_off ? ~0u : side_grid;
     const dim3 gs(grid_for(n, B, std::min(sg, 1u << 30)));
     const dim3 gs8(grid_for(n, B, std::min(sg, 8192u)));
-    if (fq == 2)
-      probed_launch("code_scatter", double(n) * (16.0 + 8.0), k_code_scatter<2>, gs, dim3(B), cs,
-                    n, (const uint4 *)rec4, codes);
-    else
-      probed_launch("code_scatter", double(n) * (16.0 + 12.0), k_code_scatter<3>, gs, dim3(B), cs,
-                    n, (const uint4 *)rec4, codes);
-    k_cmd_tails<V3><<<gs8, B, 0, cs>>>(n, cm, K, ks, vs, tm,
-                                                 reinterpret_cast<const uint8_t *>(mr),
-                                                 views_latest(), bbase);
-    // committed deps (QuorumDeps union, deps/quorum.rs:28-98) from the dot
-    // entries: no gathers
-    uint32_t *dcnt = dep_cnt.ensure(n + 1);
-    uint32_t *doff = o_dep_off.ensure(n + 1);
-    uint64_t *ddot = o_dep.ensure(M + 1);
+    // committed deps (QuorumDeps union, deps/quorum.rs:28-98): the records'
+    // entries are dots already, so each command's row is written in one pass
+    // (round 5: a scatter of the entries to command order, a count pass, a
+    // scan and the union, 4.5 ms alone)
+    uint64_t *rows = o_rows.ensure(size_t(n) * fq + 1);
     // the union's error word (results() checks it)
     FH_HIP(hipMemsetAsync(scal.get(), 0, 2 * sizeof(uint32_t), cs));
     if (fq == 2)
-      k_row_count<2><<<gs8, B, 0, cs>>>(n, codes, dcnt);
+      probed_launch("row_place", double(n) * (16.0 + 16.0), k_row_place<2>, gs, dim3(B), cs, n,
+                    (const uint4 *)rec4, (const uint64_t *)dot.get(), sb, rows, scal.get() + 1,
+                    kDiag);
     else
-      k_row_count<3><<<gs8, B, 0, cs>>>(n, codes, dcnt);
-    exclusive_scan_u32(dcnt, doff, n, cws, cs);
-    if (fq == 2)
-      probed_launch("row_union", double(n) * (8.0 + 4.0 + 16.0), k_row_union<2>, gs8, dim3(B), cs,
-                    n, (const uint32_t *)codes,
-                    (const uint64_t *)dot.get(), sb, (const uint32_t *)doff, ddot,
-                    scal.get() + 1);
-    else
-      probed_launch("row_union", double(n) * (12.0 + 4.0 + 16.0), k_row_union<3>, gs8, dim3(B), cs,
-                    n, (const uint32_t *)codes,
-                    (const uint64_t *)dot.get(), sb, (const uint32_t *)doff, ddot,
-                    scal.get() + 1);
-    deps_direct = true;
+      probed_launch("row_place", double(n) * (16.0 + 24.0), k_row_place<3>, gs, dim3(B), cs, n,
+                    (const uint4 *)rec4, (const uint64_t *)dot.get(), sb, rows, scal.get() + 1,
+                    kDiag);
+    k_cmd_tails<V3><<<gs8, B, 0, cs>>>(n, cm, K, ks, vs, tm,
+                                                 reinterpret_cast<const uint8_t *>(mr),
+                                                 views_latest(), bbase);
+    deps_rows = fq;
     // per-key offsets: a lower bound per key over the sorted keys (they
     // need nothing else; the side stream has slack beside the tile kernel)
     if (!deps_only)
@@ -2563,6 +2676,12 @@ struct EngineDevice {
     if (gout.nexec == 0) {
       // certificate failure: command-order codes for the general path
       join();
+      deps_rows = 0;
+      // the records' entries to command order (the general path's codes)
+      if (fq == 2)
+        k_code_scatter<2><<<grid_for(n, B), B, 0, stream>>>(n, (const uint4 *)rec4, codes);
+      else
+        k_code_scatter<3><<<grid_for(n, B), B, 0, stream>>>(n, (const uint4 *)rec4, codes);
       if (fq == 2)
         k_pcode_to_vid<2><<<grid_for(n, B), B, 0, stream>>>(n, vs, cm.cmask, pe8, pcode, codes);
       else
@@ -2619,7 +2738,7 @@ struct EngineDevice {
     uint64_t *vs = nullptr;
     sort_pairs_counted<uint32_t, uint64_t>(kwa, va, sk32b.ensure(n + 1), cv64b.ensure(n + 1), n,
                                            key_bits, sort_ws, stream, &ks, &vs, db);
-    uint8_t *tm = tailm.ensure(n + 4);  // (k_cmd_tails reads it by words)
+    uint8_t *tm = tailm.ensure(n + 16);  // (k_cmd_tails reads it 16 bytes at a time)
     // predecessor marks from other tiles (k_cmd_search, k_cmd_tails)
     const size_t mwords = (size_t(n) + 3) / 4;
     uint32_t *mr = mrem.ensure(mwords);
@@ -2836,16 +2955,16 @@ struct EngineDevice {
       // written by the union (k_cmd_count sized the rows)
     } else {
     if (sv_fused) {
-      // one dependency slot per command: decode + row length in one scatter,
-      // then compaction fused with the trivial order's labels and ranks
-      k_sv_unpermute<<<grid_for(n, B), B, 0, stream>>>(n, sv_vs, dep_ext.get(), bdot, dot.get(),
-                                                        dep_dot.ensure(n + 1),
-                                                        dep_cnt.ensure(n + 1));
-      exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
-      uint64_t *lb = gout.trivial ? lab.ensure(n + 1) : nullptr;
-      uint32_t *rk = gout.trivial ? rank_tmp.ensure(n + 1) : nullptr;
-      k_sv_compact<<<grid_for(n, B), B, 0, stream>>>(n, dep_dot.get(), off, o_dep.ensure(n + 1),
-                                                      bdot, lb, rk);
+      // one dependency slot per command: the rows themselves; the trivial
+      // order's labels and ranks in one coalesced pass
+      k_sv_rows<<<grid_for(n, B), B, 0, stream>>>(n, sv_vs, dep_ext.get(), bdot, dot.get(),
+                                                   o_rows.ensure(n + 1));
+      deps_rows = 1;
+      if (gout.trivial) {
+        uint64_t *lb = lab.ensure(n + 1);
+        uint32_t *rk = rank_tmp.ensure(n + 1);
+        k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, bdot, lb, rk);
+      }
       sv_labels_done = gout.trivial;
     } else {
       exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
@@ -2919,7 +3038,18 @@ struct EngineDevice {
              "deps-only run: only the committed deps are materialised");
     FH_HIP(hipStreamSynchronize(stream));
     const uint32_t n = uint32_t(desc.n);
-    if (!sv_fused && deps_direct) {
+    if (deps_rows && !rows_packed) {
+      // the rows -> the ABI's CSR (o_dep_off, o_dep) on the device, once
+      uint32_t *cnt = dep_cnt.ensure(n + 1);
+      k_rows_count<<<grid_for(n, B), B, 0, stream>>>(n, deps_rows, o_rows.get(), cnt);
+      uint32_t *off = o_dep_off.ensure(n + 1);
+      exclusive_scan_u32(cnt, off, n, scan_ws, stream);
+      k_rows_compact<<<grid_for(n, B), B, 0, stream>>>(n, deps_rows, o_rows.get(), off,
+                                                        o_dep.ensure(size_t(n) * deps_rows + 1));
+      FH_HIP(hipStreamSynchronize(stream));
+      rows_packed = true;
+    }
+    if (!sv_fused && (deps_direct || deps_rows)) {
       uint32_t bad = 0;
       FH_HIP(hipMemcpy(&bad, scal.get() + 1, sizeof(bad), hipMemcpyDeviceToHost));
       FH_CHECK(bad == 0, FH_EINVARIANT, "a dot of the batch repeats a dot of an earlier batch");
@@ -2931,25 +3061,15 @@ struct EngineDevice {
       FH_HIP(hipStreamSynchronize(stream));
       if (dep_len) *dep_len = total;
       if (dep_out) FH_CHECK(dep_cap >= total, FH_ECAP, "dep output capacity too small");
-      if (dep_off)
-        FH_HIP(hipMemcpyAsync(dep_off, o_dep_off.get(), (n + 1) * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, stream));
-      if (dep_out)
-        FH_HIP(hipMemcpyAsync(dep_out, o_dep.get(), size_t(total) * sizeof(uint64_t),
-                              hipMemcpyDeviceToHost, stream));
+      // (read back through pinned chunks, several host threads copying out:
+      // hoststage.h)
+      if (dep_off) ring.download(dep_off, o_dep_off.get(), size_t(n) + 1, stream);
+      if (dep_out) ring.download(dep_out, o_dep.get(), size_t(total), stream);
     }
-    if (scc_label)
-      FH_HIP(hipMemcpyAsync(scc_label, o_label, size_t(n) * sizeof(uint64_t),
-                            hipMemcpyDeviceToHost, stream));
-    if (exec_rank)
-      FH_HIP(hipMemcpyAsync(exec_rank, o_rank, size_t(n) * sizeof(uint32_t),
-                            hipMemcpyDeviceToHost, stream));
-    if (key_off)
-      FH_HIP(hipMemcpyAsync(key_off, key_offs.get(), (key_space + 1) * sizeof(uint32_t),
-                            hipMemcpyDeviceToHost, stream));
-    if (key_seq)
-      FH_HIP(hipMemcpyAsync(key_seq, o_seq, size_t(o_nelem) * sizeof(uint64_t),
-                            hipMemcpyDeviceToHost, stream));
+    if (scc_label) ring.download(scc_label, o_label, size_t(n), stream);
+    if (exec_rank) ring.download(exec_rank, o_rank, size_t(n), stream);
+    if (key_off) ring.download(key_off, key_offs.get(), size_t(key_space) + 1, stream);
+    if (key_seq) ring.download(key_seq, o_seq, size_t(o_nelem), stream);
     FH_HIP(hipStreamSynchronize(stream));
   }
 };

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <chrono>
 #include <cstddef>
 #include <cstdint>
 #include <stdexcept>
@@ -42,6 +43,34 @@ struct Error : std::runtime_error {
   do {                                                                        \
     if (!(cond)) throw ::fh::Error((code), (msg));                            \
   } while (0)
+
+// Host: wait for a completion word `*done == seq` that a kernel stores into
+// mapped host memory, spinning on the word and querying the stream now and
+// then (query() returns the stream's hipStreamQuery status).  A failed
+// launch raises its HIP error; a stream that finished without the word
+// raises FH_EINVARIANT; work that has not finished after deadline_ms raises
+// FH_EHIP ("<what> did not complete within ...") instead of spinning
+// forever on a kernel that never ends.
+template <class Q>
+void poll_completion(const volatile uint32_t *done, uint32_t seq, Q query, double deadline_ms,
+                     const char *what = "graph_small: the pass") {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1; *done != seq; i++) {
+    if ((i & 1023) != 0) continue;
+    const hipError_t st = query();
+    if (st == hipErrorNotReady) {
+      if ((i & 65535) == 0 &&
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() >
+              deadline_ms)
+        throw Error(FH_EHIP, std::string(what) + " did not complete within " +
+                                 std::to_string(uint64_t(deadline_ms)) +
+                                 " ms (the handle is no longer usable)");
+      continue;
+    }
+    FH_HIP(st);
+    FH_CHECK(*done == seq, FH_EINVARIANT, std::string(what) + " ended without its completion word");
+  }
+}
 
 // --- device buffer ----------------------------------------------------------
 template <class T>

@@ -2,9 +2,6 @@
 // (graph_small.hip), used by fh_graph for small batches.
 #pragma once
 
-#include <chrono>
-#include <string>
-
 #include "fh_common.h"
 
 namespace fh {
@@ -103,31 +100,7 @@ struct SmallPass {
   uint32_t delay_us;
 };
 
-// Host: wait for a small pass's completion word `*done == seq`, spinning on
-// the mapped word and querying the stream now and then (query() returns the
-// stream's hipStreamQuery status).  A failed launch raises its HIP error; a
-// stream that finished without the word raises FH_EINVARIANT; a pass that
-// has not finished after deadline_ms raises FH_EHIP (the caller's handle is
-// then unusable: the kernel may still run).
-template <class Q>
-void poll_completion(const volatile uint32_t *done, uint32_t seq, Q query, double deadline_ms) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (uint32_t i = 1; *done != seq; i++) {
-    if ((i & 1023) != 0) continue;
-    const hipError_t st = query();
-    if (st == hipErrorNotReady) {
-      if ((i & 65535) == 0 &&
-          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() >
-              deadline_ms)
-        throw Error(FH_EHIP, "graph_small: the pass did not complete within " +
-                                 std::to_string(uint64_t(deadline_ms)) +
-                                 " ms (the graph handle is no longer usable)");
-      continue;
-    }
-    FH_HIP(st);
-    FH_CHECK(*done == seq, FH_EINVARIANT, "graph_small: pass ended without its completion word");
-  }
-}
+// (host: the completion wait is fh_common.h poll_completion)
 
 void launch_graph_small(const SmallPass &p, hipStream_t s);
 

@@ -42,6 +42,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "graph_core.h"
 
@@ -61,7 +62,8 @@ static uint32_t round_r0(uint32_t x, uint32_t floor = 256) {
   return std::max<uint32_t>(floor, (x + 63) & ~63u);
 }
 
-// exclusive scan of one value per thread over the 1024-thread block
+// exclusive scan of one value per thread over the TH-thread block
+template <int TH>
 __device__ __forceinline__ uint32_t tile_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t x = v;
@@ -74,7 +76,7 @@ __device__ __forceinline__ uint32_t tile_scan(uint32_t v, uint32_t *s_w, uint32_
   __syncthreads();
   uint32_t pre = 0, tot = 0;
 #pragma unroll
-  for (int i = 0; i < kTileThreads / 64; i++) {
+  for (int i = 0; i < TH / 64; i++) {
     const uint32_t c = s_w[i];
     if (i < w) pre += c;
     tot += c;
@@ -148,7 +150,8 @@ struct TileOut {
   uint8_t *failf;         // [tiles] or null: 1 for each tile whose certificate fails
   unsigned long long *prof;  // [8] or null: per-phase clock sums (FH_GRAPH_DEBUG)
   int r0;      // certified reach bound R0 (L = 2·R0)
-  int core;    // core vertices per tile T (T + 2L <= kTileC, T <= kMaxCore·1024)
+  int core;    // core vertices per tile T (T + 2L <= tile_ctx(th), T <= kMaxCore·th)
+  int th = kTileThreads;  // threads per workgroup (1024, or 512: half the context)
   // the engine's key-order graph (GraphInput::dst_codes / dot32): edges as
   // one u32 of 8-bit distances per vertex (GraphInput::dst_codes) and the
   // dots packed src << dot_sb | seq
@@ -157,6 +160,7 @@ struct TileOut {
   int dot_sb = 0;
   const uint32_t *esc = nullptr;  // codes: escaped targets (GraphInput::dst_esc)
   bool prio = false;              // raise the waves' issue priority
+  int diag = 0;  // DIAG (temporary measurement)
   // key-order outputs (GraphInput::ko_seq; the engine's key-order path):
   // each core vertex writes its dot at its key-order execution position
   // (the per-key sequence), and a vertex of a multi-member ready group its
@@ -180,21 +184,22 @@ namespace {
 
 // One tile: core [a, a + T), context [a - L, a + T + L) with L = 2·R0 and
 // T + 2L <= kTileC.
-template <int S>
-__global__ void __launch_bounds__(kTileThreads)
+template <int S, int TH, bool D32>
+__global__ void __launch_bounds__(TH, 4)
     k_graph_tile(uint32_t V, const uint32_t *__restrict__ dst, const uint64_t *__restrict__ dot,
                  TileOut out) {
-  const int R0 = out.r0, T = out.core, L = 2 * R0;  // host: T + 2L <= kTileC
+  constexpr int CTX = TH * (kTileC / kTileThreads);  // context vertices: 10 per thread
+  const int R0 = out.r0, T = out.core, L = 2 * R0;  // host: T + 2L <= CTX
   if (out.redo && !out.redo[blockIdx.x]) return;
-  __shared__ __align__(16) uint16_t eL[S][kTileC];
-  __shared__ uint16_t sH[kTileC];
-  __shared__ uint16_t sR[kTileC];
-  __shared__ uint8_t sF[kTileC];
-  __shared__ uint16_t W1[kTileC];
-  __shared__ __align__(16) uint16_t W2[kTileC];
+  __shared__ __align__(16) uint16_t eL[S][CTX];
+  __shared__ uint16_t sH[CTX];
+  __shared__ uint16_t sR[CTX];
+  __shared__ uint8_t sF[CTX];
+  __shared__ uint16_t W1[CTX];
+  __shared__ __align__(16) uint16_t W2[CTX];
   // rank-phase member keys: S = 3 reuses the third edge row, S = 2 has room
-  __shared__ uint32_t gkey_s[S == 3 ? 1 : kTileC / 2];
-  __shared__ uint32_t s_w[kTileThreads / 64];
+  __shared__ uint32_t gkey_s[S == 3 ? 1 : CTX / 2];
+  __shared__ uint32_t s_w[TH / 64];
   __shared__ uint32_t s_ch[3];
   __shared__ uint32_t s_fail, s_maxex, s_over, s_long;
 
@@ -220,15 +225,34 @@ __global__ void __launch_bounds__(kTileThreads)
   if (tid == 0) s_fail = s_maxex = s_over = s_long = 0;
   // the core vertices' own dots, loaded now and used by the last phase (its
   // labels and dot tie-breaks): the loads complete behind the LDS phases
-  uint64_t pdot[kMaxCore];
+  // (D32: the dots packed to 32 bits, GraphInput::dot32 -- half the
+  // registers, which pays for the group roots' dots prefetched below)
+  using DotT = std::conditional_t<D32, uint32_t, uint64_t>;
+  auto unpack = [&](DotT d) -> uint64_t {
+    if constexpr (D32)
+      return (uint64_t(d >> out.dot_sb) << 56) | (d & ((1u << out.dot_sb) - 1));
+    else
+      return d;
+  };
+  auto ldot = [&](uint32_t v) -> DotT {
+    if constexpr (D32)
+      return out.dot32[v];
+    else
+      return dot[v];
+  };
+  DotT pdot[kMaxCore];
   uint32_t pcmd[kMaxCore];
+  // issued after the edge words (with codes), so that the edge decode waits
+  // for those alone (vmcnt retires in issue order)
+  auto prefetch_core = [&]() {
 #pragma unroll
-  for (int j = 0; j < kMaxCore; j++) {
-    const int x = ca + tid + j * kTileThreads;
-    pdot[j] = x < cb ? out.vdot(dot, lo + x) : 0ull;
-    pcmd[j] = out.ko_seq && x < cb ? out.ko_cmd[size_t(lo + x) * out.ko_cstride] & out.ko_cmask
-                                   : 0u;
-  }
+    for (int j = 0; j < kMaxCore; j++) {
+      const int x = ca + tid + j * TH;
+      pdot[j] = x < cb ? ldot(lo + x) : DotT(0);
+      pcmd[j] = out.ko_seq && x < cb ? out.ko_cmd[size_t(lo + x) * out.ko_cstride] & out.ko_cmask
+                                     : 0u;
+    }
+  };
 
   // 1. context edges; certificate part 2: forward spans of core vertices
   uint32_t nlong = 0;
@@ -240,16 +264,17 @@ __global__ void __launch_bounds__(kTileThreads)
   };
   if (out.codes) {
     // one word per vertex: all of the thread's words in flight at once
-    constexpr int kPI = kTileC / kTileThreads;
+    constexpr int kPI = CTX / TH;
     uint32_t ew[kPI];
 #pragma unroll
     for (int j = 0; j < kPI; j++) {
-      const int x = tid + j * kTileThreads;
+      const int x = tid + j * TH;
       ew[j] = x < C ? dst[lo + x] : 0u;
     }
+    prefetch_core();
 #pragma unroll
     for (int j = 0; j < kPI; j++) {
-      const int x = tid + j * kTileThreads;
+      const int x = tid + j * TH;
       if (x >= C) break;
       const uint32_t v = lo + x;
 #pragma unroll
@@ -262,7 +287,8 @@ __global__ void __launch_bounds__(kTileThreads)
       sH[x] = uint16_t(x);
     }
   } else {
-    for (int x = tid; x < C; x += kTileThreads) {
+    prefetch_core();
+    for (int x = tid; x < C; x += TH) {
       const uint32_t v = lo + x;
 #pragma unroll
       for (int s = 0; s < S; s++) put_edge(x, s, v, dst[size_t(v) * S + s]);
@@ -279,7 +305,7 @@ __global__ void __launch_bounds__(kTileThreads)
     int it = 0;
     for (;; it++) {
       bool ch = false;
-      for (int i = tid; i < n; i += kTileThreads) ch |= body(list ? int(list[i]) : i);
+      for (int i = tid; i < n; i += TH) ch |= body(list ? int(list[i]) : i);
       if (ch) s_ch[it % 3] = 1;
       if (tid == 0) s_ch[(it + 1) % 3] = 0;
       __syncthreads();
@@ -294,7 +320,7 @@ __global__ void __launch_bounds__(kTileThreads)
   // 2. H: max arrival position reachable (context subgraph).  H(x) is a
   // vertex x reaches, so H(H(x)) is reachable too: pointer jumping collapses
   // chains of forward dependencies in logarithmically many sweeps.
-  const int hP = 64 * ((C + kTileThreads - 1) / kTileThreads);  // per-wave block
+  const int hP = 64 * ((C + TH - 1) / TH);  // per-wave block
   // Each wave walks a contiguous block in ascending steps of 64 (updates of a
   // block's earlier vertices are seen by its later ones in the same sweep),
   // with each thread's vertices' context edges and own H in registers: the thread owning x is the only writer of sH[x], so its
@@ -302,7 +328,7 @@ __global__ void __launch_bounds__(kTileThreads)
   // sH[y] / sH[H] reads alone (the edge rows and own H were conflict-free
   // re-reads of the same words every sweep)
   auto h_sweeps_regs = [&]() {
-    constexpr int kHI = kTileC / kTileThreads;
+    constexpr int kHI = CTX / TH;
     const int w = tid >> 6, lane = tid & 63, nk = hP / 64;
     uint16_t ey[kHI][S];
     uint32_t hv[kHI];
@@ -348,7 +374,7 @@ __global__ void __launch_bounds__(kTileThreads)
   // 3. certificate part 1: core excess < R0
   {
     uint32_t mx = 0, over = 0;
-    for (int x = ca + tid; x < cb; x += kTileThreads) {
+    for (int x = ca + tid; x < cb; x += TH) {
       const uint32_t ex = uint32_t(sH[x]) - uint32_t(x);
       mx = max(mx, ex);
       over += ex >= uint32_t(R0);
@@ -372,9 +398,9 @@ __global__ void __launch_bounds__(kTileThreads)
   // multi-vertex ready group except its root is raised, so the later phases
   // work on this list only.  sF bits: 1 reached, 2 processed, 4 the group
   // rooted here has raised members.
-  constexpr int kPer = kTileC / kTileThreads;
+  constexpr int kPer = CTX / TH;
   uint32_t nraised = 0;
-  for (int x = tid; x < C; x += kTileThreads) {
+  for (int x = tid; x < C; x += TH) {
     sF[x] = 0;
     sR[x] = kNone;
   }
@@ -383,19 +409,19 @@ __global__ void __launch_bounds__(kTileThreads)
     uint32_t mine = 0;
     const int x0 = tid * kPer;
     for (int x = x0; x < x0 + kPer && x < C; x++) mine += sH[x] > x;
-    uint32_t o = tile_scan(mine, s_w, &nraised);
+    uint32_t o = tile_scan<TH>(mine, s_w, &nraised);
     for (int x = x0; x < x0 + kPer && x < C; x++)
       if (sH[x] > x) W2[o++] = uint16_t(x);
   }
   __syncthreads();
-  for (uint32_t i = tid; i < nraised; i += kTileThreads) sF[sH[W2[i]]] = 4;
+  for (uint32_t i = tid; i < nraised; i += TH) sF[sH[W2[i]]] = 4;
   __syncthreads();
   phase(2);
 
   // 5. SCCs.  Round 1: the members of each ready group reachable from its
   // root t (H(t) = t) inside the group are t's SCC.  Roots push once; then
   // the raised vertices reached push until nothing new is reached.
-  for (int x = tid; x < C; x += kTileThreads) {
+  for (int x = tid; x < C; x += TH) {
     if (sH[x] != x) continue;
     sF[x] |= 3;
     sR[x] = uint16_t(x);
@@ -431,14 +457,14 @@ __global__ void __launch_bounds__(kTileThreads)
   uint32_t left = 0;
   {
     uint32_t mine = 0;
-    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+    for (uint32_t i = tid; i < nraised; i += TH) {
       const uint16_t x = W2[i];
       if (sF[x] & 1)
         sR[x] = sH[x];
       else
         mine++;
     }
-    tile_scan(mine, s_w, &left);
+    tile_scan<TH>(mine, s_w, &left);
   }
   phase(3);
   // later rounds over the raised vertices left: H' over the unassigned
@@ -453,7 +479,7 @@ __global__ void __launch_bounds__(kTileThreads)
       }
       return;
     }
-    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+    for (uint32_t i = tid; i < nraised; i += TH) {
       const uint16_t x = W2[i];
       if (sR[x] == kNone) {
         W1[x] = x;
@@ -480,14 +506,14 @@ __global__ void __launch_bounds__(kTileThreads)
           return false;
         },
         int(nraised), nullptr);
-    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+    for (uint32_t i = tid; i < nraised; i += TH) {
       const uint16_t x = W2[i];
       if (sR[x] == kNone && W1[x] == x) sF[x] |= 1;
     }
     __syncthreads();
     reach(W1);
     uint32_t mine = 0;
-    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+    for (uint32_t i = tid; i < nraised; i += TH) {
       const uint16_t x = W2[i];
       if (sR[x] != kNone) continue;
       if (sF[x] & 1)
@@ -496,20 +522,20 @@ __global__ void __launch_bounds__(kTileThreads)
         mine++;
     }
     __syncthreads();
-    tile_scan(mine, s_w, &left);
+    tile_scan<TH>(mine, s_w, &left);
   }
   if (tid == 0 && round) atomicMax(&out.stat[5], uint32_t(round));
 
   // 6. SCC slot = min member; depth over same-group edges (W1, per slot).
   // Only raised vertices can have an edge to another SCC of their group (a
   // root's same-group dependencies reach it back), so the sweeps run over W2.
-  for (int x = tid; x < C; x += kTileThreads) W1[x] = kNone;
+  for (int x = tid; x < C; x += TH) W1[x] = kNone;
   __syncthreads();
-  for (int x = tid; x < C; x += kTileThreads) lds_min_u16(&W1[sR[x]], uint16_t(x));
+  for (int x = tid; x < C; x += TH) lds_min_u16(&W1[sR[x]], uint16_t(x));
   __syncthreads();
-  for (int x = tid; x < C; x += kTileThreads) sR[x] = W1[sR[x]];
+  for (int x = tid; x < C; x += TH) sR[x] = W1[sR[x]];
   __syncthreads();
-  for (int x = tid; x < C; x += kTileThreads) W1[x] = 0;
+  for (int x = tid; x < C; x += TH) W1[x] = 0;
   __syncthreads();
   sweeps(
       [&](int i) {
@@ -534,16 +560,16 @@ __global__ void __launch_bounds__(kTileThreads)
   // are no longer needed), then each core vertex's rank in its group by
   // (depth, min member, dot) and each core root's group size
   uint16_t *gend = eL[0], *gmem = eL[1];
-  for (int x = tid; x < C; x += kTileThreads) gend[x] = 0;
+  for (int x = tid; x < C; x += TH) gend[x] = 0;
   __syncthreads();
-  for (uint32_t i = tid; i < nraised; i += kTileThreads) lds_add_u16(&gend[sH[W2[i]]], 1);
+  for (uint32_t i = tid; i < nraised; i += TH) lds_add_u16(&gend[sH[W2[i]]], 1);
   __syncthreads();
   {
     const int x0 = tid * kPer;
     uint32_t sum = 0;
     for (int x = x0; x < x0 + kPer && x < C; x++) sum += gend[x];
     uint32_t tot = 0;
-    uint32_t base = tile_scan(sum, s_w, &tot);
+    uint32_t base = tile_scan<TH>(sum, s_w, &tot);
     for (int x = x0; x < x0 + kPer && x < C; x++) {
       const uint32_t c = gend[x];
       gend[x] = uint16_t(base);
@@ -551,7 +577,7 @@ __global__ void __launch_bounds__(kTileThreads)
     }
   }
   __syncthreads();
-  for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+  for (uint32_t i = tid; i < nraised; i += TH) {
     const uint16_t y = W2[i];
     gmem[lds_add_u16(&gend[sH[y]], 1)] = y;
   }
@@ -572,7 +598,7 @@ __global__ void __launch_bounds__(kTileThreads)
   if (out.ko_seq) {
 #pragma unroll
     for (int j = 0; j < kMaxCore; j++) {
-      const int x = ca + tid + j * kTileThreads;
+      const int x = ca + tid + j * TH;
       uint32_t l0 = 0, h0 = nraised;
       if (x < cb) {
         const uint16_t t = sH[x];
@@ -590,9 +616,9 @@ __global__ void __launch_bounds__(kTileThreads)
   }
   uint64_t *gdot = reinterpret_cast<uint64_t *>(W2);
   uint32_t *gkey = S == 3 ? reinterpret_cast<uint32_t *>(&eL[S - 1][0]) : gkey_s;
-  const bool lds_dots = nraised <= uint32_t(kTileC / 4);
+  const bool lds_dots = nraised <= uint32_t(CTX / 4);
   if (lds_dots)
-    for (uint32_t i = tid; i < nraised; i += kTileThreads) {
+    for (uint32_t i = tid; i < nraised; i += TH) {
       const uint16_t y = gmem[i];
       gdot[i] = out.vdot(dot, lo + y);
       gkey[i] = (uint32_t(W1[sR[y]]) << 16) | sR[y];
@@ -606,23 +632,33 @@ __global__ void __launch_bounds__(kTileThreads)
   // 4 waves x 128 registers fill each SIMD's file: the side stream's kernels
   // could no longer run beside the tile workgroup, C4 14.5 -> 16.4 ms.  With
   // the command alone: 105 VGPRs, C4 14.52 against 14.55 ms, r05ai)
+  // With D32 the roots' dots too: the rank loop below then issues no load.
+  // (Its stores -- the per-key sequence, the command-order records -- count
+  // in vmcnt like loads on gfx9, so a load inside the loop waited for every
+  // earlier iteration's stores: one loaded-HBM round trip per core vertex,
+  // ~65 us per tile of 128.)
   uint32_t rcv[kMaxCore];
+  DotT rdv[D32 ? kMaxCore : 1];
 #pragma unroll
   for (int j = 0; j < kMaxCore; j++) {
-    const int x = ca + tid + j * kTileThreads;
+    const int x = ca + tid + j * TH;
     rcv[j] = pcmd[j];
-    if (out.ko_seq && x < cb) {
+    if constexpr (D32) rdv[j] = 0;
+    if (x < cb) {
       const uint16_t t = sH[x];
-      if (t != uint32_t(x)) rcv[j] = out.ko_cmd[size_t(lo + t) * out.ko_cstride] & out.ko_cmask;
+      if (t != uint32_t(x)) {
+        if (out.ko_seq) rcv[j] = out.ko_cmd[size_t(lo + t) * out.ko_cstride] & out.ko_cmask;
+        if constexpr (D32) rdv[j] = out.dot32[lo + t];
+      }
     }
   }
   uint32_t gmax = 0;
 #pragma unroll
   for (int j = 0; j < kMaxCore; j++) {
-    const int x = ca + tid + j * kTileThreads;
+    const int x = ca + tid + j * TH;
     if (x >= cb) break;
     const uint32_t v = lo + x;
-    const uint64_t dotx = pdot[j];
+    const uint64_t dotx = unpack(pdot[j]);
     const uint16_t t = sH[x];
     uint32_t cnt = 0, rk = 0;
     uint64_t lab = 0;  // min dot of x's SCC (0 = x's own: a singleton group)
@@ -630,13 +666,17 @@ __global__ void __launch_bounds__(kTileThreads)
       const uint32_t b0 = t ? gend[t - 1] : 0u, b1 = gend[t];
       cnt = b1 - b0;
       const uint32_t dx = W1[sR[x]], mx = sR[x];
-      auto cmp = [&](uint32_t y) {
-        const uint32_t dy = W1[sR[y]], my = sR[y];
-        if (dy != dx) return dy < dx;
-        if (my != mx) return my < mx;
-        return out.vdot(dot, lo + y) < dotx;
+      // the root's dot (prefetched with D32)
+      auto root_dot = [&]() -> uint64_t {
+        if constexpr (D32)
+          return unpack(rdv[j]);
+        else
+          return out.vdot(dot, lo + t);
       };
-      if (t != uint32_t(x)) rk += cmp(t);
+      if (t != uint32_t(x)) {
+        const uint32_t dy = W1[sR[t]], my = sR[t];
+        rk += dy != dx ? dy < dx : my != mx ? my < mx : root_dot() < dotx;
+      }
       if (lds_dots) {
         // x's own entry (if raised) ties with itself on the dot: not before
         // x, and its dot is x's own in the label minimum
@@ -678,10 +718,10 @@ __global__ void __launch_bounds__(kTileThreads)
           if (st[u] == 0 && (lab == 0 || dy[u] < lab)) lab = dy[u];
         }
       }
-      // the root t is in x's SCC iff it shares the SCC slot (cmp(t) above
+      // the root t is in x's SCC iff it shares the SCC slot (the root test above
       // compared it; its dot was not kept)
       if (t != uint32_t(x) && sR[t] == mx) {
-        const uint64_t dt = out.vdot(dot, lo + t);
+        const uint64_t dt = root_dot();
         if (lab == 0 || dt < lab) lab = dt;
       }
       gmax = max(gmax, cnt + 1);
@@ -693,8 +733,10 @@ __global__ void __launch_bounds__(kTileThreads)
       if (t != uint32_t(x) || cnt > 0) {
         const uint32_t c = pcmd[j];
         const uint32_t ct = rcv[j];
+        if (!(out.diag & 1)) {
         out.ko_hl[c] = make_uint4(ct, rk, uint32_t(label), uint32_t(label >> 32));
         out.ko_diff[c + 1] = t != uint32_t(x) ? 1u : 0u - cnt;
+        }
       }
       continue;
     }
@@ -705,8 +747,13 @@ __global__ void __launch_bounds__(kTileThreads)
     out.gcount[v] = t == uint32_t(x) ? cnt + 1 : 0u;
   }
   if (gmax) atomicMax(&out.stat[6], gmax);
-  __syncthreads();
-  phase(6);
+  // no trailing barrier outside the phase profile: a barrier waits for every
+  // wave's stores to complete (a workgroup-scope release), and beside the
+  // side stream's row stores that drain took ~40 us of the tile's ~117
+  if (out.prof) {
+    __syncthreads();
+    phase(6);
+  }
 }
 
 __global__ void k_exec_from_groups(uint32_t V, const uint32_t *__restrict__ hgrp,
@@ -725,13 +772,16 @@ __global__ void k_exec_from_groups(uint32_t V, const uint32_t *__restrict__ hgrp
 // Cores up to 10240 vertices (kMaxCore = 10): on the key-order graph the reach
 // bound is small, so T = kTileC - 4·R0 exceeds 8192 and fewer tiles carry
 // the fixed per-tile phases (C4: 14.83 against 14.94 ms at T <= 8192, r05z)
-static int tile_core_cap() { return kMaxCore * kTileThreads; }
+static int tile_core_cap(int th = kTileThreads) { return kMaxCore * th; }
+// context vertices of a th-thread tile (10 per thread; the LDS: 15 B each)
+static int tile_ctx(int th) { return th * (kTileC / kTileThreads); }
 
 static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint64_t *dot,
                          const TileOut &to, hipStream_t stream, uint32_t ncores = 0,
                          bool count_bytes = true) {
-  FH_CHECK(to.core >= 1024 && to.core <= kMaxCore * kTileThreads &&
-               to.core + 4 * to.r0 <= kTileC && to.r0 >= 64,
+  FH_CHECK(to.core >= 1024 && to.core <= kMaxCore * to.th &&
+               to.core + 4 * to.r0 <= tile_ctx(to.th) && to.r0 >= 64 &&
+               (to.th == 1024 || to.th == 512),
            FH_EINVARIANT, "graph_tile: bad tile geometry");
   const uint32_t tiles = to.cores ? ncores : (V + to.core - 1) / to.core;
   if (tiles == 0) return;
@@ -741,15 +791,20 @@ static void launch_tiles(uint32_t V, uint32_t S, const uint32_t *dst, const uint
   // a redo pass over cores already ordered once: count_bytes = false)
   const double bytes =
       count_bytes ? double(V) * (4.0 * S + 8.0 + (to.rep ? 16.0 : 12.0) + 8.0) : 0.0;
-  switch (S) {
-    case 2:
-      probed_launch("graph_tile", bytes, k_graph_tile<2>, dim3(tiles), dim3(kTileThreads),
-                    stream, V, dst, dot, to);
-      break;
-    default:
-      probed_launch("graph_tile", bytes, k_graph_tile<3>, dim3(tiles), dim3(kTileThreads),
-                    stream, V, dst, dot, to);
-      break;
+  auto go = [&](auto kern) {
+    probed_launch("graph_tile", bytes, kern, dim3(tiles), dim3(to.th), stream, V, dst, dot, to);
+  };
+  const bool d32 = to.dot32 != nullptr;
+  if (S == 2) {
+    if (to.th == 512)
+      d32 ? go(k_graph_tile<2, 512, true>) : go(k_graph_tile<2, 512, false>);
+    else
+      d32 ? go(k_graph_tile<2, 1024, true>) : go(k_graph_tile<2, 1024, false>);
+  } else {
+    if (to.th == 512)
+      d32 ? go(k_graph_tile<3, 512, true>) : go(k_graph_tile<3, 512, false>);
+    else
+      d32 ? go(k_graph_tile<3, 1024, true>) : go(k_graph_tile<3, 1024, false>);
   }
 }
 
@@ -777,6 +832,7 @@ bool GraphCore::tiles_mixed(const GraphInput &in, TileOut &to, uint32_t r2, uint
   const uint32_t r1 = kMixR1;
   uint32_t *stat = to.stat;
   to.r0 = int(r1);
+  to.th = kTileThreads;
   to.core = std::min(kTileC - 4 * int(r1), kMaxCore * kTileThreads);
   const uint32_t t1 = uint32_t(to.core), tiles1 = (V + t1 - 1) / t1;
   uint8_t *ff = t_fail.ensure(tiles1 + 1);
@@ -859,7 +915,14 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.ko_cstride = in.ko_cstride;
   to.ko_cmask = in.ko_cmask;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
+  // (measurement, round 6: FH_TILE_TH=512|1024 for the key-order graph)
+  static const int ko_tile_threads = [] {
+    const char *e = getenv("FH_TILE_TH");
+    return e && atoi(e) == 1024 ? 1024 : 512;
+  }();
   to.prof = nullptr;
+  static const int diag = getenv("FH_DIAG") ? atoi(getenv("FH_DIAG")) : 0;  // DIAG
+  to.diag = diag;
   if (debug) {
     to.prof = reinterpret_cast<unsigned long long *>(t_prof.ensure(16));
     FH_HIP(hipMemsetAsync(to.prof, 0, 8 * sizeof(unsigned long long), stream));
@@ -886,7 +949,12 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   }
   for (int attempt = 0; attempt < 4 && !ok; attempt++) {
     to.r0 = int(r0);
-    to.core = std::min(kTileC - 4 * int(r0), tile_core_cap());
+    // the key-order graph: half-size tiles (two workgroups per CU, so one
+    // tile's loads overlap another's LDS phases) while the bound leaves a
+    // core of >= 1024 vertices
+    to.th = in.ko_seq && tile_ctx(ko_tile_threads) - 4 * int(r0) >= 1024 ? ko_tile_threads
+                                                                         : kTileThreads;
+    to.core = std::min(tile_ctx(to.th) - 4 * int(r0), tile_core_cap(to.th));
     FH_HIP(hipMemsetAsync(stat, 0, 7 * sizeof(uint32_t), stream));
     if (to.prof) FH_HIP(hipMemsetAsync(to.prof, 0, 8 * sizeof(unsigned long long), stream));
     launch_tiles(V, in.stride, in.dst, in.dot, to, stream);

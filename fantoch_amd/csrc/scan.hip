@@ -5,6 +5,8 @@
 // (sum, or max over u32).
 #include <cstdlib>
 
+#include <atomic>
+
 #include "scan.h"
 
 namespace fh {
@@ -219,17 +221,11 @@ void fetch_u32(const uint32_t *dev, uint32_t *host, int n, hipStream_t s) {
   const uint32_t seq = ++m.seq;
   k_fetch_u32<<<1, 1, 0, s>>>(dev, m.dev, n, seq);
   FH_HIP(hipGetLastError());
-  for (;;) {
-    if (__atomic_load_n(&m.host[0], __ATOMIC_ACQUIRE) == seq) break;
-    const hipError_t e = hipStreamQuery(s);
-    if (e == hipSuccess) {
-      // the stream drained: the store must be visible now
-      FH_CHECK(__atomic_load_n(&m.host[0], __ATOMIC_ACQUIRE) == seq, FH_EHIP,
-               "fetch_u32: mailbox not written");
-      break;
-    }
-    if (e != hipErrorNotReady) throw Error(FH_EHIP, std::string("fetch_u32: ") + hipGetErrorString(e));
-  }
+  // (the word waits behind everything queued on the stream before it: a
+  // generous deadline, for a kernel upstream that never ends)
+  poll_completion(reinterpret_cast<volatile uint32_t *>(m.host), seq,
+                  [&] { return hipStreamQuery(s); }, 600000.0, "fetch_u32: the stream");
+  std::atomic_thread_fence(std::memory_order_acquire);
   for (int i = 0; i < n; i++) host[i] = __atomic_load_n(&m.host[2 + i], __ATOMIC_RELAXED);
 }
 
