@@ -600,7 +600,6 @@ __global__ void __launch_bounds__(kThreads)
 // a cache-sized slice of the code array (a random 12-B store per command over
 // the whole array ran at 4.6 ms per 100M commands, confined to 4M-command
 // regions at 1.7 ms: tools/scatter_bench.hip, profiles/r05_scatter_bench.jsonl).
-static const int kDiag = getenv("FH_DIAG") ? atoi(getenv("FH_DIAG")) : 0;  // DIAG
 constexpr int kSrchHalo = 128;
 constexpr int kSrchMaxRep = 8;  // replicas (logs) of the command-level path
 constexpr uint32_t kNoArr = ~0u;
@@ -970,13 +969,7 @@ __device__ __forceinline__ void row_place_one(const uint4 o, const uint64_t *__r
 template <uint32_t FQ>
 __global__ void __launch_bounds__(256)
     k_row_place(uint32_t n, const uint4 *__restrict__ rec, const uint64_t *__restrict__ dlog,
-                int sb, uint64_t *__restrict__ rows, uint32_t *__restrict__ err, int diag) {
-  if (diag & 2) {  // DIAG: reads only
-    uint32_t acc = 0;
-    GRID_STRIDE(i, n) acc += rec[i].y;
-    if (acc == 0x12345678u) atomicOr(err, 2u);
-    return;
-  }
+                int sb, uint64_t *__restrict__ rows, uint32_t *__restrict__ err) {
   GRID_STRIDE(i, n) row_place_one<FQ>(rec[i], dlog, sb, rows, err);
 }
 
@@ -1788,11 +1781,13 @@ struct EngineDevice {
     const char *e = getenv("FH_KO_SIDE");
     return e && *e == '0';
   }();
-  // Workgroups of the side kernels: two 256-thread workgroups per CU.  The
-  // tile kernel holds one 16-wave workgroup per CU (its LDS), so 8 side waves
-  // leave room for the next tile's workgroup as soon as one retires.  C4, ms
-  // per step: 2 per CU 15.6, 1.5 per CU 16.9, 2.5 16.7, 3 16.1, 4 17.7,
-  // uncapped 16.8, no side stream 17.2 (profiles/r05_side_sweep.txt).
+  // Workgroups of the side kernels: one 256-thread workgroup per CU.  The
+  // side kernels' random row stores are what slows the tile kernel beside
+  // them (C4 with k_row_place issuing its loads but not its stores: 12.48 ->
+  // 10.87 ms, r06f), so fewer side waves, finishing later, cost the tile
+  // kernel less: C4, ms per step, 1 per CU 12.48-12.50, 2 per CU 12.81,
+  // 3 per CU 13.99 (r06e/f).  (Round 5, with the entries scatter and the
+  // union: 2 per CU 15.6, 1.5 16.9, 3 16.1, r05_side_sweep.txt.)
   unsigned side_grid = 0;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -1841,9 +1836,7 @@ struct EngineDevice {
     {
       int cus = 0;
       FH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-      // (measurement, round 6: FH_SIDE_WG workgroups per CU)
-      const char *e = getenv("FH_SIDE_WG");
-      side_grid = unsigned(e ? std::max(1, atoi(e)) : 2) * unsigned(std::max(cus, 1));
+      side_grid = unsigned(std::max(cus, 1));
     }
     FH_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     FH_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
@@ -2624,12 +2617,10 @@ struct EngineDevice {
     FH_HIP(hipMemsetAsync(scal.get(), 0, 2 * sizeof(uint32_t), cs));
     if (fq == 2)
       probed_launch("row_place", double(n) * (16.0 + 16.0), k_row_place<2>, gs, dim3(B), cs, n,
-                    (const uint4 *)rec4, (const uint64_t *)dot.get(), sb, rows, scal.get() + 1,
-                    kDiag);
+                    (const uint4 *)rec4, (const uint64_t *)dot.get(), sb, rows, scal.get() + 1);
     else
       probed_launch("row_place", double(n) * (16.0 + 24.0), k_row_place<3>, gs, dim3(B), cs, n,
-                    (const uint4 *)rec4, (const uint64_t *)dot.get(), sb, rows, scal.get() + 1,
-                    kDiag);
+                    (const uint4 *)rec4, (const uint64_t *)dot.get(), sb, rows, scal.get() + 1);
     k_cmd_tails<V3><<<gs8, B, 0, cs>>>(n, cm, K, ks, vs, tm,
                                                  reinterpret_cast<const uint8_t *>(mr),
                                                  views_latest(), bbase);

@@ -160,7 +160,6 @@ struct TileOut {
   int dot_sb = 0;
   const uint32_t *esc = nullptr;  // codes: escaped targets (GraphInput::dst_esc)
   bool prio = false;              // raise the waves' issue priority
-  int diag = 0;  // DIAG (temporary measurement)
   // key-order outputs (GraphInput::ko_seq; the engine's key-order path):
   // each core vertex writes its dot at its key-order execution position
   // (the per-key sequence), and a vertex of a multi-member ready group its
@@ -733,10 +732,8 @@ __global__ void __launch_bounds__(TH, 4)
       if (t != uint32_t(x) || cnt > 0) {
         const uint32_t c = pcmd[j];
         const uint32_t ct = rcv[j];
-        if (!(out.diag & 1)) {
         out.ko_hl[c] = make_uint4(ct, rk, uint32_t(label), uint32_t(label >> 32));
         out.ko_diff[c + 1] = t != uint32_t(x) ? 1u : 0u - cnt;
-        }
       }
       continue;
     }
@@ -915,14 +912,10 @@ bool GraphCore::run_tiles(const GraphInput &in, GraphOutput &out) {
   to.ko_cstride = in.ko_cstride;
   to.ko_cmask = in.ko_cmask;
   static const bool debug = getenv("FH_GRAPH_DEBUG") != nullptr;
-  // (measurement, round 6: FH_TILE_TH=512|1024 for the key-order graph)
-  static const int ko_tile_threads = [] {
-    const char *e = getenv("FH_TILE_TH");
-    return e && atoi(e) == 1024 ? 1024 : 512;
-  }();
+  // the key-order graph's tiles: 512 threads (C4, ms per step, three boxes:
+  // 12.30 / 12.60 / 12.81 against 12.22 / 12.95 / 12.94 at 1024, r06b/d/e)
+  constexpr int ko_tile_threads = 512;
   to.prof = nullptr;
-  static const int diag = getenv("FH_DIAG") ? atoi(getenv("FH_DIAG")) : 0;  // DIAG
-  to.diag = diag;
   if (debug) {
     to.prof = reinterpret_cast<unsigned long long *>(t_prof.ensure(16));
     FH_HIP(hipMemsetAsync(to.prof, 0, 8 * sizeof(unsigned long long), stream));
