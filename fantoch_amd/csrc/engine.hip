@@ -1557,16 +1557,22 @@ __global__ void __launch_bounds__(256)
 __global__ void k_sv_rows(uint32_t M, const uint32_t *__restrict__ vs,
                           const uint64_t *__restrict__ dep_sorted,
                           const uint64_t *__restrict__ dot, const uint64_t *__restrict__ dlog,
-                          uint64_t *__restrict__ rows) {
+                          uint64_t *__restrict__ rows, uint64_t *__restrict__ lab,
+                          uint32_t *__restrict__ rank) {
   GRID_STRIDE(j, M) {
     const uint64_t x = dep_sorted[j];
     rows[vs[j]] = x == 0 ? ~0ull
                   : is_log_ref(x) ? dlog[x - kLogFlag]  // an earlier batch
                   : (x >> 56) == 0 ? dot[x - 1]         // in-batch index + 1
                                    : x;
+    // the trivial order (every SCC a singleton, arrival order topological):
+    // label = own dot, rank = position, in command order j
+    if (lab) {
+      lab[j] = dot[j];
+      rank[j] = j;
+    }
   }
 }
-
 __global__ void k_seq_dots(uint32_t m, const uint32_t *__restrict__ pk_vid,
                            const uint64_t *__restrict__ dot, uint64_t *__restrict__ seq) {
   GRID_STRIDE(j, m) seq[j] = dot[pk_vid[j]];
@@ -1651,20 +1657,20 @@ __global__ void k_key_offsets(uint32_t m, const uint32_t *__restrict__ keys, uin
   }
 }
 
-__global__ void k_run_start(uint32_t m, const uint32_t *__restrict__ keys,
-                            uint32_t *__restrict__ start) {
-  GRID_STRIDE(j, m) if (j == 0 || keys[j - 1] != keys[j]) start[keys[j]] = j;
-}
-__global__ void k_run_count(uint32_t m, const uint32_t *__restrict__ keys,
-                            const uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
+// Key-grouped runs (the bucket path's per-key order): each run's start, and
+// its length as (end + 1) - start through two atomics into the zeroed count
+// (one launch instead of a start pass and a count pass)
+__global__ void k_run_bounds(uint32_t m, const uint32_t *__restrict__ keys,
+                             uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
   GRID_STRIDE(j, m) {
     const uint32_t k = keys[j];
-    if (j + 1 == m || keys[j + 1] != k) cnt[k] = j + 1 - start[k];
+    if (j == 0 || keys[j - 1] != k) {
+      start[k] = j;
+      atomicSub(&cnt[k], j);
+    }
+    if (j + 1 == m || keys[j + 1] != k) atomicAdd(&cnt[k], j + 1);
   }
 }
-
-// fixed-stride in-batch edges (S slots, the first cnt[i] real) -> CSR: the
-// graph's fixpoint passes then read only real edges (C5: 6.3 of 12 slots)
 __global__ void k_edges_csr(uint32_t n, uint32_t S, const uint32_t *__restrict__ ds,
                             const uint32_t *__restrict__ off, uint32_t *__restrict__ out) {
   GRID_STRIDE(i, n) {
@@ -2948,14 +2954,11 @@ struct EngineDevice {
     if (sv_fused) {
       // one dependency slot per command: the rows themselves; the trivial
       // order's labels and ranks in one coalesced pass
+      uint64_t *lb = gout.trivial ? lab.ensure(n + 1) : nullptr;
+      uint32_t *rk = gout.trivial ? rank_tmp.ensure(n + 1) : nullptr;
       k_sv_rows<<<grid_for(n, B), B, 0, stream>>>(n, sv_vs, dep_ext.get(), bdot, dot.get(),
-                                                   o_rows.ensure(n + 1));
+                                                   o_rows.ensure(n + 1), lb, rk);
       deps_rows = 1;
-      if (gout.trivial) {
-        uint64_t *lb = lab.ensure(n + 1);
-        uint32_t *rk = rank_tmp.ensure(n + 1);
-        k_identity_labels<<<grid_for(n, B), B, 0, stream>>>(n, bdot, lb, rk);
-      }
       sv_labels_done = gout.trivial;
     } else {
       exclusive_scan_u32(dep_cnt.get(), off, n, scan_ws, stream);
@@ -2988,8 +2991,7 @@ struct EngineDevice {
       uint32_t *h = key_hist.ensure(key_space + 1);
       hp = headpos.ensure(key_space + 1);
       FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
-      k_run_start<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp);
-      k_run_count<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
+      k_run_bounds<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
       exclusive_scan_u32(h, o, key_space, scan_ws, stream);
     } else {
       k_key_offsets<<<grid_for(uint32_t(key_space) + 1, B), B, 0, stream>>>(
