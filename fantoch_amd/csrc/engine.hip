@@ -360,6 +360,9 @@ constexpr uint32_t kNoCmd = ~0u;
 
 struct LogOffs {
   uint32_t off[kMaxLogs + 1];
+  // the replica id log r's records carry (identity, or for element logs the
+  // pair-level search's local ids: EngineDevice::unit_meta)
+  uint32_t rid[kMaxLogs];
 };
 
 // rec[e] for every element e = c·fq + j: which replica (log) holds it and at
@@ -414,7 +417,7 @@ __global__ void __launch_bounds__(1024)
       if (f < tot) {
         while (f >= s_pre[r + 1]) r++;
         ev[u] = ent[s_q0[r] + f];
-        vv[u] = (r << kRecT) | (s_ql[r] + f);
+        vv[u] = (lo.rid[r] << kRecT) | (s_ql[r] + f);
       }
     }
 #pragma unroll
@@ -458,6 +461,10 @@ struct CmdMeta {
   uint32_t kb, cb;          // key word: meta from bit kb; value: command in [0, cb)
   uint32_t kmask, W;
   uint64_t cmask, qmask;
+  // the pair-level search (element logs, k keys per command): the units are
+  // (command, key slot) pairs u = c << us | s, so a unit's command is u >> us
+  // (us = 0: units are commands); region records cover 2^rsh units each
+  uint32_t us, rsh;
   __device__ __forceinline__ uint64_t meta(uint32_t kw, uint64_t v) const {
     return (v >> cb) | ((uint64_t(kw) >> kb) << (64 - cb));
   }
@@ -509,6 +516,9 @@ __global__ void __launch_bounds__(kThreads)
     k_cmd_pack(uint32_t n, CmdMeta cm, const uint32_t *__restrict__ key32,
                const uint32_t *__restrict__ rec, uint32_t *__restrict__ kw,
                uint64_t *__restrict__ val, uint32_t *__restrict__ counts, uint32_t dmask) {
+  // unit x = c << us | s (us = 0: a command): view j's record is element
+  // (c·fq + j)·k + s of the element logs' layout
+  const uint32_t kmask1 = (1u << cm.us) - 1u;
   __shared__ uint32_t s_h[256];
   s_h[threadIdx.x] = 0;
   __syncthreads();
@@ -517,7 +527,8 @@ __global__ void __launch_bounds__(kThreads)
     const uint32_t key = key32[x];
     uint64_t m = 0;
     for (uint32_t j = 0; j < cm.fq; j++) {
-      const uint32_t r = rec[size_t(x) * cm.fq + j];
+      const uint32_t r =
+          rec[((size_t(x >> cm.us) * cm.fq + j) << cm.us) | (x & kmask1)];
       m |= ((uint64_t(r >> kRecT) << cm.qb) | (r & cm.qmask)) << (j * cm.vb);
     }
     val[x] = uint64_t(x) | (m << cm.cb);
@@ -677,7 +688,7 @@ __global__ void __launch_bounds__(TH)
   // the command's slot among the tile's records of its region (rec mode)
   uint32_t reg = 0, rank = 0;
   if (rec && i < n) {
-    reg = uint32_t(vload(vals, i) & cm.cmask) >> kRegShift;
+    reg = uint32_t(vload(vals, i) & cm.cmask) >> cm.rsh;
     rank = atomicAdd(&s_reg[reg], 1u);
   }
   __syncthreads();
@@ -686,7 +697,7 @@ __global__ void __launch_bounds__(TH)
   // region from the region's cursor, one atomic per (tile, region), issued
   // now and read after the scans' barrier
   if (rec && tid < uint32_t(kMaxRegions) && s_reg[tid])
-    s_rb[tid] = (tid << kRegShift) + atomicAdd(&rcur[tid], s_reg[tid]);
+    s_rb[tid] = (tid << cm.rsh) + atomicAdd(&rcur[tid], s_reg[tid]);
   const bool act = i < n;
   const uint32_t me = i - lo;
   const uint32_t W = cm.W, H = uint32_t(cm.qmask >> 1) << qs;
@@ -795,7 +806,7 @@ __global__ void __launch_bounds__(TH)
             pcode[size_t(i) * FQ + j] = p + 1u;
           }
         } else {
-          cds[j] = vs[j].bc;  // in-batch: vid + 1
+          cds[j] = ((vs[j].bc - 1u) >> cm.us) + 1u;  // in-batch: the command's vid + 1
         }
       } else {
         const uint64_t xl = latest[uint64_t(rr[j] + 1) * K + key];
@@ -878,7 +889,7 @@ __global__ void k_cmd_tails(uint32_t n, CmdMeta cm, uint32_t K, const uint32_t *
         for (uint32_t j = 0; j < cm.fq; j++) {
           const uint32_t r = cm.rep(m, j);
           if ((msk & (1u << j)) && !(rm & (1u << r)))
-            latest[uint64_t(r + 1) * K + key] = kLogFlag | (log_base + c);
+            latest[uint64_t(r + 1) * K + key] = kLogFlag | (log_base + (c >> cm.us));
         }
       }
     }
@@ -2007,6 +2018,138 @@ struct EngineDevice {
     stage_logs(d, nb, h_dot, h_key, off.data(), cmd.data());
   }
 
+  // Element logs (partial replication) through the pair-level search: the
+  // units are (command, key slot) pairs u = c·k + s, each with its fq views
+  // (elements (c·fq + j)·k + s).  Every process's KeyDeps handles one unit's
+  // key on its own (sequential.rs:72-104 per key), so the unit's dependency at
+  // view j is the latest earlier arrival of its key at that view's process,
+  // exactly the command-level search over units.  Per stage:
+  //  * the logs get replica ids: a greedy colouring of the logs in which two
+  //    logs holding elements of one key differ (a key's processes are its
+  //    shard's, so C5's 40 logs take 5 ids) -- the search indexes its
+  //    per-replica arrival slots, tail marks and latest rows by these ids,
+  //    and a key's table rows stay its own since no two of its logs share an
+  //    id; at most kSrchMaxRep ids;
+  //  * per batch: every unit's fq views lie in logs of different ids, and
+  //    h_win[b] = the logs' inversion span over units (as views_entries does
+  //    over commands).
+  // A batch failing any of it (or k not a power of two <= 8, or a key space
+  // over 2^22) keeps the chunked element path.
+  std::vector<uint32_t> h_rid;      // [kMaxLogs] replica id of each log (batch-local index)
+  std::vector<uint32_t> stage_rid;  // the ids the latest table's rows were last staged under
+  std::vector<uint8_t> h_unit_ok;   // per batch
+  uint32_t unit_colors = 0;
+  void unit_meta(size_t nb, size_t n, uint32_t fq, uint32_t k, size_t np, const uint64_t *h_off,
+                 const uint32_t *h_cmd, const uint64_t *h_key) {
+    if (k > 8 || (k & (k - 1)) || np > uint32_t(kMaxLogs) || key_space > (uint64_t(1) << 22) ||
+        size_t(n) * k >= (size_t(1) << 30))
+      return;
+    const uint32_t us = uint32_t(__builtin_ctz(k));
+    const size_t per_b = n * fq * k, T = host_threads();
+    // 1. the logs holding each key (per-thread masks, OR-reduced)
+    std::vector<std::vector<uint64_t>> km(T);
+    const uint64_t ents = h_off[nb * np];
+    par_for(ents, size_t(1) << 20, [&](size_t part, size_t l, size_t h) {
+      auto &m = km[part];
+      m.assign(key_space, 0);
+      uint32_t x = uint32_t(std::upper_bound(h_off, h_off + nb * np + 1, uint64_t(l)) - h_off) - 1;
+      for (uint64_t q = l; q < h; q++) {
+        while (h_off[x + 1] <= q) x++;
+        const size_t b = x / np, r = x % np;
+        const uint32_t e = h_cmd[q];
+        const size_t c = e / (fq * k), sl = e % k;
+        m[h_key[(b * n + c) * k + sl]] |= uint64_t(1) << r;
+      }
+    });
+    std::vector<uint64_t> adj(np, 0);
+    {
+      std::vector<std::vector<uint64_t>> ad(T, std::vector<uint64_t>(np, 0));
+      par_for(key_space, size_t(1) << 16, [&](size_t part, size_t l, size_t h) {
+        for (size_t key = l; key < h; key++) {
+          uint64_t m = 0;
+          for (auto &t : km) m |= t.empty() ? 0 : t[key];
+          for (uint64_t b = m; b; b &= b - 1) ad[part][__builtin_ctzll(b)] |= m;
+        }
+      });
+      for (auto &a : ad)
+        for (size_t r = 0; r < np; r++) adj[r] |= a[r];
+    }
+    km.clear();
+    // greedy colouring in log order
+    std::vector<uint32_t> rid(np, 0);
+    uint32_t colors = 0;
+    for (size_t r = 0; r < np; r++) {
+      uint32_t used = 0;
+      for (size_t q = 0; q < r; q++)
+        if (adj[r] >> q & 1) used |= 1u << rid[q];
+      uint32_t c = 0;
+      while (c < uint32_t(kSrchMaxRep) && (used >> c & 1)) c++;
+      if (c >= uint32_t(kSrchMaxRep)) return;
+      rid[r] = c;
+      colors = std::max(colors, c + 1);
+    }
+    // 2. per batch: distinct ids per unit, and the inversion span over units
+    std::vector<uint8_t> um(size_t(n) * k);
+    struct Seg {
+      uint32_t r, maxu, minu, win;
+    };
+    for (size_t b = 0; b < nb; b++) {
+      std::fill(um.begin(), um.end(), 0);
+      const uint64_t base = h_off[b * np], cnt = uint64_t(per_b);
+      const uint64_t *lb = h_off + b * np;
+      std::atomic<bool> bad{false};
+      std::vector<std::vector<Seg>> segs(T);
+      par_for(cnt, size_t(1) << 20, [&](size_t part, size_t l, size_t h) {
+        auto &sg = segs[part];
+        uint64_t q = base + l;
+        uint32_t r = uint32_t(std::upper_bound(lb, lb + np + 1, q) - lb) - 1;
+        while (q < base + h) {
+          while (lb[r + 1] <= q) r++;
+          const uint64_t end = std::min<uint64_t>(base + h, lb[r + 1]);
+          const uint8_t bit = uint8_t(1u << rid[r]);
+          Seg g{r, 0, ~0u, 0};
+          uint32_t pmax = 0;
+          for (; q < end; q++) {
+            const uint32_t e = h_cmd[q];
+            const uint32_t u = uint32_t(((e / (fq * k)) << us) | (e % k));
+            if (__atomic_fetch_or(&um[u], bit, __ATOMIC_RELAXED) & bit) bad = true;  // (a view twice)
+            pmax = std::max(pmax, u);
+            g.win = std::max(g.win, pmax - u);
+            g.minu = std::min(g.minu, u);
+          }
+          g.maxu = pmax;
+          sg.push_back(g);
+        }
+      });
+      if (bad) {
+        h_unit_ok.assign(nb, 0);
+        return;
+      }
+      std::vector<uint32_t> run_max(np, 0);
+      std::vector<bool> started(np, false);
+      uint32_t w = 0;
+      for (auto &sg : segs)
+        for (const Seg &g : sg) {
+          w = std::max(w, g.win);
+          if (started[g.r] && run_max[g.r] > g.minu) w = std::max(w, run_max[g.r] - g.minu);
+          run_max[g.r] = started[g.r] ? std::max(run_max[g.r], g.maxu) : g.maxu;
+          started[g.r] = true;
+        }
+      h_win[b] = w;
+      h_unit_ok[b] = 1;
+    }
+    // the latest table's replica rows follow the ids: a stage that continues
+    // an earlier one (log_len > 0) keeps that one's ids, or stays chunked
+    std::vector<uint32_t> ids(kMaxLogs);
+    for (uint32_t r = 0; r < uint32_t(kMaxLogs); r++) ids[r] = r < np ? rid[r] : r;
+    if (log_len > 0 && ids != stage_rid) {
+      h_unit_ok.assign(nb, 0);
+      return;
+    }
+    h_rid = ids;
+    unit_colors = colors;
+  }
+
   // Command logs of nb batches (stage_logs): validated per batch on
   // host_threads() threads and uploaded to dl.  Entry q of log r (command c)
   // is c·fq + j with j = the number of lower logs holding c: each command's
@@ -2176,6 +2319,10 @@ struct EngineDevice {
     // the device side from here: a stage that fails below leaves nothing staged
     staged = false;
     h_dpack = dpack;
+    h_unit_ok.assign(nb, 0);
+    h_rid.assign(kMaxLogs, 0);
+    for (uint32_t r = 0; r < uint32_t(kMaxLogs); r++) h_rid[r] = r;
+    unit_colors = 0;
     // append the batches' dots to the command log (grown by doubling, old
     // entries kept: earlier batches stay referenced by the latest table)
     const size_t need = log_len + n * nb + 1;
@@ -2230,6 +2377,7 @@ struct EngineDevice {
           });
           ring.upload_copy(dl + base, h_cmd + base, cnt, stream);
         }
+        if (!subset) unit_meta(nb, n, fq, d.keys_per_cmd, np, h_off, h_cmd, h_key);
       } else if (np <= 8) {
         views_entries<uint8_t>(nb, n, fq, np, h_off, h_cmd, dl);
       } else if (np <= 16) {
@@ -2246,6 +2394,7 @@ struct EngineDevice {
     }
     stage_base = log_len;
     log_len += n * nb;
+    stage_rid = h_rid;
     FH_HIP(hipStreamSynchronize(stream));
     desc = d;
     nbatches = nb;
@@ -2370,7 +2519,7 @@ struct EngineDevice {
       sorted_keys32 = ks;
     } else if (CmdMeta cm; cmd_meta(b, k, fq, n, &cm)) {
       sv_fused = false;
-      if (keyorder_ok(b, fq)) {
+      if (keyorder_ok(b, fq, cm)) {
         ko_done = cmd_views_keyorder(b, n, fq, bkey, bdot, bbase, cm);
       } else {
         cmd_views(b, n, fq, M, bkey, bbase, cm);
@@ -2474,17 +2623,32 @@ struct EngineDevice {
       const char *e = getenv("FH_VIEW_CMD");
       return !(e && *e == '0');
     }();
-    if (!on || k != 1 || fq > 4 || desc.nproc > uint32_t(kSrchMaxRep) || b >= h_win.size() ||
-        (desc.flags & FH_STREAM_ELEMENT_LOGS) ||
-        n >= (1u << kRecT) || n < 2)
+    // element logs: the pair-level search over (command, key slot) units
+    // when staging found it applicable (unit_meta)
+    const bool units = (desc.flags & FH_STREAM_ELEMENT_LOGS) && !codes_only &&
+                       b < h_unit_ok.size() && h_unit_ok[b];
+    if (!on || fq > 4 || b >= h_win.size() || n < 2) return false;
+    if (!units && (k != 1 || desc.nproc > uint32_t(kSrchMaxRep) ||
+                   (desc.flags & FH_STREAM_ELEMENT_LOGS) || n >= (1u << kRecT)))
       return false;
+    const uint64_t nu = uint64_t(n) * k;  // units
+    if (units && nu >= (uint64_t(1) << 30)) return false;
+    if (units) {  // log positions travel in kRecT bits of the view records
+      const uint32_t *bl = h_loff.data() + b * size_t(desc.nproc + 1);
+      for (uint32_t r = 0; r < desc.nproc; r++)
+        if (bl[r + 1] - bl[r] >= (1u << kRecT)) return false;
+    }
     CmdMeta m{};
     m.fq = fq;
-    m.rb = uint32_t(bits_for(desc.nproc));
+    m.us = units ? uint32_t(__builtin_ctz(k)) : 0u;
+    m.rb = uint32_t(bits_for(units ? unit_colors : desc.nproc));
     const int db = sort_digit_bits(key_bits, 4);
     const int passes = std::max(1, (key_bits + db - 1) / db);
     m.kb = uint32_t(passes * db);
-    m.cb = uint32_t(bits_for(n));
+    m.cb = uint32_t(bits_for(nu));
+    // region records of 2^rsh units, at most kMaxRegions of them
+    m.rsh = kRegShift;
+    while (((nu - 1) >> m.rsh) + 1 > kMaxRegions) m.rsh++;
     if (m.kb > 32) return false;
     // the meta travels in the key word's and the value's free bits and is
     // handled as one u64
@@ -2504,8 +2668,9 @@ struct EngineDevice {
   // The key-order path applies to command-level batches with fast quorums of
   // 2 or 3 whose dots pack into 31 bits (the records' top bit marks a log
   // reference).
-  bool keyorder_ok(size_t b, uint32_t fq) const {
-    return !keyorder_off && (fq == 2 || fq == 3) && b < h_dpack.size() &&
+  bool keyorder_ok(size_t b, uint32_t fq, const CmdMeta &cm) const {
+    return !keyorder_off && cm.us == 0 && desc.keys_per_cmd == 1 && (fq == 2 || fq == 3) &&
+           b < h_dpack.size() &&
            h_dpack[b].second > 0 && h_dpack[b].second <= 31 && dot32.get() != nullptr;
   }
 
@@ -2522,6 +2687,7 @@ struct EngineDevice {
     LogOffs lo{};
     const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
     for (uint32_t r = 0; r <= np; r++) lo.off[r] = bl[r];
+    for (uint32_t r = 0; r < np; r++) lo.rid[r] = h_rid[r];
     const uint32_t *bent = lent.get() + b * size_t(n) * fq;
     const uint32_t M = n * fq;
     uint32_t *rec = vrec.ensure(M + 1);
@@ -2708,20 +2874,30 @@ struct EngineDevice {
     return true;
   }
 
-  void cmd_views(size_t b, uint32_t n, uint32_t fq, uint32_t M, const uint32_t *bkey,
+  // (units: element logs through the pair-level search, n commands of k
+  // keys = n·k units; cm.us = log2 k; every array below is per unit)
+  void cmd_views(size_t b, uint32_t nc, uint32_t fq, uint32_t M, const uint32_t *bkey,
                  uint64_t bbase, const CmdMeta &cm) {
     const uint32_t np = desc.nproc;
+    const uint32_t n = nc << cm.us;  // units
+    // replica ids the search indexes its per-replica slots by: the logs, or
+    // their colouring (units; unit_meta)
+    const uint32_t nrep = cm.us || (desc.flags & FH_STREAM_ELEMENT_LOGS) ? unit_colors : np;
+    FH_CHECK(nrep >= 1 && nrep <= uint32_t(kSrchMaxRep), FH_EINVARIANT, "search replicas");
     LogOffs lo{};
     const uint32_t *bl = h_loff.data() + b * size_t(np + 1);
     for (uint32_t r = 0; r <= np; r++) lo.off[r] = bl[r];
-    const uint32_t *bent = lent.get() + b * size_t(n) * fq;
+    for (uint32_t r = 0; r < np; r++) lo.rid[r] = h_rid[r];
+    const uint32_t *bent = lent.get() + b * size_t(M);
     uint32_t *rec = vrec.ensure(M + 1);
     // ~4800 commands per workgroup: fq·4800 + slack positions fit the window
-    // (tried: 8K windows 1391 us per C4 launch, 32K 1072, 16K 935)
-    const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * rec_slack(kRecWin)) / fq);
-    const uint32_t G = std::max<uint32_t>(1, (n + per - 1) / per);
+    // (tried: 8K windows 1391 us per C4 launch, 32K 1072, 16K 935); element
+    // logs hold fq·k elements per command
+    const uint32_t epc = fq << cm.us;
+    const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * rec_slack(kRecWin)) / epc);
+    const uint32_t G = std::max<uint32_t>(1, (nc + per - 1) / per);
     probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records<kRecWin>, dim3(G),
-                  dim3(1024), stream, n, fq, np, G, lo, bent, rec);
+                  dim3(1024), stream, nc, epc, np, G, lo, bent, rec);
     const uint32_t tiles = (n + kTile - 1) / kTile;
     sort_ws.prepare(tiles, 1, stream);
     const int db = sort_digit_bits(key_bits, 4);
@@ -2745,7 +2921,7 @@ struct EngineDevice {
     // fq <= 3) and the tail mask.  1024 threads (tried 256 / 512: flat)
     uint32_t *codes = dep32.ensure(size_t(M) + 1);
     const uint32_t stiles = (n + kSrchThreads - 1) / kSrchThreads;
-    const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> kRegShift) + 1;
+    const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> cm.rsh) + 1;
     FH_CHECK(nreg <= kMaxRegions, FH_EINVARIANT, "command regions");
     uint4 *rec4 = nullptr;
     uint32_t *rcur = nullptr;
@@ -2758,7 +2934,7 @@ struct EngineDevice {
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
     auto go = [&](auto kern) {
-      probed_launch("cmd_search", sb, kern, dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, np,
+      probed_launch("cmd_search", sb, kern, dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, nrep,
                     (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, rec4, rcur, tm, mr,
                     (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr);
     };

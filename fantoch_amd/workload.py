@@ -183,6 +183,32 @@ class Workload:
         return s
 
 
+# Per-command cost of a key relative to a cold one, as a function of the
+# key's share of the stream: a hot key's commands scan more same-key
+# neighbours in the KeyDeps search and form larger ready groups in the tile
+# kernel.  Measured on the C4 stream's 8 balanced shards (12.5M commands
+# each, tools/shard_probe.py, profiles/r06_shards_balanced.jsonl): shards
+# whose hottest key holds 0.8-2.2M commands run 1.62-1.70 ms, 3.3M 1.78 ms,
+# 6.5M (the stream's hottest key, 6.5 % of it) 2.25 ms -- about 1.7x per
+# command for that key, 1.35x for the 3.3 % one: 1 + 10.8 x share.
+HOT_KEY_COST = 14.0
+
+
+def key_weights(hist: np.ndarray) -> np.ndarray:
+    """Per-key work estimates for the key map: the command count times
+    1 + HOT_KEY_COST x the key's share of the stream (x16, integral)."""
+    h = np.asarray(hist, dtype=np.float64)
+    tot = max(1.0, h.sum())
+    return np.rint(16.0 * h * (1.0 + HOT_KEY_COST * h / tot)).astype(np.uint64)
+
+
+def key_owners_weighted(hist: np.ndarray, nshards: int) -> np.ndarray:
+    """key_owners_balanced over key_weights(hist): balances the estimated
+    work per shard instead of the command count (the shard holding the
+    hottest key gets fewer commands)."""
+    return key_owners_balanced(key_weights(hist), nshards)
+
+
 def key_owners_balanced(hist: np.ndarray, nshards: int) -> np.ndarray:
     """u32[key_space] key -> shard map balancing the per-key command counts
     `hist` over `nshards` (fh_key_owners_balanced: greedy largest-first

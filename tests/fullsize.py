@@ -28,6 +28,13 @@ CONFIGS = {
                              "owner = fh_key_owners_balanced over the stream's key counts)",
                         total=20_000_000, nshards=8, shard=0, balanced=True,
                         workload=lambda: Workload.zipf(0.99, 1 << 20, k=1, seed=SEED + 4, **KW)),
+    # the shard holding the hottest key under the work-weighted key map
+    # bench.py --gpus N uses (key_owners_weighted: the hot key's commands
+    # weighted by their cost, so this shard holds fewer commands)
+    "c4shard_w": dict(desc="C4 work-weighted key shard 0 of 8 of a 20M-command stream (global "
+                           "dots; owner = key_owners_weighted over the stream's key counts)",
+                      total=20_000_000, nshards=8, shard=0, weighted=True,
+                      workload=lambda: Workload.zipf(0.99, 1 << 20, k=1, seed=SEED + 4, **KW)),
     "c3": dict(desc="C3 EPaxos ConflictPool 100% (key 0 + 16-key pool), 2 keys: deps at 10M, "
                     "everything on the first 50k", n=10_000_000, prefix=50_000,
                workload=lambda: Workload.conflict_pool(100, 16, k=2, seed=SEED + 3, **KW)),

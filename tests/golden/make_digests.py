@@ -20,7 +20,9 @@ Configurations (seeds as tools/bench_configs.py):
             (full size, bench.py's stream)
   c4shard   key shard 0 of 8 of a 20M-command C4 stream (global dots)
   c4shard_bal  the same stream's shard 0 of 8 under the balanced key map
-            (fh_key_owners_balanced over its key counts; bench.py --gpus N)
+            (fh_key_owners_balanced over its key counts)
+  c4shard_w the same stream's shard 0 of 8 under the work-weighted key map
+            (key_owners_weighted; bench.py --gpus N)
   c3        EPaxos ConflictPool 100% (key 0 + 16-key pool), 2 keys: deps at the
             full 10M, everything on the first 50k (the incremental Tarjan is
             quadratic on its one stream-wide SCC)
@@ -96,9 +98,10 @@ def main():
         entry = {"desc": c["desc"]}
         if name.startswith("c4shard"):
             full = w.generate(c["total"])
-            if c.get("balanced"):
-                from fantoch_amd.workload import key_owners_balanced
-                owner = key_owners_balanced(w.key_histogram(c["total"]), c["nshards"])
+            if c.get("balanced") or c.get("weighted"):
+                from fantoch_amd.workload import key_owners_balanced, key_owners_weighted
+                om = key_owners_weighted if c.get("weighted") else key_owners_balanced
+                owner = om(w.key_histogram(c["total"]), c["nshards"])
                 mine = np.nonzero(owner[full.keys[:, 0]] == c["shard"])[0]
             else:
                 mine = np.nonzero(full.keys[:, 0] % c["nshards"] == c["shard"])[0]

@@ -78,6 +78,19 @@ def test_c4_balanced_key_shard_digest():
     check_digests(g, run_engine(s))
 
 
+def test_c4_weighted_key_shard_digest():
+    """Shard 0 of 8 under the work-weighted key map (key_owners_weighted),
+    as bench.py --gpus 8 gives rank 0: the shard holding the hottest key."""
+    from fantoch_amd.workload import key_owners_weighted
+    g = gold("c4shard_w")
+    c = CONFIGS["c4shard_w"]
+    w = c["workload"]()
+    owner = key_owners_weighted(w.key_histogram(c["total"]), c["nshards"])
+    s = w.generate_shard(c["total"], c["nshards"], c["shard"], owner=owner)
+    assert s.n == g["n"]
+    check_digests(g, run_engine(s))
+
+
 @pytest.mark.parametrize("name", ["c3", "c5_12m", "c5"])
 def test_prefix_digest(name):
     """C3 / the unsharded 4-key stream / C5's partial replication: everything

@@ -50,3 +50,24 @@ def test_owned_shards_partition_the_stream():
         seen.append(g.dots)
     allv = np.sort(np.concatenate(seen))
     assert np.array_equal(allv, np.sort(full.dots))
+
+
+def test_c4_100m_work_weighted_map():
+    """key_owners_weighted: the same packing over key_weights (count x (1 +
+    HOT_KEY_COST x share)); the shard holding the hottest key gets fewer
+    commands, every shard's estimated work stays within 5 % of the mean, and
+    the map is a function of the counts alone (every rank computes it)."""
+    from fantoch_amd.workload import HOT_KEY_COST, key_owners_weighted, key_weights
+    w = c4()
+    h = w.key_histogram(100_000_000)
+    wt = key_weights(h)
+    hot = int(np.argmax(h))
+    share = float(h[hot]) / float(h.sum())
+    assert abs(float(wt[hot]) / (16.0 * float(h[hot])) - (1 + HOT_KEY_COST * share)) < 1e-6
+    for n in (2, 4, 8):
+        o = key_owners_weighted(h, n)
+        assert np.array_equal(o, key_owners_weighted(h.copy(), n))
+        work = np.bincount(o, weights=wt.astype(np.float64), minlength=n)
+        assert work.max() <= 1.05 * work.mean(), (n, work)
+        cmds = np.bincount(o, weights=h.astype(np.float64), minlength=n)
+        assert cmds[o[hot]] == cmds.min()

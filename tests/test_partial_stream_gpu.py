@@ -54,10 +54,14 @@ def test_partial_stream_matches_oracle(shards, keys, k, n, seed):
     assert np.array_equal(r["key_off"], kso) and np.array_equal(r["key_seq"], ks), "per-key"
 
 
-def test_partial_stream_in_chunks_matches_oracle():
-    """Small KeyDeps chunks (FH_VIEW_CHUNK, read once per process: a child
-    process), so each of the 40 replicas' (replica, key) segments crosses
-    chunks and bucketing workgroups."""
+@pytest.mark.parametrize("env", [{"FH_VIEW_CHUNK": "30000"},
+                                 {"FH_VIEW_CHUNK": "30000", "FH_VIEW_CMD": "0"}])
+def test_partial_stream_in_chunks_matches_oracle(env):
+    """Element logs through the pair-level search (default), and through the
+    chunked element path (FH_VIEW_CMD=0) with small KeyDeps chunks
+    (FH_VIEW_CHUNK; both read once per process: a child process), so each of
+    the 40 replicas' (replica, key) segments crosses chunks and bucketing
+    workgroups."""
     import os
     import subprocess
     import sys
@@ -78,9 +82,8 @@ got_off, got = eng.deps()
 assert np.array_equal(got_off, off) and np.array_equal(got, deps)
 print("ok")
 """
-    env = dict(os.environ, FH_VIEW_CHUNK="30000")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=200,
-                       env=env)
+                       env=dict(os.environ, **env))
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
@@ -144,3 +147,39 @@ def test_partial_replication_changes_the_graph():
     largest = np.unique(r["scc_label"], return_counts=True)[1].max()
     largest1 = np.unique(r1["scc_label"], return_counts=True)[1].max()
     assert largest > largest1, (largest, largest1)
+
+
+@pytest.mark.parametrize("shards,keys,n,seed", [(8, 4096, 20_000, 61), (8, 1 << 20, 20_000, 62),
+                                                (2, 256, 8000, 63)])
+def test_pair_search_equals_chunked_path(shards, keys, n, seed):
+    """The pair-level search ((command, key slot) units, engine.hip
+    unit_meta) and the chunked element path (FH_VIEW_CMD=0, a child process)
+    give identical outputs on partially replicated 4-key streams."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import numpy as np, sys
+sys.path.insert(0, {root!r})
+from fantoch_amd.engine import Engine
+from fantoch_amd.workload import Workload
+s = Workload.zipf(0.99, {keys}, k=4, views=3, window=64, seed={seed}, n=5,
+                  shards={shards}).generate({n}, logs=True)
+eng = Engine(s.key_space, n=5)
+eng.stage(s)
+eng.run()
+r = eng.results()
+np.savez(sys.argv[1], **r)
+"""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        outs = []
+        for i, env in enumerate(({}, {"FH_VIEW_CMD": "0"})):
+            f = os.path.join(d, f"r{i}.npz")
+            p = subprocess.run([sys.executable, "-c", code, f], capture_output=True, text=True,
+                               timeout=200, env=dict(os.environ, **env))
+            assert p.returncode == 0, p.stdout + p.stderr
+            outs.append(np.load(f))
+        for key in ("dep_off", "deps", "scc_label", "key_off", "key_seq"):
+            assert np.array_equal(outs[0][key], outs[1][key]), key

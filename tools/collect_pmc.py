@@ -44,6 +44,9 @@ PROBES = {
     "region_count": r"k_region_count<",
     "row_count": r"k_row_count<",
     "row_union": r"k_row_union<",
+    "row_place": r"k_row_place<",
+    "sv_rows": r"k_sv_rows",
+    "run_bounds": r"k_run_bounds",
     "ko_final": r"k_ko_final",
     "key_counts": r"k_key_counts",
     "sort_up": r"k_up<",

@@ -19,18 +19,31 @@ sys.path.insert(0, ROOT)
 from fantoch_amd.engine import Engine  # noqa: E402
 from fantoch_amd.workload import Workload, key_owners_balanced  # noqa: E402
 
+try:
+    from fantoch_amd.workload import key_owners_weighted  # noqa: E402
+except ImportError:  # (older trees)
+    key_owners_weighted = None
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--commands", type=int, default=100_000_000)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--shards", default="", help="comma-separated shard ids (default: the largest)")
+    ap.add_argument("--owners", default="balanced", help="balanced | weighted (key map)")
     a = ap.parse_args()
     w = Workload.zipf(0.99, 1 << 20, k=1, views=3, window=64, seed=0xFA170C4000000004, n=5)
     h = w.key_histogram(a.commands)
-    owner = key_owners_balanced(h, a.ranks)
+    owner = key_owners_balanced(h, a.ranks) if a.owners == "balanced" else \
+        key_owners_weighted(h, a.ranks)
     loads = np.bincount(owner, weights=h.astype(np.float64), minlength=a.ranks)
-    q = int(np.argmax(loads))
+    shards = [int(x) for x in a.shards.split(",")] if a.shards else [int(np.argmax(loads))]
+    for q in shards:
+        probe(w, a, owner, q)
+
+
+def probe(w, a, owner, q):
     s = w.generate_shard(a.commands, a.ranks, q, owner=owner)
     eng = Engine(s.key_space, n=5, device=0)
     eng.stage(s)
@@ -49,7 +62,9 @@ def main():
     phases = {k: round(v, 4) for k, v in eng.kernel_times()}
     eng.set_profiling(False)
     eng.close()
-    print(json.dumps({"ranks": a.ranks, "shard": q, "commands": int(s.n), "ms_per_step": round(ms, 4),
+    hot = int(np.bincount(s.keys[:, 0].astype(np.int64)).max())
+    print(json.dumps({"ranks": a.ranks, "owners": a.owners, "shard": q, "commands": int(s.n),
+                      "hottest_key_commands": hot, "ms_per_step": round(ms, 4),
                       "phases_ms": phases}), flush=True)
 
 
