@@ -2898,6 +2898,7 @@ struct EngineDevice {
     const uint32_t G = std::max<uint32_t>(1, (nc + per - 1) / per);
     probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records<kRecWin>, dim3(G),
                   dim3(1024), stream, nc, epc, np, G, lo, bent, rec);
+    mark(cm.us ? "unit_records" : "cmd_records");
     const uint32_t tiles = (n + kTile - 1) / kTile;
     sort_ws.prepare(tiles, 1, stream);
     const int db = sort_digit_bits(key_bits, 4);
@@ -2911,6 +2912,7 @@ struct EngineDevice {
     uint64_t *vs = nullptr;
     sort_pairs_counted<uint32_t, uint64_t>(kwa, va, sk32b.ensure(n + 1), cv64b.ensure(n + 1), n,
                                            key_bits, sort_ws, stream, &ks, &vs, db);
+    mark(cm.us ? "unit_sort" : "cmd_sort");
     uint8_t *tm = tailm.ensure(n + 16);  // (k_cmd_tails reads it 16 bytes at a time)
     // predecessor marks from other tiles (k_cmd_search, k_cmd_tails)
     const size_t mwords = (size_t(n) + 3) / 4;
@@ -2944,6 +2946,7 @@ struct EngineDevice {
       case 3: go(k_cmd_search<3, kSrchThreads, uint64_t, false>); break;
       default: go(k_cmd_search<4, kSrchThreads, uint64_t, false>); break;
     }
+    mark(cm.us ? "unit_search" : "cmd_search");
     if (rec4) {
       auto sc = [&](auto kern) {
         probed_launch("code_scatter", double(n) * (16.0 + 4.0 * fq), kern,

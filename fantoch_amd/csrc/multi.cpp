@@ -2,8 +2,9 @@
 // from one process (SURVEY §8b "fh_multi_create / fh_multi_run", §8e).
 //
 // Key-shard partition: owner(key) from fh_key_owners_balanced over the
-// staged stream's per-key command counts (G = engines; key mod G left the
-// largest of 8 shards at 1.37x the mean under Zipf 0.99).  With one key
+// staged stream's per-key work estimates (command counts weighted up for
+// hot keys; G = engines; key mod G left the largest of 8 shards at 1.37x the
+// mean under Zipf 0.99).  With one key
 // per command every dependency joins two commands of one key (each
 // replica's KeyDeps chains a key's commands, keys/sequential.rs:72-104), so
 // a shard's dependency graph is closed: the shards order independently and
@@ -132,8 +133,17 @@ fh_status fh_multi_stage_logs(fh_multi *h, const fh_stream_desc *desc, const uin
     FH_CHECK(key_id[i] < K, FH_EINVAL, "key id >= key_space");
     hist[key_id[i]]++;
   }
+  // packed by estimated work, not by count: a hot key's commands cost more
+  // (longer same-key scans in the search, larger ready groups in the tile
+  // kernel), count x (1 + 14 x share), x16 -- fantoch_amd/workload.py
+  // key_weights, measured on the C4 stream's 8 shards
+  std::vector<uint64_t> wt(K);
+  for (size_t x = 0; x < K; x++) {
+    const double h = double(hist[x]);
+    wt[x] = uint64_t(16.0 * h * (1.0 + 14.0 * h / double(std::max<size_t>(n, 1))) + 0.5);
+  }
   std::vector<uint32_t> owner(K);
-  check_status(fh_key_owners_balanced(hist.data(), K, uint32_t(G), owner.data()));
+  check_status(fh_key_owners_balanced(wt.data(), K, uint32_t(G), owner.data()));
   std::vector<uint32_t> shard_of(n), local(n);
   std::vector<std::vector<uint32_t>> cmds(G);
   for (size_t i = 0; i < n; i++) {

@@ -1,6 +1,6 @@
 """MultiEngine -- the fused engine over several GPUs from one process
 (fh_multi_*): one engine per device over key shards (owner from
-fh_key_owners_balanced over the staged stream's key counts); see
+fh_key_owners_balanced over the staged stream's per-key work estimates); see
 include/fantoch_hip.h."""
 from __future__ import annotations
 
