@@ -381,7 +381,8 @@ constexpr uint32_t rec_slack(uint32_t win) { return win / 16; }
 template <uint32_t WIN>
 __global__ void __launch_bounds__(1024)
     k_view_records(uint32_t n, uint32_t fq, uint32_t np, uint32_t G, LogOffs lo,
-                   const uint32_t *__restrict__ ent, uint32_t *__restrict__ rec) {
+                   const uint32_t *__restrict__ ent, uint32_t *__restrict__ rec,
+                   const uint32_t *__restrict__ bounds) {
   __shared__ uint32_t s_v[WIN];
   __shared__ uint32_t s_pre[kMaxLogs + 1], s_q0[kMaxLogs], s_ql[kMaxLogs];
   const uint32_t w = blockIdx.x;
@@ -392,11 +393,17 @@ __global__ void __launch_bounds__(1024)
   // entry f is ent[s_q0[r] + f], position s_ql[r] + f of log r), sixteen per
   // thread with their loads issued together (tried: log by log, four loads
   // per trip: 836 us per C4 launch)
+  // bounds (element logs, staged): slice w of log r is its entries from the
+  // first one of command >= c0 -- a log's share of the commands drifts
+  // along the stream when which processes hold a command depends on its
+  // keys, so proportional slices would leave most records outside the window
   if (threadIdx.x == 0) {
     uint32_t t = 0;
     for (uint32_t r = 0; r < np; r++) {
       const uint64_t len = lo.off[r + 1] - lo.off[r];
-      const uint32_t q0 = lo.off[r] + uint32_t(len * w / G), q1 = lo.off[r] + uint32_t(len * (w + 1) / G);
+      const uint32_t q0 = lo.off[r] + (bounds ? bounds[size_t(w) * np + r] : uint32_t(len * w / G));
+      const uint32_t q1 = lo.off[r] + (bounds ? bounds[size_t(w + 1) * np + r]
+                                             : uint32_t(len * (w + 1) / G));
       s_pre[r] = t;
       s_q0[r] = q0 - t;
       s_ql[r] = q0 - lo.off[r] - t;
@@ -615,7 +622,7 @@ constexpr int kSrchHalo = 128;
 constexpr int kSrchMaxRep = 8;  // replicas (logs) of the command-level path
 constexpr uint32_t kNoArr = ~0u;
 constexpr uint32_t kRegShift = 22;   // code regions of 4M commands (48 MB of codes)
-constexpr uint32_t kMaxRegions = 32; // n < 2^27
+constexpr uint32_t kMaxRegions = 128;  // units < 2^29 at 4M per region (C4: 24 regions)
 
 // Per-view scan state; `bc` is the best candidate's command + 1 (0: none),
 // `bp` its sorted position.  Arrivals are shifted left by 32 - qb, so `close`
@@ -2037,6 +2044,11 @@ struct EngineDevice {
   // over 2^22) keeps the chunked element path.
   std::vector<uint32_t> h_rid;      // [kMaxLogs] replica id of each log (batch-local index)
   std::vector<uint32_t> stage_rid;  // the ids the latest table's rows were last staged under
+  // per batch: the view records' slice bounds of the element logs (k_view_records
+  // `bounds`, (G + 1) x np entries at vbnd + h_vbnd_off[b]) and their G
+  std::vector<uint32_t> h_vbnd_g;
+  std::vector<size_t> h_vbnd_off;
+  DBuf<uint32_t> vbnd;
   std::vector<uint8_t> h_unit_ok;   // per batch
   uint32_t unit_colors = 0;
   void unit_meta(size_t nb, size_t n, uint32_t fq, uint32_t k, size_t np, const uint64_t *h_off,
@@ -2148,6 +2160,31 @@ struct EngineDevice {
     }
     h_rid = ids;
     unit_colors = colors;
+    // the view records' slices (cmd_views' G): per log, the first entry of
+    // each slice's first command, one monotone walk per log
+    const uint32_t epc = fq * k;
+    const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * rec_slack(kRecWin)) / epc);
+    const uint32_t G = std::max<uint32_t>(1, uint32_t((n + per - 1) / per));
+    std::vector<uint32_t> bnd(nb * size_t(G + 1) * np);
+    h_vbnd_g.assign(nb, G);
+    h_vbnd_off.assign(nb, 0);
+    for (size_t b = 0; b < nb; b++) {
+      h_vbnd_off[b] = b * size_t(G + 1) * np;
+      par_for(np, 1, [&](size_t, size_t l, size_t h) {
+        for (size_t r = l; r < h; r++) {
+          const uint64_t q0 = h_off[b * np + r], len = h_off[b * np + r + 1] - q0;
+          uint64_t q = 0;
+          for (uint32_t w = 0; w <= G; w++) {
+            const uint64_t c0 = w == G ? ~uint64_t(0) : uint64_t(n) * w / G;
+            while (q < len && h_cmd[q0 + q] / epc < c0) q++;
+            bnd[h_vbnd_off[b] + size_t(w) * np + r] = uint32_t(q);
+          }
+        }
+      });
+    }
+    FH_HIP(hipMemcpyAsync(vbnd.ensure(bnd.size() + 1), bnd.data(), bnd.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, stream));
+    FH_HIP(hipStreamSynchronize(stream));
   }
 
   // Command logs of nb batches (stage_logs): validated per batch on
@@ -2709,7 +2746,7 @@ struct EngineDevice {
     k_key_counts<<<dim3(tiles), dim3(kThreads), 0, ks0>>>(n, bkey, sort_ws.meta.get(),
                                                           (1u << db) - 1);
     probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records<kRecWin>, dim3(G),
-                  dim3(1024), stream, n, fq, np, G, lo, bent, rec);
+                  dim3(1024), stream, n, fq, np, G, lo, bent, rec, (const uint32_t *)nullptr);
     if (!side_off) {
       FH_HIP(hipEventRecord(ev_join, side));
       FH_HIP(hipStreamWaitEvent(stream, ev_join, 0));
@@ -2896,8 +2933,13 @@ struct EngineDevice {
     const uint32_t epc = fq << cm.us;
     const uint32_t per = std::max<uint32_t>(1, (kRecWin - 2 * rec_slack(kRecWin)) / epc);
     const uint32_t G = std::max<uint32_t>(1, (nc + per - 1) / per);
+    const uint32_t *vb = nullptr;
+    if (cm.us || (desc.flags & FH_STREAM_ELEMENT_LOGS)) {
+      FH_CHECK(b < h_vbnd_g.size() && h_vbnd_g[b] == G, FH_EINVARIANT, "view record slices");
+      vb = vbnd.get() + h_vbnd_off[b];
+    }
     probed_launch("view_records", double(M) * (4.0 + 4.0), k_view_records<kRecWin>, dim3(G),
-                  dim3(1024), stream, nc, epc, np, G, lo, bent, rec);
+                  dim3(1024), stream, nc, epc, np, G, lo, bent, rec, vb);
     mark(cm.us ? "unit_records" : "cmd_records");
     const uint32_t tiles = (n + kTile - 1) / kTile;
     sort_ws.prepare(tiles, 1, stream);
@@ -2922,7 +2964,11 @@ struct EngineDevice {
     // the heads' latest entries, writes fq codes (through region records when
     // fq <= 3) and the tail mask.  1024 threads (tried 256 / 512: flat)
     uint32_t *codes = dep32.ensure(size_t(M) + 1);
-    const uint32_t stiles = (n + kSrchThreads - 1) / kSrchThreads;
+    // units (element logs): 512-unit tiles, four workgroups per CU, as the
+    // key-order path measured faster than 1024 (§5.1 item 4)
+    const bool t512 = (cm.us || (desc.flags & FH_STREAM_ELEMENT_LOGS)) && (fq == 2 || fq == 3);
+    const uint32_t sth = t512 ? 512u : uint32_t(kSrchThreads);
+    const uint32_t stiles = (n + sth - 1) / sth;
     const uint32_t nreg = uint32_t((uint64_t(n) - 1) >> cm.rsh) + 1;
     FH_CHECK(nreg <= kMaxRegions, FH_EINVARIANT, "command regions");
     uint4 *rec4 = nullptr;
@@ -2936,16 +2982,21 @@ struct EngineDevice {
     const uint32_t K = uint32_t(key_space);
     const uint64_t *lat = views_latest();
     auto go = [&](auto kern) {
-      probed_launch("cmd_search", sb, kern, dim3(stiles), dim3(kSrchThreads), stream, n, cm, K, nrep,
+      probed_launch("cmd_search", sb, kern, dim3(stiles), dim3(sth), stream, n, cm, K, nrep,
                     (const uint32_t *)ks, (const uint64_t *)vs, lat, codes, rec4, rcur, tm, mr,
                     (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr);
     };
-    switch (fq) {
-      case 1: go(k_cmd_search<1, kSrchThreads, uint64_t, false>); break;
-      case 2: go(k_cmd_search<2, kSrchThreads, uint64_t, false>); break;
-      case 3: go(k_cmd_search<3, kSrchThreads, uint64_t, false>); break;
-      default: go(k_cmd_search<4, kSrchThreads, uint64_t, false>); break;
-    }
+    if (t512 && fq == 3)
+      go(k_cmd_search<3, 512, uint64_t, false>);
+    else if (t512 && fq == 2)
+      go(k_cmd_search<2, 512, uint64_t, false>);
+    else
+      switch (fq) {
+        case 1: go(k_cmd_search<1, kSrchThreads, uint64_t, false>); break;
+        case 2: go(k_cmd_search<2, kSrchThreads, uint64_t, false>); break;
+        case 3: go(k_cmd_search<3, kSrchThreads, uint64_t, false>); break;
+        default: go(k_cmd_search<4, kSrchThreads, uint64_t, false>); break;
+      }
     mark(cm.us ? "unit_search" : "cmd_search");
     if (rec4) {
       auto sc = [&](auto kern) {
