@@ -972,8 +972,8 @@ __device__ __forceinline__ void row_place_one(const uint4 o, const uint64_t *__r
   // tile kernel beside this one waits on the same unit)
   uint64_t *d = rows + size_t(o.x) * FQ;
   if constexpr (FQ == 3) {
-    *reinterpret_cast<u32x4u *>(d) =
-        u32x4u{uint32_t(w[0]), uint32_t(w[0] >> 32), uint32_t(w[1]), uint32_t(w[1] >> 32)};
+    const u32x4u lo4{uint32_t(w[0]), uint32_t(w[0] >> 32), uint32_t(w[1]), uint32_t(w[1] >> 32)};
+    *reinterpret_cast<u32x4u *>(d) = lo4;
     d[2] = w[2];
   } else {
 #pragma unroll
@@ -983,7 +983,9 @@ __device__ __forceinline__ void row_place_one(const uint4 o, const uint64_t *__r
 // One record per thread per trip: eight per trip (loads issued together)
 // doubled it beside the tile kernel, 3.1 -> 7.0 ms, and slowed the tile
 // kernel 5.3 -> 7.5 ms -- more random row stores in flight congest the
-// write path the tile kernel's own stores wait on.
+// write path the tile kernel's own stores wait on.  (Nontemporal row stores,
+// here or for the tile kernel's outputs, measured no different: 12.28 ms per
+// C4 step against 12.26-12.32.)
 template <uint32_t FQ>
 __global__ void __launch_bounds__(256)
     k_row_place(uint32_t n, const uint4 *__restrict__ rec, const uint64_t *__restrict__ dlog,
@@ -1625,13 +1627,18 @@ __global__ void k_frontier_update(const unsigned long long *__restrict__ mx,
   excount[s] += cnt[s];
 }
 
-__global__ void k_run_scatter(uint32_t m, const uint32_t *__restrict__ keys,
-                              const uint32_t *__restrict__ vids, const uint32_t *__restrict__ hp,
-                              const uint32_t *__restrict__ off, const uint64_t *__restrict__ dot,
-                              uint64_t *__restrict__ out) {
+// The bucket path's per-key sequence: element j of the key-grouped order
+// moves by its run's shift (run_offsets) to its ascending-key place; the
+// trivial order's labels (own dot) and ranks (position) in the same pass
+// (one element per command: single view, one key).
+__global__ void k_run_place(uint32_t m, const uint32_t *__restrict__ keys,
+                            const uint32_t *__restrict__ delta, const uint64_t *__restrict__ seqg,
+                            uint64_t *__restrict__ out, const uint64_t *__restrict__ dot,
+                            uint64_t *__restrict__ lab, uint32_t *__restrict__ rank) {
   GRID_STRIDE(j, m) {
-    const uint32_t k = keys[j];
-    out[off[k] + (j - hp[k])] = dot[vids[j]];
+    out[j + delta[keys[j]]] = seqg[j];
+    lab[j] = dot[j];
+    rank[j] = j;
   }
 }
 
@@ -1675,20 +1682,6 @@ __global__ void k_key_offsets(uint32_t m, const uint32_t *__restrict__ keys, uin
   }
 }
 
-// Key-grouped runs (the bucket path's per-key order): each run's start, and
-// its length as (end + 1) - start through two atomics into the zeroed count
-// (one launch instead of a start pass and a count pass)
-__global__ void k_run_bounds(uint32_t m, const uint32_t *__restrict__ keys,
-                             uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
-  GRID_STRIDE(j, m) {
-    const uint32_t k = keys[j];
-    if (j == 0 || keys[j - 1] != k) {
-      start[k] = j;
-      atomicSub(&cnt[k], j);
-    }
-    if (j + 1 == m || keys[j + 1] != k) atomicAdd(&cnt[k], j + 1);
-  }
-}
 __global__ void k_edges_csr(uint32_t n, uint32_t S, const uint32_t *__restrict__ ds,
                             const uint32_t *__restrict__ off, uint32_t *__restrict__ out) {
   GRID_STRIDE(i, n) {
@@ -1724,7 +1717,11 @@ struct EngineDevice {
   KeyBucketSched kb_sched;          // largest-first order-workgroup schedule
   uint64_t kb_launches = 0;         // order launches (schedule refresh cadence)
   bool bucket_order = false;  // single-view per-key runs are key-grouped, not ascending
-  DBuf<uint32_t> key_hist, key_offs, headpos;
+  DBuf<uint32_t> key_offs;
+  // bucket path outputs: per-key run bounds in key-grouped order (zeroed per
+  // batch), their shifts to ascending-key order, the key-grouped dots
+  DBuf<uint32_t> kb_runs, kb_delta;
+  DBuf<uint64_t> kb_seq;
   // persistent state
   DBuf<uint64_t> latest;     // [(nproc+1) * K]
   DBuf<uint64_t> frontier;   // [256] executed-clock frontier per source
@@ -2483,7 +2480,14 @@ struct EngineDevice {
       if (plan.ok) {
         // two launches: tile partition by key bucket, per-bucket order + deps
         ks = sk32a.ensure(M + 1);
-        vs = sva.ensure(M + 1);
+        KeyBucketOut kout;
+        kout.sk = ks;
+        kout.seq = kb_seq.ensure(M + 1);
+        kout.rows = o_rows.ensure(M + 1);
+        kout.runs = kb_runs.ensure(2 * size_t(key_space) + 2);
+        kout.bdot = bdot;
+        kout.dlog = dot.get();
+        FH_HIP(hipMemsetAsync(kout.runs, 0, 2 * size_t(key_space) * sizeof(uint32_t), stream));
         // one launch per step: order this batch (partitioned by the previous
         // step, or now) and partition the next staged batch in the same grid
         const size_t q = b & 1;
@@ -2492,12 +2496,12 @@ struct EngineDevice {
           keybucket_partition(plan, M, bkey, bdot, clock.fold, kb_ws[q], stream, &kb_sched);
         kb_next_part = ~size_t(0);
         if (b + 1 < nbatches) {
-          keybucket_step(plan, M, bbase, latest.get(), kb_ws[q], ks, vs, dsorted, clock, plan, M,
+          keybucket_step(plan, M, bbase, latest.get(), kb_ws[q], kout, clock, plan, M,
                          bkey + M, bdot + M, kb_clock(b + 1).fold, kb_ws[q ^ 1], stream,
                          &kb_sched);
           kb_next_part = b + 1;
         } else {
-          keybucket_order(plan, M, bbase, latest.get(), kb_ws[q], ks, vs, dsorted, clock, stream,
+          keybucket_order(plan, M, bbase, latest.get(), kb_ws[q], kout, clock, stream,
                           &kb_sched);
         }
         // refresh the schedule from the sizes just recorded: after the first
@@ -3181,7 +3185,11 @@ struct EngineDevice {
     if (!sv_fused && deps_direct) {
       // written by the union (k_cmd_count sized the rows)
     } else {
-    if (sv_fused) {
+    if (sv_fused && bucket_order) {
+      // the order launch wrote each command's row (one slot per command)
+      deps_rows = 1;
+      sv_labels_done = false;
+    } else if (sv_fused) {
       // one dependency slot per command: the rows themselves; the trivial
       // order's labels and ranks in one coalesced pass
       uint64_t *lb = gout.trivial ? lab.ensure(n + 1) : nullptr;
@@ -3198,7 +3206,11 @@ struct EngineDevice {
     }
     mark("out_deps");
     if (deps_only) return;
-    if (gout.trivial && sv_fused && sv_labels_done) {
+    if (gout.trivial && sv_fused && bucket_order) {
+      // (written with the per-key sequence below)
+      o_label = lab.ensure(n + 1);
+      o_rank = rank_tmp.ensure(n + 1);
+    } else if (gout.trivial && sv_fused && sv_labels_done) {
       o_label = lab.get();
       o_rank = rank_tmp.get();
     } else if (gout.trivial) {
@@ -3215,14 +3227,12 @@ struct EngineDevice {
     // per-key offsets over the ascending key space (histogram + scan)
     o_nelem = gout.nelem;
     uint32_t *o = key_offs.ensure(key_space + 2);
-    uint32_t *hp = nullptr;
+    uint32_t *dl = nullptr;
     if (sv_fused && bucket_order) {
-      // key-grouped runs (not ascending): histogram of the runs and its scan
-      uint32_t *h = key_hist.ensure(key_space + 1);
-      hp = headpos.ensure(key_space + 1);
-      FH_HIP(hipMemsetAsync(h, 0, key_space * sizeof(uint32_t), stream));
-      k_run_bounds<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, hp, h);
-      exclusive_scan_u32(h, o, key_space, scan_ws, stream);
+      // key-grouped runs (not ascending): one scan over the run bounds the
+      // order launch wrote gives the offsets and each run's shift
+      dl = kb_delta.ensure(key_space + 1);
+      run_offsets(kb_runs.get(), o, dl, key_space, scan_ws, stream);
     } else {
       k_key_offsets<<<grid_for(uint32_t(key_space) + 1, B), B, 0, stream>>>(
           o_nelem, gout.pk_key, uint32_t(key_space), o);
@@ -3230,9 +3240,10 @@ struct EngineDevice {
     if (sv_fused) {
       uint64_t *sq = seq_dot.ensure(o_nelem + 1);
       if (bucket_order) {
-        // key-grouped runs -> ascending keys (hp holds each run's start)
-        k_run_scatter<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, gout.pk_vid,
-                                                               hp, o, bdot, sq);
+        // key-grouped runs -> ascending keys; the trivial labels and ranks
+        // in the same pass
+        k_run_place<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_key, dl, kb_seq.get(),
+                                                             sq, bdot, lab.get(), rank_tmp.get());
       } else {  // (sorted keys, sorted vids): gather the dots
         k_seq_dots<<<grid_for(o_nelem, B), B, 0, stream>>>(o_nelem, gout.pk_vid, bdot, sq);
       }

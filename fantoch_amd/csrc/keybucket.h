@@ -18,8 +18,9 @@
 //                   offsets (u16), executed-clock partials
 //   k_kb_order      per bucket: gather its runs from every tile in tile
 //                   (= arrival) order, stable LDS sort by slot (wave64 ballot
-//                   ranks), write the key-grouped sequence and each command's
-//                   dependency; tails update latest
+//                   ranks), write the key-grouped sequence of dots, each
+//                   command's dependency dot and each key's run bounds;
+//                   tails update latest
 #pragma once
 
 #include "fh_common.h"
@@ -85,16 +86,29 @@ struct KeyBucketSched {
 };
 void keybucket_sched(KeyBucketSched &sc, hipStream_t s);
 
-// Both launches on stream s.  Outputs, in key-grouped order (buckets
-// ascending, slots ascending, arrival order inside a key): sk = key ids,
-// sv = command indices, dep_sorted = dependency of that command (0 none,
-// index + 1 in-batch, otherwise the latest entry: a command-log reference,
-// kLogFlag | position).  latest is indexed by the mapped key; the batch's
-// commands sit at log positions log_base + index.
+// What the order launch writes.  In key-grouped order (buckets ascending,
+// slots ascending, arrival order inside a key): sk = key ids, seq = the
+// commands' dots.  By command index: rows = the command's dependency as a
+// dot (~0 for none; the previous command on its key, or latest[key] from an
+// earlier batch, resolved through dlog).  Per key id: runs[2 key] = the
+// first position of the key's run, runs[2 key + 1] = its end; runs must be
+// zero on entry (a key the batch does not hold stays (0, 0)).  latest is
+// indexed by the mapped key; the batch's commands sit at log positions
+// log_base + index.
+struct KeyBucketOut {
+  uint32_t *sk = nullptr;
+  uint64_t *seq = nullptr;
+  uint64_t *rows = nullptr;
+  uint32_t *runs = nullptr;
+  const uint64_t *bdot = nullptr;  // the batch's dots
+  const uint64_t *dlog = nullptr;  // the dot log
+};
+
+// Both launches on stream s.
 void keybucket_run(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32, const uint64_t *dot,
                    uint64_t log_base, uint64_t *latest, const KeyBucketClock &clock,
-                   KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                   hipStream_t s, KeyBucketSched *sc = nullptr);
+                   KeyBucketWorkspace &ws, const KeyBucketOut &out, hipStream_t s,
+                   KeyBucketSched *sc = nullptr);
 
 // The two launches separately: keybucket_order reads the workspace
 // keybucket_partition filled; clk = the shard set of that batch.
@@ -102,15 +116,14 @@ void keybucket_partition(const KeyBucketPlan &p, uint32_t n, const uint32_t *key
                          const uint64_t *dot, unsigned long long *clk, KeyBucketWorkspace &ws,
                          hipStream_t s, KeyBucketSched *sc = nullptr);
 void keybucket_order(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
-                     KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                     const KeyBucketClock &clock, hipStream_t s, KeyBucketSched *sc = nullptr);
+                     KeyBucketWorkspace &ws, const KeyBucketOut &out, const KeyBucketClock &clock,
+                     hipStream_t s, KeyBucketSched *sc = nullptr);
 
 // One launch that orders batch b (partitioned earlier into ws, clock shards
 // clock.fold) and partitions batch b+1 (p2 / n2 / key32_2 / dot_2) into ws2
 // with its clock shards in clk.
 void keybucket_step(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
-                    KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                    const KeyBucketClock &clock, const KeyBucketPlan &p2, uint32_t n2,
+                    KeyBucketWorkspace &ws, const KeyBucketOut &out, const KeyBucketClock &clock, const KeyBucketPlan &p2, uint32_t n2,
                     const uint32_t *key32_2, const uint64_t *dot_2, unsigned long long *clk,
                     KeyBucketWorkspace &ws2, hipStream_t s, KeyBucketSched *sc = nullptr);
 

@@ -468,6 +468,49 @@ __device__ __forceinline__ const uint32_t *sort_chunk(const uint32_t (&xe)[IT], 
   return a;
 }
 
+// What the order role writes for each command, in key-grouped order (the
+// position of a command is its bucket's base + its rank in the sorted
+// bucket): the key id (sk) and the command's dot (seq); by command index: its
+// dependency as a dot (rows, ~0 for none); per key: the bounds of its run
+// (runs[2 key] = first position, runs[2 key + 1] = last + 1; zero for keys
+// the batch does not hold).  The run bounds feed one scan over the key space
+// (ascending per-key offsets) and one scatter; no pass re-reads the keys to
+// find the runs.
+struct OrderOut {
+  uint32_t *sk;
+  uint64_t *seq;
+  uint64_t *rows;
+  uint32_t *runs;
+  const uint64_t *bdot;  // the batch's dots (command index -> dot)
+  const uint64_t *dlog;  // the dot log (latest entries of earlier batches)
+  // a dependency code (0 none, in-batch index + 1, a log reference, or a
+  // dot) as the dot it names
+  __device__ __forceinline__ uint64_t dep_dot(uint64_t x) const {
+    return x == 0 ? ~0ull
+           : is_log_ref(x) ? dlog[x - kLogFlag]
+           : (x >> 56) == 0 ? bdot[x - 1]
+                            : x;
+  }
+  __device__ __forceinline__ void put(uint32_t pos, uint32_t key, uint32_t vid,
+                                      uint64_t dep) const {
+    sk[pos] = key;
+    seq[pos] = bdot[vid];
+    rows[vid] = dep_dot(dep);
+  }
+};
+// The order sweeps go over a thread's items in groups of kPutGroup: every
+// gather of a group (the command's dot, its dependency's dot) is issued
+// before the group's stores, so a group costs one gather latency rather than
+// one per item, and the second half recomputes its indices from LDS instead
+// of holding them.  Element j - 1 of a sweep is lane - 1's item, so a
+// non-head's dependency dot (its left neighbour's dot) comes from a lane
+// shuffle; heads (latest of an earlier batch) and lane 0 gather it.
+constexpr int kPutGroup = 4;
+__device__ __forceinline__ uint64_t left_lane(uint64_t x) {
+  const uint32_t lo = __shfl_up(uint32_t(x), 1, 64), hi = __shfl_up(uint32_t(x >> 32), 1, 64);
+  return (uint64_t(hi) << 32) | lo;
+}
+
 // A bucket that fits one chunk: gather into registers, sort, write the
 // sorted chunk as is (contiguous output).  With the bucket's latest slice
 // staged in LDS (s_lat, `staged`) heads read it there and tails write latest
@@ -496,8 +539,7 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
                                              int vb, uint32_t kinv, uint32_t kmask,
                                              uint32_t tiles, const uint32_t *__restrict__ part,
                                              uint64_t log_base, uint64_t *__restrict__ latest,
-                                             uint32_t *__restrict__ sk, uint32_t *__restrict__ sv,
-                                             uint64_t *__restrict__ dep_sorted, uint32_t *s_a,
+                                             const OrderOut &out, uint32_t *s_a,
                                              uint32_t *s_b, uint32_t (*s_h0)[1 << kDigit],
                                              uint32_t (*s_h1)[1 << kDigit], uint32_t *s_db,
                                              const uint32_t *s_rs, const uint32_t *s_src,
@@ -508,37 +550,58 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
   uint32_t xe[IT];
   gather_items<IT>(part, s_rs, s_src, tiles, 0, Nb, xe);
   const uint32_t *S = sort_chunk<IT>(xe, s_a, s_b, Nb, vb, hb, s_h0, s_h1, s_db, true);
-  if (staged) {
-    for (uint32_t j = tid; j < Nb; j += kOThreads) {
+#pragma unroll
+  for (int r0 = 0; r0 < IT; r0 += kPutGroup) {
+    uint64_t d[kPutGroup], w[kPutGroup];
+    bool nb[kPutGroup];  // the dependency is the left lane's dot
+#pragma unroll
+    for (int g = 0; g < kPutGroup; g++) {
+      const uint32_t j = uint32_t(r0 + g) * kOThreads + tid;
+      d[g] = 0;
+      nb[g] = false;
+      if (r0 + g >= IT || j >= Nb) continue;
+      const uint32_t e = S[j], slot = e >> vb;
+      const bool head = j == 0 || (S[j - 1] >> vb) != slot;
+      d[g] = out.bdot[e & vmask];
+      nb[g] = !head && (tid & 63) != 0;
+      if (!nb[g])
+        w[g] = out.dep_dot(!head   ? uint64_t(S[j - 1] & vmask) + 1
+                           : staged ? s_lat[slot]
+                                    : latest[(b << hb) | slot]);
+    }
+#pragma unroll
+    for (int g = 0; g < kPutGroup; g++) {
+      const uint64_t l = left_lane(d[g]);
+      if (nb[g]) w[g] = l;
+    }
+#pragma unroll
+    for (int g = 0; g < kPutGroup; g++) {
+      const uint32_t j = uint32_t(r0 + g) * kOThreads + tid;
+      if (r0 + g >= IT || j >= Nb) continue;
       const uint32_t e = S[j], slot = e >> vb, vid = e & vmask;
       const uint32_t mk = (b << hb) | slot;  // mapped key
-      const uint32_t pos = gbase + j;
-      sk[pos] = (mk * kinv) & kmask;
-      sv[pos] = vid;
-      dep_sorted[pos] = j == 0 || (S[j - 1] >> vb) != slot ? s_lat[slot]
-                                                            : uint64_t(S[j - 1] & vmask) + 1;
-      if (j + 1 == Nb || (S[j + 1] >> vb) != slot) {
+      const uint32_t key = (mk * kinv) & kmask, pos = gbase + j;
+      out.sk[pos] = key;
+      out.seq[pos] = d[g];
+      out.rows[vid] = w[g];
+      if (j == 0 || (S[j - 1] >> vb) != slot) out.runs[2 * key] = pos;
+      // staged: heads read latest from LDS, so tails write it in this sweep
+      if (staged && (j + 1 == Nb || (S[j + 1] >> vb) != slot)) {
+        out.runs[2 * key + 1] = pos + 1;
         latest[mk] = kLogFlag | (log_base + vid);
         note_hot(S, j, slot, vb, mk, hot_min, cand);
       }
     }
-    return;
   }
-  for (uint32_t j = tid; j < Nb; j += kOThreads) {
-    const uint32_t e = S[j], slot = e >> vb, vid = e & vmask;
-    const uint32_t mk = (b << hb) | slot;  // mapped key
-    const bool head = j == 0 || (S[j - 1] >> vb) != slot;
-    const uint32_t pos = gbase + j;
-    sk[pos] = (mk * kinv) & kmask;
-    sv[pos] = vid;
-    dep_sorted[pos] = head ? latest[mk] : uint64_t(S[j - 1] & vmask) + 1;
-  }
+  if (staged) return;
   __syncthreads();  // every head has read latest
   for (uint32_t j = tid; j < Nb; j += kOThreads) {
     const uint32_t e = S[j], slot = e >> vb;
     if (j + 1 == Nb || (S[j + 1] >> vb) != slot) {
-      latest[(b << hb) | slot] = kLogFlag | (log_base + (e & vmask));
-      note_hot(S, j, slot, vb, (b << hb) | slot, hot_min, cand);
+      const uint32_t mk = (b << hb) | slot;
+      out.runs[2 * ((mk * kinv) & kmask) + 1] = gbase + j + 1;
+      latest[mk] = kLogFlag | (log_base + (e & vmask));
+      note_hot(S, j, slot, vb, mk, hot_min, cand);
     }
   }
 }
@@ -548,10 +611,9 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
 __device__ __forceinline__ void order_hot(uint32_t Nb, uint32_t gbase, uint32_t mk, int vb,
                                           uint32_t kinv, uint32_t kmask, uint32_t tiles,
                                           const uint32_t *__restrict__ part, uint64_t log_base,
-                                          uint64_t *__restrict__ latest,
-                                          uint32_t *__restrict__ sk, uint32_t *__restrict__ sv,
-                                          uint64_t *__restrict__ dep_sorted, uint32_t *s_a,
-                                          const uint32_t *s_rs, const uint32_t *s_src) {
+                                          uint64_t *__restrict__ latest, const OrderOut &out,
+                                          uint32_t *s_a, const uint32_t *s_rs,
+                                          const uint32_t *s_src) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t vmask = (1u << vb) - 1;
   const uint32_t key = (mk * kinv) & kmask;
@@ -567,16 +629,41 @@ __device__ __forceinline__ void order_hot(uint32_t Nb, uint32_t gbase, uint32_t 
       if (q < c) s_a[q] = xe[i] & vmask;
     }
     __syncthreads();
-    for (uint32_t j = tid; j < c; j += kOThreads) {
-      const uint32_t pos = gbase + c0 + j;
-      sk[pos] = key;
-      sv[pos] = s_a[j];
-      dep_sorted[pos] = j ? uint64_t(s_a[j - 1]) + 1 : prev;
+#pragma unroll
+    for (int r0 = 0; r0 < 8; r0 += kPutGroup) {
+      uint64_t dd[kPutGroup], ww[kPutGroup];
+#pragma unroll
+      for (int g = 0; g < kPutGroup; g++) {
+        const uint32_t j = uint32_t(r0 + g) * kOThreads + tid;
+        dd[g] = 0;
+        if (j >= c) continue;
+        dd[g] = out.bdot[s_a[j]];
+        if (lane == 0 || j == 0) ww[g] = out.dep_dot(j ? uint64_t(s_a[j - 1]) + 1 : prev);
+      }
+#pragma unroll
+      for (int g = 0; g < kPutGroup; g++) {
+        const uint64_t l = left_lane(dd[g]);
+        const uint32_t j = uint32_t(r0 + g) * kOThreads + tid;
+        if (lane != 0 && j != 0) ww[g] = l;
+      }
+#pragma unroll
+      for (int g = 0; g < kPutGroup; g++) {
+        const uint32_t j = uint32_t(r0 + g) * kOThreads + tid;
+        if (j >= c) continue;
+        const uint32_t pos = gbase + c0 + j, vid = s_a[j];
+        out.sk[pos] = key;
+        out.seq[pos] = dd[g];
+        out.rows[vid] = ww[g];
+      }
     }
     prev = uint64_t(s_a[c - 1]) + 1;
     __syncthreads();  // s_a is rewritten by the next chunk
   }
-  if (tid == 0) latest[mk] = kLogFlag | (log_base + (prev - 1));
+  if (tid == 0) {
+    latest[mk] = kLogFlag | (log_base + (prev - 1));
+    out.runs[2 * key] = gbase;
+    out.runs[2 * key + 1] = gbase + Nb;
+  }
 }
 
 // One bucket per 1024-thread workgroup.  The bucket's commands are the
@@ -609,9 +696,7 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
                                              const uint32_t *__restrict__ part,
                                              const uint32_t *__restrict__ toff,
                                              uint64_t log_base, uint64_t *__restrict__ latest,
-                                             uint32_t *__restrict__ sk, uint32_t *__restrict__ sv,
-                                             uint64_t *__restrict__ dep_sorted,
-                                             uint32_t *__restrict__ mc,
+                                             const OrderOut &out, uint32_t *__restrict__ mc,
                                              unsigned long long *__restrict__ clk_fold,
                                              unsigned long long *__restrict__ frontier,
                                              unsigned long long *__restrict__ excount,
@@ -695,14 +780,14 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
   __syncthreads();
 
   if (hot) {
-    order_hot(Nb, gbase, hot_snap[b - B], vb, kinv, kmask, tiles, part, log_base, latest, sk, sv,
-              dep_sorted, s_a, s_rs, s_src);
+    order_hot(Nb, gbase, hot_snap[b - B], vb, kinv, kmask, tiles, part, log_base, latest, out, s_a,
+              s_rs, s_src);
     return;
   }
   if (Nb <= uint32_t(kChunk)) {
 #define FH_ORDER_SINGLE(IT)                                                                 \
-  order_single<IT>(Nb, gbase, b, hb, vb, kinv, kmask, tiles, part, log_base, latest, sk, sv, \
-                   dep_sorted, s_a, s_b, s_h, s_h1, s_db, s_rs, s_src, s_lat, staged, hot_min, cand)
+  order_single<IT>(Nb, gbase, b, hb, vb, kinv, kmask, tiles, part, log_base, latest, out, s_a, \
+                   s_b, s_h, s_h1, s_db, s_rs, s_src, s_lat, staged, hot_min, cand)
     if (Nb <= 2048) FH_ORDER_SINGLE(2);
     else if (Nb <= 4096) FH_ORDER_SINGLE(4);
     else if (Nb <= 6144) FH_ORDER_SINGLE(6);
@@ -773,9 +858,7 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
       uint64_t dep;
       if (j != hp) dep = uint64_t(S[j - 1] & vmask) + 1;
       else dep = cc ? uint64_t(g_clast[slot]) + 1 : latest[mk];
-      sk[pos] = (mk * kinv) & kmask;
-      sv[pos] = vid;
-      dep_sorted[pos] = dep;
+      out.put(pos, (mk * kinv) & kmask, vid, dep);
     }
     __threadfence_block();
     __syncthreads();
@@ -792,7 +875,12 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
   // the key's last command becomes latest (after every head read above)
   for (uint32_t k = tid; k < H; k += kOThreads) {
     const uint32_t cnt = g_ccnt[k];
-    if (cnt) latest[(b << hb) | k] = kLogFlag | (log_base + g_clast[k]);
+    if (cnt) {
+      const uint32_t key = (((b << hb) | k) * kinv) & kmask, p0 = gbase + g_kbase[k];
+      latest[(b << hb) | k] = kLogFlag | (log_base + g_clast[k]);
+      out.runs[2 * key] = p0;
+      out.runs[2 * key + 1] = p0 + cnt;
+    }
     if (cand && hot_min && cnt >= hot_min) {  // hot-key candidate (see note_hot)
       const uint32_t i = atomicAdd(&cand[kHot], 1u);
       if (i < uint32_t(kCand)) {
@@ -812,8 +900,7 @@ struct OrderArgs {
   const uint32_t *toff;
   uint64_t log_base;
   uint64_t *latest;
-  uint32_t *sk, *sv;
-  uint64_t *dep_sorted;
+  OrderOut out;
   uint32_t *mc;
   unsigned long long *clk_fold, *frontier, *excount;
   const uint32_t *perm;      // workgroup -> bucket (null: identity)
@@ -843,7 +930,7 @@ __device__ __forceinline__ void part_role(const PartArgs &a, uint32_t t, const T
 
 __device__ __forceinline__ void order_role(const OrderArgs &a, uint32_t r, unsigned char *smem) {
   order_bucket(a.perm ? a.perm[r] : r, a.tiles, a.bb, a.hb, a.vb, a.kinv, a.kmask, a.part, a.toff,
-               a.log_base, a.latest, a.sk, a.sv, a.dep_sorted, a.mc, a.clk_fold, a.frontier,
+               a.log_base, a.latest, a.out, a.mc, a.clk_fold, a.frontier,
                a.excount, a.sizes, a.hot_snap, a.hot_min, a.cand, smem);
 }
 
@@ -1031,9 +1118,8 @@ static PartArgs part_args(const KeyBucketPlan &p, uint32_t n, const uint32_t *ke
 }
 
 static OrderArgs order_args(const KeyBucketPlan &p, uint64_t log_base, uint64_t *latest,
-                            KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv,
-                            uint64_t *dep_sorted, const KeyBucketClock &clock,
-                            KeyBucketSched *sc) {
+                            KeyBucketWorkspace &ws, const KeyBucketOut &out,
+                            const KeyBucketClock &clock, KeyBucketSched *sc) {
   OrderArgs a;
   a.tiles = p.tiles;
   a.bb = p.bb;
@@ -1045,9 +1131,12 @@ static OrderArgs order_args(const KeyBucketPlan &p, uint64_t log_base, uint64_t 
   a.toff = ws.toff.get();
   a.log_base = log_base;
   a.latest = latest;
-  a.sk = sk;
-  a.sv = sv;
-  a.dep_sorted = dep_sorted;
+  a.out.sk = out.sk;
+  a.out.seq = out.seq;
+  a.out.rows = out.rows;
+  a.out.runs = out.runs;
+  a.out.bdot = out.bdot;
+  a.out.dlog = out.dlog;
   // slot tables of buckets larger than one LDS chunk (rare)
   a.mc = ws.mc.ensure(size_t(1u << p.bb) * 4 * (size_t(1) << kSlotBits));
   a.clk_fold = clock.fold;
@@ -1080,40 +1169,39 @@ void keybucket_partition(const KeyBucketPlan &p, uint32_t n, const uint32_t *key
 }
 
 void keybucket_order(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
-                     KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                     const KeyBucketClock &clock, hipStream_t s, KeyBucketSched *sc) {
+                     KeyBucketWorkspace &ws, const KeyBucketOut &out, const KeyBucketClock &clock,
+                     hipStream_t s, KeyBucketSched *sc) {
   FH_CHECK(p.ok, FH_EINVARIANT, "keybucket: batch does not fit the bucket plan");
   if (n == 0) return;
   sched_prepare(sc, p, s);
-  const OrderArgs a = order_args(p, log_base, latest, ws, sk, sv, dep_sorted, clock, sc);
-  // read the packed element (4), write key + command index + dependency (16)
-  probed_launch("kb_order", double(n) * 20.0, k_kb_order, dim3(buckets_total(p)),
+  const OrderArgs a = order_args(p, log_base, latest, ws, out, clock, sc);
+  // read the packed element (4) and the dot (8), write key + dot + row (20)
+  probed_launch("kb_order", double(n) * 32.0, k_kb_order, dim3(buckets_total(p)),
                 dim3(kOThreads), s, a);
 }
 
 void keybucket_step(const KeyBucketPlan &p, uint32_t n, uint64_t log_base, uint64_t *latest,
-                    KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                    const KeyBucketClock &clock, const KeyBucketPlan &p2, uint32_t n2,
+                    KeyBucketWorkspace &ws, const KeyBucketOut &out, const KeyBucketClock &clock, const KeyBucketPlan &p2, uint32_t n2,
                     const uint32_t *key32_2, const uint64_t *dot_2, unsigned long long *clk,
                     KeyBucketWorkspace &ws2, hipStream_t s, KeyBucketSched *sc) {
   FH_CHECK(p.ok && p2.ok, FH_EINVARIANT, "keybucket: batch does not fit the bucket plan");
   FH_CHECK(p.bb == p2.bb, FH_EINVARIANT, "keybucket: step over plans of different widths");
   sched_prepare(sc, p, s);
-  const OrderArgs a = order_args(p, log_base, latest, ws, sk, sv, dep_sorted, clock, sc);
+  const OrderArgs a = order_args(p, log_base, latest, ws, out, clock, sc);
   const PartArgs pa = part_args(p2, n2, key32_2, dot_2, clk, ws2, sc);
   const uint32_t BT = buckets_total(p);
   auto k = by_bits(id_bits(p2), k_kb_step<8>, k_kb_step<9>, k_kb_step<10>);
-  // order (20 B / command of batch b) + partition (16 B / command of b+1)
-  probed_launch("kb_step", double(n) * 20.0 + double(n2) * 16.0, k, dim3(BT + p2.tiles),
+  // order (32 B / command of batch b) + partition (16 B / command of b+1)
+  probed_launch("kb_step", double(n) * 32.0 + double(n2) * 16.0, k, dim3(BT + p2.tiles),
                 dim3(kOThreads), s, a, BT, pa);
 }
 
 void keybucket_run(const KeyBucketPlan &p, uint32_t n, const uint32_t *key32, const uint64_t *dot,
                    uint64_t log_base, uint64_t *latest, const KeyBucketClock &clock,
-                   KeyBucketWorkspace &ws, uint32_t *sk, uint32_t *sv, uint64_t *dep_sorted,
-                   hipStream_t s, KeyBucketSched *sc) {
+                   KeyBucketWorkspace &ws, const KeyBucketOut &out, hipStream_t s,
+                   KeyBucketSched *sc) {
   keybucket_partition(p, n, key32, dot, clock.fold, ws, s, sc);
-  keybucket_order(p, n, log_base, latest, ws, sk, sv, dep_sorted, clock, s, sc);
+  keybucket_order(p, n, log_base, latest, ws, out, clock, s, sc);
 }
 
 }  // namespace fh

@@ -6,6 +6,7 @@
 #include <cstdlib>
 
 #include <atomic>
+#include <type_traits>
 
 #include "scan.h"
 
@@ -18,6 +19,19 @@ constexpr int kTile = kThreads * kItems;
 
 struct OpAdd {
   static __device__ __forceinline__ uint32_t f(uint32_t a, uint32_t b) { return a + b; }
+};
+// Element loaders: a plain array, or run bounds (start, end) pairs whose
+// value is the run length (0 for an absent run, end == 0)
+struct LdPlain {
+  const uint32_t *in;
+  __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return in[i]; }
+};
+struct LdRuns {
+  const uint2 *runs;
+  __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
+    const uint2 r = runs[i];
+    return r.y ? r.y - r.x : 0u;
+  }
 };
 struct OpMax {
   static __device__ __forceinline__ uint32_t f(uint32_t a, uint32_t b) { return a > b ? a : b; }
@@ -49,16 +63,16 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_tmp,
   return Op::f(pre, ex);
 }
 
-template <class Op>
+template <class Op, class Ld>
 __global__ void __launch_bounds__(kThreads)
-    k_scan_reduce(const uint32_t *__restrict__ in, uint32_t n, uint32_t *__restrict__ bsum) {
+    k_scan_reduce(const Ld in, uint32_t n, uint32_t *__restrict__ bsum) {
   __shared__ uint32_t s_tmp[kThreads / 64];
   const uint32_t base = blockIdx.x * kTile;
   uint32_t s = 0;
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + i * kThreads + threadIdx.x;
-    s = Op::f(s, idx < n ? in[idx] : 0u);
+    s = Op::f(s, idx < n ? in(idx) : 0u);
   }
   uint32_t tot = 0;
   block_excl_scan<Op>(s, s_tmp, &tot);
@@ -110,10 +124,12 @@ __global__ void __launch_bounds__(kTopThreads) k_scan_top(uint32_t *__restrict__
 // shuffles and chained by the row total (lane 63), then the waves' totals.
 // (A blocked layout -- 16 consecutive elements per thread -- made every load
 // instruction touch 64 lines: 382 us per 100M-element scan, 2 TB/s.)
-template <class Op>
+// With LdRuns, delta[i] = out[i] - the run's start as well (the shift that
+// moves a run from key-grouped positions to ascending-key positions).
+template <class Op, class Ld>
 __global__ void __launch_bounds__(kThreads)
-    k_scan_down(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint32_t n,
-                const uint32_t *__restrict__ bsum) {
+    k_scan_down(const Ld in, uint32_t *__restrict__ out, uint32_t n,
+                const uint32_t *__restrict__ bsum, uint32_t *__restrict__ delta) {
   __shared__ uint32_t s_tmp[kThreads / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t base = blockIdx.x * kTile + uint32_t(w) * 64 * kItems;
@@ -121,7 +137,7 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + i * 64 + lane;
-    v[i] = idx < n ? in[idx] : 0u;
+    v[i] = idx < n ? in(idx) : 0u;
   }
   // inclusive scan of each row across the lanes, chained row to row
   uint32_t carry = 0;
@@ -146,15 +162,20 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
     const uint32_t idx = base + i * 64 + lane;
-    if (idx < n) out[idx] = Op::f(pre, v[i]);
+    if (idx < n) {
+      out[idx] = Op::f(pre, v[i]);
+      if constexpr (std::is_same<Ld, LdRuns>::value)
+        if (delta) delta[idx] = Op::f(pre, v[i]) - in.runs[idx].x;
+    }
   }
   // out[n] = the total: the wave holding element n - 1 (its elements past
   // n - 1 are the identity)
   if (lane == 0 && n - 1 >= base && n - 1 < base + 64 * kItems) out[n] = Op::f(pre, carry);
 }
 
-template <class Op>
-void scan_impl(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws, hipStream_t s) {
+template <class Op, class Ld>
+void scan_impl(const Ld in, uint32_t *out, size_t n, ScanWorkspace &ws, hipStream_t s,
+               uint32_t *delta = nullptr) {
   FH_CHECK(n < (size_t(1) << 31), FH_EINVAL, "scan: too many elements");
   if (n == 0) {
     FH_HIP(hipMemsetAsync(out, 0, sizeof(uint32_t), s));
@@ -162,21 +183,26 @@ void scan_impl(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws, h
   }
   const uint32_t nb = uint32_t((n + kTile - 1) / kTile);
   uint32_t *bsum = ws.status.ensure(nb + 1);
-  k_scan_reduce<Op><<<nb, kThreads, 0, s>>>(in, uint32_t(n), bsum);
+  k_scan_reduce<Op, Ld><<<nb, kThreads, 0, s>>>(in, uint32_t(n), bsum);
   k_scan_top<Op><<<1, kTopThreads, 0, s>>>(bsum, nb);
-  k_scan_down<Op><<<nb, kThreads, 0, s>>>(in, out, uint32_t(n), bsum);
+  k_scan_down<Op, Ld><<<nb, kThreads, 0, s>>>(in, out, uint32_t(n), bsum, delta);
 }
 
 }  // namespace
 
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
                         hipStream_t s) {
-  scan_impl<OpAdd>(in, out, n, ws, s);
+  scan_impl<OpAdd>(LdPlain{in}, out, n, ws, s);
+}
+
+void run_offsets(const uint32_t *runs, uint32_t *off, uint32_t *delta, size_t n,
+                 ScanWorkspace &ws, hipStream_t s) {
+  scan_impl<OpAdd>(LdRuns{reinterpret_cast<const uint2 *>(runs)}, off, n, ws, s, delta);
 }
 
 void exclusive_scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
                             hipStream_t s) {
-  scan_impl<OpMax>(in, out, n, ws, s);
+  scan_impl<OpMax>(LdPlain{in}, out, n, ws, s);
 }
 
 namespace {

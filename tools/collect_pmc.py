@@ -46,7 +46,7 @@ PROBES = {
     "row_union": r"k_row_union<",
     "row_place": r"k_row_place<",
     "sv_rows": r"k_sv_rows",
-    "run_bounds": r"k_run_bounds",
+    "run_place": r"k_run_place",
     "ko_final": r"k_ko_final",
     "key_counts": r"k_key_counts",
     "sort_up": r"k_up<",
