@@ -1721,6 +1721,7 @@ struct EngineDevice {
   // bucket path outputs: per-key run bounds in key-grouped order (zeroed per
   // batch), their shifts to ascending-key order, the key-grouped dots
   DBuf<uint32_t> kb_runs, kb_delta;
+  uint32_t kb_run_tag = 0;  // the last batch's run tag
   DBuf<uint64_t> kb_seq;
   // persistent state
   DBuf<uint64_t> latest;     // [(nproc+1) * K]
@@ -2484,10 +2485,17 @@ struct EngineDevice {
         kout.sk = ks;
         kout.seq = kb_seq.ensure(M + 1);
         kout.rows = o_rows.ensure(M + 1);
+        // run bounds tagged per batch: cleared only when the tags wrap (or the
+        // table is new)
+        const bool fresh = kb_runs.cap < 2 * size_t(key_space) + 2;
         kout.runs = kb_runs.ensure(2 * size_t(key_space) + 2);
+        if (fresh || ++kb_run_tag >= kRunTags) {
+          FH_HIP(hipMemsetAsync(kout.runs, 0, 2 * size_t(key_space) * sizeof(uint32_t), stream));
+          kb_run_tag = 1;
+        }
+        kout.run_tag = kb_run_tag;
         kout.bdot = bdot;
         kout.dlog = dot.get();
-        FH_HIP(hipMemsetAsync(kout.runs, 0, 2 * size_t(key_space) * sizeof(uint32_t), stream));
         // one launch per step: order this batch (partitioned by the previous
         // step, or now) and partition the next staged batch in the same grid
         const size_t q = b & 1;
@@ -3232,7 +3240,7 @@ struct EngineDevice {
       // key-grouped runs (not ascending): one scan over the run bounds the
       // order launch wrote gives the offsets and each run's shift
       dl = kb_delta.ensure(key_space + 1);
-      run_offsets(kb_runs.get(), o, dl, key_space, scan_ws, stream);
+      run_offsets(kb_runs.get(), kb_run_tag, o, dl, key_space, scan_ws, stream);
     } else {
       k_key_offsets<<<grid_for(uint32_t(key_space) + 1, B), B, 0, stream>>>(
           o_nelem, gout.pk_key, uint32_t(key_space), o);

@@ -91,15 +91,19 @@ void keybucket_sched(KeyBucketSched &sc, hipStream_t s);
 // commands' dots.  By command index: rows = the command's dependency as a
 // dot (~0 for none; the previous command on its key, or latest[key] from an
 // earlier batch, resolved through dlog).  Per key id: runs[2 key] = the
-// first position of the key's run, runs[2 key + 1] = its end; runs must be
-// zero on entry (a key the batch does not hold stays (0, 0)).  latest is
+// first position of the key's run, runs[2 key + 1] = its end | run_tag <<
+// kRunEndBits.  A key the batch does not hold keeps an entry of another tag,
+// so runs is cleared only when the tags wrap (zero is no tag).  latest is
 // indexed by the mapped key; the batch's commands sit at log positions
 // log_base + index.
+constexpr int kRunEndBits = 23;  // run ends <= 2^22 (the plan's batch bound)
+constexpr uint32_t kRunTags = 1u << (32 - kRunEndBits);
 struct KeyBucketOut {
   uint32_t *sk = nullptr;
   uint64_t *seq = nullptr;
   uint64_t *rows = nullptr;
   uint32_t *runs = nullptr;
+  uint32_t run_tag = 1;  // 1 .. kRunTags - 1
   const uint64_t *bdot = nullptr;  // the batch's dots
   const uint64_t *dlog = nullptr;  // the dot log
 };

@@ -472,8 +472,8 @@ __device__ __forceinline__ const uint32_t *sort_chunk(const uint32_t (&xe)[IT], 
 // position of a command is its bucket's base + its rank in the sorted
 // bucket): the key id (sk) and the command's dot (seq); by command index: its
 // dependency as a dot (rows, ~0 for none); per key: the bounds of its run
-// (runs[2 key] = first position, runs[2 key + 1] = last + 1; zero for keys
-// the batch does not hold).  The run bounds feed one scan over the key space
+// (runs[2 key] = first position, runs[2 key + 1] = (last + 1) | tag; keys
+// the batch does not hold keep an older tag).  The run bounds feed one scan over the key space
 // (ascending per-key offsets) and one scatter; no pass re-reads the keys to
 // find the runs.
 struct OrderOut {
@@ -481,6 +481,7 @@ struct OrderOut {
   uint64_t *seq;
   uint64_t *rows;
   uint32_t *runs;
+  uint32_t tag;          // this batch's run tag (KeyBucketOut)
   const uint64_t *bdot;  // the batch's dots (command index -> dot)
   const uint64_t *dlog;  // the dot log (latest entries of earlier batches)
   // a dependency code (0 none, in-batch index + 1, a log reference, or a
@@ -587,7 +588,7 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
       if (j == 0 || (S[j - 1] >> vb) != slot) out.runs[2 * key] = pos;
       // staged: heads read latest from LDS, so tails write it in this sweep
       if (staged && (j + 1 == Nb || (S[j + 1] >> vb) != slot)) {
-        out.runs[2 * key + 1] = pos + 1;
+        out.runs[2 * key + 1] = (pos + 1) | out.tag;
         latest[mk] = kLogFlag | (log_base + vid);
         note_hot(S, j, slot, vb, mk, hot_min, cand);
       }
@@ -599,7 +600,7 @@ __device__ __forceinline__ void order_single(uint32_t Nb, uint32_t gbase, uint32
     const uint32_t e = S[j], slot = e >> vb;
     if (j + 1 == Nb || (S[j + 1] >> vb) != slot) {
       const uint32_t mk = (b << hb) | slot;
-      out.runs[2 * ((mk * kinv) & kmask) + 1] = gbase + j + 1;
+      out.runs[2 * ((mk * kinv) & kmask) + 1] = (gbase + j + 1) | out.tag;
       latest[mk] = kLogFlag | (log_base + (e & vmask));
       note_hot(S, j, slot, vb, mk, hot_min, cand);
     }
@@ -662,7 +663,7 @@ __device__ __forceinline__ void order_hot(uint32_t Nb, uint32_t gbase, uint32_t 
   if (tid == 0) {
     latest[mk] = kLogFlag | (log_base + (prev - 1));
     out.runs[2 * key] = gbase;
-    out.runs[2 * key + 1] = gbase + Nb;
+    out.runs[2 * key + 1] = (gbase + Nb) | out.tag;
   }
 }
 
@@ -879,7 +880,7 @@ __device__ __forceinline__ void order_bucket(uint32_t b, uint32_t tiles, int bb,
       const uint32_t key = (((b << hb) | k) * kinv) & kmask, p0 = gbase + g_kbase[k];
       latest[(b << hb) | k] = kLogFlag | (log_base + g_clast[k]);
       out.runs[2 * key] = p0;
-      out.runs[2 * key + 1] = p0 + cnt;
+      out.runs[2 * key + 1] = (p0 + cnt) | out.tag;
     }
     if (cand && hot_min && cnt >= hot_min) {  // hot-key candidate (see note_hot)
       const uint32_t i = atomicAdd(&cand[kHot], 1u);
@@ -1135,6 +1136,7 @@ static OrderArgs order_args(const KeyBucketPlan &p, uint64_t log_base, uint64_t 
   a.out.seq = out.seq;
   a.out.rows = out.rows;
   a.out.runs = out.runs;
+  a.out.tag = out.run_tag << kRunEndBits;
   a.out.bdot = out.bdot;
   a.out.dlog = out.dlog;
   // slot tables of buckets larger than one LDS chunk (rare)

@@ -17,11 +17,12 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspa
 void exclusive_scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
                             hipStream_t s);
 
-// Per-key offsets from run bounds: runs holds n (start, end) u32 pairs (end
-// 0: no run); off[i] = the total length of the runs before i (off[n] = the
-// total) and delta[i] = off[i] - start_i, the shift that moves run i from its
-// position to its place in ascending order.
-void run_offsets(const uint32_t *runs, uint32_t *off, uint32_t *delta, size_t n,
+// Per-key offsets from run bounds: runs holds n (start, end | tag' << 23)
+// u32 pairs, a run of this batch where tag' == tag (1..511); off[i] = the
+// total length of the runs before i (off[n] = the total) and delta[i] =
+// off[i] - start_i, the shift that moves run i from its position to its
+// place in ascending order.
+void run_offsets(const uint32_t *runs, uint32_t tag, uint32_t *off, uint32_t *delta, size_t n,
                  ScanWorkspace &ws, hipStream_t s);
 
 // Low-latency read-back of n <= 14 device u32 words (fixpoint flags,

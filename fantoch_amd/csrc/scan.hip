@@ -1,5 +1,5 @@
 // scan.hip -- exclusive prefix sum / prefix max for gfx950, reduce-then-scan
-// (see scan.h).  Three launches, no inter-workgroup hand-off inside a launch
+// (see scan.h).  Three launches (two up to 4M elements), no inter-workgroup hand-off inside a launch
 // (cross-XCD hand-offs cost microseconds each on MI355X; a chained scan
 // serialises on them).  The operator is a template parameter with identity 0
 // (sum, or max over u32).
@@ -20,17 +20,18 @@ constexpr int kTile = kThreads * kItems;
 struct OpAdd {
   static __device__ __forceinline__ uint32_t f(uint32_t a, uint32_t b) { return a + b; }
 };
-// Element loaders: a plain array, or run bounds (start, end) pairs whose
-// value is the run length (0 for an absent run, end == 0)
+// Element loaders: a plain array, or run bounds (start, end | tag << 23)
+// pairs whose value is the run length (0 for an entry of another tag)
 struct LdPlain {
   const uint32_t *in;
   __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return in[i]; }
 };
 struct LdRuns {
   const uint2 *runs;
+  uint32_t tag;
   __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
     const uint2 r = runs[i];
-    return r.y ? r.y - r.x : 0u;
+    return (r.y >> 23) == tag ? (r.y & 0x7FFFFFu) - r.x : 0u;
   }
 };
 struct OpMax {
@@ -129,8 +130,8 @@ __global__ void __launch_bounds__(kTopThreads) k_scan_top(uint32_t *__restrict__
 template <class Op, class Ld>
 __global__ void __launch_bounds__(kThreads)
     k_scan_down(const Ld in, uint32_t *__restrict__ out, uint32_t n,
-                const uint32_t *__restrict__ bsum, uint32_t *__restrict__ delta) {
-  __shared__ uint32_t s_tmp[kThreads / 64];
+                const uint32_t *__restrict__ bsum, uint32_t *__restrict__ delta, int inl) {
+  __shared__ uint32_t s_tmp[kThreads / 64], s_top[kThreads / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t base = blockIdx.x * kTile + uint32_t(w) * 64 * kItems;
   uint32_t v[kItems];
@@ -155,9 +156,18 @@ __global__ void __launch_bounds__(kThreads)
     v[i] = Op::f(carry, ex);  // exclusive prefix inside the wave's run
     carry = Op::f(carry, row);
   }
+  uint32_t pre;
+  if (inl) {
+    // few blocks: this block's prefix from the raw block sums (no k_scan_top
+    // launch; a launch costs more than the ~nb/256 loads per thread)
+    uint32_t t = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += kThreads) t = Op::f(t, bsum[i]);
+    block_excl_scan<Op>(t, s_top, &pre);
+  } else {
+    pre = bsum[blockIdx.x];
+  }
   if (lane == 0) s_tmp[w] = carry;
   __syncthreads();
-  uint32_t pre = bsum[blockIdx.x];
   for (int i = 0; i < w; i++) pre = Op::f(pre, s_tmp[i]);
 #pragma unroll
   for (int i = 0; i < kItems; i++) {
@@ -184,8 +194,9 @@ void scan_impl(const Ld in, uint32_t *out, size_t n, ScanWorkspace &ws, hipStrea
   const uint32_t nb = uint32_t((n + kTile - 1) / kTile);
   uint32_t *bsum = ws.status.ensure(nb + 1);
   k_scan_reduce<Op, Ld><<<nb, kThreads, 0, s>>>(in, uint32_t(n), bsum);
-  k_scan_top<Op><<<1, kTopThreads, 0, s>>>(bsum, nb);
-  k_scan_down<Op, Ld><<<nb, kThreads, 0, s>>>(in, out, uint32_t(n), bsum, delta);
+  const bool inl = nb <= 1024;  // (4M elements)
+  if (!inl) k_scan_top<Op><<<1, kTopThreads, 0, s>>>(bsum, nb);
+  k_scan_down<Op, Ld><<<nb, kThreads, 0, s>>>(in, out, uint32_t(n), bsum, delta, int(inl));
 }
 
 }  // namespace
@@ -195,9 +206,10 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspa
   scan_impl<OpAdd>(LdPlain{in}, out, n, ws, s);
 }
 
-void run_offsets(const uint32_t *runs, uint32_t *off, uint32_t *delta, size_t n,
+void run_offsets(const uint32_t *runs, uint32_t tag, uint32_t *off, uint32_t *delta, size_t n,
                  ScanWorkspace &ws, hipStream_t s) {
-  scan_impl<OpAdd>(LdRuns{reinterpret_cast<const uint2 *>(runs)}, off, n, ws, s, delta);
+  FH_CHECK(tag >= 1 && tag < 512, FH_EINVAL, "run_offsets: tag out of range");
+  scan_impl<OpAdd>(LdRuns{reinterpret_cast<const uint2 *>(runs), tag}, off, n, ws, s, delta);
 }
 
 void exclusive_scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, ScanWorkspace &ws,
