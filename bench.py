@@ -101,8 +101,9 @@ def parse():
                     help="N > 1: exchange backend of the C5 leg (default: the process group's, "
                          "RCCL; gloo for a dry run of N ranks sharing one GPU)")
     ap.add_argument("--c5-solo", action="store_true",
-                    help="dry runs: the C5 condense / solve stages one rank at a time, so their "
-                         "stage times are those of an unshared GPU (not a throughput run)")
+                    help="dry runs: the C5 KeyDeps / local / condense / solve stages one rank at a "
+                         "time, so their stage times are those of an unshared GPU (not a "
+                         "throughput run)")
     ap.add_argument("--no-cpu-sharded", action="store_true",
                     help="skip the key-sharded multi-process CPU baseline")
     return ap.parse_args()

@@ -2597,7 +2597,15 @@ struct EngineDevice {
         const char *e = getenv("FH_VIEW_CHUNK");  // tests: small chunks
         return e ? size_t(std::max(1L, atol(e))) : size_t(15) << 20;
       }();
-      const uint32_t nch = uint32_t(std::max<size_t>(1, (size_t(M) + chunk_elems - 1) / chunk_elems));
+      // (chunks of chunk_elems log elements: with subset logs (fh_dgraph, one
+      // rank's shards) the elements are a fraction of the M positions, and a
+      // chunk's positions spread past the placement window, whose strays
+      // k_place writes directly -- each bucket's strays fall in a few 128-KB
+      // stripes.  Chunks of 15M positions instead made 77 chunks of 2.6M
+      // elements at C5 / 8 ranks: 19.6 ms of per-chunk launches.)
+      const uint32_t per_entry = elem ? 1u : k;  // elements per log entry
+      const size_t tot = size_t(bl[np] - bl[0]) * per_entry;
+      const uint32_t nch = uint32_t(std::max<size_t>(1, (tot + chunk_elems - 1) / chunk_elems));
       // the sentinel kPlaceNone is the code of log reference 2^31 - 1
       FH_CHECK(bbase + n < 0x7FFFFFFFull, FH_ENOTIMPL, "replica views: command log >= 2^31 - 1");
       uint32_t *pbase = place_base.ensure(nch);
@@ -2610,7 +2618,6 @@ struct EngineDevice {
       // 23-bit composite)
       const bool pow2 = (key_space & (key_space - 1)) == 0;
       const int bits = pow2 ? bits_for(key_space) : bits_for(uint64_t(np + 1) * key_space);
-      const uint32_t per_entry = elem ? 1u : k;  // elements per log entry
       const uint32_t *bent = lent.get() + (codes_only ? 0 : b * size_t(n) * fq * (elem ? k : 1));
       for (uint32_t c = 0; c < nch; c++) {
         LogChunk lc;

@@ -154,6 +154,9 @@ class HipStages:
         return {"dep_off": dep_off, "deps": deps[:ln.value], "scc_label": label[:count],
                 "pk_key": pk_key[:pk.value], "pk_dot": pk_dot[:pk.value]}
 
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
     def set_profiling(self, on):
         L.check(self.lib.fh_dgraph_set_profiling(self.h, 1 if on else 0))
 
@@ -239,9 +242,9 @@ class DistPartial:
 
     def __init__(self, rank: int, world: int, key_space: int, group=None, device: int = 0,
                  backend=None, n: int = 5, solo: bool = False):
-        """solo (measurement, for N ranks sharing one GPU): the condense and
-        solve stages run one rank at a time between barriers, so their stage
-        times are those of a GPU of their own."""
+        """solo (measurement, for N ranks sharing one GPU): the KeyDeps,
+        local, condense and solve stages run one rank at a time between
+        barriers, so their stage times are those of a GPU of their own."""
         self.rank, self.world = rank, world
         self.solo = solo
         self.stages = backend if backend is not None else HipStages(rank, world, key_space, device, n)
@@ -260,9 +263,9 @@ class DistPartial:
         """One step over the staged stream; returns its wall time (s)."""
         st, ex = self.stages, self.ex
         t0 = time.perf_counter()
-        codes = st.keydeps(int(self.send_counts.sum()))
+        codes = self._solo(lambda: st.keydeps(int(self.send_counts.sum())))
         recv = ex.a2a(codes, self.send_counts, self.recv_counts)
-        qc = st.local(recv)
+        qc = self._solo(lambda: st.local(recv))
         q = st.queries(int(qc.sum()))
         qin = ex.counts(qc)
         incoming = ex.a2a(q, qc, qin)
@@ -286,6 +289,9 @@ class DistPartial:
         for q in range(self.world):
             if q == self.rank:
                 out = fn()
+                sync = getattr(self.stages, "sync", None)
+                if sync is not None:
+                    sync()  # the stage's kernels end before the next rank's start
             self.ex.dist.barrier(group=self.ex.group)
         return out
 
