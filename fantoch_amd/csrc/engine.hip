@@ -104,7 +104,12 @@ __global__ void __launch_bounds__(kThreads)
                uint32_t dmask) {
   __shared__ uint32_t s_h[256];
   __shared__ uint32_t s_r0;
+  // the chunk's log table in LDS: indexed per lane, the kernel argument was a
+  // vector load from the argument segment per element and lookup
+  __shared__ uint32_t s_cum[kMaxLogs + 1], s_first[kMaxLogs];
   s_h[threadIdx.x] = 0;
+  if (threadIdx.x <= nlog) s_cum[threadIdx.x] = ch.cum[threadIdx.x];
+  if (threadIdx.x < nlog) s_first[threadIdx.x] = ch.first[threadIdx.x];
   const uint32_t base = blockIdx.x * uint32_t(kTile), end = min(M, base + uint32_t(kTile));
   // the tile's first log, searched once: a tile spans a log or two, so each
   // element advances from there (element logs: 40 logs, a search per element
@@ -114,14 +119,14 @@ __global__ void __launch_bounds__(kThreads)
   uint32_t r = s_r0;
   const uint32_t per = fq * k;
   for (uint32_t x = base + threadIdx.x; x < end; x += kThreads) {
-    while (r + 1 < nlog && ch.cum[r + 1] <= x) r++;
-    const uint32_t y = x - ch.cum[r];
+    while (r + 1 < nlog && s_cum[r + 1] <= x) r++;
+    const uint32_t y = x - s_cum[r];
     uint32_t key, val;
     if (elem) {
-      val = ent[ch.first[r] + y];
+      val = ent[s_first[r] + y];
       key = (r + 1) * K + key32[(val / per) * k + val % k];
     } else {
-      const uint32_t q = ch.first[r] + y / k, s = y % k;
+      const uint32_t q = s_first[r] + y / k, s = y % k;
       const uint32_t e = ent[q];
       key = (r + 1) * K + key32[(e / fq) * k + s];
       val = e * k + s;
