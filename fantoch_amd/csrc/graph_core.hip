@@ -284,9 +284,32 @@ __global__ void __launch_bounds__(256)
   }
   if (!__any(fwd)) return;  // no forward edge inside: no local cycle
   // pivots 0..63 live in rows r[0][*] of lane k, pivots 64..127 in r[1][*];
-  // the two halves are separate loops so every register index is static
+  // the two halves are separate loops so every register index is static.
+  // Only pivots with an edge out and an edge in inside the window can lie on
+  // a path through them, and Warshall never fills an empty row (a row grows
+  // only through a pivot it has an edge to) or an empty column (a column
+  // grows only from a row already holding one of its bits): the loops visit
+  // those pivots alone (wave-uniform masks, so the lane indices stay scalar)
+  uint64_t piv[2];
+  {
+    uint64_t c0 = r[0][0] | r[1][0], c1 = r[0][1] | r[1][1];  // columns, this lane's rows
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      c0 |= __shfl_xor(c0, o, 64);
+      c1 |= __shfl_xor(c1, o, 64);
+    }
+    piv[0] = __ballot((r[0][0] | r[0][1]) != 0) & c0;
+    piv[1] = __ballot((r[1][0] | r[1][1]) != 0) & c1;
+    // uniform: into scalar registers (a pivot index in a vector register
+    // would turn every readlane below into a waterfall)
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+      piv[h] = (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(piv[h] >> 32)))) << 32) |
+               uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(piv[h])));
+  }
 #define FH_WARSHALL_HALF(H)                                  \
-  for (int k = 0; k < 64; k++) {                             \
+  for (uint64_t pm = piv[H]; pm; pm &= pm - 1) {             \
+    const int k = __builtin_ctzll(pm);                       \
     const uint64_t k0 = rl64(r[H][0], k);                    \
     const uint64_t k1 = rl64(r[H][1], k);                    \
     const uint64_t m = uint64_t(1) << k;                     \
