@@ -329,8 +329,11 @@ __global__ void __launch_bounds__(256)
   // columns of its vertices l and 64 + l; then the vertices x mutually
   // reaches are row AND column, and the smallest of them below x is x's
   // local SCC minimum -- no LDS, no per-candidate loop
+  // (only for the pivots: a vertex without an edge in or out inside the
+  // window is on no cycle there, and its row or column stays empty)
   uint64_t col[2][2] = {{0, 0}, {0, 0}};
-  for (int xl = 0; xl < 64; xl++) {
+  for (uint64_t pm = piv[0] | piv[1]; pm; pm &= pm - 1) {
+    const int xl = __builtin_ctzll(pm);
     const uint64_t c00 = __ballot((r[0][0] >> xl) & 1);
     const uint64_t c01 = __ballot((r[1][0] >> xl) & 1);
     const uint64_t c10 = __ballot((r[0][1] >> xl) & 1);
