@@ -141,6 +141,7 @@ struct GraphCore {
   DBuf<uint64_t> t_prof;  // tile path: ready time, group rank/count/start
   uint32_t dbg_tile_fail = 0, dbg_tile_ok = 0;
   DBuf<uint8_t> fb_pushed;    // coloring reach: vertices that pushed this round
+  DBuf<uint32_t> fb_bits;     // coloring H propagation: three class bitmaps (frontier)
   bool prefer_full = false;   // the last global-path run needed the full coloring
   bool kap_seed_ok = true;    // kap holds a bounded run's ready times (k_fb_seed)
   DBuf<uint32_t> conv;        // device-side convergence flags (converge())

@@ -534,11 +534,28 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
                            const uint8_t *__restrict__ blocked,
                            const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep,
                            uint32_t *H, uint32_t *changed, const uint32_t *__restrict__ prev,
-                           int nodone) {
+                           int nodone, const uint32_t *__restrict__ bprev,
+                           uint32_t *__restrict__ bnow, uint32_t *__restrict__ bclr,
+                           uint32_t nwords) {
   // nodone: the first round of the full coloring (nothing done yet): the
   // done[] gathers per edge are skipped
+  // Frontier (the full first round, from its third launch; bprev non-null):
+  // bprev holds the classes whose H the previous launch raised.  A vertex
+  // took every target's H when it last ran and H only grows, so a target
+  // outside bprev has not risen since (a raise after the vertex's turn in
+  // the previous launch is in bprev; one in this launch, in bnow for the
+  // next): only the flagged targets are gathered, and a vertex with none
+  // (and its own class unflagged) contributes nothing new.  A launch that
+  // raises nothing leaves bnow empty, so the fixpoint test is unchanged.
+  // bnow records this launch's raises; bclr (the bitmap the launch before
+  // last wrote and the previous one read) is cleared for the next launch.
   // the previous launch of the group changed nothing: converged, return
+  // (tried: a coarse level of a bit per 8 classes, 1.6 MB at C5, probed
+  // first: 23.9 against 24.1 ms of H propagation per C5 step -- the probes
+  // are not what the later launches wait on)
   if (prev && ld_u32(prev) == 0) return;
+  if (bclr)
+    for (uint32_t w = blockIdx.x * B + threadIdx.x; w < nwords; w += gridDim.x * B) bclr[w] = 0;
   __shared__ AggTable<uint32_t> tb;
   agg_init<uint32_t, true>(tb);
   __syncthreads();
@@ -547,7 +564,9 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
     const uint32_t v = j < n ? FB_VID(j) : 0u;
     const bool act = j < n && !blocked[v] && !done[v];
     const uint32_t r = act ? rep[v] : 0u;
+    auto flagged = [&](uint32_t c) { return !bprev || ((bprev[c >> 5] >> (c & 31)) & 1u); };
     uint32_t best = 0;
+    bool any = act && flagged(r);
     if (act) {
       // done is uniform over a representative's class (members share
       // reached[r]; blocked is closed under cycles), so done[ru] == done[u]
@@ -558,12 +577,18 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
           uint32_t ru[4];
 #pragma unroll
           for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
+          bool fl[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            fl[j] = ru[j] != r && flagged(ru[j]);
+            any |= fl[j];
+          }
           uint8_t dn[4];
           uint32_t h[4];
 #pragma unroll
           for (int j = 0; j < 4; j++) {
-            dn[j] = ru[j] != r ? (nodone ? uint8_t(0) : done[ru[j]]) : uint8_t(1);
-            h[j] = ru[j] != r ? ld_u32(&H[ru[j]]) : 0;
+            dn[j] = fl[j] ? (nodone ? uint8_t(0) : done[ru[j]]) : uint8_t(1);
+            h[j] = fl[j] ? ld_u32(&H[ru[j]]) : 0;
           }
 #pragma unroll
           for (int j = 0; j < 4; j++)
@@ -583,16 +608,21 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
       // that t's class reaches (H over the same active subgraph: a lower
       // bound of the fixpoint, which stays the same); long forward chains
       // collapse in logarithmically many launches
-      const uint32_t t = max(best, ld_u32(&H[r]));
-      if (t < V && (nodone || !done[t]) && !blocked[t]) {
-        const uint32_t hj = ld_u32(&H[rep[t]]);
-        best = hj > best ? hj : best;
+      if (any) {
+        const uint32_t t = max(best, ld_u32(&H[r]));
+        if (t < V && (nodone || !done[t]) && !blocked[t]) {
+          const uint32_t hj = ld_u32(&H[rep[t]]);
+          best = hj > best ? hj : best;
+        }
       }
     }
     agg_lane<uint32_t, true>(tb, r, best, act && best != 0);
   }
   __syncthreads();
-  agg_flush<uint32_t, true>(tb, H, [&](uint32_t) { *changed = 1; });
+  agg_flush<uint32_t, true>(tb, H, [&](uint32_t k) {
+    *changed = 1;
+    if (bnow) atomicOr(&bnow[k >> 5], 1u << (k & 31));
+  });
 }
 
 // parent (the merge's union-find forest) starts as a copy of rep for every
@@ -1187,10 +1217,30 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
     if (full && !list && kap_seed_ok)
       k_fb_seed<<<G, B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get(), H);
     dbg_rounds++;
+    // the full first round (every class active, erep): launches from the
+    // third gather only the targets the previous launch raised (k_fb_hprop);
+    // three class bitmaps rotate (written, read, cleared).  C5: the first
+    // round's launches after the first took 3.5 ms each, most of them
+    // re-reading H of targets that no longer move (C5: 26.6 -> 24.1 ms of H
+    // propagation per step; each later launch 3.5 -> 2.4 ms, one launch
+    // more to the fixpoint: a vertex without a flagged target skips the
+    // pointer jump too)
+    const bool frontier = first_full && er != nullptr;
+    const uint32_t nw = (V + 31) / 32;
+    uint32_t *fbits = frontier ? fb_bits.ensure(3 * size_t(nw) + 1) : nullptr;
+    uint32_t li = 0;
     converge(1, dbg_hprop, [&](uint32_t *changed, const uint32_t *prev) {
+      const uint32_t *bp = nullptr;
+      uint32_t *bn = nullptr, *bc = nullptr;
+      if (frontier) {
+        bp = li >= 2 ? fbits + size_t((li - 1) % 3) * nw : nullptr;
+        bn = li >= 1 ? fbits + size_t(li % 3) * nw : nullptr;
+        bc = fbits + size_t((li + 1) % 3) * nw;
+      }
       k_fb_hprop<<<agg_blocks(n), B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er,
                                                   blocked.get(), done, rep.get(), H, changed, prev,
-                                                  int(first_full));
+                                                  int(first_full), bp, bn, bc, nw);
+      li++;
     });
     if (!list && !recent_iter) {
       k_fb_save_h<<<grid_for(V, B), B, 0, stream>>>(V, blocked.get(), rep.get(), H, hseed.ensure(V));
