@@ -536,7 +536,10 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
                            uint32_t *H, uint32_t *changed, const uint32_t *__restrict__ prev,
                            int nodone, const uint32_t *__restrict__ bprev,
                            uint32_t *__restrict__ bnow, uint32_t *__restrict__ bclr,
-                           uint32_t nwords) {
+                           uint32_t nwords, uint32_t *__restrict__ erep_out) {
+  // erep_out (the full round's first launch): the edge targets'
+  // representatives are gathered here, rep[dst[e]], and written to erep for
+  // the launches after it -- k_edge_rep's pass folded into this one
   // nodone: the first round of the full coloring (nothing done yet): the
   // done[] gathers per edge are skipped
   // Frontier (the full first round, from its third launch; bprev non-null):
@@ -575,8 +578,16 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
         // four edges per trip, every gather issued before the first is used
         for (uint32_t e = eb; e < ee; e += 4) {
           uint32_t ru[4];
+          if (erep_out) {
+            uint32_t u[4];
 #pragma unroll
-          for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
+            for (int j = 0; j < 4; j++) u[j] = e + j < ee ? dst[e + j] : v;
+#pragma unroll
+            for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? rep[u[j]] : r;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) ru[j] = e + j < ee ? erep[e + j] : r;
+          }
           bool fl[4];
 #pragma unroll
           for (int j = 0; j < 4; j++) {
@@ -593,6 +604,11 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
 #pragma unroll
           for (int j = 0; j < 4; j++)
             if (!dn[j]) best = h[j] > best ? h[j] : best;
+          if (erep_out) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if (e + j < ee) erep_out[e + j] = ru[j];
+          }
         }
       } else {
         for (uint32_t e = eb; e < ee; e++) {
@@ -1204,8 +1220,8 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
   const bool full = list == nullptr;
   const uint32_t *er = nullptr;
   if (full) {
-    refresh_edge_rep(in);
-    er = erep.get();
+    // (written by the first H-propagation launch below: k_fb_hprop erep_out)
+    er = nedges ? erep.ensure(nedges) : nullptr;
   }
   bool first_full = full;  // round 1 over every vertex: done[] is all zero
   for (;;) {
@@ -1239,7 +1255,9 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
       }
       k_fb_hprop<<<agg_blocks(n), B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er,
                                                   blocked.get(), done, rep.get(), H, changed, prev,
-                                                  int(first_full), bp, bn, bc, nw);
+                                                  int(first_full), bp, bn, bc, nw,
+                                                  first_full && li == 0 && er ? const_cast<uint32_t *>(er)
+                                                                       : nullptr);
       li++;
     });
     if (!list && !recent_iter) {
