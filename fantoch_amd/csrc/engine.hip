@@ -1856,7 +1856,7 @@ struct EngineDevice {
     const char *e = getenv("FH_KO_SIDE");
     return e && *e == '0';
   }();
-  // Workgroups of the side kernels: one 256-thread workgroup per CU.  The
+  // Workgroups of the side kernels: 256 threads, three per four CUs (below).  The
   // side kernels' random row stores are what slows the tile kernel beside
   // them (C4 with k_row_place issuing its loads but not its stores: 12.48 ->
   // 10.87 ms, r06f), so fewer side waves, finishing later, cost the tile
@@ -1911,7 +1911,12 @@ struct EngineDevice {
     {
       int cus = 0;
       FH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-      side_grid = unsigned(std::max(cus, 1));
+      // three workgroups per four CUs: the side stream's work (2.3 ms of
+      // row placement at one per CU) has slack beside the tile kernel (4.1
+      // ms), and fewer row stores in flight slow the tile kernel less (C4,
+      // ms per step, 256 / 224 / 192 / 160 / 128 workgroups: 11.37-11.56 /
+      // 11.30-11.43 / 11.27-11.29 / 11.30 / 12.27 on one box, r06sg)
+      side_grid = unsigned(std::max(cus * 3 / 4, 1));
     }
     FH_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     FH_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
