@@ -487,10 +487,21 @@ __global__ void k_fb_hreset(uint32_t n, const uint32_t *__restrict__ list,
   GRID_STRIDE(j, n) H[rep[FB_VID(j)]] = 0;
 }
 
+// the full first round's start (every vertex listed, nothing done): H[v] =
+// v and nothing reached, so that k_fb_init (reps_set) only folds in the
+// members that are not their class's representative -- the representative
+// (its minimum) is already there, and most classes hold one vertex
+__global__ void k_fb_iota(uint32_t V, uint32_t *__restrict__ H, uint8_t *__restrict__ reached) {
+  GRID_STRIDE(v, V) {
+    H[v] = v;
+    reached[v] = 0;
+  }
+}
+
 __global__ void __launch_bounds__(256)
     k_fb_init(uint32_t n, const uint32_t *__restrict__ list, const uint8_t *__restrict__ blocked,
               const uint8_t *__restrict__ done, const uint32_t *__restrict__ rep, uint32_t *H,
-              uint8_t *reached) {
+              uint8_t *reached, int reps_set) {
   // class maximum, block-aggregated (one item per thread)
   __shared__ AggTable<uint32_t> t;
   agg_init<uint32_t, true>(t);
@@ -498,8 +509,8 @@ __global__ void __launch_bounds__(256)
   const uint32_t j = blockIdx.x * B + threadIdx.x;
   const uint32_t v = j < n ? FB_VID(j) : 0u;
   const uint32_t r = j < n ? rep[v] : 0u;
-  if (j < n && r == v) reached[v] = 0;
-  const bool act = j < n && !blocked[v] && !done[v];
+  if (j < n && r == v && !reps_set) reached[v] = 0;
+  const bool act = j < n && !blocked[v] && !done[v] && !(reps_set && r == v);
   agg_lane<uint32_t, true>(t, r, v, act);
   __syncthreads();
   agg_flush<uint32_t, true>(t, H, [](uint32_t) {});
@@ -1227,9 +1238,12 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
   for (;;) {
     if (list)
       k_fb_hreset<<<G, B, 0, stream>>>(n, list, rep.get(), H);
+    else if (first_full)
+      k_fb_iota<<<grid_for(V, B), B, 0, stream>>>(V, H, reached);
     else
       FH_HIP(hipMemsetAsync(H, 0, size_t(V) * sizeof(uint32_t), stream));
-    k_fb_init<<<agg_blocks(n), B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached);
+    k_fb_init<<<agg_blocks(n), B, 0, stream>>>(n, list, blocked.get(), done, rep.get(), H, reached,
+                                                int(first_full && !list));
     if (full && !list && kap_seed_ok)
       k_fb_seed<<<G, B, 0, stream>>>(V, blocked.get(), rep.get(), kap.get(), H);
     dbg_rounds++;
