@@ -577,10 +577,6 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
     const uint32_t j = blockIdx.x * B + threadIdx.x;
     const uint32_t v = j < n ? FB_VID(j) : 0u;
     const bool act = j < n && !blocked[v] && !done[v];
-    // (the first launch covers every edge of erep / esrc: an inactive
-    // vertex's edges get a sentinel target that k_fb_hprop_edges skips)
-    if (erep_out && j < n && !act)
-      for (uint32_t e = EB(v); e < EE(v); e++) erep_out[e] = ~0u;
     const uint32_t r = act ? rep[v] : 0u;
     auto flagged = [&](uint32_t c) { return !bprev || ((bprev[c >> 5] >> (c & 31)) & 1u); };
     uint32_t best = 0;
@@ -654,57 +650,6 @@ __global__ void __launch_bounds__(256) k_fb_hprop(uint32_t V, uint32_t n, const 
     *changed = 1;
     if (bnow) atomicOr(&bnow[k >> 5], 1u << (k & 31));
   });
-}
-
-// Frontier launches of the first full round, edge by edge (from the third
-// launch): workgroup w takes the edges of vertices [256w, 256w + 256) and
-// its threads stride over them together, so erep streams coalesced (the
-// vertex-parallel launch read each vertex's own edge run per lane, 2.4 ms a
-// launch at C5 whatever the frontier held); an edge whose target class rose
-// in the previous launch finds its source in the workgroup's offsets (LDS)
-// and raises the source's class directly.  Exact as k_fb_hprop's frontier
-// (H only grows; a class outside bprev has not risen since each of its
-// sources last read it); no pointer jump, which only accelerates (the
-// fixpoint over the edges is the same).
-__global__ void __launch_bounds__(256)
-    k_fb_hprop_edges(uint32_t V, const uint32_t *__restrict__ off, uint32_t stride,
-                     const uint32_t *__restrict__ erep, const uint32_t *__restrict__ rep,
-                     uint32_t *H, uint32_t *changed, const uint32_t *__restrict__ prev,
-                     const uint32_t *__restrict__ bprev, uint32_t *__restrict__ bnow,
-                     uint32_t *__restrict__ bclr, uint32_t nwords) {
-  if (prev && ld_u32(prev) == 0) return;
-  __shared__ uint32_t s_off[B + 1];
-  for (uint32_t w = blockIdx.x * B + threadIdx.x; w < nwords; w += gridDim.x * B) bclr[w] = 0;
-  const uint32_t v0 = blockIdx.x * B, nv = min(uint32_t(B), V - v0);
-  // the block's nv + 1 offsets (B threads: the end offset by thread 0)
-  if (threadIdx.x < nv) s_off[threadIdx.x] = EB(v0 + threadIdx.x);
-  if (threadIdx.x == 0) s_off[nv] = EE(v0 + nv - 1);
-  __syncthreads();
-  bool ch = false;
-  for (uint32_t e = s_off[0] + threadIdx.x; e < s_off[nv]; e += B) {
-    const uint32_t ru = erep[e];
-    // (~0: an inactive source's edge, written so by the round's first launch)
-    if (ru == ~0u || !((bprev[ru >> 5] >> (ru & 31)) & 1u)) continue;
-    uint32_t lo = 0, hi = nv - 1;  // the last i with s_off[i] <= e
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (s_off[mid] <= e)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    const uint32_t r = rep[v0 + lo];
-    if (r == ru) continue;
-    const uint32_t h = ld_u32(&H[ru]);
-    if (h > ld_u32(&H[r])) {
-      const uint32_t old = atomicMax(&H[r], h);
-      if (old < h) {
-        ch = true;
-        atomicOr(&bnow[r >> 5], 1u << (r & 31));
-      }
-    }
-  }
-  if (__any(ch) && (threadIdx.x & 63) == 0) *changed = 1;
 }
 
 // parent (the merge's union-find forest) starts as a copy of rep for every
@@ -1322,15 +1267,11 @@ bool GraphCore::coloring_fallback(const GraphInput &in, uint32_t recent_iter) {
         bn = li >= 1 ? fbits + size_t(li % 3) * nw : nullptr;
         bc = fbits + size_t((li + 1) % 3) * nw;
       }
-      if (bp) {
-        k_fb_hprop_edges<<<agg_blocks(V), B, 0, stream>>>(V, in.off, in.stride, er, rep.get(), H,
-                                                           changed, prev, bp, bn, bc, nw);
-      } else {
-        k_fb_hprop<<<agg_blocks(n), B, 0, stream>>>(
-            V, n, list, in.off, in.stride, in.dst, er, blocked.get(), done, rep.get(), H, changed,
-            prev, int(first_full), bp, bn, bc, nw,
-            first_full && li == 0 && er ? const_cast<uint32_t *>(er) : nullptr);
-      }
+      k_fb_hprop<<<agg_blocks(n), B, 0, stream>>>(V, n, list, in.off, in.stride, in.dst, er,
+                                                  blocked.get(), done, rep.get(), H, changed, prev,
+                                                  int(first_full), bp, bn, bc, nw,
+                                                  first_full && li == 0 && er ? const_cast<uint32_t *>(er)
+                                                                       : nullptr);
       li++;
     });
     if (!list && !recent_iter) {
